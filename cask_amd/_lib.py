@@ -1,0 +1,118 @@
+"""ctypes binding of include/cask_scan.h (libcask_scan.so, built in-tree by __graft_entry__.build()).
+
+There is no fallback: if the native library is missing, every entry point raises
+NativeLibraryMissing. This is the only module that loads the shared object.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libcask_scan.so")
+
+c_u8p = C.POINTER(C.c_uint8)
+c_u16p = C.POINTER(C.c_uint16)
+c_u32p = C.POINTER(C.c_uint32)
+c_u64p = C.POINTER(C.c_uint64)
+
+
+class NativeLibraryMissing(ImportError):
+    pass
+
+
+class FileView(C.Structure):
+    _fields_ = [("file_id", C.c_uint32), ("flags", C.c_uint32), ("data", C.c_void_p), ("len", C.c_uint64)]
+
+
+class Rows(C.Structure):
+    _fields_ = [("capacity", C.c_uint64), ("count", C.c_uint64), ("pos", C.c_void_p), ("seq", C.c_void_p),
+                ("vsz", C.c_void_p), ("ksz", C.c_void_p), ("status", C.c_void_p)]
+
+
+class ScanError(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("file_id", C.c_uint32), ("pos", C.c_uint64), ("expected", C.c_uint32),
+                ("found", C.c_uint32), ("row", C.c_uint64)]
+
+
+class Options(C.Structure):
+    _fields_ = [("create", C.c_int32), ("write_hints", C.c_int32), ("max_file_size", C.c_uint64),
+                ("device", C.c_int32), ("reserved", C.c_int32)]
+
+
+class OpenError(C.Structure):
+    _fields_ = [("status", C.c_int32), ("file_id", C.c_uint32), ("pos", C.c_uint64), ("expected", C.c_uint32),
+                ("found", C.c_uint32)]
+
+
+class IndexEntry(C.Structure):
+    _fields_ = [("file_id", C.c_uint32), ("pad", C.c_uint32), ("entry_pos", C.c_uint64),
+                ("entry_size", C.c_uint64), ("sequence", C.c_uint64)]
+
+
+VIEW_DEVICE = 1
+ROW_OK, ROW_CHECKSUM, ROW_EOF = 0, 1, 2
+
+# cask_status
+OK = 0
+E_CHECKSUM = -1
+E_EOF = -2
+E_IO = -3
+E_INVALID_PATH = -4
+E_INVALID_FILE_ID = -5
+E_INVALID_ARG = -10
+E_DEVICE = -11
+E_CAPACITY = -12
+E_NOMEM = -13
+E_LOCKED = -14
+
+# (name, restype, argtypes) for every symbol declared in include/cask_scan.h
+SIGNATURES = [
+    ("cask_ctx_create", C.c_void_p, [C.c_int, C.POINTER(C.c_int)]),
+    ("cask_ctx_destroy", None, [C.c_void_p]),
+    ("cask_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("cask_ctx_stream", C.c_void_p, [C.c_void_p]),
+    ("cask_ctx_device", C.c_int, [C.c_void_p]),
+    ("cask_scan_chunk_bytes", C.c_uint32, []),
+    ("cask_rows_bound", C.c_uint64, [C.POINTER(FileView), C.c_uint32]),
+    ("cask_scan_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
+                                   C.POINTER(ScanError)]),
+    ("cask_scan_host", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
+                                 C.POINTER(ScanError)]),
+    ("cask_last_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    ("cask_last_counters", C.c_int, [C.c_void_p, c_u64p]),
+    ("cask_encode_synthetic_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
+                                               C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("cask_encode_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("cask_xxh32", C.c_uint32, [C.c_void_p, C.c_uint64]),
+    ("cask_options_default", None, [C.POINTER(Options)]),
+    ("cask_db_open", C.c_void_p, [C.c_char_p, C.POINTER(Options), C.POINTER(OpenError)]),
+    ("cask_db_close", None, [C.c_void_p]),
+    ("cask_db_len", C.c_uint64, [C.c_void_p]),
+    ("cask_db_get_entry", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.POINTER(IndexEntry)]),
+    ("cask_db_export", C.c_int64, [C.c_void_p, C.c_void_p, C.c_uint64, c_u64p, c_u64p, C.POINTER(IndexEntry),
+                                   C.c_uint64]),
+    ("cask_db_stats", C.c_uint64, [C.c_void_p, c_u32p, c_u64p, c_u64p, c_u64p, C.c_uint64]),
+    ("cask_db_current_sequence", C.c_uint64, [C.c_void_p]),
+    ("cask_db_files", C.c_uint64, [C.c_void_p, c_u32p, C.c_uint64]),
+    ("cask_db_open_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+]
+
+_lib = None
+
+
+def lib():
+    """Load libcask_scan.so once and bind every signature. Raises if it is absent."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise NativeLibraryMissing(
+                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib

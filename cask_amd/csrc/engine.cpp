@@ -1,0 +1,585 @@
+// Host engine above the C ABI: the Cask::open replay (cask.rs:335-382) with the data-file scan
+// on the GPU. Mirrors Log::open (log.rs:36-85), find_data_files (log.rs:483-510), the hint-file
+// fast path (log.rs:121-135, 432-447, 512-539; data.rs:258-276), hint recreation
+// (log.rs:137-148, 367-395, 449-471), and the keydir fold Index::update + Stats
+// (cask.rs:28-95; stats.rs:6-67). The scan itself is cask_scan_host (scan_runtime.cpp).
+#include <dirent.h>
+#include <fcntl.h>
+#include <sys/file.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <regex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/cask_scan.h"
+#include "xxh32.h"
+
+namespace {
+
+inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+inline uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+inline uint64_t rd64(const uint8_t* p) { return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32); }
+inline void wr16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+inline void wr32(uint8_t* p, uint32_t v) { for (int i = 0; i < 4; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
+inline void wr64(uint8_t* p, uint64_t v) { for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (8 * i)); }
+
+inline uint64_t hash_key(const uint8_t* k, uint32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xC2B2AE3D27D4EB4Full);
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    memcpy(&w, k + i, 8);
+    h = (h ^ w) * 0xBF58476D1CE4E5B9ull;
+    h ^= h >> 31;
+  }
+  uint64_t t = 0;
+  for (uint32_t j = 0; i + j < n; ++j) t |= (uint64_t)k[i + j] << (8 * j);
+  h = (h ^ t) * 0x94D049BB133111EBull;
+  return h ^ (h >> 29);
+}
+
+struct StatsEntry {  // stats.rs:7-11
+  uint64_t entries = 0, dead_entries = 0, dead_bytes = 0;
+};
+
+// HashMap<Vec<u8>, IndexEntry> + Stats (cask.rs:28-31). Open addressing; keys live in an
+// append-only arena (the reference copies every key: hint.key.to_vec(), cask.rs:68).
+class KeyDir {
+ public:
+  struct Slot {
+    uint64_t hash;
+    uint64_t key_off;
+    uint32_t ksz;
+    uint32_t state;  // 0 empty, 1 live, 2 deleted
+    cask_index_entry e;
+  };
+  std::vector<Slot> slots;
+  std::vector<uint8_t> arena;
+  uint64_t live = 0, used = 0;
+  std::unordered_map<uint32_t, StatsEntry> stats;
+
+  KeyDir() { slots.assign(1024, Slot{}); }
+
+  const uint8_t* key_of(const Slot& s) const { return arena.data() + s.key_off; }
+
+  int64_t find(const uint8_t* k, uint32_t n, uint64_t h) const {
+    const uint64_t m = slots.size() - 1;
+    for (uint64_t i = h & m;; i = (i + 1) & m) {
+      const Slot& s = slots[i];
+      if (s.state == 0) return -(int64_t)i - 1;
+      if (s.state == 1 && s.hash == h && s.ksz == n && (n == 0 || memcmp(key_of(s), k, n) == 0)) return (int64_t)i;
+    }
+  }
+
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(slots);
+    slots.assign(old.size() * 2, Slot{});
+    used = 0;
+    const uint64_t m = slots.size() - 1;
+    for (const Slot& s : old) {
+      if (s.state != 1) continue;
+      uint64_t i = s.hash & m;
+      while (slots[i].state) i = (i + 1) & m;
+      slots[i] = s;
+      ++used;
+    }
+  }
+
+  // Stats::add_entry / remove_entry (stats.rs:23-48)
+  void stats_add(uint32_t file_id) { stats[file_id].entries += 1; }
+  void stats_remove(uint32_t file_id, uint64_t size) {
+    auto it = stats.find(file_id);
+    if (it == stats.end()) return;  // "Tried to reclaim non-existant entry": warn only
+    it->second.dead_entries += 1;
+    it->second.dead_bytes += size;
+  }
+
+  // Index::update (cask.rs:60-90). vsz_raw is the hint's value_size field.
+  void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+    const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
+    cask_index_entry ie{};
+    ie.file_id = file_id;
+    ie.entry_pos = pos;
+    ie.entry_size = 18ull + ksz + (deleted ? 0ull : (uint64_t)vsz_raw);  // data.rs:238-240
+    ie.sequence = seq;
+    if ((used + 1) * 4 > slots.size() * 3) grow();
+    const uint64_t h = hash_key(key, ksz);
+    int64_t f = find(key, ksz, h);
+    if (f >= 0) {  // Occupied
+      Slot& s = slots[f];
+      if (s.e.sequence <= seq) {
+        stats_remove(s.e.file_id, s.e.entry_size);
+        if (deleted) {
+          s.state = 2;
+          --live;
+        } else {
+          stats_add(file_id);
+          s.e = ie;
+        }
+      } else {
+        stats_add(file_id);
+        stats_remove(file_id, ie.entry_size);
+      }
+      return;
+    }
+    if (deleted) return;  // Vacant + tombstone: nothing
+    stats_add(file_id);
+    Slot& s = slots[(uint64_t)(-f - 1)];
+    s.hash = h;
+    s.key_off = arena.size();
+    s.ksz = ksz;
+    s.state = 1;
+    s.e = ie;
+    arena.insert(arena.end(), key, key + ksz);
+    ++live;
+    ++used;
+  }
+};
+
+bool is_dir(const std::string& p) {
+  struct stat st;
+  return stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+bool exists(const std::string& p) {
+  struct stat st;
+  return stat(p.c_str(), &st) == 0;
+}
+bool is_file_follow(const std::string& p) {  // Path::is_file (follows symlinks)
+  struct stat st;
+  return stat(p.c_str(), &st) == 0 && S_ISREG(st.st_mode);
+}
+
+std::string data_path(const std::string& dir, uint32_t id) {  // log.rs:473-476
+  char b[32];
+  snprintf(b, sizeof(b), "%010u.cask.data", id);
+  return dir + "/" + b;
+}
+std::string hint_path(const std::string& dir, uint32_t id) {  // log.rs:478-481
+  char b[32];
+  snprintf(b, sizeof(b), "%010u.cask.hint", id);
+  return dir + "/" + b;
+}
+
+bool read_file(const std::string& p, std::vector<uint8_t>& out) {
+  int fd = open(p.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return false;
+  }
+  out.resize((size_t)st.st_size);
+  size_t got = 0;
+  while (got < out.size()) {
+    ssize_t r = read(fd, out.data() + got, out.size() - got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      close(fd);
+      return false;
+    }
+    if (r == 0) break;
+    got += (size_t)r;
+  }
+  out.resize(got);
+  close(fd);
+  return true;
+}
+
+bool write_file(const std::string& p, const std::vector<uint8_t>& body, uint32_t trailer) {
+  int fd = open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);  // util.rs:45-49
+  if (fd < 0) return false;
+  std::vector<uint8_t> buf(body);
+  uint8_t t[4];
+  wr32(t, trailer);
+  buf.insert(buf.end(), t, t + 4);
+  size_t off = 0;
+  while (off < buf.size()) {
+    ssize_t w = write(fd, buf.data() + off, buf.size() - off);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      close(fd);
+      return false;
+    }
+    off += (size_t)w;
+  }
+  close(fd);
+  return true;
+}
+
+// find_data_files (log.rs:483-510): regex "(\d+).cask.data$" (unescaped '.', unanchored),
+// regular files only (DirEntry::metadata does not follow symlinks), u32 parse, ascending.
+bool find_data_files(const std::string& dir, std::vector<uint32_t>& out) {
+  DIR* d = opendir(dir.c_str());
+  if (!d) return false;
+  static const std::regex re("(\\d+).cask.data$");
+  while (struct dirent* e = readdir(d)) {
+    std::string name = e->d_name;
+    std::string full = dir + "/" + name;
+    struct stat st;
+    if (lstat(full.c_str(), &st) != 0 || !S_ISREG(st.st_mode)) continue;
+    std::smatch m;
+    if (!std::regex_search(name, m, re)) continue;
+    const std::string digits = m[1].str();
+    // str::parse::<u32>: overflow -> Err -> skipped
+    uint64_t v = 0;
+    bool okp = true;
+    for (char ch : digits) {
+      v = v * 10 + (uint64_t)(ch - '0');
+      if (v > 0xFFFFFFFFull) {
+        okp = false;
+        break;
+      }
+    }
+    if (okp) out.push_back((uint32_t)v);
+  }
+  closedir(d);
+  std::sort(out.begin(), out.end());
+  return true;
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+struct cask_db {
+  std::string path;
+  cask_options opts{};
+  int lock_fd = -1;
+  std::vector<uint32_t> files;
+  KeyDir index;
+  uint64_t sequence = 0;
+  double timings[5] = {0, 0, 0, 0, 0};
+  ~cask_db() {
+    if (lock_fd >= 0) {
+      flock(lock_fd, LOCK_UN);  // Drop for Log (log.rs:225-229)
+      close(lock_fd);
+    }
+  }
+};
+
+extern "C" {
+
+void cask_options_default(cask_options* o) {
+  if (!o) return;
+  memset(o, 0, sizeof(*o));
+  o->create = 1;
+  o->write_hints = 1;
+  o->max_file_size = 2ull * 1024 * 1024 * 1024;  // cask.rs:225
+  o->device = 0;
+}
+
+static void set_err(cask_open_error* err, int status, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0,
+                    uint32_t f = 0) {
+  if (!err) return;
+  err->status = status;
+  err->file_id = fid;
+  err->pos = pos;
+  err->expected = e;
+  err->found = f;
+}
+
+cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
+  set_err(err, CASK_OK);
+  if (!path_c) {
+    set_err(err, CASK_E_INVALID_ARG);
+    return nullptr;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  cask_options opts;
+  if (opts_in) opts = *opts_in; else cask_options_default(&opts);
+  std::string path = path_c;
+  // Log::open path checks (log.rs:46-56)
+  if (opts.create) {
+    if (exists(path) && !is_dir(path)) {
+      set_err(err, CASK_E_INVALID_PATH);
+      return nullptr;
+    }
+    if (!exists(path) && mkdir(path.c_str(), 0755) != 0) {
+      set_err(err, CASK_E_IO);
+      return nullptr;
+    }
+  } else if (!exists(path) || !is_dir(path)) {
+    set_err(err, CASK_E_INVALID_PATH);
+    return nullptr;
+  }
+  cask_db* db = new (std::nothrow) cask_db();
+  if (!db) {
+    set_err(err, CASK_E_NOMEM);
+    return nullptr;
+  }
+  db->path = path;
+  db->opts = opts;
+  // File::create("cask.lock") + try_lock_exclusive (log.rs:58-59)
+  db->lock_fd = open((path + "/cask.lock").c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (db->lock_fd < 0) {
+    delete db;
+    set_err(err, CASK_E_IO);
+    return nullptr;
+  }
+  if (flock(db->lock_fd, LOCK_EX | LOCK_NB) != 0) {
+    close(db->lock_fd);
+    db->lock_fd = -1;
+    delete db;
+    set_err(err, CASK_E_LOCKED);
+    return nullptr;
+  }
+  if (!find_data_files(path, db->files)) {
+    delete db;
+    set_err(err, CASK_E_IO);
+    return nullptr;
+  }
+
+  // Which files have a valid hint file (log.rs:121-135, 512-539)?
+  const size_t nf = db->files.size();
+  std::vector<std::vector<uint8_t>> hints(nf), data(nf);
+  std::vector<char> use_hint(nf, 0), data_ok(nf, 1);
+  std::vector<uint32_t> scan_idx;
+  for (size_t i = 0; i < nf; ++i) {
+    const std::string hp = hint_path(path, db->files[i]);
+    if (is_file_follow(hp) && read_file(hp, hints[i]) && hints[i].size() >= 4) {
+      const size_t n = hints[i].size();
+      if (cask_xxh::xxh32(hints[i].data(), n - 4, 0) == rd32(hints[i].data() + n - 4)) {
+        use_hint[i] = 1;
+        continue;
+      }
+    }
+    hints[i].clear();
+    if (!read_file(data_path(path, db->files[i]), data[i])) data_ok[i] = 0;
+    scan_idx.push_back((uint32_t)i);
+  }
+  db->timings[0] = ms_since(t0);
+
+  // Device scan of every data file that needs its hints recreated, in one batch.
+  std::vector<uint64_t> pos, seq;
+  std::vector<uint32_t> vsz;
+  std::vector<uint16_t> ksz;
+  std::vector<uint8_t> status;
+  std::vector<uint64_t> row_off;
+  std::vector<int> scan_slot(nf, -1);
+  auto t1 = std::chrono::steady_clock::now();
+  if (!scan_idx.empty()) {
+    std::vector<cask_file_view> views;
+    for (uint32_t i : scan_idx) {
+      if (!data_ok[i]) continue;
+      scan_slot[i] = (int)views.size();
+      cask_file_view v{};
+      v.file_id = db->files[i];
+      v.flags = 0;
+      v.data = data[i].data();
+      v.len = data[i].size();
+      views.push_back(v);
+    }
+    if (!views.empty()) {
+      int st = CASK_OK;
+      cask_ctx* ctx = cask_ctx_create(opts.device, &st);
+      if (!ctx) {
+        delete db;
+        set_err(err, CASK_E_DEVICE);
+        return nullptr;
+      }
+      uint64_t bound = cask_rows_bound(views.data(), (uint32_t)views.size());
+      pos.resize(bound);
+      seq.resize(bound);
+      vsz.resize(bound);
+      ksz.resize(bound);
+      status.resize(bound);
+      row_off.resize(views.size() + 1);
+      cask_rows rows{};
+      rows.capacity = bound;
+      rows.pos = pos.data();
+      rows.seq = seq.data();
+      rows.vsz = vsz.data();
+      rows.ksz = ksz.data();
+      rows.status = status.data();
+      cask_scan_error se{};
+      st = cask_scan_host(ctx, views.data(), (uint32_t)views.size(), &rows, row_off.data(), &se);
+      cask_ctx_destroy(ctx);
+      if (st != CASK_OK) {
+        delete db;
+        set_err(err, st);
+        return nullptr;
+      }
+    }
+  }
+  db->timings[1] = ms_since(t1);
+
+  // Replay in ascending file order (cask.rs:348-369); the first Err aborts open().
+  double t_hint = 0, t_fold = 0;
+  for (size_t i = 0; i < nf; ++i) {
+    const uint32_t fid = db->files[i];
+    if (use_hint[i]) {
+      auto tf = std::chrono::steady_clock::now();
+      const std::vector<uint8_t>& hb = hints[i];
+      const uint64_t body = hb.size() - 4;  // Take(size - 4) (log.rs:129)
+      uint64_t p = 0;
+      while (p < body) {  // Hints::next / Hint::from_read (log.rs:437-447; data.rs:258-276)
+        if (body - p < 22) {
+          t_fold += ms_since(tf);
+          delete db;
+          set_err(err, CASK_E_EOF, fid, p);
+          return nullptr;
+        }
+        const uint8_t* h = hb.data() + p;
+        const uint64_t s = rd64(h);
+        const uint16_t k = rd16(h + 8);
+        const uint32_t v = rd32(h + 10);
+        const uint64_t epos = rd64(h + 14);
+        if (body - p - 22 < k) {
+          delete db;
+          set_err(err, CASK_E_EOF, fid, p);
+          return nullptr;
+        }
+        if (s > db->sequence) db->sequence = s;
+        db->index.update(h + 22, k, fid, epos, v == CASK_ENTRY_TOMBSTONE ? CASK_ENTRY_TOMBSTONE : v, s);
+        p += 22ull + k;
+      }
+      t_fold += ms_since(tf);
+      continue;
+    }
+    if (!data_ok[i]) {
+      // HintWriter::new truncated the hint file before Log::entries failed; its Drop then wrote
+      // the trailer of an empty body (log.rs:141-142, 389-395).
+      if (opts.write_hints) write_file(hint_path(path, fid), {}, cask_xxh::xxh32(nullptr, 0, 0));
+      delete db;
+      set_err(err, CASK_E_IO, fid);
+      return nullptr;
+    }
+    const int slot = scan_slot[i];
+    const uint64_t r0 = row_off[slot], r1 = row_off[slot + 1];
+    const uint8_t* buf = data[i].data();
+    // Hint file: every Ok row (RecreateHints::drop keeps draining after an error), + trailer.
+    auto th = std::chrono::steady_clock::now();
+    if (opts.write_hints) {
+      std::vector<uint8_t> hb;
+      hb.reserve((r1 - r0) * 38);
+      for (uint64_t r = r0; r < r1; ++r) {
+        if (status[r] != CASK_ROW_OK) continue;
+        uint8_t h[22];
+        wr64(h, seq[r]);
+        wr16(h + 8, ksz[r]);
+        wr32(h + 10, vsz[r]);
+        wr64(h + 14, pos[r]);
+        hb.insert(hb.end(), h, h + 22);
+        hb.insert(hb.end(), buf + pos[r] + 18, buf + pos[r] + 18 + ksz[r]);
+      }
+      if (!write_file(hint_path(path, fid), hb, cask_xxh::xxh32(hb.data(), hb.size(), 0))) {
+        delete db;
+        set_err(err, CASK_E_IO, fid);
+        return nullptr;
+      }
+    }
+    t_hint += ms_since(th);
+    auto tf = std::chrono::steady_clock::now();
+    for (uint64_t r = r0; r < r1; ++r) {
+      if (status[r] != CASK_ROW_OK) {
+        const uint64_t p = pos[r];
+        uint32_t e = 0, f = 0;
+        if (p + 18 <= data[i].size()) {
+          e = rd32(buf + p);
+          if (status[r] == CASK_ROW_CHECKSUM) {
+            const uint64_t rl = 18ull + ksz[r] + (vsz[r] == CASK_ENTRY_TOMBSTONE ? 0ull : (uint64_t)vsz[r]);
+            f = cask_xxh::xxh32(buf + p + 4, rl - 4, 0);
+          }
+        }
+        delete db;
+        set_err(err, status[r] == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF, fid, p, e, f);
+        return nullptr;
+      }
+      if (seq[r] > db->sequence) db->sequence = seq[r];
+      db->index.update(buf + pos[r] + 18, ksz[r], fid, pos[r], vsz[r], seq[r]);
+    }
+    t_fold += ms_since(tf);
+    std::vector<uint8_t>().swap(data[i]);
+  }
+  db->timings[2] = t_hint;
+  db->timings[3] = t_fold;
+  db->timings[4] = ms_since(t0);
+  return db;
+}
+
+void cask_db_close(cask_db* db) { delete db; }
+
+uint64_t cask_db_len(const cask_db* db) { return db ? db->index.live : 0; }
+
+int cask_db_get_entry(const cask_db* db, const uint8_t* key, uint64_t ksz, cask_index_entry* out) {
+  if (!db || (ksz && !key) || ksz > 0xFFFF) return 0;
+  int64_t f = db->index.find(key, (uint32_t)ksz, hash_key(key, (uint32_t)ksz));
+  if (f < 0) return 0;
+  if (out) *out = db->index.slots[f].e;
+  return 1;
+}
+
+int64_t cask_db_export(const cask_db* db, uint8_t* key_bytes, uint64_t key_cap, uint64_t* key_off,
+                       uint64_t* key_len, cask_index_entry* entries, uint64_t nkeys) {
+  if (!db) return CASK_E_INVALID_ARG;
+  const KeyDir& ix = db->index;
+  std::vector<uint64_t> idx;
+  idx.reserve(ix.live);
+  for (uint64_t i = 0; i < ix.slots.size(); ++i)
+    if (ix.slots[i].state == 1) idx.push_back(i);
+  std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) {
+    const auto& A = ix.slots[a];
+    const auto& B = ix.slots[b];
+    const uint32_t n = std::min(A.ksz, B.ksz);
+    int c = n ? memcmp(ix.key_of(A), ix.key_of(B), n) : 0;
+    if (c) return c < 0;
+    return A.ksz < B.ksz;
+  });
+  uint64_t total = 0;
+  for (uint64_t j = 0; j < idx.size(); ++j) total += ix.slots[idx[j]].ksz;
+  if (nkeys < idx.size() || (key_bytes && key_cap < total)) return CASK_E_CAPACITY;
+  uint64_t off = 0;
+  for (uint64_t j = 0; j < idx.size(); ++j) {
+    const auto& s = ix.slots[idx[j]];
+    if (key_bytes && s.ksz) memcpy(key_bytes + off, ix.key_of(s), s.ksz);
+    if (key_off) key_off[j] = off;
+    if (key_len) key_len[j] = s.ksz;
+    if (entries) entries[j] = s.e;
+    off += s.ksz;
+  }
+  return (int64_t)total;
+}
+
+uint64_t cask_db_stats(const cask_db* db, uint32_t* file_id, uint64_t* entries, uint64_t* dead_entries,
+                       uint64_t* dead_bytes, uint64_t cap) {
+  if (!db) return 0;
+  std::vector<std::pair<uint32_t, StatsEntry>> v(db->index.stats.begin(), db->index.stats.end());
+  std::sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+  for (uint64_t i = 0; i < v.size() && i < cap; ++i) {
+    if (file_id) file_id[i] = v[i].first;
+    if (entries) entries[i] = v[i].second.entries;
+    if (dead_entries) dead_entries[i] = v[i].second.dead_entries;
+    if (dead_bytes) dead_bytes[i] = v[i].second.dead_bytes;
+  }
+  return v.size();
+}
+
+uint64_t cask_db_current_sequence(const cask_db* db) { return db ? db->sequence + 1 : 0; }
+
+uint64_t cask_db_files(const cask_db* db, uint32_t* ids, uint64_t cap) {
+  if (!db) return 0;
+  for (uint64_t i = 0; i < db->files.size() && i < cap; ++i) ids[i] = db->files[i];
+  return db->files.size();
+}
+
+int cask_db_open_timings(const cask_db* db, double* ms5) {
+  if (!db || !ms5) return CASK_E_INVALID_ARG;
+  memcpy(ms5, db->timings, sizeof(db->timings));
+  return CASK_OK;
+}
+
+}  // extern "C"

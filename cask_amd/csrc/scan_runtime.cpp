@@ -1,0 +1,426 @@
+// Host runtime behind include/cask_scan.h: device contexts, scratch management, the scan
+// pipeline (speculative chunk scan -> long records -> validate -> [repair] -> summary) and the
+// batched encoder. Compiled with hipcc into libcask_scan.so.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "../../include/cask_scan.h"
+#include "scan_kernels.h"
+#include "xxh32.h"
+
+using namespace cask_dev;
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 4 + 256;
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <typename T>
+  T* as() const { return (T*)p; }
+};
+
+struct HostPinned {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool ensure(size_t bytes) {
+    if (bytes <= cap) return true;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = bytes + bytes / 4 + 256;
+    if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
+      p = nullptr;
+      return false;
+    }
+    cap = want;
+    return true;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+};
+
+inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct cask_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  DevBuf chunk;      // lb | spec | exit | base | tin (u64 x5) | count (u32)
+  DevBuf ctr;        // Counters
+  DevBuf longbuf;    // long_row (u64) | long_file (u32)
+  DevBuf filebuf;    // FileDesc[] | file_err_row[] | first_bad[] | summary
+  DevBuf err2;       // 2 x u32
+  HostPinned hfiles;
+  HostPinned hsum;
+  // host-scan staging
+  DevBuf stage_data;
+  DevBuf stage_rows;
+  hipEvent_t ev[6] = {};
+  float last_ms[5] = {0, 0, 0, 0, 0};
+  uint64_t last_counters[3] = {0, 0, 0};
+  std::mutex mu;
+};
+
+static int set_dev(const cask_ctx* c) {
+  return hipSetDevice(c->device) == hipSuccess ? CASK_OK : CASK_E_DEVICE;
+}
+
+extern "C" {
+
+cask_ctx* cask_ctx_create(int device, int* status) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+    if (status) *status = CASK_E_DEVICE;
+    return nullptr;
+  }
+  cask_ctx* c = new (std::nothrow) cask_ctx();
+  if (!c) {
+    if (status) *status = CASK_E_NOMEM;
+    return nullptr;
+  }
+  c->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    if (status) *status = CASK_E_DEVICE;
+    return nullptr;
+  }
+  c->stream = c->own;
+  for (auto& e : c->ev) (void)hipEventCreate(&e);
+  if (!c->ctr.ensure(sizeof(Counters)) || !c->err2.ensure(16)) {
+    cask_ctx_destroy(c);
+    if (status) *status = CASK_E_NOMEM;
+    return nullptr;
+  }
+  if (status) *status = CASK_OK;
+  return c;
+}
+
+void cask_ctx_destroy(cask_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  c->chunk.release();
+  c->ctr.release();
+  c->longbuf.release();
+  c->filebuf.release();
+  c->err2.release();
+  c->stage_data.release();
+  c->stage_rows.release();
+  c->hfiles.release();
+  c->hsum.release();
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+int cask_ctx_set_stream(cask_ctx* c, void* s) {
+  if (!c) return CASK_E_INVALID_ARG;
+  c->stream = s ? (hipStream_t)s : c->own;
+  return CASK_OK;
+}
+
+void* cask_ctx_stream(cask_ctx* c) { return c ? (void*)c->stream : nullptr; }
+int cask_ctx_device(const cask_ctx* c) { return c ? c->device : -1; }
+uint32_t cask_scan_chunk_bytes(void) { return kChunk; }
+
+uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles) {
+  uint64_t b = 0;
+  for (uint32_t i = 0; i < nfiles; ++i) b += files[i].len / CASK_ENTRY_STATIC_SIZE + 1;
+  return b;
+}
+
+uint32_t cask_xxh32(const uint8_t* data, uint64_t len) { return cask_xxh::xxh32(data, len, 0); }
+
+int cask_last_timings(const cask_ctx* c, float* ms5) {
+  if (!c || !ms5) return CASK_E_INVALID_ARG;
+  memcpy(ms5, c->last_ms, sizeof(c->last_ms));
+  return CASK_OK;
+}
+
+int cask_last_counters(const cask_ctx* c, uint64_t* c3) {
+  if (!c || !c3) return CASK_E_INVALID_ARG;
+  memcpy(c3, c->last_counters, sizeof(c->last_counters));
+  return CASK_OK;
+}
+
+}  // extern "C"
+
+// Core pipeline on device-resident files and rows.
+static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                            uint64_t* file_row_offset, cask_scan_error* err) {
+  if (!rows) return CASK_E_INVALID_ARG;
+  if (nfiles && !files) return CASK_E_INVALID_ARG;
+  if (rows->capacity && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status))
+    return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (files[i].len && !files[i].data) return CASK_E_INVALID_ARG;
+  if (set_dev(c)) return CASK_E_DEVICE;
+  hipStream_t st = c->stream;
+
+  // file table
+  uint64_t total_chunks = 0, long_cap = 0;
+  const size_t head_words = sizeof(SummaryHead) / 8;
+  const size_t sum_words = head_words + (nfiles + 1) + 3ull * nfiles;
+  if (!c->hfiles.ensure(sizeof(FileDesc) * (nfiles + 1)) || !c->hsum.ensure(sum_words * 8)) return CASK_E_NOMEM;
+  FileDesc* fd = (FileDesc*)c->hfiles.p;
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    fd[i].data = files[i].data;
+    fd[i].len = files[i].len;
+    fd[i].first_chunk = total_chunks;
+    fd[i].nchunks = (files[i].len + kChunk - 1) / kChunk;
+    total_chunks += fd[i].nchunks;
+    long_cap += files[i].len / kHalo + 1;
+  }
+  // device scratch
+  const size_t fd_bytes = align_up(sizeof(FileDesc) * (nfiles + 1), 256);
+  const size_t fe_bytes = align_up(8ull * (nfiles + 1), 256);
+  const size_t fb_bytes = align_up(8ull * (nfiles + 1), 256);
+  const size_t sum_bytes = align_up(sum_words * 8, 256);
+  if (!c->filebuf.ensure(fd_bytes + fe_bytes + fb_bytes + sum_bytes)) return CASK_E_NOMEM;
+  if (!c->chunk.ensure((total_chunks + 1) * (5 * 8 + 4) + 1024)) return CASK_E_NOMEM;
+  if (!c->longbuf.ensure((long_cap + 1) * 12 + 256)) return CASK_E_NOMEM;
+
+  uint8_t* fbase = c->filebuf.as<uint8_t>();
+  FileDesc* d_files = (FileDesc*)fbase;
+  unsigned long long* d_ferr = (unsigned long long*)(fbase + fd_bytes);
+  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + fe_bytes);
+  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + fe_bytes + fb_bytes);
+
+  uint64_t* cb = c->chunk.as<uint64_t>();
+  const uint64_t C = total_chunks + 1;
+  ScanArgs a{};
+  a.files = d_files;
+  a.nfiles = nfiles;
+  a.exact = 0;
+  a.total_chunks = total_chunks;
+  a.lb = (unsigned long long*)cb;
+  a.spec = cb + C;
+  a.exit = cb + 2 * C;
+  a.base = cb + 3 * C;
+  a.tin = cb + 4 * C;
+  a.count = (uint32_t*)(cb + 5 * C);
+  a.ctr = c->ctr.as<Counters>();
+  a.long_row = c->longbuf.as<uint64_t>();
+  a.long_file = (uint32_t*)(a.long_row + long_cap + 1);
+  a.long_cap = long_cap;
+  a.file_err_row = d_ferr;
+  a.pos = rows->pos;
+  a.seq = rows->seq;
+  a.vsz = rows->vsz;
+  a.ksz = rows->ksz;
+  a.status = rows->status;
+  a.row_cap = rows->capacity;
+
+  bool ok = true;
+  auto H = [&](hipError_t e) { ok = ok && (e == hipSuccess); };
+  H(hipEventRecord(c->ev[0], st));
+  H(hipMemcpyAsync(d_files, fd, sizeof(FileDesc) * (nfiles ? nfiles : 1), hipMemcpyHostToDevice, st));
+  auto reset = [&]() {
+    if (total_chunks) H(hipMemsetAsync(a.lb, 0, total_chunks * 8, st));
+    H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st));
+    H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st));
+  };
+  reset();
+  H(hipEventRecord(c->ev[1], st));
+  launch_scan_chunks(a, st);
+  H(hipEventRecord(c->ev[2], st));
+  launch_long(a, st);
+  H(hipEventRecord(c->ev[3], st));
+  launch_validate(a, d_fbad, st);
+  launch_summary(a, d_fbad, d_sum, st);
+  H(hipEventRecord(c->ev[4], st));
+  H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st));
+  H(hipStreamSynchronize(st));
+  if (!ok || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+
+  uint64_t* hs = (uint64_t*)c->hsum.p;
+  SummaryHead* head = (SummaryHead*)hs;
+  float repair_ms = 0.f;
+  uint64_t invalid_chunks = 0;
+  if (head->timeout) return CASK_E_DEVICE;
+  if (head->any_invalid) {
+    // Repair: exact boundary walk from each file's first invalid chunk, then a full re-scan
+    // with known starts (exact=1). Chunks before the first invalid one keep their (validated)
+    // speculative starts.
+    invalid_chunks = head->invalid_chunks;
+    launch_walk(a, d_sum, st);
+    a.exact = 1;
+    reset();
+    launch_scan_chunks(a, st);
+    launch_long(a, st);
+    launch_validate(a, d_fbad, st);
+    launch_summary(a, d_fbad, d_sum, st);
+    H(hipEventRecord(c->ev[5], st));
+    H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st));
+    H(hipStreamSynchronize(st));
+    if (!ok || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+    if (head->timeout || head->any_invalid) return CASK_E_DEVICE;  // exact pass must validate
+    (void)hipEventElapsedTime(&repair_ms, c->ev[4], c->ev[5]);
+  }
+  float t_all = 0, t_k1 = 0, t_long = 0, t_val = 0;
+  (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
+  (void)hipEventElapsedTime(&t_long, c->ev[2], c->ev[3]);
+  (void)hipEventElapsedTime(&t_val, c->ev[3], c->ev[4]);
+  (void)hipEventElapsedTime(&t_all, c->ev[0], c->ev[4]);
+  c->last_ms[0] = t_all + repair_ms;
+  c->last_ms[1] = t_k1;
+  c->last_ms[2] = t_long;
+  c->last_ms[3] = t_val;
+  c->last_ms[4] = repair_ms;
+  c->last_counters[0] = total_chunks;
+  c->last_counters[1] = head->nlong;
+  c->last_counters[2] = invalid_chunks;
+
+  const uint64_t* row_off = hs + head_words;
+  const uint64_t* ferr = row_off + nfiles + 1 + 2ull * nfiles;
+  rows->count = head->total_rows;
+  if (file_row_offset) memcpy(file_row_offset, row_off, 8ull * (nfiles + 1));
+  if (head->overflow || head->total_rows > rows->capacity) return CASK_E_CAPACITY;
+
+  if (err) {
+    memset(err, 0, sizeof(*err));
+    for (uint32_t f = 0; f < nfiles; ++f) {
+      if (ferr[f] == kNone) continue;
+      const uint64_t r = ferr[f];
+      uint8_t status = 0;
+      uint64_t pos = 0;
+      uint32_t eh[2] = {0, 0};
+      H(hipMemcpyAsync(&status, rows->status + r, 1, hipMemcpyDeviceToHost, st));
+      H(hipMemcpyAsync(&pos, rows->pos + r, 8, hipMemcpyDeviceToHost, st));
+      launch_err_detail(a, f, r, c->err2.as<uint32_t>(), st);
+      H(hipMemcpyAsync(eh, c->err2.p, 8, hipMemcpyDeviceToHost, st));
+      H(hipStreamSynchronize(st));
+      if (!ok) return CASK_E_DEVICE;
+      err->kind = status;
+      err->file_id = files[f].file_id;
+      err->pos = pos;
+      err->row = r;
+      if (status == CASK_ROW_CHECKSUM) {
+        err->expected = eh[0];
+        err->found = eh[1];
+      } else {
+        err->expected = eh[0];
+        err->found = 0;
+      }
+      break;
+    }
+  }
+  return CASK_OK;
+}
+
+extern "C" int cask_scan_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                                uint64_t* file_row_offset, cask_scan_error* err) {
+  if (!c) return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return scan_device_impl(c, files, nfiles, rows, file_row_offset, err);
+}
+
+extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                              uint64_t* file_row_offset, cask_scan_error* err) {
+  if (!c || !rows || (nfiles && !files)) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  hipStream_t st = c->stream;
+  // stage every file at a 256-B aligned offset of one device buffer
+  std::vector<uint64_t> off(nfiles + 1, 0);
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    off[i] = total;
+    total = align_up(total + files[i].len, 256);
+  }
+  const uint64_t bound = cask_rows_bound(files, nfiles);
+  const uint64_t rcap = std::min<uint64_t>(bound, rows->capacity ? rows->capacity : bound);
+  if (!c->stage_data.ensure(total + 256)) return CASK_E_NOMEM;
+  if (!c->stage_rows.ensure(rcap * 23 + 5 * 256)) return CASK_E_NOMEM;
+  std::vector<cask_file_view> dv(nfiles);
+  uint8_t* d = c->stage_data.as<uint8_t>();
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    dv[i] = files[i];
+    dv[i].flags = CASK_VIEW_DEVICE;
+    dv[i].data = d + off[i];
+    if (files[i].len && hipMemcpyAsync(d + off[i], files[i].data, files[i].len, hipMemcpyHostToDevice, st) != hipSuccess)
+      return CASK_E_DEVICE;
+  }
+  uint8_t* rb = c->stage_rows.as<uint8_t>();
+  cask_rows dr{};
+  dr.capacity = rcap;
+  dr.pos = (uint64_t*)rb;
+  dr.seq = (uint64_t*)(rb + align_up(rcap * 8, 256));
+  dr.vsz = (uint32_t*)(rb + 2 * align_up(rcap * 8, 256));
+  dr.ksz = (uint16_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256));
+  dr.status = (uint8_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256) + align_up(rcap * 2, 256));
+  int rc = scan_device_impl(c, dv.data(), nfiles, &dr, file_row_offset, err);
+  rows->count = dr.count;
+  if (rc != CASK_OK) return rc;
+  if (dr.count > rows->capacity) return CASK_E_CAPACITY;
+  const uint64_t n = dr.count;
+  bool ok = true;
+  auto H = [&](hipError_t e) { ok = ok && (e == hipSuccess); };
+  if (n) {
+    H(hipMemcpyAsync(rows->pos, dr.pos, n * 8, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(rows->seq, dr.seq, n * 8, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(rows->vsz, dr.vsz, n * 4, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(rows->ksz, dr.ksz, n * 2, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(rows->status, dr.status, n, hipMemcpyDeviceToHost, st));
+  }
+  H(hipStreamSynchronize(st));
+  return ok ? CASK_OK : CASK_E_DEVICE;
+}
+
+extern "C" int cask_encode_synthetic_device(cask_ctx* c, uint64_t nrec, const uint64_t* off, const uint64_t* seq,
+                                            const uint16_t* ksz, const uint32_t* vsz_raw, const uint64_t* key_id,
+                                            uint64_t value_seed, uint8_t* out) {
+  if (!c || (nrec && (!off || !seq || !ksz || !vsz_raw || !key_id || !out))) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  launch_encode_synth(nrec, off, seq, ksz, vsz_raw, key_id, value_seed, out, c->stream);
+  launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+  return CASK_OK;
+}
+
+extern "C" int cask_encode_device(cask_ctx* c, uint64_t nrec, const uint64_t* off, const uint64_t* seq,
+                                  const uint16_t* ksz, const uint32_t* vsz_raw, const uint8_t* keys,
+                                  const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
+                                  uint8_t* out) {
+  if (!c || (nrec && (!off || !seq || !ksz || !vsz_raw || !keys || !key_off || !out))) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  launch_encode(nrec, off, seq, ksz, vsz_raw, keys, key_off, vals, val_off, out, c->stream);
+  launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+  return CASK_OK;
+}

@@ -1,0 +1,204 @@
+/*
+ * cask_scan.h — C ABI of the MI355X-native Cask log-record scan (libcask_scan.so).
+ *
+ * Drop-in boundary for the replay/compaction hot path of andresilva/cask v0.7.1. The reference
+ * is a Rust crate whose `log`/`data` modules are private (src/lib.rs:46,49), so it has no FFI of
+ * its own; the seams these entry points replace are cited per function. A Rust binding
+ * (`extern "C"` block + safe wrapper) is shown in INTEGRATION.md.
+ *
+ * Conventions: plain pointers and sizes only; the caller owns every buffer it passes in; the
+ * library never frees caller memory. Return 0 (CASK_OK) on success, a negative cask_status on
+ * failure. No C++ exception crosses this boundary.
+ */
+#ifndef CASK_SCAN_H
+#define CASK_SCAN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CASK_SCAN_ABI_VERSION 1
+
+/* Status codes. The first five map onto the reference's Error enum (src/errors.rs:12-25). */
+typedef enum cask_status {
+  CASK_OK = 0,
+  CASK_E_CHECKSUM = -1,        /* Error::InvalidChecksum { expected, found } (errors.rs:22) */
+  CASK_E_EOF = -2,             /* Error::Io(UnexpectedEof) from read_exact (data.rs:163,172,181) */
+  CASK_E_IO = -3,              /* Error::Io(other) (errors.rs:14) */
+  CASK_E_INVALID_PATH = -4,    /* Error::InvalidPath (errors.rs:24; log.rs:46-56) */
+  CASK_E_INVALID_FILE_ID = -5, /* Error::InvalidFileId (errors.rs:16; log.rs:200-202) */
+  CASK_E_INVALID_ARG = -10,    /* bad argument to this ABI */
+  CASK_E_DEVICE = -11,         /* HIP runtime / device failure */
+  CASK_E_CAPACITY = -12,       /* caller's row buffer too small; needed count is reported */
+  CASK_E_NOMEM = -13,
+  CASK_E_LOCKED = -14          /* cask.lock held by another process (log.rs:58-59) */
+} cask_status;
+
+/* Per-row status (what Entries::next yields for the record at `pos`, log.rs:403-429). */
+enum { CASK_ROW_OK = 0, CASK_ROW_CHECKSUM = 1, CASK_ROW_EOF = 2 };
+
+/* Record format constants (data.rs:11-14). */
+#define CASK_ENTRY_STATIC_SIZE 18u
+#define CASK_ENTRY_TOMBSTONE 0xFFFFFFFFu
+
+/* ------------------------------------------------------------------------------------------ */
+/* Device scan context                                                                         */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct cask_ctx cask_ctx;
+
+/* One context per GPU: owns a HIP stream, chunk scratch and pinned staging. Contexts are
+ * independent and may be used from different threads; one context is not re-entrant. */
+cask_ctx* cask_ctx_create(int device, int* status);
+void cask_ctx_destroy(cask_ctx* ctx);
+/* Use a caller stream (hipStream_t passed as void*) instead of the context's own; NULL resets. */
+int cask_ctx_set_stream(cask_ctx* ctx, void* hip_stream);
+void* cask_ctx_stream(cask_ctx* ctx);
+int cask_ctx_device(const cask_ctx* ctx);
+/* Chunk size in bytes used by the scan kernels (the unit of speculation and staging). */
+uint32_t cask_scan_chunk_bytes(void);
+
+/* A data file to scan: `{:010}.cask.data` contents (log.rs:473-476), no header/footer. */
+#define CASK_VIEW_DEVICE 1u /* data points to device memory (else host memory) */
+typedef struct cask_file_view {
+  uint32_t file_id;
+  uint32_t flags;
+  const uint8_t* data;
+  uint64_t len;
+} cask_file_view;
+
+/* Rows in (file, pos) order, struct-of-arrays. One row per record the reference iterator
+ * yields: Ok records, InvalidChecksum records (iteration continues past them, log.rs:467-471)
+ * and at most one trailing UnexpectedEof record per file (iteration ends there).
+ * The key of row i lives at data[pos[i] + 18 .. + ksz[i]] of its file (not copied). */
+typedef struct cask_rows {
+  uint64_t capacity; /* in: slots in every array */
+  uint64_t count;    /* out: rows produced (also set on CASK_E_CAPACITY = rows needed) */
+  uint64_t* pos;     /* entry_pos (log.rs:413) */
+  uint64_t* seq;     /* Entry.sequence (data.rs:167) */
+  uint32_t* vsz;     /* raw value_size field; 0xFFFFFFFF = tombstone (data.rs:169,174) */
+  uint16_t* ksz;     /* key_size (data.rs:168) */
+  uint8_t* status;   /* CASK_ROW_* */
+} cask_rows;
+
+/* First failing record in (call file order, pos) order — what Cask::open's `?` returns
+ * (cask.rs:360,365). kind = 0 when every record verified. */
+typedef struct cask_scan_error {
+  int32_t kind;      /* 0, CASK_ROW_CHECKSUM or CASK_ROW_EOF */
+  uint32_t file_id;
+  uint64_t pos;
+  uint32_t expected; /* stored checksum (InvalidChecksum.expected) */
+  uint32_t found;    /* computed XXH32 (InvalidChecksum.found) */
+  uint64_t row;      /* index of that row in the output */
+} cask_scan_error;
+
+/* Upper bound on rows for a set of files (every record is >= 18 bytes). */
+uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles);
+
+/* Device-resident scan: replaces `Log::entries`/`Entries::next` + `Entry::from_read`
+ * (log.rs:108-119, 403-429; data.rs:161-206) and the per-record work of
+ * `Log::recreate_hints`/`RecreateHints::next` (log.rs:137-148, 454-465) for many files at once.
+ * files[i].data must be device pointers (CASK_VIEW_DEVICE); rows arrays must be device memory.
+ * file_row_offset (host, nfiles+1 entries, may be NULL) receives each file's first row index.
+ * Returns CASK_OK even when records fail verification: those are reported per row and in
+ * *err (first failure). Synchronous: returns after the results are complete. */
+int cask_scan_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
+                     cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);
+
+/* Same, for host-resident files and host row arrays: stages H2D, scans, copies rows D2H. */
+int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
+                   cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);
+
+/* Timing of the last cask_scan_* call on the context's stream (HIP events, milliseconds):
+ * [0] whole device pipeline, [1] chunk-scan kernel, [2] long-record kernel,
+ * [3] validate kernel, [4] repair (0 when speculation held). */
+int cask_last_timings(const cask_ctx* ctx, float* ms5);
+/* Counters of the last call: [0] chunks, [1] long records, [2] invalid chunks repaired. */
+int cask_last_counters(const cask_ctx* ctx, uint64_t* c3);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Batched record encoder (Entry::write_bytes, data.rs:90-121) — the bulk write path and the   */
+/* synthetic workload generator. Record r is written at out[off[r]]:                            */
+/*   [xxh32 | seq[r] | ksz[r] | vsz_raw[r] | key | value], key/value bytes generated from        */
+/*   key_id[r] and (value_seed, r) by the generator documented in DESIGN.md §Synthetic data.    */
+/* All arrays are device memory.                                                               */
+/* ------------------------------------------------------------------------------------------ */
+int cask_encode_synthetic_device(cask_ctx* ctx, uint64_t nrec, const uint64_t* off,
+                                 const uint64_t* seq, const uint16_t* ksz,
+                                 const uint32_t* vsz_raw, const uint64_t* key_id,
+                                 uint64_t value_seed, uint8_t* out);
+
+/* Encode caller-supplied keys/values (device memory): key r = keys[key_off[r] .. +ksz[r]],
+ * value r = vals[val_off[r] .. +vsz] (ignored for tombstones). */
+int cask_encode_device(cask_ctx* ctx, uint64_t nrec, const uint64_t* off, const uint64_t* seq,
+                       const uint16_t* ksz, const uint32_t* vsz_raw, const uint8_t* keys,
+                       const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
+                       uint8_t* out);
+
+/* XXH32 seed 0 on the host (util.rs:37-41) — convenience for bindings. */
+uint32_t cask_xxh32(const uint8_t* data, uint64_t len);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Engine: the Cask::open replay (cask.rs:335-382) with the device scan underneath.            */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct cask_db cask_db;
+
+/* CaskOptions (cask.rs:194-237); only the fields the replay/compaction path reads. */
+typedef struct cask_options {
+  int32_t create;               /* default 1 (cask.rs:223) */
+  int32_t write_hints;          /* recreate missing/corrupt hint files (log.rs:137-148); 1 */
+  uint64_t max_file_size;       /* default 2 GiB (cask.rs:225) */
+  int32_t device;               /* GPU ordinal for the scan */
+  int32_t reserved;
+} cask_options;
+
+void cask_options_default(cask_options* o);
+
+/* Open error detail (mirrors Error::InvalidChecksum / Io(UnexpectedEof) plus location). */
+typedef struct cask_open_error {
+  int32_t status;    /* cask_status */
+  uint32_t file_id;
+  uint64_t pos;
+  uint32_t expected;
+  uint32_t found;
+} cask_open_error;
+
+/* CaskOptions::open / Cask::open (cask.rs:328-330, 335-382). On failure returns NULL and fills
+ * *err; hint files already recreated stay on disk, as in the reference. */
+cask_db* cask_db_open(const char* path, const cask_options* opts, cask_open_error* err);
+void cask_db_close(cask_db* db);
+
+/* IndexEntry (cask.rs:20-26). */
+typedef struct cask_index_entry {
+  uint32_t file_id;
+  uint32_t pad;
+  uint64_t entry_pos;
+  uint64_t entry_size;
+  uint64_t sequence;
+} cask_index_entry;
+
+uint64_t cask_db_len(const cask_db* db);
+/* Index::get (cask.rs:41-43). Returns 1 if present, 0 if absent. */
+int cask_db_get_entry(const cask_db* db, const uint8_t* key, uint64_t ksz, cask_index_entry* out);
+/* All live keys sorted bytewise: keys concatenated into key_bytes (capacity key_cap), with
+ * key_off/key_len/entries of nkeys slots. Returns total key bytes, or negative on error. */
+int64_t cask_db_export(const cask_db* db, uint8_t* key_bytes, uint64_t key_cap,
+                       uint64_t* key_off, uint64_t* key_len, cask_index_entry* entries,
+                       uint64_t nkeys);
+/* Stats (stats.rs:6-67) sorted by file id. Returns the number of rows (may exceed cap). */
+uint64_t cask_db_stats(const cask_db* db, uint32_t* file_id, uint64_t* entries,
+                       uint64_t* dead_entries, uint64_t* dead_bytes, uint64_t cap);
+/* current_sequence = max sequence seen + 1 (cask.rs:379). */
+uint64_t cask_db_current_sequence(const cask_db* db);
+/* Data file ids in ascending order (Log::files, log.rs:104-106). Returns count (may exceed cap). */
+uint64_t cask_db_files(const cask_db* db, uint32_t* ids, uint64_t cap);
+/* Timing of the replay phases (ms): [0] discover+read, [1] device scan, [2] hint write,
+ * [3] keydir fold, [4] total. */
+int cask_db_open_timings(const cask_db* db, double* ms5);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CASK_SCAN_H */

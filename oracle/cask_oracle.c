@@ -1,0 +1,608 @@
+/*
+ * cask_oracle.c — CPU restatement of Cask's replay hot path. TEST INFRASTRUCTURE ONLY
+ * (see cask_oracle.h for who may call it). Not linked into the product.
+ */
+#define _GNU_SOURCE
+#include "cask_oracle.h"
+
+#include <errno.h>
+#include <fcntl.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+/* ------------------------------------------------------------------------------------ */
+/* XXH32: published algorithm (the arithmetic of twox-hash XxHash32, util.rs:10-41).      */
+/* Streaming form mirrors Hasher::write + finish (util.rs:18-23): buffering of partial    */
+/* stripes makes any split of the input give the one-shot digest (data.rs:102-108 vs :83). */
+/* ------------------------------------------------------------------------------------ */
+#define P1 2654435761u
+#define P2 2246822519u
+#define P3 3266489917u
+#define P4 668265263u
+#define P5 374761393u
+
+static inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+static inline uint32_t rd32(const uint8_t* p) {
+  return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+static inline uint64_t rd64(const uint8_t* p) {
+  return (uint64_t)rd32(p) | ((uint64_t)rd32(p + 4) << 32);
+}
+static inline uint16_t rd16(const uint8_t* p) { return (uint16_t)(p[0] | (p[1] << 8)); }
+static inline void wr32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+static inline void wr64(uint8_t* p, uint64_t v) { wr32(p, (uint32_t)v); wr32(p + 4, (uint32_t)(v >> 32)); }
+static inline void wr16(uint8_t* p, uint16_t v) { p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); }
+
+static inline uint32_t xround(uint32_t acc, uint32_t w) { return rotl32(acc + w * P2, 13) * P1; }
+
+void orc_xxh32_reset(orc_xxh32_state* s, uint32_t seed) {
+  memset(s, 0, sizeof(*s));
+  s->seed = seed;
+  s->v[0] = seed + P1 + P2;
+  s->v[1] = seed + P2;
+  s->v[2] = seed;
+  s->v[3] = seed - P1;
+}
+
+void orc_xxh32_update(orc_xxh32_state* s, const uint8_t* p, size_t len) {
+  s->total_len += len;
+  if (s->memsize + len < 16) {
+    memcpy(s->mem + s->memsize, p, len);
+    s->memsize += (uint32_t)len;
+    return;
+  }
+  if (s->memsize) {
+    size_t fill = 16 - s->memsize;
+    memcpy(s->mem + s->memsize, p, fill);
+    s->v[0] = xround(s->v[0], rd32(s->mem));
+    s->v[1] = xround(s->v[1], rd32(s->mem + 4));
+    s->v[2] = xround(s->v[2], rd32(s->mem + 8));
+    s->v[3] = xround(s->v[3], rd32(s->mem + 12));
+    p += fill;
+    len -= fill;
+    s->memsize = 0;
+  }
+  while (len >= 16) {
+    s->v[0] = xround(s->v[0], rd32(p));
+    s->v[1] = xround(s->v[1], rd32(p + 4));
+    s->v[2] = xround(s->v[2], rd32(p + 8));
+    s->v[3] = xround(s->v[3], rd32(p + 12));
+    p += 16;
+    len -= 16;
+  }
+  if (len) {
+    memcpy(s->mem, p, len);
+    s->memsize = (uint32_t)len;
+  }
+}
+
+uint32_t orc_xxh32_digest(const orc_xxh32_state* s) {
+  uint32_t h;
+  if (s->total_len >= 16)
+    h = rotl32(s->v[0], 1) + rotl32(s->v[1], 7) + rotl32(s->v[2], 12) + rotl32(s->v[3], 18);
+  else
+    h = s->seed + P5;
+  h += (uint32_t)s->total_len;
+  const uint8_t* p = s->mem;
+  uint32_t n = s->memsize;
+  while (n >= 4) {
+    h = rotl32(h + rd32(p) * P3, 17) * P4;
+    p += 4;
+    n -= 4;
+  }
+  while (n) {
+    h = rotl32(h + (*p) * P5, 11) * P1;
+    ++p;
+    --n;
+  }
+  h ^= h >> 15;
+  h *= P2;
+  h ^= h >> 13;
+  h *= P3;
+  h ^= h >> 16;
+  return h;
+}
+
+uint32_t orc_xxh32(const uint8_t* p, size_t len, uint32_t seed) {
+  orc_xxh32_state s;
+  orc_xxh32_reset(&s, seed);
+  orc_xxh32_update(&s, p, len);
+  return orc_xxh32_digest(&s);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Record codec                                                                           */
+/* ------------------------------------------------------------------------------------ */
+
+/* Entry::write_bytes (data.rs:90-121): header tail seq|ksz|vsz-or-tombstone at [4,18),
+ * checksum = XXH32 streamed over header tail, key, value (data.rs:102-108), then key and
+ * (unless deleted) value. */
+size_t orc_entry_encode(uint64_t seq, const uint8_t* key, uint16_t ksz, const uint8_t* value,
+                        uint32_t vsz, int deleted, uint8_t* out) {
+  wr64(out + 4, seq);
+  wr16(out + 12, ksz);
+  wr32(out + 14, deleted ? ORC_ENTRY_TOMBSTONE : vsz);
+  orc_xxh32_state s;
+  orc_xxh32_reset(&s, 0);
+  orc_xxh32_update(&s, out + 4, 14);
+  orc_xxh32_update(&s, key, ksz);
+  if (!deleted) orc_xxh32_update(&s, value, vsz);  /* a deleted Entry has an empty value */
+  wr32(out, orc_xxh32_digest(&s));
+  if (ksz) memcpy(out + 18, key, ksz);
+  if (!deleted && vsz) memcpy(out + 18 + ksz, value, vsz);
+  return 18 + (size_t)ksz + (deleted ? 0 : vsz);
+}
+
+/* Entries::next over a Take<File> of the whole file (log.rs:108-119, 403-429) with
+ * Entry::from_read per record (data.rs:161-206):
+ *   header read_exact(18) -> key read_exact(ksz) -> value read_exact(vsz) unless tombstone;
+ *   any short read is Io(UnexpectedEof) and consumes the rest of the limit (iteration ends);
+ *   otherwise all 18+ksz+vsz_eff bytes are consumed and XXH32 decides Ok vs InvalidChecksum.
+ * Rows after a checksum error keep coming, as RecreateHints::drop drains them (log.rs:467-471). */
+int64_t orc_scan_buffer(const uint8_t* buf, uint64_t len, orc_row* rows, uint64_t cap) {
+  uint64_t pos = 0;
+  int64_t n = 0;
+  while (pos < len) {  /* Entries::next: limit == 0 -> None (log.rs:408-410) */
+    if ((uint64_t)n >= cap) return -1;
+    orc_row* r = &rows[n++];
+    memset(r, 0, sizeof(*r));
+    r->pos = pos;
+    uint64_t rem = len - pos;
+    if (rem < 18) {  /* data.rs:163 read_exact(header) */
+      r->status = ORC_ROW_EOF;
+      return n;
+    }
+    const uint8_t* h = buf + pos;
+    r->expected = rd32(h);
+    r->seq = rd64(h + 4);
+    r->ksz = rd16(h + 12);
+    r->vsz_raw = rd32(h + 14);
+    uint64_t vsz_eff = (r->vsz_raw == ORC_ENTRY_TOMBSTONE) ? 0 : r->vsz_raw;
+    uint64_t rec = 18 + (uint64_t)r->ksz + vsz_eff;
+    if (rem < 18 + (uint64_t)r->ksz || rem < rec) { /* data.rs:172 / :181 */
+      r->status = ORC_ROW_EOF;
+      return n;
+    }
+    r->found = orc_xxh32(h + 4, rec - 4, 0); /* data.rs:185-191 (stream == one-shot) */
+    r->status = (r->found == r->expected) ? ORC_ROW_OK : ORC_ROW_CHECKSUM; /* data.rs:193-198 */
+    pos += rec;  /* log.rs:415-417; entry.size() == read (log.rs:421) */
+  }
+  return n;
+}
+
+/* Hint::write_bytes (data.rs:242-256). */
+size_t orc_hint_encode(uint64_t seq, uint16_t ksz, uint32_t vsz_raw, uint64_t pos,
+                       const uint8_t* key, uint8_t* out) {
+  wr64(out, seq);
+  wr16(out + 8, ksz);
+  wr32(out + 10, vsz_raw == ORC_ENTRY_TOMBSTONE ? ORC_ENTRY_TOMBSTONE : vsz_raw);
+  wr64(out + 14, pos);
+  if (ksz) memcpy(out + 22, key, ksz);
+  return 22 + (size_t)ksz;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Keydir: HashMap<Vec<u8>, IndexEntry> (cask.rs:28-31) + Stats (stats.rs:14-16)          */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  uint8_t* key;  /* owned copy: hint.key.to_vec() (cask.rs:68) */
+  uint64_t hash;
+  uint64_t pos, size, seq;
+  uint32_t file_id;
+  uint16_t ksz;
+  uint8_t used;  /* 0 empty, 1 live, 2 tombstone slot (removed) */
+} orc_slot;
+
+typedef struct {
+  uint32_t file_id;
+  uint64_t entries, dead_entries, dead_bytes;
+  uint8_t used;
+} orc_stat;
+
+struct orc_index {
+  orc_slot* slots;
+  uint64_t cap, live, used_slots;
+  orc_stat* stats;
+  uint64_t stats_cap, stats_n;
+};
+
+static uint64_t key_hash(const uint8_t* k, uint16_t n) {
+  uint64_t h = 1469598103934665603ull;
+  for (uint16_t i = 0; i < n; ++i) {
+    h ^= k[i];
+    h *= 1099511628211ull;
+  }
+  return h ^ (h >> 29);
+}
+
+orc_index* orc_index_new(void) {
+  orc_index* ix = (orc_index*)calloc(1, sizeof(orc_index));
+  ix->cap = 1024;
+  ix->slots = (orc_slot*)calloc(ix->cap, sizeof(orc_slot));
+  ix->stats_cap = 64;
+  ix->stats = (orc_stat*)calloc(ix->stats_cap, sizeof(orc_stat));
+  return ix;
+}
+
+void orc_index_free(orc_index* ix) {
+  if (!ix) return;
+  for (uint64_t i = 0; i < ix->cap; ++i)
+    if (ix->slots[i].used == 1) free(ix->slots[i].key);
+  free(ix->slots);
+  free(ix->stats);
+  free(ix);
+}
+
+static orc_stat* stat_find(orc_index* ix, uint32_t file_id, int create) {
+  uint64_t m = ix->stats_cap - 1;
+  uint64_t i = (file_id * 2654435761u) & m;
+  for (;;) {
+    orc_stat* s = &ix->stats[i];
+    if (!s->used) {
+      if (!create) return NULL;
+      if ((ix->stats_n + 1) * 2 > ix->stats_cap) {
+        orc_stat* old = ix->stats;
+        uint64_t oc = ix->stats_cap;
+        ix->stats_cap *= 2;
+        ix->stats = (orc_stat*)calloc(ix->stats_cap, sizeof(orc_stat));
+        ix->stats_n = 0;
+        for (uint64_t j = 0; j < oc; ++j)
+          if (old[j].used) {
+            orc_stat* d = stat_find(ix, old[j].file_id, 1);
+            *d = old[j];
+          }
+        free(old);
+        return stat_find(ix, file_id, 1);
+      }
+      s->used = 1;
+      s->file_id = file_id;
+      ix->stats_n++;
+      return s;
+    }
+    if (s->file_id == file_id) return s;
+    i = (i + 1) & m;
+  }
+}
+
+/* Stats::add_entry (stats.rs:23-36) */
+static void stats_add(orc_index* ix, uint32_t file_id) {
+  orc_stat* s = stat_find(ix, file_id, 0);
+  if (s) {
+    s->entries += 1;
+  } else {
+    s = stat_find(ix, file_id, 1);
+    s->entries = 1;
+    s->dead_entries = 0;
+    s->dead_bytes = 0;
+  }
+}
+
+/* Stats::remove_entry (stats.rs:38-48): a missing row only warns. */
+static void stats_remove(orc_index* ix, uint32_t file_id, uint64_t size) {
+  orc_stat* s = stat_find(ix, file_id, 0);
+  if (s) {
+    s->dead_entries += 1;
+    s->dead_bytes += size;
+  }
+}
+
+static void index_grow(orc_index* ix) {
+  orc_slot* old = ix->slots;
+  uint64_t oc = ix->cap;
+  ix->cap *= 2;
+  ix->slots = (orc_slot*)calloc(ix->cap, sizeof(orc_slot));
+  ix->used_slots = 0;
+  uint64_t m = ix->cap - 1;
+  for (uint64_t i = 0; i < oc; ++i) {
+    if (old[i].used != 1) continue;
+    uint64_t j = old[i].hash & m;
+    while (ix->slots[j].used) j = (j + 1) & m;
+    ix->slots[j] = old[i];
+    ix->used_slots++;
+  }
+  free(old);
+}
+
+/* Index::update (cask.rs:60-90). */
+void orc_index_update(orc_index* ix, const uint8_t* key, uint16_t ksz, uint32_t file_id,
+                      uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+  int deleted = (vsz_raw == ORC_ENTRY_TOMBSTONE);
+  /* Hint.value_size is 0 for a tombstone (data.rs:222/232, :272); entry_size :238-240 */
+  uint64_t size = 18 + (uint64_t)ksz + (deleted ? 0 : vsz_raw);
+  if ((ix->used_slots + 1) * 4 > ix->cap * 3) index_grow(ix);
+  uint64_t h = key_hash(key, ksz);
+  uint64_t m = ix->cap - 1;
+  uint64_t i = h & m;
+  int64_t tomb = -1;
+  for (;;) {
+    orc_slot* s = &ix->slots[i];
+    if (s->used == 0) break;
+    if (s->used == 2) {
+      if (tomb < 0) tomb = (int64_t)i;
+    } else if (s->hash == h && s->ksz == ksz && memcmp(s->key, key, ksz) == 0) {
+      /* HashMapEntry::Occupied (cask.rs:69-82) */
+      if (s->seq <= seq) {
+        stats_remove(ix, s->file_id, s->size);
+        if (deleted) {
+          free(s->key);
+          s->key = NULL;
+          s->used = 2;
+          ix->live--;
+        } else {
+          stats_add(ix, file_id);
+          s->file_id = file_id;
+          s->pos = pos;
+          s->size = size;
+          s->seq = seq;
+        }
+      } else {
+        stats_add(ix, file_id);
+        stats_remove(ix, file_id, size);
+      }
+      return;
+    }
+    i = (i + 1) & m;
+  }
+  /* HashMapEntry::Vacant (cask.rs:83-88) */
+  if (deleted) return;
+  stats_add(ix, file_id);
+  orc_slot* s = (tomb >= 0) ? &ix->slots[tomb] : &ix->slots[i];
+  if (tomb < 0) ix->used_slots++;
+  s->key = (uint8_t*)malloc(ksz ? ksz : 1);
+  if (ksz) memcpy(s->key, key, ksz);
+  s->ksz = ksz;
+  s->hash = h;
+  s->file_id = file_id;
+  s->pos = pos;
+  s->size = size;
+  s->seq = seq;
+  s->used = 1;
+  ix->live++;
+}
+
+uint64_t orc_index_len(const orc_index* ix) { return ix->live; }
+
+static int cmp_key(const uint8_t* a, uint16_t an, const uint8_t* b, uint16_t bn) {
+  uint16_t n = an < bn ? an : bn;
+  int c = n ? memcmp(a, b, n) : 0;
+  if (c) return c;
+  return (int)an - (int)bn;
+}
+
+static const orc_index* g_sort_ix;
+static int cmp_slot_idx(const void* x, const void* y) {
+  const orc_slot* a = &g_sort_ix->slots[*(const uint64_t*)x];
+  const orc_slot* b = &g_sort_ix->slots[*(const uint64_t*)y];
+  return cmp_key(a->key, a->ksz, b->key, b->ksz);
+}
+
+void orc_index_export(const orc_index* ix, uint8_t* keys_out, uint64_t* key_off,
+                      uint16_t* key_len, uint32_t* file_id, uint64_t* pos, uint64_t* size,
+                      uint64_t* seq) {
+  uint64_t* idx = (uint64_t*)malloc((ix->live + 1) * sizeof(uint64_t));
+  uint64_t n = 0;
+  for (uint64_t i = 0; i < ix->cap; ++i)
+    if (ix->slots[i].used == 1) idx[n++] = i;
+  g_sort_ix = ix;
+  qsort(idx, n, sizeof(uint64_t), cmp_slot_idx);
+  uint64_t off = 0;
+  for (uint64_t j = 0; j < n; ++j) {
+    const orc_slot* s = &ix->slots[idx[j]];
+    if (keys_out) memcpy(keys_out + off, s->key, s->ksz);
+    if (key_off) key_off[j] = off;
+    if (key_len) key_len[j] = s->ksz;
+    if (file_id) file_id[j] = s->file_id;
+    if (pos) pos[j] = s->pos;
+    if (size) size[j] = s->size;
+    if (seq) seq[j] = s->seq;
+    off += s->ksz;
+  }
+  free(idx);
+}
+
+static int cmp_stat(const void* x, const void* y) {
+  uint32_t a = ((const orc_stat*)x)->file_id, b = ((const orc_stat*)y)->file_id;
+  return a < b ? -1 : a > b;
+}
+
+uint64_t orc_index_stats(const orc_index* ix, uint32_t* file_id, uint64_t* entries,
+                         uint64_t* dead_entries, uint64_t* dead_bytes, uint64_t cap) {
+  orc_stat* tmp = (orc_stat*)malloc((ix->stats_n + 1) * sizeof(orc_stat));
+  uint64_t n = 0;
+  for (uint64_t i = 0; i < ix->stats_cap; ++i)
+    if (ix->stats[i].used) tmp[n++] = ix->stats[i];
+  qsort(tmp, n, sizeof(orc_stat), cmp_stat);
+  uint64_t m = n < cap ? n : cap;
+  for (uint64_t j = 0; j < m; ++j) {
+    file_id[j] = tmp[j].file_id;
+    entries[j] = tmp[j].entries;
+    dead_entries[j] = tmp[j].dead_entries;
+    dead_bytes[j] = tmp[j].dead_bytes;
+  }
+  free(tmp);
+  return n;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Replay drivers                                                                         */
+/* ------------------------------------------------------------------------------------ */
+
+/* std::io::Read::read_exact over an unbuffered File: read(2) until filled or EOF. */
+static int read_exact_fd(int fd, uint8_t* p, uint64_t n, uint64_t* limit) {
+  /* Take<File> caps reads at the file size measured at open (log.rs:112-115). */
+  uint64_t want = n;
+  int short_read = 0;
+  if (want > *limit) {
+    want = *limit;
+    short_read = 1;
+  }
+  uint64_t got = 0;
+  while (got < want) {
+    ssize_t r = read(fd, p + got, (size_t)(want - got));
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    if (r == 0) {
+      short_read = 1;
+      break;
+    }
+    got += (uint64_t)r;
+  }
+  *limit -= got;
+  return short_read ? 1 : 0;
+}
+
+static int write_all_fd(int fd, const uint8_t* p, size_t n) {
+  while (n) {
+    ssize_t w = write(fd, p, n);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    p += w;
+    n -= (size_t)w;
+  }
+  return 0;
+}
+
+int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint32_t file_id,
+                             orc_index* ix, orc_replay_result* res) {
+  memset(res, 0, sizeof(*res));
+  int fd = open(data_path, O_RDONLY);
+  if (fd < 0) return -1;
+  off_t fsz = lseek(fd, 0, SEEK_END);
+  lseek(fd, 0, SEEK_SET);
+  uint64_t limit = (uint64_t)fsz;
+  /* HintWriter::new: create + truncate (log.rs:373-380, util.rs:45-49) */
+  int hfd = hint_path ? open(hint_path, O_WRONLY | O_CREAT | O_TRUNC, 0644) : -1;
+  orc_xxh32_state hint_hasher;
+  orc_xxh32_reset(&hint_hasher, 0);
+  uint64_t pos = 0;
+  int stop = 0;
+  while (limit > 0 && !stop) {
+    uint64_t before = limit;
+    /* Entry::from_read (data.rs:161-206): three Vec allocations per record */
+    uint8_t* header = (uint8_t*)calloc(18, 1);
+    int eof = read_exact_fd(fd, header, 18, &limit);
+    uint8_t* key = NULL;
+    uint8_t* value = NULL;
+    uint16_t ksz = 0;
+    uint32_t vsz_raw = 0;
+    int deleted = 0;
+    if (eof == 0) {
+      ksz = rd16(header + 12);
+      vsz_raw = rd32(header + 14);
+      key = (uint8_t*)calloc(ksz ? ksz : 1, 1);
+      eof = read_exact_fd(fd, key, ksz, &limit);
+      deleted = (vsz_raw == ORC_ENTRY_TOMBSTONE);
+      if (eof == 0 && !deleted) {
+        value = (uint8_t*)calloc(vsz_raw ? vsz_raw : 1, 1);
+        eof = read_exact_fd(fd, value, vsz_raw, &limit);
+      }
+    }
+    if (eof != 0) {
+      if (!res->err_kind) {
+        res->err_kind = eof < 0 ? -1 : ORC_ROW_EOF;
+        res->err_file_id = file_id;
+        res->err_pos = pos;
+      }
+      free(header); free(key); free(value);
+      break;  /* the Take limit is exhausted: Entries::next yields None next */
+    }
+    orc_xxh32_state hs;
+    orc_xxh32_reset(&hs, 0);
+    orc_xxh32_update(&hs, header + 4, 14);
+    orc_xxh32_update(&hs, key, ksz);
+    if (!deleted) orc_xxh32_update(&hs, value, vsz_raw);
+    uint32_t hash = orc_xxh32_digest(&hs);
+    uint32_t stored = rd32(header);
+    uint64_t read_bytes = before - limit;
+    res->bytes += read_bytes;
+    if (hash != stored) {
+      /* InvalidChecksum aborts open() at the `?` (cask.rs:365); the drain that follows in
+       * RecreateHints::drop is not part of the timed replay. */
+      if (!res->err_kind) {
+        res->err_kind = ORC_ROW_CHECKSUM;
+        res->err_file_id = file_id;
+        res->err_pos = pos;
+        res->err_expected = stored;
+        res->err_found = hash;
+      }
+      stop = 1;
+    } else {
+      uint64_t seq = rd64(header + 4);
+      /* HintWriter::write: Hint::write_bytes into the file (5 write(2)) and the hasher. */
+      if (hfd >= 0) {
+        uint8_t b8[8], b2[2], b4[4];
+        wr64(b8, seq);
+        write_all_fd(hfd, b8, 8);
+        orc_xxh32_update(&hint_hasher, b8, 8);
+        wr16(b2, ksz);
+        write_all_fd(hfd, b2, 2);
+        orc_xxh32_update(&hint_hasher, b2, 2);
+        wr32(b4, deleted ? ORC_ENTRY_TOMBSTONE : vsz_raw);
+        write_all_fd(hfd, b4, 4);
+        orc_xxh32_update(&hint_hasher, b4, 4);
+        wr64(b8, pos);
+        write_all_fd(hfd, b8, 8);
+        orc_xxh32_update(&hint_hasher, b8, 8);
+        write_all_fd(hfd, key, ksz);
+        orc_xxh32_update(&hint_hasher, key, ksz);
+      }
+      /* Cask::open closure (cask.rs:349-355) */
+      if (seq > res->max_seq) res->max_seq = seq;
+      orc_index_update(ix, key, ksz, file_id, pos, deleted ? ORC_ENTRY_TOMBSTONE : vsz_raw, seq);
+      res->records++;
+    }
+    pos += read_bytes;
+    free(header); free(key); free(value);
+  }
+  if (hfd >= 0) {
+    uint8_t b4[4];
+    wr32(b4, orc_xxh32_digest(&hint_hasher));  /* HintWriter::drop (log.rs:389-395) */
+    write_all_fd(hfd, b4, 4);
+    close(hfd);
+  }
+  close(fd);
+  res->live_keys = orc_index_len(ix);
+  return 0;
+}
+
+int orc_replay_buffer_fast(const uint8_t* buf, uint64_t len, uint32_t file_id, orc_index* ix,
+                           orc_replay_result* res) {
+  memset(res, 0, sizeof(*res));
+  uint64_t pos = 0;
+  while (pos < len) {
+    uint64_t rem = len - pos;
+    if (rem < 18) {
+      res->err_kind = ORC_ROW_EOF; res->err_file_id = file_id; res->err_pos = pos;
+      break;
+    }
+    const uint8_t* h = buf + pos;
+    uint16_t ksz = rd16(h + 12);
+    uint32_t vsz_raw = rd32(h + 14);
+    uint64_t rec = 18 + (uint64_t)ksz + (vsz_raw == ORC_ENTRY_TOMBSTONE ? 0 : vsz_raw);
+    if (rem < rec) {
+      res->err_kind = ORC_ROW_EOF; res->err_file_id = file_id; res->err_pos = pos;
+      break;
+    }
+    uint32_t hash = orc_xxh32(h + 4, rec - 4, 0);
+    if (hash != rd32(h)) {
+      res->err_kind = ORC_ROW_CHECKSUM; res->err_file_id = file_id; res->err_pos = pos;
+      res->err_expected = rd32(h); res->err_found = hash;
+      break;
+    }
+    uint64_t seq = rd64(h + 4);
+    if (seq > res->max_seq) res->max_seq = seq;
+    orc_index_update(ix, h + 18, ksz, file_id, pos, vsz_raw, seq);
+    res->records++;
+    res->bytes += rec;
+    pos += rec;
+  }
+  res->live_keys = orc_index_len(ix);
+  return 0;
+}

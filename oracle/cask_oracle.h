@@ -1,0 +1,111 @@
+/*
+ * cask_oracle.h — CPU restatement of Cask's replay hot path. TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this
+ * library, and only as the checker / the timed CPU baseline. The product path
+ * (cask_amd/, include/cask_scan.h) never links or calls it.
+ *
+ * Reference: andresilva/cask v0.7.1 (Rust). Each function cites the reference lines it
+ * restates. The Rust crate cannot be built here (no rustc/cargo), so there is no
+ * oracle/_ref build; the XXH32 arithmetic lives in the absent crate `twox-hash`
+ * ("1.1.0", caret: Cargo.toml:18) and is restated from the published XXH32 spec, pinned
+ * against libxxhash 0.8.2 (python-xxhash 3.8.1) by tests/test_oracle.py.
+ */
+#ifndef CASK_ORACLE_H
+#define CASK_ORACLE_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- XXH32 (util.rs:10-41 -> twox-hash XxHash32::with_seed(0)) ---- */
+typedef struct {
+  uint64_t total_len;
+  uint32_t v[4];
+  uint8_t mem[16];
+  uint32_t memsize;
+  uint32_t seed;
+} orc_xxh32_state;
+
+void orc_xxh32_reset(orc_xxh32_state* s, uint32_t seed);
+void orc_xxh32_update(orc_xxh32_state* s, const uint8_t* p, size_t len);
+uint32_t orc_xxh32_digest(const orc_xxh32_state* s);
+uint32_t orc_xxh32(const uint8_t* p, size_t len, uint32_t seed);
+
+/* ---- record codec (data.rs) ---- */
+#define ORC_ENTRY_STATIC_SIZE 18u        /* data.rs:11 */
+#define ORC_ENTRY_TOMBSTONE 0xFFFFFFFFu  /* data.rs:12 */
+
+/* Entry::write_bytes (data.rs:90-121). Returns bytes written to out (18+ksz+vsz_eff). */
+size_t orc_entry_encode(uint64_t seq, const uint8_t* key, uint16_t ksz, const uint8_t* value,
+                        uint32_t vsz, int deleted, uint8_t* out);
+
+/* Row = what Entries::next yields per record (log.rs:403-429) in the scan's SoA form. */
+enum { ORC_ROW_OK = 0, ORC_ROW_CHECKSUM = 1, ORC_ROW_EOF = 2 };
+typedef struct {
+  uint64_t pos;      /* entry_pos (log.rs:413) */
+  uint64_t seq;      /* Entry.sequence */
+  uint32_t vsz_raw;  /* value_size header field; 0xFFFFFFFF = tombstone */
+  uint16_t ksz;
+  uint8_t status;    /* ORC_ROW_* */
+  uint8_t pad;
+  uint32_t expected; /* stored checksum (InvalidChecksum.expected) */
+  uint32_t found;    /* computed XXH32 (InvalidChecksum.found) */
+} orc_row;
+
+/* Entries over an in-memory data file: Entry::from_read per record (data.rs:161-206),
+ * position advances by the bytes consumed (log.rs:415-417); iteration keeps going after a
+ * checksum error (the RecreateHints::drop drain, log.rs:467-471) and ends after an EOF.
+ * Returns the number of rows (>= 0), or -1 if cap is too small. */
+int64_t orc_scan_buffer(const uint8_t* buf, uint64_t len, orc_row* rows, uint64_t cap);
+
+/* Hint bytes for one OK row (Hint::write_bytes, data.rs:242-256). Returns bytes (22+ksz). */
+size_t orc_hint_encode(uint64_t seq, uint16_t ksz, uint32_t vsz_raw, uint64_t pos,
+                       const uint8_t* key, uint8_t* out);
+
+/* ---- keydir fold (cask.rs:60-90) + stats (stats.rs:23-48) ---- */
+typedef struct orc_index orc_index;
+orc_index* orc_index_new(void);
+void orc_index_free(orc_index* ix);
+/* Index::update for one Hint of file file_id. vsz_raw is the hint value_size field. */
+void orc_index_update(orc_index* ix, const uint8_t* key, uint16_t ksz, uint32_t file_id,
+                      uint64_t pos, uint32_t vsz_raw, uint64_t seq);
+uint64_t orc_index_len(const orc_index* ix);
+/* Export live entries sorted by key bytes (memcmp order, shorter first on tie).
+ * keys_out receives concatenated keys; each array has orc_index_len() slots. */
+void orc_index_export(const orc_index* ix, uint8_t* keys_out, uint64_t* key_off,
+                      uint16_t* key_len, uint32_t* file_id, uint64_t* pos, uint64_t* size,
+                      uint64_t* seq);
+/* Stats rows sorted by file_id; returns the number of stats rows (<= cap). */
+uint64_t orc_index_stats(const orc_index* ix, uint32_t* file_id, uint64_t* entries,
+                         uint64_t* dead_entries, uint64_t* dead_bytes, uint64_t cap);
+
+/* ---- replay drivers: Cask::open (cask.rs:335-382) for data files with no hint file ---- */
+typedef struct {
+  uint64_t records;      /* rows folded */
+  uint64_t bytes;        /* data-file bytes consumed */
+  uint64_t max_seq;      /* sequence = max(sequence, hint.sequence) (cask.rs:350-352) */
+  int32_t err_kind;      /* 0 none, ORC_ROW_CHECKSUM, ORC_ROW_EOF, -1 io */
+  uint32_t err_file_id;
+  uint64_t err_pos;
+  uint32_t err_expected, err_found;
+  uint64_t live_keys;
+} orc_replay_result;
+
+/* Reference-faithful replay of one data file: unbuffered read(2) of header/key/value per
+ * record (data.rs:162-183), streaming XXH32 in 3 updates (data.rs:185-191), 5 write(2) per
+ * hint into hint_path (data.rs:242-256, log.rs:382-386) plus the trailer (log.rs:389-395),
+ * and Index::update with a key copy (cask.rs:60-90). Single thread (cask.rs:348). */
+int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint32_t file_id,
+                             orc_index* ix, orc_replay_result* res);
+
+/* Fast restatement (mmap'd buffer, tight loop): scan + fold, no hint file. Context only. */
+int orc_replay_buffer_fast(const uint8_t* buf, uint64_t len, uint32_t file_id, orc_index* ix,
+                           orc_replay_result* res);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
