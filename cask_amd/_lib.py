@@ -9,7 +9,8 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcask_scan.so")
+# CASK_LIB_PATH selects a diagnostic build (e.g. build/stamps/libcask_scan.so) for profiling tools.
+LIB_PATH = os.environ.get("CASK_LIB_PATH") or os.path.join(_HERE, "libcask_scan.so")
 
 c_u8p = C.POINTER(C.c_uint8)
 c_u16p = C.POINTER(C.c_uint16)
@@ -33,6 +34,11 @@ class Rows(C.Structure):
 class ScanError(C.Structure):
     _fields_ = [("kind", C.c_int32), ("file_id", C.c_uint32), ("pos", C.c_uint64), ("expected", C.c_uint32),
                 ("found", C.c_uint32), ("row", C.c_uint64)]
+
+
+class Segments(C.Structure):
+    _fields_ = [("nchunks", C.c_uint64), ("chunk_bytes", C.c_uint32), ("slot_cap", C.c_uint32),
+                ("slots", C.c_void_p), ("count", C.c_void_p), ("base", C.c_void_p), ("total_rows", C.c_uint64)]
 
 
 class Options(C.Structure):
@@ -73,10 +79,13 @@ SIGNATURES = [
     ("cask_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("cask_ctx_stream", C.c_void_p, [C.c_void_p]),
     ("cask_ctx_device", C.c_int, [C.c_void_p]),
+    ("cask_ctx_last_error", C.c_char_p, [C.c_void_p]),
     ("cask_scan_chunk_bytes", C.c_uint32, []),
     ("cask_rows_bound", C.c_uint64, [C.POINTER(FileView), C.c_uint32]),
     ("cask_scan_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                    C.POINTER(ScanError)]),
+    ("cask_scan_device_segmented", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Segments),
+                                             c_u64p, C.POINTER(ScanError)]),
     ("cask_scan_host", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                  C.POINTER(ScanError)]),
     ("cask_last_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
@@ -109,6 +118,13 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise NativeLibraryMissing(
                 f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        # torch (device-memory plumbing) bundles its own libamdhip64.so.7; whichever copy loads
+        # first serves the whole process. Load torch's first so torch and this library share one
+        # HIP runtime; loading ours first leaves torch with "No HIP GPUs are available".
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
             fn = getattr(L, name)

@@ -1,0 +1,374 @@
+// The kernels around k_scan_chunks: long records, validation of the speculated boundaries with
+// per-file row prefixes, the summary the host reads back, dense compaction, and the exact repair
+// walk. All are small next to the scan; none needs inter-workgroup hand-offs.
+#include "device_util.h"
+
+namespace cask_dev {
+
+// ------------------------------------------------------------------------------------------
+// K_long: records longer than the LDS window, one lane each, straight from HBM.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_long(ScanArgs a) {
+  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < a.total_chunks;
+       t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t r = a.long_r[t];
+    if (r == 0xFFFFFFFFu) continue;
+    atomicAdd(&a.ctr->nlong, 1ull);
+    const uint32_t fi = find_file(a.files, a.nfiles, t);
+    const FileDesc fd = a.files[fi];
+    const uint64_t slot = t * a.slot_cap + r;
+    uint32_t* w = a.slots + slot * 4;
+    const uint64_t p = (t - fd.first_chunk) * (uint64_t)a.chunk + ((w[3] >> 16) & 0x7FFFu);
+    const uint32_t vsz = w[2];
+    const uint64_t rl = 18ull + (w[3] & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+    const uint32_t stored = gld4(fd.data + p);
+    if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {
+      w[3] |= kSlotBad;
+      atomicMin(&a.file_err[fi], (unsigned long long)slot);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Validation, as a three-launch segmented scan over tiles of kTile chunks (a tile never spans
+// two files):
+//  * T[c] = max over earlier chunks' exits (0 for chunks that found no start) is the true chain
+//    position entering chunk c as long as every earlier chunk of the file is valid; chunk c is
+//    valid iff its speculated start equals T[c] (or it found none and T[c] is past its end);
+//  * base[c] = exclusive sum of the earlier chunks' row counts within the file.
+// ------------------------------------------------------------------------------------------
+constexpr uint32_t kTile = kTileChunks;  // chunks per tile (256 threads x 4)
+
+__device__ __forceinline__ uint32_t tile_file(const ScanArgs& a, uint64_t T) {
+  uint32_t lo = 0, hi = a.nfiles;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.files[mid].first_tile <= T) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ uint64_t chunk_exit(const ScanArgs& a, uint64_t g) {
+  return a.spec[g] == kNone ? 0ull : a.exit[g];
+}
+
+// Block-wide (256 threads) exclusive max-scan and sum-scan of one value pair per thread, plus the
+// block totals.
+__device__ __forceinline__ void block_excl_scan2(unsigned long long mx, unsigned long long sm,
+                                                 unsigned long long& ex_mx, unsigned long long& ex_sm,
+                                                 unsigned long long& tot_mx, unsigned long long& tot_sm) {
+  __shared__ unsigned long long smx[4], ssm[4];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned long long u = __shfl_up(mx, o, 64), us = __shfl_up(sm, o, 64);
+    if ((int)lane >= o) {
+      mx = mx > u ? mx : u;
+      sm += us;
+    }
+  }
+  const unsigned long long pm = __shfl_up(mx, 1, 64), ps = __shfl_up(sm, 1, 64);
+  if (lane == 63) {
+    smx[wave] = mx;
+    ssm[wave] = sm;
+  }
+  __syncthreads();
+  unsigned long long wm = 0, ws = 0;
+  for (uint32_t k = 0; k < wave; ++k) {
+    wm = wm > smx[k] ? wm : smx[k];
+    ws += ssm[k];
+  }
+  ex_mx = wm;
+  ex_sm = ws;
+  if (lane > 0) {
+    ex_mx = ex_mx > pm ? ex_mx : pm;
+    ex_sm += ps;
+  }
+  tot_mx = 0;
+  tot_sm = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    tot_mx = tot_mx > smx[k] ? tot_mx : smx[k];
+    tot_sm += ssm[k];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_val_reduce(ScanArgs a) {
+  const uint64_t T = blockIdx.x;
+  const uint32_t f = tile_file(a, T);
+  const FileDesc fd = a.files[f];
+  const uint64_t c_lo = (T - fd.first_tile) * kTile;
+  unsigned long long mx = 0, sm = 0;
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint64_t c = c_lo + threadIdx.x * 4 + j;
+    if (c < fd.nchunks) {
+      const uint64_t g = fd.first_chunk + c;
+      const unsigned long long e = chunk_exit(a, g);
+      mx = mx > e ? mx : e;
+      sm += a.count[g];
+    }
+  }
+  unsigned long long em, es, tm, ts;
+  block_excl_scan2(mx, sm, em, es, tm, ts);
+  if (threadIdx.x == 0) {
+    a.tile_max[T] = tm;
+    a.tile_sum[T] = ts;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_val_files(ScanArgs a) {
+  const uint32_t f = blockIdx.x;
+  const FileDesc fd = a.files[f];
+  const uint64_t nt = (fd.nchunks + kTile - 1) / kTile;
+  unsigned long long cmx = 0, csm = 0;
+  for (uint64_t b = 0; b < nt; b += 256) {
+    const uint64_t i = b + threadIdx.x;
+    unsigned long long mx = 0, sm = 0;
+    if (i < nt) {
+      mx = a.tile_max[fd.first_tile + i];
+      sm = a.tile_sum[fd.first_tile + i];
+    }
+    unsigned long long em, es, tm, ts;
+    block_excl_scan2(mx, sm, em, es, tm, ts);
+    if (i < nt) {
+      a.tile_pmax[fd.first_tile + i] = cmx > em ? cmx : em;
+      a.tile_psum[fd.first_tile + i] = csm + es;
+    }
+    cmx = cmx > tm ? cmx : tm;
+    csm += ts;
+  }
+  if (threadIdx.x == 0) a.file_total[f] = csm;
+}
+
+__global__ __launch_bounds__(256) void k_val_apply(ScanArgs a) {
+  const uint64_t T = blockIdx.x;
+  const uint32_t f = tile_file(a, T);
+  const FileDesc fd = a.files[f];
+  const uint64_t c_lo = (T - fd.first_tile) * kTile;
+  unsigned long long e[4], cn[4];
+  unsigned long long mx = 0, sm = 0;
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint64_t c = c_lo + threadIdx.x * 4 + j;
+    e[j] = 0;
+    cn[j] = 0;
+    if (c < fd.nchunks) {
+      const uint64_t g = fd.first_chunk + c;
+      e[j] = chunk_exit(a, g);
+      cn[j] = a.count[g];
+    }
+    mx = mx > e[j] ? mx : e[j];
+    sm += cn[j];
+  }
+  unsigned long long em, es, tm, ts;
+  block_excl_scan2(mx, sm, em, es, tm, ts);
+  const unsigned long long pmax = a.tile_pmax[T];
+  unsigned long long run_max = pmax > em ? pmax : em;
+  unsigned long long run_sum = a.tile_psum[T] + es;
+  for (uint32_t j = 0; j < 4; ++j) {
+    const uint64_t c = c_lo + threadIdx.x * 4 + j;
+    if (c < fd.nchunks) {
+      const uint64_t g = fd.first_chunk + c;
+      a.tin[g] = run_max;
+      a.base[g] = run_sum;
+      const uint64_t c0 = c * (uint64_t)a.chunk;
+      const uint64_t c1 = (c0 + a.chunk < fd.len) ? c0 + a.chunk : fd.len;
+      const uint64_t sp = a.spec[g];
+      bool ok;
+      if (c == 0) ok = true;
+      else if (sp != kNone) ok = (sp == run_max);
+      else ok = (run_max >= c1);
+      if (!ok) atomicMin((unsigned long long*)&a.first_bad[f], (unsigned long long)c);
+    }
+    run_max = run_max > e[j] ? run_max : e[j];
+    run_sum += cn[j];
+  }
+}
+
+// Summary: row offsets per file, first failing row per file, flags -> one buffer for the host.
+__global__ void k_summary(ScanArgs a, uint64_t* out) {
+  SummaryHead* h = (SummaryHead*)out;
+  uint64_t* row_off = out + sizeof(SummaryHead) / 8;
+  uint64_t* fbad = row_off + a.nfiles + 1;
+  uint64_t* badT = fbad + a.nfiles;
+  uint64_t* err = badT + a.nfiles;
+  uint64_t* err_slot = err + a.nfiles;
+  __shared__ uint64_t total;
+  if (threadIdx.x == 0) {
+    uint64_t acc = 0;
+    for (uint32_t f = 0; f < a.nfiles; ++f) {
+      row_off[f] = acc;
+      acc += a.file_total[f];
+    }
+    row_off[a.nfiles] = acc;
+    total = acc;
+  }
+  __syncthreads();
+  for (uint32_t f = threadIdx.x; f < a.nfiles; f += blockDim.x) {
+    const FileDesc fd = a.files[f];
+    const uint64_t b = a.first_bad[f];
+    fbad[f] = b;
+    badT[f] = (b != kNone) ? a.tin[fd.first_chunk + b] : 0;
+    const unsigned long long s = a.file_err[f];
+    err_slot[f] = s;
+    if (s == kNone) {
+      err[f] = kNone;
+    } else {
+      const uint64_t t = s / a.slot_cap, r = s % a.slot_cap;
+      err[f] = row_off[f] + a.base[t] + r;
+    }
+  }
+  if (threadIdx.x == 0) {
+    h->total_rows = total;
+    h->nlong = a.ctr->nlong;
+    uint64_t any = 0, cnt = 0;
+    for (uint32_t f = 0; f < a.nfiles; ++f)
+      if (a.first_bad[f] != kNone) {
+        any = 1;
+        cnt += a.files[f].nchunks - a.first_bad[f];
+      }
+    h->any_invalid = any;
+    h->invalid_chunks = cnt;
+    h->walk_steps = a.ctr->walk_steps;
+  }
+}
+
+// K_compact: slot rows -> dense SoA rows in (file, pos) order. One wave per chunk.
+__global__ __launch_bounds__(256) void k_compact(ScanArgs a, const uint64_t* summary) {
+  const uint64_t* row_off = summary + sizeof(SummaryHead) / 8;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  for (uint64_t t = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); t < a.total_chunks; t += nw) {
+    const uint32_t fi = find_file(a.files, a.nfiles, t);
+    const FileDesc fd = a.files[fi];
+    const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+    const uint32_t n = a.count[t];
+    const uint64_t dst0 = row_off[fi] + a.base[t];
+    const u32x4* src = (const u32x4*)(a.slots + (uint64_t)t * a.slot_cap * 4);
+    for (uint32_t r = lane; r < n; r += 64) {
+      const u32x4 w = src[r];
+      const uint64_t p = c0 + ((w.w >> 16) & 0x7FFFu);
+      const uint32_t ksz = w.w & 0xFFFFu;
+      const uint64_t end = p + 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+      const uint8_t st = (p + 18 > fd.len || end > fd.len) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
+      const uint64_t d = dst0 + r;
+      if (d < a.row_cap) {
+        a.pos[d] = p;
+        a.seq[d] = (uint64_t)w.x | ((uint64_t)w.y << 32);
+        a.vsz[d] = w.z;
+        a.ksz[d] = (uint16_t)ksz;
+        a.status[d] = st;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K_walk (repair): exact boundary chain from the first invalid chunk of a file, one wave per
+// file. Rewrites spec[] for that chunk onward; the re-scan then runs with exact=1.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void k_walk(ScanArgs a, const uint64_t* summary) {
+  const uint32_t f = blockIdx.x, lane = threadIdx.x;
+  const uint64_t* row_off = summary + sizeof(SummaryHead) / 8;
+  const uint64_t* fbad = row_off + a.nfiles + 1;
+  const uint64_t* badT = fbad + a.nfiles;
+  const uint64_t cb = fbad[f];
+  if (cb == kNone) return;
+  const FileDesc fd = a.files[f];
+  const uint64_t len = fd.len;
+  const uint64_t CHK = a.chunk;
+  uint64_t* spec = a.spec + fd.first_chunk;
+  uint64_t cur = cb;  // next chunk whose start is not yet written
+  uint64_t p = badT[f];
+  uint64_t steps = 0;
+  while (p < len) {
+    ++steps;
+    const uint8_t* hp = fd.data + p;
+    bool eof = (p + 18 > len);
+    const uint64_t rl = eof ? 0 : g_reclen(hp);
+    if (!eof && p + rl > len) eof = true;
+    if (eof) {  // the chain ends with this record (an UnexpectedEof row)
+      const uint64_t ci = p / CHK;
+      for (uint64_t g = cur + lane; g < ci; g += 64) spec[g] = kNone;
+      if (lane == 0 && ci >= cur) spec[ci] = p;
+      cur = ci + 1 > cur ? ci + 1 : cur;
+      break;
+    }
+    const uint64_t q = p + (uint64_t)lane * rl;
+    bool v = true;
+    if (lane) {
+      v = (q + 18 <= len);
+      if (v) v = (g_reclen(fd.data + q) == rl) && (q + rl <= len);
+    }
+    const unsigned long long okm = __ballot(v);
+    const uint32_t k = (~okm) ? (uint32_t)__builtin_ctzll(~okm) : 64u;
+    if (lane < k) {
+      const uint64_t ci = q / CHK;
+      const uint64_t prevc = (lane == 0) ? (cur == 0 ? ~0ull : cur - 1) : (q - rl) / CHK;
+      if (lane == 0 ? (ci >= cur) : (ci != prevc)) {
+        spec[ci] = q;
+        const uint64_t gs = (lane == 0) ? cur : prevc + 1;
+        for (uint64_t g = gs; g < ci; ++g) spec[g] = kNone;
+      }
+    }
+    const uint64_t lastq = p + (uint64_t)(k - 1) * rl;
+    const uint64_t lc = lastq / CHK;
+    cur = lc + 1 > cur ? lc + 1 : cur;
+    p += (uint64_t)k * rl;
+  }
+  for (uint64_t g = cur + lane; g < fd.nchunks; g += 64) spec[g] = kNone;
+  if (lane == 0) atomicAdd(&a.ctr->walk_steps, (unsigned long long)steps);
+}
+
+// Error detail of one failing slot row (error path only):
+// out[0] stored checksum, out[1] computed XXH32, out[2] row status, out[3..4] pos.
+__global__ void k_err_detail(ScanArgs a, uint32_t fi, uint64_t slot, uint32_t* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  const FileDesc fd = a.files[fi];
+  const uint32_t* w = a.slots + slot * 4;
+  const uint64_t t = slot / a.slot_cap;
+  const uint64_t p = (t - fd.first_chunk) * (uint64_t)a.chunk + ((w[3] >> 16) & 0x7FFFu);
+  out[0] = 0;
+  out[1] = 0;
+  out[2] = kRowEof;
+  out[3] = (uint32_t)p;
+  out[4] = (uint32_t)(p >> 32);
+  if (p + 18 > fd.len) return;
+  const uint8_t* hp = fd.data + p;
+  const uint64_t rl = g_reclen(hp);
+  out[0] = gld4(hp);
+  if (p + rl > fd.len) return;
+  out[1] = gbl_xxh32(hp + 4, rl - 4);
+  out[2] = (w[3] & kSlotBad) ? kRowChecksum : kRowOk;
+}
+
+// ------------------------------------------------------------------------------------------
+static inline hipStream_t S(void* s) { return (hipStream_t)s; }
+
+void launch_long(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  hipLaunchKernelGGL(k_long, dim3(1024), dim3(256), 0, S(stream), a);
+}
+void launch_validate(const ScanArgs& a, void* stream) {
+  if (!a.nfiles) return;
+  // k_val_files runs even with no tiles at all (every file empty): it writes the file totals
+  if (a.total_tiles) hipLaunchKernelGGL(k_val_reduce, dim3((uint32_t)a.total_tiles), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(k_val_files, dim3(a.nfiles), dim3(256), 0, S(stream), a);
+  if (a.total_tiles) hipLaunchKernelGGL(k_val_apply, dim3((uint32_t)a.total_tiles), dim3(256), 0, S(stream), a);
+}
+void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream) {
+  hipLaunchKernelGGL(k_summary, dim3(1), dim3(256), 0, S(stream), a, summary);
+}
+void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream) {
+  if (!a.total_chunks) return;
+  uint64_t g = (a.total_chunks + 3) / 4;
+  if (g > 4096) g = 4096;
+  hipLaunchKernelGGL(k_compact, dim3((uint32_t)g), dim3(256), 0, S(stream), a, summary);
+}
+void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream) {
+  if (!a.nfiles) return;
+  hipLaunchKernelGGL(k_walk, dim3(a.nfiles), dim3(64), 0, S(stream), a, summary);
+}
+void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(k_err_detail, dim3(1), dim3(64), 0, S(stream), a, fi, slot, out);
+}
+
+}  // namespace cask_dev

@@ -4,30 +4,33 @@
 
 namespace cask_dev {
 
-// Chunking: the unit a workgroup stages into LDS and speculates a record boundary for.
-constexpr uint32_t kWG = 256;                 // threads per workgroup (4 waves of 64)
-constexpr uint32_t kChunk = 32768;            // bytes of file owned by one workgroup
-constexpr uint32_t kHalo = 4096;              // extra bytes staged so boundary records hash in LDS
-constexpr uint32_t kWin = kChunk + kHalo;     // staged window
-constexpr uint32_t kMaxStarts = kChunk / 18 + 2;  // every record is >= 18 bytes (data.rs:11)
-constexpr uint64_t kNone = ~0ull;             // "no record starts in this chunk"
+// A chunk is the unit one workgroup stages into LDS and speculates a record boundary for; the
+// geometry (chunk bytes, halo bytes, threads) is a template of k_scan_chunks chosen per call.
+constexpr int kDefaultGeometry = 0;           // index into the k_scan_chunks instantiations
+constexpr uint64_t kNone = ~0ull;             // "no record starts in this chunk" / no error
 constexpr uint64_t kTerm = ~0ull;             // chain ended by an UnexpectedEof record
 
-enum : uint8_t { kRowOk = 0, kRowChecksum = 1, kRowEof = 2, kRowPendingLong = 3 };
+enum : uint8_t { kRowOk = 0, kRowChecksum = 1, kRowEof = 2 };
+
+// Slot row (16 B) written by the chunk scan at slots[chunk * slot_cap + r]:
+//   w0,w1 = seq (u64), w2 = vsz raw, w3 = ksz | offset-in-chunk << 16 | checksum-bad << 31.
+// Status is implied: EOF if the record runs past the file end, else bad bit ? CHECKSUM : OK.
+constexpr uint32_t kSlotBad = 0x80000000u;
 
 struct FileDesc {
   const uint8_t* data;   // device pointer to the file's bytes
   uint64_t len;
   uint64_t first_chunk;  // global chunk index of this file's chunk 0
-  uint64_t nchunks;      // ceil(len / kChunk)
+  uint64_t nchunks;      // ceil(len / chunk)
+  uint64_t first_tile;   // first validation tile (kTile chunks) of this file
+  uint64_t pad;
 };
 
+constexpr uint32_t kTileChunks = 1024;  // chunks per validation tile (k_pipeline.hip kTile)
+
 struct Counters {
-  unsigned long long ticket;   // chunk tickets handed out (in-order grab => deadlock-free look-back)
-  unsigned long long nlong;    // records longer than the LDS window
-  unsigned int overflow;       // row capacity exceeded
-  unsigned int timeout;        // a bounded spin gave up (never expected)
-  unsigned long long walk_steps;
+  unsigned long long nlong;      // records longer than the LDS window
+  unsigned long long walk_steps; // repair walk iterations
 };
 
 struct ScanArgs {
@@ -35,48 +38,58 @@ struct ScanArgs {
   uint32_t nfiles;
   uint32_t exact;              // 1: spec[] holds exact chunk starts (repair pass), no search
   uint64_t total_chunks;
-  // per-chunk scratch
-  unsigned long long* lb;      // decoupled look-back words: flag(2) | value(62)
+  uint32_t chunk;              // chunk bytes of the geometry in use
+  uint32_t slot_cap;           // row slots per chunk (chunk / 18 + 2)
+  // per-chunk
   uint64_t* spec;              // start used by the chunk (kNone if none)
   uint64_t* exit;              // first chain position >= chunk end, or kTerm
-  uint64_t* base;              // exclusive row prefix
-  uint32_t* count;             // rows emitted by the chunk
+  uint32_t* count;             // rows in the chunk
+  uint64_t* base;              // exclusive row prefix of the chunk within its file
   uint64_t* tin;               // validate: chain position entering the chunk
+  uint32_t* slots;             // 4 words per slot row
+  // validation tiles
+  uint64_t total_tiles;
+  uint64_t* tile_max;          // per tile: max exit
+  uint64_t* tile_sum;          // per tile: row count
+  uint64_t* tile_pmax;         // per tile: exclusive max within the file
+  uint64_t* tile_psum;         // per tile: exclusive row prefix within the file
+  // per-file
+  uint64_t* file_total;        // rows per file
+  unsigned long long* file_err;  // min slot index with a failing row
+  uint64_t* first_bad;         // first chunk whose speculated start is wrong (kNone: none)
   // global
   Counters* ctr;
-  uint64_t* long_row;          // row index of each long record
-  uint32_t* long_file;         // file index of each long record
-  uint64_t long_cap;
-  unsigned long long* file_err_row;  // per file: min row index with a failing status
-  // rows (device)
+  uint32_t* long_r;            // per chunk: row of its record longer than the window, or !0
+  // dense rows (compaction output, device)
   uint64_t* pos;
   uint64_t* seq;
   uint32_t* vsz;
   uint16_t* ksz;
   uint8_t* status;
   uint64_t row_cap;
+  unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums
 };
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
 struct SummaryHead {
   uint64_t total_rows;
   uint64_t nlong;
-  uint64_t overflow;
-  uint64_t timeout;
   uint64_t any_invalid;
   uint64_t invalid_chunks;
   uint64_t walk_steps;
-  uint64_t pad;
+  uint64_t pad[3];
 };
-// followed by, per file f: row_off[f] (nfiles+1 entries), first_bad[f], bad_T[f], err_row[f]
+// followed by row_off[nfiles+1], then per file: first_bad, bad_T, err_row, err_slot
 
 // Host-callable launchers (defined in scan_kernels.hip).
-void launch_scan_chunks(const ScanArgs& a, void* stream);
+uint32_t geometry_chunk(int geo);
+void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
 void launch_long(const ScanArgs& a, void* stream);
-void launch_validate(const ScanArgs& a, uint64_t* first_bad, void* stream);
-void launch_summary(const ScanArgs& a, const uint64_t* first_bad, uint64_t* summary, void* stream);
+void launch_validate(const ScanArgs& a, void* stream);
+void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
+void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
-void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t row, uint32_t* out2, void* stream);
+void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,
                          const uint16_t* ksz, const uint32_t* vsz_raw, const uint64_t* key_id,
                          uint64_t value_seed, uint8_t* out, void* stream);

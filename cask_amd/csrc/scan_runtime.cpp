@@ -75,20 +75,28 @@ struct cask_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  DevBuf chunk;      // lb | spec | exit | base | tin (u64 x5) | count (u32)
+  DevBuf chunk;      // spec | exit | base | tin (u64 x4) | count (u32)
+  DevBuf slots;      // 16-B slot rows, slot_cap per chunk
   DevBuf ctr;        // Counters
-  DevBuf longbuf;    // long_row (u64) | long_file (u32)
-  DevBuf filebuf;    // FileDesc[] | file_err_row[] | first_bad[] | summary
-  DevBuf err2;       // 2 x u32
+  DevBuf filebuf;    // FileDesc[] | file_err[] | first_bad[] | file_total[] | summary
+  DevBuf err2;       // error detail words
+  DevBuf stamps;     // diagnostic builds (-DCASK_STAMPS) only
+  uint64_t* dbg_spec = nullptr;
+  uint64_t* dbg_exit = nullptr;
+  uint64_t* dbg_tin = nullptr;
+  uint32_t* dbg_count = nullptr;
+  uint64_t dbg_n = 0;
   HostPinned hfiles;
   HostPinned hsum;
   // host-scan staging
   DevBuf stage_data;
   DevBuf stage_rows;
-  hipEvent_t ev[6] = {};
-  float last_ms[5] = {0, 0, 0, 0, 0};
+  int geo = 0;       // k_scan_chunks geometry (CASK_SCAN_GEOMETRY overrides the default)
+  hipEvent_t ev[7] = {};
+  float last_ms[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_counters[3] = {0, 0, 0};
   std::mutex mu;
+  char last_error[256] = {0};
 };
 
 static int set_dev(const cask_ctx* c) {
@@ -115,8 +123,10 @@ cask_ctx* cask_ctx_create(int device, int* status) {
     return nullptr;
   }
   c->stream = c->own;
+  c->geo = kDefaultGeometry;
+  if (const char* g = getenv("CASK_SCAN_GEOMETRY")) c->geo = atoi(g);
   for (auto& e : c->ev) (void)hipEventCreate(&e);
-  if (!c->ctr.ensure(sizeof(Counters)) || !c->err2.ensure(16)) {
+  if (!c->ctr.ensure(sizeof(Counters)) || !c->err2.ensure(64)) {
     cask_ctx_destroy(c);
     if (status) *status = CASK_E_NOMEM;
     return nullptr;
@@ -130,8 +140,8 @@ void cask_ctx_destroy(cask_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->chunk.release();
+  c->slots.release();
   c->ctr.release();
-  c->longbuf.release();
   c->filebuf.release();
   c->err2.release();
   c->stage_data.release();
@@ -152,7 +162,8 @@ int cask_ctx_set_stream(cask_ctx* c, void* s) {
 
 void* cask_ctx_stream(cask_ctx* c) { return c ? (void*)c->stream : nullptr; }
 int cask_ctx_device(const cask_ctx* c) { return c ? c->device : -1; }
-uint32_t cask_scan_chunk_bytes(void) { return kChunk; }
+const char* cask_ctx_last_error(const cask_ctx* c) { return c ? c->last_error : ""; }
+uint32_t cask_scan_chunk_bytes(void) { return geometry_chunk(kDefaultGeometry); }
 
 uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles) {
   uint64_t b = 0;
@@ -162,9 +173,9 @@ uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles) {
 
 uint32_t cask_xxh32(const uint8_t* data, uint64_t len) { return cask_xxh::xxh32(data, len, 0); }
 
-int cask_last_timings(const cask_ctx* c, float* ms5) {
-  if (!c || !ms5) return CASK_E_INVALID_ARG;
-  memcpy(ms5, c->last_ms, sizeof(c->last_ms));
+int cask_last_timings(const cask_ctx* c, float* ms6) {
+  if (!c || !ms6) return CASK_E_INVALID_ARG;
+  memcpy(ms6, c->last_ms, sizeof(c->last_ms));
   return CASK_OK;
 }
 
@@ -176,12 +187,12 @@ int cask_last_counters(const cask_ctx* c, uint64_t* c3) {
 
 }  // extern "C"
 
-// Core pipeline on device-resident files and rows.
+// Core pipeline on device-resident files. rows == nullptr: segmented output only (slots + chunk
+// table, owned by the context); otherwise dense SoA rows are compacted into the caller's arrays.
 static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
-                            uint64_t* file_row_offset, cask_scan_error* err) {
-  if (!rows) return CASK_E_INVALID_ARG;
+                            cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err) {
   if (nfiles && !files) return CASK_E_INVALID_ARG;
-  if (rows->capacity && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status))
+  if (rows && rows->capacity && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status))
     return CASK_E_INVALID_ARG;
   for (uint32_t i = 0; i < nfiles; ++i)
     if (files[i].len && !files[i].data) return CASK_E_INVALID_ARG;
@@ -189,33 +200,37 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   hipStream_t st = c->stream;
 
   // file table
-  uint64_t total_chunks = 0, long_cap = 0;
+  const uint32_t chunk = geometry_chunk(c->geo);
+  const uint32_t slot_cap = chunk / 18 + 2;
+  uint64_t total_chunks = 0, total_tiles = 0;
   const size_t head_words = sizeof(SummaryHead) / 8;
-  const size_t sum_words = head_words + (nfiles + 1) + 3ull * nfiles;
+  const size_t sum_words = head_words + (nfiles + 1) + 4ull * nfiles;
   if (!c->hfiles.ensure(sizeof(FileDesc) * (nfiles + 1)) || !c->hsum.ensure(sum_words * 8)) return CASK_E_NOMEM;
   FileDesc* fd = (FileDesc*)c->hfiles.p;
   for (uint32_t i = 0; i < nfiles; ++i) {
     fd[i].data = files[i].data;
     fd[i].len = files[i].len;
     fd[i].first_chunk = total_chunks;
-    fd[i].nchunks = (files[i].len + kChunk - 1) / kChunk;
+    fd[i].nchunks = (files[i].len + chunk - 1) / chunk;
+    fd[i].first_tile = total_tiles;
+    fd[i].pad = 0;
     total_chunks += fd[i].nchunks;
-    long_cap += files[i].len / kHalo + 1;
+    total_tiles += (fd[i].nchunks + kTileChunks - 1) / kTileChunks;
   }
   // device scratch
   const size_t fd_bytes = align_up(sizeof(FileDesc) * (nfiles + 1), 256);
-  const size_t fe_bytes = align_up(8ull * (nfiles + 1), 256);
-  const size_t fb_bytes = align_up(8ull * (nfiles + 1), 256);
+  const size_t pf_bytes = align_up(8ull * (nfiles + 1), 256);
   const size_t sum_bytes = align_up(sum_words * 8, 256);
-  if (!c->filebuf.ensure(fd_bytes + fe_bytes + fb_bytes + sum_bytes)) return CASK_E_NOMEM;
-  if (!c->chunk.ensure((total_chunks + 1) * (5 * 8 + 4) + 1024)) return CASK_E_NOMEM;
-  if (!c->longbuf.ensure((long_cap + 1) * 12 + 256)) return CASK_E_NOMEM;
+  if (!c->filebuf.ensure(fd_bytes + 3 * pf_bytes + sum_bytes)) return CASK_E_NOMEM;
+  if (!c->chunk.ensure((total_chunks + 1) * (4 * 8 + 4 + 4) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
+  if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
   unsigned long long* d_ferr = (unsigned long long*)(fbase + fd_bytes);
-  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + fe_bytes);
-  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + fe_bytes + fb_bytes);
+  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + pf_bytes);
+  uint64_t* d_ftot = (uint64_t*)(fbase + fd_bytes + 2 * pf_bytes);
+  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + 3 * pf_bytes);
 
   uint64_t* cb = c->chunk.as<uint64_t>();
   const uint64_t C = total_chunks + 1;
@@ -224,115 +239,169 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.nfiles = nfiles;
   a.exact = 0;
   a.total_chunks = total_chunks;
-  a.lb = (unsigned long long*)cb;
-  a.spec = cb + C;
-  a.exit = cb + 2 * C;
-  a.base = cb + 3 * C;
-  a.tin = cb + 4 * C;
-  a.count = (uint32_t*)(cb + 5 * C);
+  a.chunk = chunk;
+  a.slot_cap = slot_cap;
+  a.spec = cb;
+  a.exit = cb + C;
+  a.base = cb + 2 * C;
+  a.tin = cb + 3 * C;
+  a.count = (uint32_t*)(cb + 4 * C);
+  {
+    uint64_t* tb = cb + 4 * C + (C + 1) / 2 + 1;
+    const uint64_t TT = total_tiles + 1;
+    a.long_r = (uint32_t*)(tb + 4 * TT);
+    a.total_tiles = total_tiles;
+    a.tile_max = tb;
+    a.tile_sum = tb + TT;
+    a.tile_pmax = tb + 2 * TT;
+    a.tile_psum = tb + 3 * TT;
+  }
+  a.slots = c->slots.as<uint32_t>();
+  a.file_total = d_ftot;
+  a.file_err = d_ferr;
+  a.first_bad = d_fbad;
   a.ctr = c->ctr.as<Counters>();
-  a.long_row = c->longbuf.as<uint64_t>();
-  a.long_file = (uint32_t*)(a.long_row + long_cap + 1);
-  a.long_cap = long_cap;
-  a.file_err_row = d_ferr;
-  a.pos = rows->pos;
-  a.seq = rows->seq;
-  a.vsz = rows->vsz;
-  a.ksz = rows->ksz;
-  a.status = rows->status;
-  a.row_cap = rows->capacity;
+  if (rows) {
+    a.pos = rows->pos;
+    a.seq = rows->seq;
+    a.vsz = rows->vsz;
+    a.ksz = rows->ksz;
+    a.status = rows->status;
+    a.row_cap = rows->capacity;
+  }
+  a.stamps = nullptr;
+#ifdef CASK_STAMPS
+  if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
+#endif
 
   bool ok = true;
-  auto H = [&](hipError_t e) { ok = ok && (e == hipSuccess); };
+  auto H = [&](hipError_t e, const char* what = "hip call") {
+    if (e != hipSuccess && ok) {
+      ok = false;
+      snprintf(c->last_error, sizeof(c->last_error), "%s: %s", what, hipGetErrorString(e));
+    }
+  };
+  auto reset = [&]() {
+    H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
+    H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
+    H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
+    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 16 * 8, st));
+  };
+  // CASK_SYNC_EACH=1 (diagnostic): synchronise after every launch so a fault names its kernel
+  static const bool sync_each = getenv("CASK_SYNC_EACH") != nullptr;
+  auto L = [&](const char* what) {
+    H(hipGetLastError(), what);
+    if (sync_each) H(hipStreamSynchronize(st), what);
+  };
+  // one pass of the pipeline; events 1..4 bracket scan / long / validate+summary / compact
+  auto pass = [&](bool timed) {
+    reset();
+    if (timed) H(hipEventRecord(c->ev[1], st));
+    launch_scan_chunks(a, c->geo, st);
+    L("k_scan_chunks");
+    if (timed) H(hipEventRecord(c->ev[2], st));
+    launch_long(a, st);
+    L("k_long");
+    if (timed) H(hipEventRecord(c->ev[3], st));
+    launch_validate(a, st);
+    L("k_val");
+    launch_summary(a, d_sum, st);
+    L("k_summary");
+    if (timed) H(hipEventRecord(c->ev[4], st));
+    if (rows) {
+      launch_compact(a, d_sum, st);
+      L("k_compact");
+    }
+    H(hipEventRecord(timed ? c->ev[5] : c->ev[6], st));
+    H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st), "summary D2H");
+    H(hipStreamSynchronize(st), "stream sync");
+  };
   H(hipEventRecord(c->ev[0], st));
   H(hipMemcpyAsync(d_files, fd, sizeof(FileDesc) * (nfiles ? nfiles : 1), hipMemcpyHostToDevice, st));
-  auto reset = [&]() {
-    if (total_chunks) H(hipMemsetAsync(a.lb, 0, total_chunks * 8, st));
-    H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st));
-    H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st));
-  };
-  reset();
-  H(hipEventRecord(c->ev[1], st));
-  launch_scan_chunks(a, st);
-  H(hipEventRecord(c->ev[2], st));
-  launch_long(a, st);
-  H(hipEventRecord(c->ev[3], st));
-  launch_validate(a, d_fbad, st);
-  launch_summary(a, d_fbad, d_sum, st);
-  H(hipEventRecord(c->ev[4], st));
-  H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st));
-  H(hipStreamSynchronize(st));
-  if (!ok || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+  c->last_error[0] = 0;
+  (void)hipGetLastError();  // drop any stale error another library left on this thread
+  pass(true);
+  if (!ok) return CASK_E_DEVICE;
 
   uint64_t* hs = (uint64_t*)c->hsum.p;
   SummaryHead* head = (SummaryHead*)hs;
   float repair_ms = 0.f;
   uint64_t invalid_chunks = 0;
-  if (head->timeout) return CASK_E_DEVICE;
+#ifdef CASK_STAMPS
+  if (getenv("CASK_NO_REPAIR")) {  // diagnostic: keep the speculative pass for inspection
+    c->dbg_spec = a.spec;
+    c->dbg_exit = a.exit;
+    c->dbg_count = a.count;
+    c->dbg_tin = a.tin;
+    c->dbg_n = total_chunks;
+    return head->any_invalid ? 1 : 0;
+  }
+#endif
   if (head->any_invalid) {
     // Repair: exact boundary walk from each file's first invalid chunk, then a full re-scan
     // with known starts (exact=1). Chunks before the first invalid one keep their (validated)
     // speculative starts.
     invalid_chunks = head->invalid_chunks;
     launch_walk(a, d_sum, st);
+    L("k_walk");
     a.exact = 1;
-    reset();
-    launch_scan_chunks(a, st);
-    launch_long(a, st);
-    launch_validate(a, d_fbad, st);
-    launch_summary(a, d_fbad, d_sum, st);
-    H(hipEventRecord(c->ev[5], st));
-    H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st));
-    H(hipStreamSynchronize(st));
-    if (!ok || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
-    if (head->timeout || head->any_invalid) return CASK_E_DEVICE;  // exact pass must validate
-    (void)hipEventElapsedTime(&repair_ms, c->ev[4], c->ev[5]);
+    pass(false);
+    if (!ok) return CASK_E_DEVICE;
+    if (head->any_invalid) {  // the exact pass must validate
+      snprintf(c->last_error, sizeof(c->last_error), "exact re-scan did not validate");
+      return CASK_E_DEVICE;
+    }
+    (void)hipEventElapsedTime(&repair_ms, c->ev[5], c->ev[6]);
   }
-  float t_all = 0, t_k1 = 0, t_long = 0, t_val = 0;
+  float t_all = 0, t_k1 = 0, t_long = 0, t_val = 0, t_cmp = 0;
   (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
   (void)hipEventElapsedTime(&t_long, c->ev[2], c->ev[3]);
   (void)hipEventElapsedTime(&t_val, c->ev[3], c->ev[4]);
-  (void)hipEventElapsedTime(&t_all, c->ev[0], c->ev[4]);
+  (void)hipEventElapsedTime(&t_cmp, c->ev[4], c->ev[5]);
+  (void)hipEventElapsedTime(&t_all, c->ev[0], c->ev[5]);
   c->last_ms[0] = t_all + repair_ms;
   c->last_ms[1] = t_k1;
   c->last_ms[2] = t_long;
   c->last_ms[3] = t_val;
   c->last_ms[4] = repair_ms;
+  c->last_ms[5] = t_cmp;
   c->last_counters[0] = total_chunks;
   c->last_counters[1] = head->nlong;
   c->last_counters[2] = invalid_chunks;
 
   const uint64_t* row_off = hs + head_words;
-  const uint64_t* ferr = row_off + nfiles + 1 + 2ull * nfiles;
-  rows->count = head->total_rows;
+  const uint64_t* ferr_row = row_off + nfiles + 1 + 2ull * nfiles;
+  const uint64_t* ferr_slot = ferr_row + nfiles;
   if (file_row_offset) memcpy(file_row_offset, row_off, 8ull * (nfiles + 1));
-  if (head->overflow || head->total_rows > rows->capacity) return CASK_E_CAPACITY;
+  if (seg) {
+    seg->nchunks = total_chunks;
+    seg->chunk_bytes = chunk;
+    seg->slot_cap = slot_cap;
+    seg->slots = a.slots;
+    seg->count = a.count;
+    seg->base = a.base;
+    seg->total_rows = head->total_rows;
+  }
+  if (rows) {
+    rows->count = head->total_rows;
+    if (head->total_rows > rows->capacity) return CASK_E_CAPACITY;
+  }
 
   if (err) {
     memset(err, 0, sizeof(*err));
     for (uint32_t f = 0; f < nfiles; ++f) {
-      if (ferr[f] == kNone) continue;
-      const uint64_t r = ferr[f];
-      uint8_t status = 0;
-      uint64_t pos = 0;
-      uint32_t eh[2] = {0, 0};
-      H(hipMemcpyAsync(&status, rows->status + r, 1, hipMemcpyDeviceToHost, st));
-      H(hipMemcpyAsync(&pos, rows->pos + r, 8, hipMemcpyDeviceToHost, st));
-      launch_err_detail(a, f, r, c->err2.as<uint32_t>(), st);
-      H(hipMemcpyAsync(eh, c->err2.p, 8, hipMemcpyDeviceToHost, st));
+      if (ferr_slot[f] == kNone) continue;
+      uint32_t e5[6] = {0, 0, 0, 0, 0, 0};
+      launch_err_detail(a, f, ferr_slot[f], c->err2.as<uint32_t>(), st);
+      H(hipMemcpyAsync(e5, c->err2.p, 24, hipMemcpyDeviceToHost, st));
       H(hipStreamSynchronize(st));
       if (!ok) return CASK_E_DEVICE;
-      err->kind = status;
+      err->kind = (int32_t)e5[2];
       err->file_id = files[f].file_id;
-      err->pos = pos;
-      err->row = r;
-      if (status == CASK_ROW_CHECKSUM) {
-        err->expected = eh[0];
-        err->found = eh[1];
-      } else {
-        err->expected = eh[0];
-        err->found = 0;
-      }
+      err->pos = (uint64_t)e5[3] | ((uint64_t)e5[4] << 32);
+      err->row = ferr_row[f];
+      err->expected = e5[0];
+      err->found = e5[2] == CASK_ROW_CHECKSUM ? e5[1] : 0;
       break;
     }
   }
@@ -341,11 +410,20 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
 
 extern "C" int cask_scan_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
                                 uint64_t* file_row_offset, cask_scan_error* err) {
-  if (!c) return CASK_E_INVALID_ARG;
+  if (!c || !rows) return CASK_E_INVALID_ARG;
   for (uint32_t i = 0; i < nfiles; ++i)
     if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  return scan_device_impl(c, files, nfiles, rows, file_row_offset, err);
+  return scan_device_impl(c, files, nfiles, rows, nullptr, file_row_offset, err);
+}
+
+extern "C" int cask_scan_device_segmented(cask_ctx* c, const cask_file_view* files, uint32_t nfiles,
+                                          cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err) {
+  if (!c || !seg) return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return scan_device_impl(c, files, nfiles, nullptr, seg, file_row_offset, err);
 }
 
 extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
@@ -382,7 +460,7 @@ extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t
   dr.vsz = (uint32_t*)(rb + 2 * align_up(rcap * 8, 256));
   dr.ksz = (uint16_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256));
   dr.status = (uint8_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256) + align_up(rcap * 2, 256));
-  int rc = scan_device_impl(c, dv.data(), nfiles, &dr, file_row_offset, err);
+  int rc = scan_device_impl(c, dv.data(), nfiles, &dr, nullptr, file_row_offset, err);
   rows->count = dr.count;
   if (rc != CASK_OK) return rc;
   if (dr.count > rows->capacity) return CASK_E_CAPACITY;
@@ -424,3 +502,21 @@ extern "C" int cask_encode_device(cask_ctx* c, uint64_t nrec, const uint64_t* of
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
   return CASK_OK;
 }
+
+#ifdef CASK_STAMPS
+// Diagnostic build only: per-phase cycle sums of the last k_scan_chunks launch.
+extern "C" int cask_debug_stamps(cask_ctx* c, uint64_t* out16) {
+  if (!c || !c->stamps.p) return CASK_E_INVALID_ARG;
+  if (hipMemcpy(out16, c->stamps.p, 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return CASK_E_DEVICE;
+  return CASK_OK;
+}
+// Diagnostic build only: per-chunk spec / exit / tin / count of the last (unrepaired) pass.
+extern "C" int cask_debug_chunks(cask_ctx* c, uint64_t* spec, uint64_t* exitv, uint64_t* tin, uint32_t* count, uint64_t n) {
+  if (!c || !c->dbg_spec || n > c->dbg_n) return CASK_E_INVALID_ARG;
+  hipMemcpy(spec, c->dbg_spec, n * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(exitv, c->dbg_exit, n * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(tin, c->dbg_tin, n * 8, hipMemcpyDeviceToHost);
+  hipMemcpy(count, c->dbg_count, n * 4, hipMemcpyDeviceToHost);
+  return CASK_OK;
+}
+#endif

@@ -121,9 +121,27 @@ class ScanContext:
             if raise_on_capacity:
                 raise CapacityError(int(r.count))
         else:
-            raise_status(rc, what="cask_scan_device")
+            raise_status(rc, what=f"cask_scan_device: {self.last_error()}")
         return ScanResult(int(r.count), rows["pos"], rows["seq"], rows["vsz"], rows["ksz"], rows["status"],
                           list(off), _err(e))
+
+    def scan_device_segmented(self, files):
+        """Segmented output (cask_scan_device_segmented): per-chunk slot rows owned by the context,
+        valid until the next call. Returns (Segments, file_row_offset, ScanFailure|None)."""
+        n = len(files)
+        views = (L.FileView * max(n, 1))()
+        for i, (fid, t) in enumerate(files):
+            assert t.is_cuda and t.dtype.itemsize == 1 and t.is_contiguous()
+            views[i].file_id = int(fid)
+            views[i].flags = L.VIEW_DEVICE
+            views[i].data = t.data_ptr() if t.numel() else None
+            views[i].len = t.numel()
+        seg = L.Segments()
+        off = (C.c_uint64 * (n + 1))()
+        e = L.ScanError()
+        rc = self.lib.cask_scan_device_segmented(self._h, views, n, C.byref(seg), off, C.byref(e))
+        raise_status(rc, what=f"cask_scan_device_segmented: {self.last_error()}")
+        return seg, list(off), _err(e)
 
     # -- host-resident ------------------------------------------------------------------------
     def scan_host(self, files) -> ScanResult:
@@ -150,16 +168,20 @@ class ScanContext:
         off = (C.c_uint64 * (n + 1))()
         e = L.ScanError()
         rc = self.lib.cask_scan_host(self._h, views, n, C.byref(r), off, C.byref(e))
-        raise_status(rc, what="cask_scan_host")
+        raise_status(rc, what=f"cask_scan_host: {self.last_error()}")
         c = int(r.count)
         return ScanResult(c, pos[:c], seq[:c], vsz[:c], ksz[:c], status[:c], list(off), _err(e))
 
     # -- instrumentation ----------------------------------------------------------------------
+    def last_error(self) -> str:
+        v = self.lib.cask_ctx_last_error(self._h)
+        return v.decode() if v else ""
+
     def last_timings(self) -> dict[str, float]:
-        t = (C.c_float * 5)()
+        t = (C.c_float * 6)()
         self.lib.cask_last_timings(self._h, t)
         return {"pipeline_ms": t[0], "chunk_scan_ms": t[1], "long_ms": t[2], "validate_ms": t[3],
-                "repair_ms": t[4]}
+                "repair_ms": t[4], "compact_ms": t[5]}
 
     def last_counters(self) -> dict[str, int]:
         c = (C.c_uint64 * 3)()

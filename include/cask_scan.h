@@ -57,6 +57,8 @@ void cask_ctx_destroy(cask_ctx* ctx);
 int cask_ctx_set_stream(cask_ctx* ctx, void* hip_stream);
 void* cask_ctx_stream(cask_ctx* ctx);
 int cask_ctx_device(const cask_ctx* ctx);
+/* Human-readable cause of the last CASK_E_DEVICE returned on this context ("" if none). */
+const char* cask_ctx_last_error(const cask_ctx* ctx);
 /* Chunk size in bytes used by the scan kernels (the unit of speculation and staging). */
 uint32_t cask_scan_chunk_bytes(void);
 
@@ -107,14 +109,35 @@ uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles);
 int cask_scan_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
                      cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);
 
+/* Segmented device output (no dense compaction): the scan's own per-chunk slot rows. Chunk c of
+ * the call holds count[c] rows at slots[(c * slot_cap + r) * 4 .. +4] (r < count[c]) as four u32:
+ * seq low, seq high, value_size raw, ksz | (pos - chunk_start) << 16 | checksum_failed << 31,
+ * where chunk_start = (c - first chunk of its file) * chunk_bytes; a row whose record runs past
+ * the file end is the UnexpectedEof row. Row r of chunk c is row file_row_offset[f] + base[c] + r
+ * of the dense order. All pointers are device memory owned by the context, valid until its next
+ * call. Files map to consecutive chunk ranges of ceil(len / chunk_bytes) chunks each. */
+typedef struct cask_segments {
+  uint64_t nchunks;
+  uint32_t chunk_bytes;
+  uint32_t slot_cap;
+  const uint32_t* slots;
+  const uint32_t* count;
+  const uint64_t* base;
+  uint64_t total_rows;
+} cask_segments;
+
+int cask_scan_device_segmented(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
+                               cask_segments* out, uint64_t* file_row_offset,
+                               cask_scan_error* err);
+
 /* Same, for host-resident files and host row arrays: stages H2D, scans, copies rows D2H. */
 int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
                    cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);
 
 /* Timing of the last cask_scan_* call on the context's stream (HIP events, milliseconds):
  * [0] whole device pipeline, [1] chunk-scan kernel, [2] long-record kernel,
- * [3] validate kernel, [4] repair (0 when speculation held). */
-int cask_last_timings(const cask_ctx* ctx, float* ms5);
+ * [3] validate + summary kernels, [4] repair (0 when speculation held), [5] compaction. */
+int cask_last_timings(const cask_ctx* ctx, float* ms6);
 /* Counters of the last call: [0] chunks, [1] long records, [2] invalid chunks repaired. */
 int cask_last_counters(const cask_ctx* ctx, uint64_t* c3);
 

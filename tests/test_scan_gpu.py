@@ -1,0 +1,320 @@
+"""Parity of the HIP scan (through the C ABI) with the CPU oracle. Needs an MI355X.
+
+Bit-exact comparisons on the golden fixtures and on seeded inputs the oracle finishes in seconds
+(uniform, variable, long records, many/empty files, adversarial values, corruption, truncation,
+all-zero data); size-independent properties at BASELINE configs[1] size (8 x 1,073,741,820 B).
+"""
+import json
+import os
+import random
+import shutil
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, golden_cases
+
+import cask_ref as R
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _expected(case):
+    with open(os.path.join(GOLDEN, case, "expected.json")) as f:
+        return json.load(f)
+
+
+def _file_bytes(case, fid):
+    with open(R.data_file_path(os.path.join(GOLDEN, case), fid), "rb") as f:
+        return f.read()
+
+
+def rows_list(res, sl):
+    return [[int(res.pos[i]), int(res.seq[i]) & 0xFFFFFFFFFFFFFFFF, int(res.ksz[i]) & 0xFFFF, int(res.vsz[i]) & 0xFFFFFFFF, int(res.status[i])]
+            for i in range(sl.start, sl.stop)]
+
+
+def oracle_rows(buf):
+    rows = O.scan(buf)
+    return [[int(r["pos"]), int(r["seq"]), int(r["ksz"]), int(r["vsz_raw"]), int(r["status"])] for r in rows], rows
+
+
+def check_against_oracle(ctx, bufs, device=False):
+    """Scan `bufs` (list of bytes) in one call; compare every row and the first error."""
+    files = list(enumerate(bufs, start=1))
+    if device:
+        import torch
+        tens = [(fid, torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()) for fid, b in files]
+        res = ctx.scan_device(tens)
+        res.pos, res.seq, res.vsz, res.ksz, res.status = [t[:res.count].cpu().numpy() for t in
+                                                          (res.pos, res.seq, res.vsz, res.ksz, res.status)]
+    else:
+        res = ctx.scan_host(files)
+    first_err = None
+    total = 0
+    for i, (fid, b) in enumerate(files):
+        want, orows = oracle_rows(b)
+        got = rows_list(res, res.file_rows(i))
+        assert len(got) == len(want), (fid, len(got), len(want))
+        if got != want:
+            bad = next(j for j in range(len(got)) if got[j] != want[j])
+            raise AssertionError(f"file {fid} row {bad}: got {got[bad]} want {want[bad]}")
+        total += len(want)
+        if first_err is None:
+            for r in orows:
+                if int(r["status"]) != 0:
+                    first_err = (int(r["status"]), fid, int(r["pos"]), int(r["expected"]),
+                                 int(r["found"]) if int(r["status"]) == 1 else 0)
+                    break
+    assert res.count == total
+    if first_err is None:
+        assert res.error is None
+    else:
+        e = res.error
+        assert e is not None
+        assert (e.kind, e.file_id, e.pos, e.expected, e.found) == first_err
+    return res
+
+
+# ------------------------------------------------------------------------------------- golden
+@pytest.mark.parametrize("case", golden_cases())
+def test_golden_rows_host(gpu_ctx, case):
+    exp = _expected(case)
+    bufs = [_file_bytes(case, fe["file_id"]) for fe in exp["files"]]
+    files = [(fe["file_id"], b) for fe, b in zip(exp["files"], bufs)]
+    res = gpu_ctx.scan_host(files)
+    for i, fe in enumerate(exp["files"]):
+        assert rows_list(res, res.file_rows(i)) == [r[:5] for r in fe["rows"]], fe["file_id"]
+    rep = exp["replay"]["error"]
+    if rep is not None and not case.startswith("hints"):
+        assert res.error is not None
+        assert res.error.file_id == rep["file_id"] and res.error.pos == rep["pos"]
+        if rep["kind"] == "checksum":
+            assert (res.error.kind, res.error.expected, res.error.found) == (1, rep["expected"], rep["found"])
+        else:
+            assert res.error.kind == 2
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_golden_rows_device(gpu_ctx, case):
+    exp = _expected(case)
+    bufs = [_file_bytes(case, fe["file_id"]) for fe in exp["files"]]
+    check_against_oracle(gpu_ctx, bufs, device=True)
+
+
+@pytest.mark.parametrize("case", golden_cases())
+def test_golden_engine_open(native, case, tmp_path):
+    """Cask::open on the fixture directory: keydir, stats, sequence or error, hint files."""
+    from cask_amd import CaskOptions, errors
+    exp = _expected(case)
+    rep = exp["replay"]
+    d = tmp_path / case
+    shutil.copytree(os.path.join(GOLDEN, case), d)
+    os.remove(d / "expected.json")
+    if rep["error"] is None:
+        with CaskOptions().open(str(d)) as db:
+            got = sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence] for k, e in db.index().items())
+            assert got == rep["keydir"]
+            assert sorted([f, *s] for f, s in db.stats().items()) == rep["stats"]
+            assert db.current_sequence == rep["current_sequence"]
+    else:
+        want = errors.InvalidChecksum if rep["error"]["kind"] == "checksum" else errors.UnexpectedEof
+        with pytest.raises(want) as ei:
+            CaskOptions().open(str(d))
+        assert ei.value.file_id == rep["error"]["file_id"] and ei.value.pos == rep["error"]["pos"]
+        if rep["error"]["kind"] == "checksum":
+            assert (ei.value.expected, ei.value.found) == (rep["error"]["expected"], rep["error"]["found"])
+    for fid, hx in rep["hint_files_after"].items():
+        with open(R.hint_file_path(str(d), int(fid)), "rb") as f:
+            assert f.read().hex() == hx, fid
+
+
+# ------------------------------------------------------------------------------ seeded inputs
+def make_records(rng, n, ksz_fn, vsz_fn, seq0=1, tomb_p=0.0):
+    out = []
+    for i in range(n):
+        k = rng.randbytes(ksz_fn(rng))
+        if rng.random() < tomb_p:
+            out.append(R.entry_deleted(seq0 + i, k).write_bytes())
+        else:
+            out.append(R.entry_new(seq0 + i, k, rng.randbytes(vsz_fn(rng))).write_bytes())
+    return b"".join(out)
+
+
+def test_uniform_290(gpu_ctx):
+    rng = random.Random(1)
+    buf = make_records(rng, 20000, lambda r: 16, lambda r: 256)
+    res = check_against_oracle(gpu_ctx, [buf])
+    assert gpu_ctx.last_counters()["repaired_chunks"] == 0
+
+
+def test_uniform_82_device(gpu_ctx):
+    rng = random.Random(2)
+    check_against_oracle(gpu_ctx, [make_records(rng, 60000, lambda r: 16, lambda r: 48)], device=True)
+
+
+def test_variable_sizes_with_long_records(gpu_ctx):
+    rng = random.Random(3)
+
+    def vsz(r):
+        x = r.random()
+        if x < 0.5:
+            return r.randrange(0, 64)
+        if x < 0.9:
+            return r.randrange(64, 4096)
+        return r.randrange(4096, 70000)
+    buf = make_records(rng, 3000, lambda r: r.randrange(0, 40), vsz, tomb_p=0.1)
+    check_against_oracle(gpu_ctx, [buf])
+    assert gpu_ctx.last_counters()["long_records"] > 0
+
+
+def test_many_files_empty_and_tiny(gpu_ctx):
+    rng = random.Random(4)
+    bufs = []
+    for i in range(40):
+        kind = i % 5
+        if kind == 0:
+            bufs.append(b"")
+        elif kind == 1:
+            bufs.append(rng.randbytes(rng.randrange(1, 18)))  # shorter than a header: EOF row
+        else:
+            bufs.append(make_records(rng, rng.randrange(1, 400), lambda r: r.randrange(1, 20),
+                                     lambda r: r.randrange(0, 600)))
+    check_against_oracle(gpu_ctx, bufs)
+
+
+def test_adversarial_embedded_records_repair(gpu_ctx):
+    """Values made of valid serialized records defeat the speculative boundary search; the
+    validate pass must catch it and the exact walk must repair it."""
+    rng = random.Random(5)
+    inner = [R.entry_new(10_000 + i, rng.randbytes(8), rng.randbytes(rng.randrange(0, 40))).write_bytes()
+             for i in range(64)]
+    out = []
+    for i in range(3000):
+        v = b"".join(rng.choice(inner) for _ in range(rng.randrange(1, 30)))
+        out.append(R.entry_new(i + 1, b"outer%d" % i, v).write_bytes())
+    check_against_oracle(gpu_ctx, [b"".join(out)])
+    assert gpu_ctx.last_counters()["repaired_chunks"] > 0
+
+
+def test_all_zero_file(gpu_ctx):
+    """Zero bytes parse as 18-byte records that all fail their checksum."""
+    res = check_against_oracle(gpu_ctx, [bytes(300_000)])
+    assert res.error.kind == 1 and res.error.pos == 0
+
+
+@pytest.mark.parametrize("seed", [6, 7, 8])
+def test_random_corruption(gpu_ctx, seed):
+    rng = random.Random(seed)
+    base = bytearray(make_records(rng, 30000, lambda r: r.randrange(4, 24), lambda r: r.randrange(0, 300)))
+    for _ in range(5):
+        p = rng.randrange(len(base))
+        base[p] ^= 1 << rng.randrange(8)
+    check_against_oracle(gpu_ctx, [bytes(base)])
+
+
+@pytest.mark.parametrize("seed", [9, 10])
+def test_truncation(gpu_ctx, seed):
+    rng = random.Random(seed)
+    base = make_records(rng, 5000, lambda r: 16, lambda r: r.randrange(0, 500))
+    cut = rng.randrange(len(base) // 2, len(base))
+    check_against_oracle(gpu_ctx, [base[:cut], base])
+
+
+def test_engine_scan_path_large(native, tmp_path):
+    """Cask::open with no hint files over a multi-file DB: GPU scan + hint recreation + fold vs
+    the Python restatement of the replay."""
+    from cask_amd import CaskOptions
+    rng = random.Random(12)
+    keys = [rng.randbytes(rng.randrange(1, 30)) for _ in range(3000)]
+    ents = []
+    for i in range(40000):
+        k = rng.choice(keys)
+        if rng.random() < 0.1:
+            ents.append(R.entry_deleted(i + 1, k))
+        else:
+            ents.append(R.entry_new(i + 1, k, rng.randbytes(rng.randrange(0, 200))))
+    path = str(tmp_path / "db")
+    R.write_log(path, ents, max_file_size=1 << 20, write_hints=False)
+    ref_dir = str(tmp_path / "ref")
+    shutil.copytree(path, ref_dir)
+    py = R.replay(ref_dir)
+    with CaskOptions().open(path) as db:
+        assert db.current_sequence == py.current_sequence
+        assert db.stats() == {f: tuple(s) for f, s in py.index.stats.map.items()}
+        got = db.index()
+        assert len(got) == len(py.index.map)
+        for k, v in py.index.map.items():
+            e = got[k]
+            assert (e.file_id, e.entry_pos, e.entry_size, e.sequence) == (v.file_id, v.entry_pos, v.entry_size,
+                                                                           v.sequence)
+    for fid in R.find_data_files(path):
+        with open(R.hint_file_path(path, fid), "rb") as a, open(R.hint_file_path(ref_dir, fid), "rb") as b:
+            assert a.read() == b.read()
+
+
+# ------------------------------------------------------------------------------------ encoder
+def _splitmix64(z):
+    z = (z + 0x9E3779B97F4A7C15) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def test_encoder_matches_oracle(gpu_ctx):
+    import torch
+    rng = np.random.default_rng(13)
+    n = 5000
+    ksz = rng.integers(0, 40, n).astype(np.int16)
+    vsz = rng.integers(0, 2000, n).astype(np.int64)
+    vsz[rng.random(n) < 0.1] = 0xFFFFFFFF
+    veff = np.where(vsz == 0xFFFFFFFF, 0, vsz)
+    rl = 18 + ksz.astype(np.int64) + veff
+    off = np.cumsum(rl) - rl
+    seq = np.arange(n, dtype=np.int64) * 3 + 7
+    kid = rng.integers(0, 1 << 40, n).astype(np.int64)
+    dev = torch.device("cuda")
+    out = torch.empty(int(rl.sum()), dtype=torch.uint8, device=dev)
+    t = lambda a, dt: torch.from_numpy(a.astype(dt)).to(dev)
+    gpu_ctx.encode_synthetic(t(off, np.int64), t(seq, np.int64), t(ksz, np.int16),
+                             t(vsz.astype(np.uint32).view(np.int32), np.int32), t(kid, np.int64), 0xABCDEF, out)
+    buf = out.cpu().numpy().tobytes()
+    rows = O.scan(buf)
+    assert len(rows) == n and (rows["status"] == 0).all()
+    assert (rows["pos"] == off.astype(np.uint64)).all() and (rows["seq"] == seq.astype(np.uint64)).all()
+    assert (rows["ksz"] == ksz.astype(np.uint16)).all()
+    assert (rows["vsz_raw"] == vsz.astype(np.uint32)).all()
+    # key bytes follow the documented generator: word i of key id k = splitmix64((k << 16) | i)
+    for r in range(0, n, 97):
+        k = int(ksz[r])
+        want = b"".join(_splitmix64(((int(kid[r]) << 16) | i) & 0xFFFFFFFFFFFFFFFF).to_bytes(8, "little")
+                        for i in range((k + 7) // 8))[:k]
+        assert buf[int(off[r]) + 18:int(off[r]) + 18 + k] == want
+
+
+# ------------------------------------------------------------------------- full-size properties
+def test_cfg2_full_size_properties(gpu_ctx):
+    """BASELINE configs[1] at full size: 8 x 3,702,558 records of 290 B. Every row verifies, rows
+    are exactly the encoded layout, and a 64 MiB slice of file 1 matches the oracle row for row."""
+    import torch
+    from cask_amd.workloads import CFG2_RECORDS_PER_FILE, cfg2_files
+    files = cfg2_files(gpu_ctx)
+    res = gpu_ctx.scan_device([(f.file_id, f.data) for f in files])
+    n = CFG2_RECORDS_PER_FILE
+    assert res.count == 8 * n and res.error is None
+    assert int((res.status[:res.count] != 0).sum().item()) == 0
+    idx = torch.arange(n, device=res.pos.device, dtype=torch.int64)
+    for i, f in enumerate(files):
+        sl = res.file_rows(i)
+        assert sl.stop - sl.start == n
+        assert torch.equal(res.pos[sl], idx * 290)
+        assert torch.equal(res.seq[sl], idx + f.seq0)
+    assert int((res.ksz[:res.count] != 16).sum().item()) == 0
+    assert int((res.vsz[:res.count] != 256).sum().item()) == 0
+    assert gpu_ctx.last_counters()["repaired_chunks"] == 0
+    sl_bytes = (64 << 20) // 290 * 290
+    host = files[0].data[:sl_bytes].cpu().numpy()
+    want = O.scan(host)
+    assert len(want) == sl_bytes // 290 and (want["status"] == 0).all()
+    assert np.array_equal(want["seq"], res.seq[:len(want)].cpu().numpy().astype(np.uint64))

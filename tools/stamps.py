@@ -1,0 +1,47 @@
+"""Phase breakdown of k_scan_chunks from the diagnostic build (make -C cask_amd stamps).
+
+CASK_LIB_PATH=cask_amd/build/stamps/libcask_scan.so python tools/stamps.py [--files N]
+Prints the average s_memtime cycles per workgroup spent in each phase (shares, not wall time:
+the stamps serialise what the real kernel overlaps).
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("CASK_LIB_PATH", os.path.join(ROOT, "cask_amd", "build", "stamps", "libcask_scan.so"))
+
+PHASES = ["search", "walk", "hash+slots"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--files", type=int, default=2)
+    ap.add_argument("--iters", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    import cask_amd
+    from cask_amd.workloads import cfg2_files
+    L = cask_amd.lib()
+    L.cask_debug_stamps.restype = C.c_int
+    L.cask_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    ctx = cask_amd.ScanContext(0)
+    files = cfg2_files(ctx, nfiles=args.files)
+    views = [(f.file_id, f.data) for f in files]
+    rows = ctx.alloc_rows(sum(f.nrec for f in files))
+    for _ in range(args.iters):
+        res = ctx.scan_device(views, rows)
+    st = (C.c_uint64 * 16)()
+    L.cask_debug_stamps(ctx._h, st)
+    chunks = ctx.last_counters()["chunks"]
+    t = ctx.last_timings()
+    print(f"chunks={chunks} rows={res.count} timings={t}")
+    tot = sum(st[i] for i in range(3))
+    for i, p in enumerate(PHASES):
+        print(f"{p:14s} {st[i] / chunks:12.0f} cyc/WG  {100.0 * st[i] / max(tot, 1):5.1f}%")
+
+
+if __name__ == "__main__":
+    main()
