@@ -12,15 +12,21 @@ using namespace cask_xxh;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Diagnostic build (-DCASK_STAMPS): lane 0 of each workgroup adds the s_memtime cycles of every
-// phase of k_scan_chunks into a.stamps[]; never compiled into the shipped library.
+// Per-thread diagnostic state of k_scan_chunks (unused, and compiled away, in the shipped library).
+struct Diag {
+  uint32_t nb;      // -DCASK_BAR_CHECK: barriers passed
+  uint64_t st[5];   // -DCASK_STAMPS: s_memtime cycles per phase, summed over the workgroup's chunks
+};
+
+// Diagnostic build (-DCASK_STAMPS): every thread sums the s_memtime cycles of each phase of
+// k_scan_chunks in registers; thread 0 adds its sums into a.stamps[] once, at the end.
 #ifdef CASK_STAMPS
 #define STAMP_INIT uint64_t st_prev_ = __builtin_amdgcn_s_memtime();
-#define STAMP(i)                                                       \
-  if (a.stamps && threadIdx.x == 0) {                                  \
-    uint64_t st_now_ = __builtin_amdgcn_s_memtime();                   \
-    atomicAdd(&a.stamps[i], (unsigned long long)(st_now_ - st_prev_)); \
-    st_prev_ = st_now_;                                                \
+#define STAMP(i)                                             \
+  {                                                          \
+    const uint64_t st_now_ = __builtin_amdgcn_s_memtime();   \
+    dg.st[i] += st_now_ - st_prev_;                          \
+    st_prev_ = st_now_;                                      \
   }
 #else
 #define STAMP_INIT

@@ -40,7 +40,7 @@ constexpr uint32_t kShortMax = 1024;
 #define BAR()        \
   {                  \
     __syncthreads(); \
-    ++nb_;           \
+    ++dg.nb;         \
   }
 #else
 #define BAR() __syncthreads()
@@ -135,7 +135,7 @@ __device__ __forceinline__ void stage_store(ScanLdsT<G>& L, const u32x4 (&v)[G::
 
 template <class G, bool EXACT>
 __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a, uint64_t t, const ChunkPos& c,
-                                              uint64_t s_exact, uint32_t& nb_) {
+                                              uint64_t s_exact, Diag& dg) {
   constexpr uint32_t NT = G::kNT;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t* W = L.win;
@@ -226,7 +226,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     }
     if (lane == 0) {
 #ifdef CASK_BAR_CHECK
-      L.nb0 = nb_;
+      L.nb0 = dg.nb;
 #endif
       L.n = n;
       {
@@ -245,9 +245,9 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   STAMP(1)
   const uint32_t n = L.n;
 #ifdef CASK_BAR_CHECK
-  if (L.nb0 + 1 != nb_ && a.stamps && atomicCAS(&a.stamps[8], 0ull, 7ull) == 0ull) {
+  if (L.nb0 + 1 != dg.nb && a.stamps && atomicCAS(&a.stamps[8], 0ull, 7ull) == 0ull) {
     a.stamps[9] = L.nb0;
-    a.stamps[10] = nb_;
+    a.stamps[10] = dg.nb;
     a.stamps[11] = n;
     a.stamps[12] = t;
     a.stamps[13] = blockIdx.x | ((uint64_t)threadIdx.x << 32);
@@ -317,13 +317,20 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
   const uint64_t tend = (x + 1) * per < a.total_chunks ? (x + 1) * per : a.total_chunks;
   if (t >= tend) return;
   if (threadIdx.x == 0) L.found = 0xFFFFFFFFu;
-  uint32_t nb_ = 0;
+  Diag dg{};
   ChunkPos cur = locate<G>(files, a.nfiles, t);
   u32x4 v[G::kNL];
   stage_issue<G>(v, cur, a.stamps, t);
   for (;;) {
+#ifdef CASK_STAMPS
+    const uint64_t st_top_ = __builtin_amdgcn_s_memtime();
+#endif
     stage_store<G>(L, v, cur);
     BAR();
+#ifdef CASK_STAMPS
+    dg.st[3] += __builtin_amdgcn_s_memtime() - st_top_;  // phase 3: window wait + LDS store
+    dg.st[4] += 1;
+#endif
 #ifdef CASK_VERIFY_LDS
     if (a.stamps) {  // diagnostic: the staged window must equal HBM
       const volatile gu32x4* src = (const volatile gu32x4*)cur.a0;
@@ -348,13 +355,17 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
     const uint64_t tn = t + nx;
     const bool more = tn < tend;
     if (more) stage_issue<G>(v, locate<G>(files, a.nfiles, tn), a.stamps, tn);  // prefetch the next window
-    process_chunk<G, EXACT>(L, a, t, cur, s_exact, nb_);
+    process_chunk<G, EXACT>(L, a, t, cur, s_exact, dg);
     if (threadIdx.x == 0) L.found = 0xFFFFFFFFu;
     BAR();
     if (!more) break;
     t = tn;
     cur = locate<G>(files, a.nfiles, t);
   }
+#ifdef CASK_STAMPS
+  if (a.stamps && threadIdx.x == 0)
+    for (int i = 0; i < 5; ++i) atomicAdd(&a.stamps[i], (unsigned long long)dg.st[i]);
+#endif
 }
 
 using GeoA = Geo<32768, 4096, 256, 4>;

@@ -70,6 +70,12 @@ class ScanContext:
         except Exception:
             pass
 
+    def _inputs_ready(self):
+        """The context runs on its own non-blocking HIP stream, which does not wait for torch's
+        stream: tensors torch is still producing must be complete before the library reads them."""
+        import torch
+        torch.cuda.current_stream(self.device).synchronize()
+
     def set_stream(self, stream_ptr: int | None):
         self.lib.cask_ctx_set_stream(self._h, C.c_void_p(stream_ptr or 0))
 
@@ -116,6 +122,7 @@ class ScanContext:
         r.vsz, r.ksz, r.status = rows["vsz"].data_ptr(), rows["ksz"].data_ptr(), rows["status"].data_ptr()
         off = (C.c_uint64 * (n + 1))()
         e = L.ScanError()
+        self._inputs_ready()
         rc = self.lib.cask_scan_device(self._h, views, n, C.byref(r), off, C.byref(e))
         if rc == L.E_CAPACITY:
             if raise_on_capacity:
@@ -139,6 +146,7 @@ class ScanContext:
         seg = L.Segments()
         off = (C.c_uint64 * (n + 1))()
         e = L.ScanError()
+        self._inputs_ready()
         rc = self.lib.cask_scan_device_segmented(self._h, views, n, C.byref(seg), off, C.byref(e))
         raise_status(rc, what=f"cask_scan_device_segmented: {self.last_error()}")
         return seg, list(off), _err(e)
@@ -193,6 +201,7 @@ class ScanContext:
         """Batched Entry::write_bytes (data.rs:90-121) of generated keys/values (DESIGN.md
         §Synthetic data). All tensors on this device; out is a uint8 tensor."""
         n = off.numel()
+        self._inputs_ready()
         rc = self.lib.cask_encode_synthetic_device(self._h, n, off.data_ptr(), seq.data_ptr(), ksz.data_ptr(),
                                                    vsz_raw.data_ptr(), key_id.data_ptr(),
                                                    int(value_seed) & 0xFFFFFFFFFFFFFFFF, out.data_ptr())
@@ -201,6 +210,7 @@ class ScanContext:
     def encode(self, off, seq, ksz, vsz_raw, keys, key_off, vals, val_off, out):
         """Batched Entry::write_bytes of caller keys/values (device tensors)."""
         n = off.numel()
+        self._inputs_ready()
         rc = self.lib.cask_encode_device(self._h, n, off.data_ptr(), seq.data_ptr(), ksz.data_ptr(),
                                          vsz_raw.data_ptr(), keys.data_ptr(), key_off.data_ptr(),
                                          vals.data_ptr(), val_off.data_ptr(), out.data_ptr())

@@ -53,7 +53,10 @@ typedef struct cask_ctx cask_ctx;
  * independent and may be used from different threads; one context is not re-entrant. */
 cask_ctx* cask_ctx_create(int device, int* status);
 void cask_ctx_destroy(cask_ctx* ctx);
-/* Use a caller stream (hipStream_t passed as void*) instead of the context's own; NULL resets. */
+/* Use a caller stream (hipStream_t passed as void*) instead of the context's own; NULL resets.
+ * The context's own stream is non-blocking: it does not wait for work queued on other streams,
+ * so device inputs still being produced elsewhere must be complete (or produced on the stream
+ * set here) before a call reads them. */
 int cask_ctx_set_stream(cask_ctx* ctx, void* hip_stream);
 void* cask_ctx_stream(cask_ctx* ctx);
 int cask_ctx_device(const cask_ctx* ctx);

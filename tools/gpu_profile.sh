@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU call: full bench line, rocprofv3 kernel-trace stats, and two PMC passes (FETCH_SIZE,
+# WRITE_SIZE) for the HBM traffic of k_scan_chunks. Outputs under gpurun_out/; tools/pmc_summary.py
+# turns them into profiles/.
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; mkdir -p gpurun_out
+TAG=${TAG:-r01}
+step() {
+  local name=$1 to=$2; shift 2
+  echo "=== $name"; date
+  timeout -k 10 "$to" "$@" > "$R/gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "rc=$rc"; tail -${TAILN:-3} "$R/gpurun_out/$name.log"
+  if [ $rc -ne 0 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+}
+if [ -z "$SKIP_BENCH" ]; then
+  TAILN=1 step bench_full 600 python bench.py
+fi
+export TMPDIR=/tmp
+B="$R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e"
+rm -rf "$R/gpurun_out/prof_$TAG"
+step prof_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG/kt" -o kt --output-format csv -- python3 $B
+step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_$TAG/fetch" -o fetch --output-format csv -- python3 $B
+step prof_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/prof_$TAG/write" -o write --output-format csv -- python3 $B
+find "$R/gpurun_out/prof_$TAG" -name "*.csv" | head -20

@@ -1,0 +1,61 @@
+"""Turn a tools/gpu_profile.sh run (gpurun_out/prof_<tag>/) into the committed evidence under
+profiles/: the rocprofv3 kernel stats, a per-kernel HBM-traffic table from the FETCH_SIZE and
+WRITE_SIZE passes, and profiles/pmc_traffic.json (read by bench.py for roofline.traffic).
+
+FETCH_SIZE / WRITE_SIZE are in KiB-scaled units of 1024 B per rocprofv3. Per
+/opt/skills/guides/MI355X_MICROARCH.md §HBM, gfx950 FETCH_SIZE reports half of the bytes of a
+wide coalesced streaming read, so it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("cask_dev::", "")
+
+
+def per_kernel(path, counter):
+    vals = defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] == counter and "cask_dev::" in r["Kernel_Name"]:
+            vals[short(r["Kernel_Name"])].append(float(r["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()}
+
+
+def main():
+    tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
+    src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    out = os.path.join(ROOT, "profiles")
+    shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
+    fetch, nf = per_kernel(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")
+    write, nw = per_kernel(os.path.join(src, "write", "write_counter_collection.csv"), "WRITE_SIZE")
+    stats = {short(r["Name"]): r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv")))}
+    lines = [f"# HBM traffic per launch ({tag}): FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, bytes",
+             "kernel,launches,avg_ns,fetch_bytes_corrected,write_bytes,hbm_bytes"]
+    table = {}
+    for k in sorted(set(fetch) | set(write)):
+        f2 = 2.0 * fetch.get(k, 0.0)
+        w = write.get(k, 0.0)
+        avg = float(stats[k]["AverageNs"]) if k in stats else float("nan")
+        table[k] = {"fetch_bytes": f2, "write_bytes": w, "hbm_bytes": f2 + w, "avg_ns": avg}
+        lines.append(f"{k},{nf.get(k, 0)},{avg:.0f},{f2:.0f},{w:.0f},{f2 + w:.0f}")
+    with open(os.path.join(out, f"{tag}_pmc_traffic.csv"), "w") as f:
+        f.write("\n".join(lines) + "\n")
+    scan = next(k for k in table if k.startswith("k_scan_chunks"))
+    with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
+        json.dump({"kernel": scan, "hbm_bytes_per_launch": table[scan]["hbm_bytes"],
+                   "fetch_bytes_per_launch": table[scan]["fetch_bytes"],
+                   "write_bytes_per_launch": table[scan]["write_bytes"],
+                   "source": f"profiles/{tag}_pmc_traffic.csv (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                             f"separate passes, bench.py configs[1])"}, f, indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
