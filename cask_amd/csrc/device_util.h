@@ -14,8 +14,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Per-thread diagnostic state of k_scan_chunks (unused, and compiled away, in the shipped library).
 struct Diag {
-  uint32_t nb;      // -DCASK_BAR_CHECK: barriers passed
-  uint64_t st[5];   // -DCASK_STAMPS: s_memtime cycles per phase, summed over the workgroup's chunks
+  uint64_t st[10];  // -DCASK_STAMPS: s_memtime cycles per phase, summed over the workgroup's chunks
 };
 
 // Diagnostic build (-DCASK_STAMPS): every thread sums the s_memtime cycles of each phase of
@@ -44,20 +43,30 @@ struct Diag {
 #define DCHECK(cond, fmt, ...)
 #endif
 
-// The window is staged 16-B aligned; records start at arbitrary byte offsets, so every unaligned
-// 32-bit word is assembled from two aligned dword reads with v_alignbyte_b32 (a funnel shift).
-__device__ __forceinline__ uint32_t funnel(uint32_t hi, uint32_t lo, uint32_t sh) {
-  return __builtin_amdgcn_alignbyte(hi, lo, sh);
+// The window is staged 16-B aligned; records start at arbitrary byte offsets. gfx950 serves
+// unaligned LDS reads (unaligned-ds-access): a memcpy from a byte address compiles to one
+// ds_read_b32/b64/b128 at that address, so no funnel shifts are needed to assemble words.
+__device__ __forceinline__ uint32_t lds_u32(const uint32_t* w, uint32_t x) {
+  uint32_t v;
+  __builtin_memcpy(&v, (const uint8_t*)w + x, 4);
+  return v;
+}
+__device__ __forceinline__ uint64_t lds_u64(const uint32_t* w, uint32_t x) {
+  uint64_t v;
+  __builtin_memcpy(&v, (const uint8_t*)w + x, 8);
+  return v;
+}
+__device__ __forceinline__ u32x4 lds_u128(const uint32_t* w, uint32_t x) {
+  u32x4 v;
+  __builtin_memcpy(&v, (const uint8_t*)w + x, 16);
+  return v;
 }
 
 // Record length at LDS byte index x: 18 + ksz + vsz_eff (data.rs:63-65; tombstone vsz = !0).
 __device__ __forceinline__ uint64_t lds_reclen(const uint32_t* w, uint32_t x) {
-  const uint32_t q = (x + 12) >> 2, sh = (x + 12) & 3;
-  const uint32_t d0 = w[q], d1 = w[q + 1], d2 = w[q + 2];
-  const uint32_t b3 = funnel(d1, d0, sh);  // bytes x+12..x+15: ksz | vsz.lo16
-  const uint32_t b4 = funnel(d2, d1, sh);  // bytes x+16..x+19: vsz.hi16 | ...
-  const uint32_t ksz = b3 & 0xFFFFu;
-  const uint32_t vsz = (b3 >> 16) | (b4 << 16);
+  const uint64_t b = lds_u64(w, x + 12);  // ksz u16 | vsz u32 | 2 bytes of what follows
+  const uint32_t ksz = (uint32_t)b & 0xFFFFu;
+  const uint32_t vsz = (uint32_t)(b >> 16);
   return 18ull + ksz + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
 }
 
@@ -70,32 +79,49 @@ struct Hdr {
 };
 
 __device__ __forceinline__ Hdr lds_hdr(const uint32_t* w, uint32_t x) {
-  const uint32_t q = x >> 2, sh = x & 3;
-  const uint32_t d0 = w[q], d1 = w[q + 1], d2 = w[q + 2], d3 = w[q + 3], d4 = w[q + 4], d5 = w[q + 5];
+  const u32x4 d = lds_u128(w, x);          // bytes x .. x+15
+  const uint32_t e = lds_u32(w, x + 14);   // bytes x+14 .. x+17: vsz
   Hdr h;
-  h.stored = funnel(d1, d0, sh);
-  const uint32_t s0 = funnel(d2, d1, sh), s1 = funnel(d3, d2, sh);
-  h.seq = (uint64_t)s0 | ((uint64_t)s1 << 32);
-  const uint32_t b3 = funnel(d4, d3, sh), b4 = funnel(d5, d4, sh);
-  h.ksz = b3 & 0xFFFFu;
-  h.vsz = (b3 >> 16) | (b4 << 16);
+  h.stored = d.x;
+  h.seq = (uint64_t)d.y | ((uint64_t)d.z << 32);
+  h.ksz = d.w & 0xFFFFu;
+  h.vsz = e;
   return h;
 }
 
-// XXH32 (seed 0) of LDS bytes [xs, xs + len): aligned dword reads + funnel, 16-B stripes.
+// XXH32 (seed 0) of LDS bytes [xs, xs + len), 16-B stripes read with unaligned ds_read_b128.
+// Two stripes are mixed per step while the next two are in flight: under load an LDS read takes
+// longer than one stripe's multiplies.
+template <bool FAKE = false>  // FAKE (diagnostic): stripes from registers, not LDS; wrong hash
 __device__ __forceinline__ uint32_t lds_xxh32(const uint32_t* w, uint32_t xs, uint32_t len) {
-  const uint32_t sh = xs & 3;
-  uint32_t wi = xs >> 2;
-  uint32_t prev = w[wi];
   uint32_t h;
   const uint32_t nstr = len >> 4;
+  uint32_t x = xs;
   if (nstr) {
     Acc a = acc_init(0);
-    for (uint32_t s = 0; s < nstr; ++s) {
-      const uint32_t d1 = w[wi + 1], d2 = w[wi + 2], d3 = w[wi + 3], d4 = w[wi + 4];
-      acc_stripe(a, funnel(d1, prev, sh), funnel(d2, d1, sh), funnel(d3, d2, sh), funnel(d4, d3, sh));
-      prev = d4;
-      wi += 4;
+    auto ld = [&](uint32_t y) -> u32x4 {
+      if (!FAKE) return lds_u128(w, y);
+      u32x4 v;
+      v.x = y;
+      v.y = y ^ 0x5bd1e995u;
+      v.z = y * 3u;
+      v.w = y + 0x27d4eb2fu;
+      return v;
+    };
+    u32x4 d0 = ld(x), d1 = ld(x + 16);  // reads past the record stay in LDS
+    uint32_t s = 0;
+    for (; s + 2 <= nstr; s += 2) {
+      const u32x4 e0 = ld(x + 32), e1 = ld(x + 48);  // next pair in flight
+      __builtin_amdgcn_sched_barrier(0);  // keep them issued ahead of this pair's multiplies
+      acc_stripe(a, d0.x, d0.y, d0.z, d0.w);
+      acc_stripe(a, d1.x, d1.y, d1.z, d1.w);
+      d0 = e0;
+      d1 = e1;
+      x += 32;
+    }
+    if (s < nstr) {
+      acc_stripe(a, d0.x, d0.y, d0.z, d0.w);
+      x += 16;
     }
     h = acc_merge(a);
   } else {
@@ -104,17 +130,14 @@ __device__ __forceinline__ uint32_t lds_xxh32(const uint32_t* w, uint32_t xs, ui
   h += len;
   uint32_t rem = len & 15;
   while (rem >= 4) {
-    const uint32_t d1 = w[wi + 1];
-    h = tail4(h, funnel(d1, prev, sh));
-    prev = d1;
-    ++wi;
+    h = tail4(h, lds_u32(w, x));
+    x += 4;
     rem -= 4;
   }
   const uint8_t* b = (const uint8_t*)w;
-  uint32_t xb = (wi << 2) + sh;
   while (rem) {
-    h = tail1(h, b[xb]);
-    ++xb;
+    h = tail1(h, b[x]);
+    ++x;
     --rem;
   }
   return avalanche(h);

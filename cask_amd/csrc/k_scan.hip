@@ -34,26 +34,15 @@ struct Geo {
 // Records no longer than this are "short": the boundary search verifies them first.
 constexpr uint32_t kShortMax = 1024;
 
-// Diagnostic (-DCASK_BAR_CHECK): every thread counts the barriers it passed; after the walk
-// barrier each wave compares its count with wave 0's and records a mismatch in stamps[8..].
-#ifdef CASK_BAR_CHECK
-#define BAR()        \
-  {                  \
-    __syncthreads(); \
-    ++dg.nb;         \
-  }
-#else
 #define BAR() __syncthreads()
-#endif
 
 template <class G>
 struct __attribute__((aligned(16))) ScanLdsT {
   uint32_t win[G::kWinWords];        // staged bytes (16-B aligned base + <= 15 B shift + slop)
   uint16_t starts[G::kMaxStartsG];   // record starts relative to the chunk start
-  uint32_t found, n;
-#ifdef CASK_BAR_CHECK
-  uint32_t nb0;
-#endif
+  uint32_t found, n;  // search result; slow path: rows of the chunk
+  uint32_t ffail;     // stride pass: first row whose header breaks the stride
+  uint64_t exitv, lastp, lastrl;  // slow path: walk results (wave 0 -> workgroup)
 };
 
 struct ChunkPos {
@@ -92,13 +81,13 @@ __device__ __forceinline__ ChunkPos locate(const FileDesc* files, uint32_t nfile
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
 // Diagnostic (-DCASK_ADDR_GUARD, stamps builds): an address outside [lo, hi) is recorded in
-// stamps[8..15] and replaced by lo instead of being accessed.
+// stamps[10..15] and replaced by lo instead of being accessed.
 #ifdef CASK_ADDR_GUARD
 #define ADDR_GUARD(stamps, ptr, lo, hi, tag, t)                                                      \
   if ((uintptr_t)(ptr) < (uintptr_t)(lo) || (uintptr_t)(ptr) >= (uintptr_t)(hi)) {                  \
-    if ((stamps) && atomicCAS(&(stamps)[8], 0ull, (unsigned long long)(tag)) == 0ull) {            \
-      (stamps)[9] = (uintptr_t)(ptr); (stamps)[10] = (uintptr_t)(lo); (stamps)[11] = (uintptr_t)(hi); \
-      (stamps)[12] = (t); (stamps)[13] = blockIdx.x | ((uint64_t)threadIdx.x << 32);                \
+    if ((stamps) && atomicCAS(&(stamps)[10], 0ull, (unsigned long long)(tag)) == 0ull) {            \
+      (stamps)[11] = (uintptr_t)(ptr); (stamps)[12] = (uintptr_t)(lo); (stamps)[13] = (uintptr_t)(hi); \
+      (stamps)[14] = (t); (stamps)[15] = blockIdx.x | ((uint64_t)threadIdx.x << 32);                \
     }                                                                                                \
     (ptr) = (decltype(ptr))(lo);                                                                     \
   }
@@ -133,9 +122,64 @@ __device__ __forceinline__ void stage_store(ScanLdsT<G>& L, const u32x4 (&v)[G::
   }
 }
 
+// The slot row of the record at chunk offset `off` (row r of chunk t): header fields, and the
+// checksum verified out of LDS unless the record runs past the window (then k_long does it).
+// Returns whether the row is a failure (InvalidChecksum, or the UnexpectedEof row).
+template <class G>
+__device__ __forceinline__ bool record_row(const uint32_t* W, const ChunkPos& c, uint32_t* slots, uint32_t r,
+                                           uint32_t off, Diag& dg) {
+#ifdef CASK_STAMPS
+  const uint64_t st_h0_ = __builtin_amdgcn_s_memtime();
+#endif
+  const uint64_t p = c.c0 + off;
+  uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = off << 16;
+  bool fail = false;
+  if (p + 18 > c.len) {
+    fail = true;  // EOF row: seq/ksz/vsz stay 0
+  } else {
+    const uint32_t x = off + c.shift;
+    const Hdr h = lds_hdr(W, x);
+    w0 = (uint32_t)h.seq;
+    w1 = (uint32_t)(h.seq >> 32);
+    w2 = h.vsz;
+    w3 |= h.ksz;
+    const uint64_t rl = 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
+    if (p + rl > c.len) {
+      fail = true;  // EOF row (data.rs:172,181)
+    } else if (p + rl <= c.wend) {
+#ifndef CASK_DIAG_NO_LDS_HASH
+      if (lds_xxh32(W, x + 4, (uint32_t)rl - 4) != h.stored) {  // data.rs:193-198
+#else  // diagnostic: same instruction stream without LDS stripe reads; treated as verified
+      if (lds_xxh32<true>(W, x + 4, (uint32_t)rl - 4) == 0x9E3779B1u) {
+#endif
+        w3 |= kSlotBad;
+        fail = true;
+      }
+    }  // else: longer than the window, left to k_long
+  }
+  u32x4 row;
+  row.x = w0;
+  row.y = w1;
+  row.z = w2;
+  row.w = w3;
+#ifdef CASK_STAMPS
+  const uint64_t st_h1_ = __builtin_amdgcn_s_memtime();
+  dg.st[8] += st_h1_ - st_h0_;  // phase 8: header + hash of one record
+#endif
+#ifndef CASK_NO_SLOT_STORE
+  *(u32x4*)(slots + 4ull * r) = row;
+#else  // diagnostic: rows computed, not stored
+  if (row.x == 0x9E3779B9u && row.y == 0x7F4A7C15u) *(u32x4*)(slots + 4ull * r) = row;
+#endif
+#ifdef CASK_STAMPS
+  dg.st[9] += __builtin_amdgcn_s_memtime() - st_h1_;  // phase 9: issuing the slot store
+#endif
+  return fail;
+}
+
 template <class G, bool EXACT>
 __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a, uint64_t t, const ChunkPos& c,
-                                              uint64_t s_exact, Diag& dg) {
+                                              uint64_t s_exact, uint64_t& carry, bool& known, Diag& dg) {
   constexpr uint32_t NT = G::kNT;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const uint32_t* W = L.win;
@@ -149,6 +193,9 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     s = s_exact;
   } else if (c0 == 0) {
     s = 0;  // a file's first record starts at 0 (log.rs:116)
+  } else if (known) {
+    // the previous chunk of this range ended its chain at `carry` (>= c0): no search needed
+    s = (carry == kTerm || carry >= c1) ? kNone : carry;
   } else {
     const uint32_t span = (uint32_t)(c1 - c0);
     // pass A: short records starting in the first kShortMax bytes; pass B: everything, in order.
@@ -184,120 +231,150 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   }
   STAMP(0)
 
-  // 3. walk the chain inside the window (wave 0). Each step tests 64 equal-stride successors.
-  if (wave == 0) {
-    uint32_t n = 0;
-    uint64_t exitv = 0;
-    uint64_t lastp = 0, lastrl = 0;  // last record of the chunk: the only one that can be long
-    if (s != kNone) {
-      uint64_t p = s;
+  // 3. The chunk's records. Stride pass: assume every record from s on has the first record's
+  // length rl0 and let thread i take the record at s + i*rl0 — check its header, verify it,
+  // write its row. The first i whose header breaks the stride (L.ffail) ends the run of true
+  // records; rows past it are discarded. A file of equal-length records never leaves this pass.
+  uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
+  const unsigned long long err_base = (unsigned long long)t * a.slot_cap;
+  uint32_t n = 0;
+  uint64_t exitv = 0, lastp = 0, lastrl = 0;
+  uint32_t k = 0;  // rows settled by the stride pass
+  bool slow = false;
+  if (s != kNone) {
+    uint64_t rl0 = 0;
+    uint32_t cnt = 0;
+    if (s + 18 <= len) {
+      rl0 = lds_reclen(W, (uint32_t)(s - c0) + shift);
+      if (s + rl0 <= len) cnt = (uint32_t)((c1 - s + rl0 - 1) / rl0);
+    }
+    uint32_t failmask = 0;  // bit j: this thread's j-th record failed verification
+    for (uint32_t i = tid, j = 0; i < cnt; i += NT, ++j) {
+      const uint64_t q = s + (uint64_t)i * rl0;
+      bool ok = true;
+      if (i) {
+        ok = (q + 18 <= len);
+        if (ok) ok = (lds_reclen(W, (uint32_t)(q - c0) + shift) == rl0) && (q + rl0 <= len);
+      }
+      if (!ok) {
+        atomicMin(&L.ffail, i);
+      } else if (record_row<G>(W, c, slots, i, (uint32_t)(q - c0), dg)) {
+        failmask |= 1u << j;
+      }
+    }
+    BAR();
+    k = L.ffail < cnt ? L.ffail : cnt;
+    for (uint32_t m = failmask; m; m &= m - 1) {
+      const uint32_t i = tid + (uint32_t)__builtin_ctz(m) * NT;
+      if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
+    }
+    if (k == cnt && cnt) {
+      n = cnt;
+      lastp = s + (uint64_t)(cnt - 1) * rl0;
+      lastrl = rl0;
+      exitv = lastp + rl0;  // >= c1
+    } else {
+      slow = true;  // the stride broke at row k (or the first record is cut short)
+    }
+  }
+  STAMP(1)
+
+  // 4. Slow path: walk the chain from the first record the stride pass did not settle (wave 0;
+  // each step tests up to 256 equal-stride successors with one LDS round trip), then verify
+  // those records, one per thread.
+  if (slow) {
+    if (wave == 0) {
+      uint32_t nn = k;
+      uint64_t ex = 0, lp = 0, lr = 0;
+      uint64_t p = s + (k ? (uint64_t)k * lds_reclen(W, (uint32_t)(s - c0) + shift) : 0ull);
       for (;;) {
         if (p >= c1) {
-          exitv = p;
+          ex = p;
           break;
         }
         if (p + 18 > len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
-          if (lane == 0) L.starts[n] = (uint16_t)(p - c0);
-          ++n;
-          exitv = kTerm;
+          if (lane == 0) L.starts[nn] = (uint16_t)(p - c0);
+          ++nn;
+          ex = kTerm;
           break;
         }
         const uint64_t rl = lds_reclen(W, (uint32_t)(p - c0) + shift);
         if (p + rl > len) {  // key/value cut short (data.rs:172,181)
-          if (lane == 0) L.starts[n] = (uint16_t)(p - c0);
-          ++n;
-          exitv = kTerm;
+          if (lane == 0) L.starts[nn] = (uint16_t)(p - c0);
+          ++nn;
+          ex = kTerm;
           break;
         }
-        const uint64_t q = p + (uint64_t)lane * rl;
-        bool v = true;
-        if (lane) {
-          v = (q < c1) && (q + 18 <= len);
-          if (v) v = (lds_reclen(W, (uint32_t)(q - c0) + shift) == rl) && (q + rl <= len);
+        const uint64_t span = c1 - p;
+        const uint32_t M = span > 192ull * rl ? 4u : span > 128ull * rl ? 3u : span > 64ull * rl ? 2u : 1u;
+        bool vj[4];
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) {  // all reads first: they do not wait on each other
+          const uint64_t i = (uint64_t)lane + 64u * jj;
+          const uint64_t q = p + i * rl;
+          bool v = jj < M;
+          if (v && i) {
+            v = (q < c1) && (q + 18 <= len);
+            if (v) v = (lds_reclen(W, (uint32_t)(q - c0) + shift) == rl) && (q + rl <= len);
+          }
+          vj[jj] = v;
         }
-        const unsigned long long okm = __ballot(v);
-        const uint32_t k = (~okm) ? (uint32_t)__builtin_ctzll(~okm) : 64u;
-        if (lane < k) L.starts[n + lane] = (uint16_t)(q - c0);
-        n += k;
-        lastp = p + (uint64_t)(k - 1) * rl;
-        lastrl = rl;
-        p += (uint64_t)k * rl;
+        uint32_t kk = 0;
+        bool open = true;
+#pragma unroll
+        for (uint32_t jj = 0; jj < 4; ++jj) {
+          const unsigned long long okm = __ballot(vj[jj]);
+          if (open) {
+            const uint32_t kj = (~okm) ? (uint32_t)__builtin_ctzll(~okm) : 64u;
+            if (lane < kj) L.starts[nn + kk + lane] = (uint16_t)(p + ((uint64_t)lane + 64u * jj) * rl - c0);
+            kk += kj;
+            open = kj == 64u;
+          }
+        }
+        nn += kk;
+        lp = p + (uint64_t)(kk - 1) * rl;
+        lr = rl;
+        p += (uint64_t)kk * rl;
+      }
+      if (lane == 0) {
+        L.n = nn;
+        L.exitv = ex;
+        L.lastp = lp;
+        L.lastrl = lr;
       }
     }
-    if (lane == 0) {
-#ifdef CASK_BAR_CHECK
-      L.nb0 = dg.nb;
-#endif
-      L.n = n;
-      {
-        uint64_t* sp = a.spec + t;
-        ADDR_GUARD(a.stamps, sp, a.spec, a.spec + a.total_chunks, 2, t)
-        (void)sp;
-      }
-      if (!EXACT) a.spec[t] = s;
-      a.exit[t] = (s == kNone) ? 0 : exitv;
-      a.count[t] = n;
-      // a record that does not fit the window is hashed from HBM by k_long
-      a.long_r[t] = (exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
+    BAR();
+    n = L.n;
+    exitv = L.exitv;
+    lastp = L.lastp;
+    lastrl = L.lastrl;
+    for (uint32_t r = k + tid; r < n; r += NT) {
+      if (record_row<G>(W, c, slots, r, L.starts[r], dg)) atomicMin(&a.file_err[c.fi], err_base + r);
     }
   }
-  BAR();
-  STAMP(1)
-  const uint32_t n = L.n;
-#ifdef CASK_BAR_CHECK
-  if (L.nb0 + 1 != dg.nb && a.stamps && atomicCAS(&a.stamps[8], 0ull, 7ull) == 0ull) {
-    a.stamps[9] = L.nb0;
-    a.stamps[10] = dg.nb;
-    a.stamps[11] = n;
-    a.stamps[12] = t;
-    a.stamps[13] = blockIdx.x | ((uint64_t)threadIdx.x << 32);
-  }
-#endif
   DCHECK(n <= a.slot_cap && t < a.total_chunks, "n %u t %llu", n, (unsigned long long)t);
-
-  // 4. verify one record per lane out of LDS and write its slot row.
-  uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
-  for (uint32_t r = tid; r < n; r += NT) {
-    const uint32_t off = L.starts[r];
-    const uint64_t p = c0 + off;
-    uint32_t w0 = 0, w1 = 0, w2 = 0, w3 = off << 16;
-    bool fail = false;
-    if (p + 18 > len) {
-      fail = true;  // EOF row: seq/ksz/vsz stay 0
-    } else {
-      const uint32_t x = off + shift;
-      const Hdr h = lds_hdr(W, x);
-      w0 = (uint32_t)h.seq;
-      w1 = (uint32_t)(h.seq >> 32);
-      w2 = h.vsz;
-      w3 |= h.ksz;
-      const uint64_t rl = 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
-      if (p + rl > len) {
-        fail = true;  // EOF row
-      } else if (p + rl <= wend) {
-        if (lds_xxh32(W, x + 4, (uint32_t)rl - 4) != h.stored) {
-          w3 |= kSlotBad;
-          fail = true;
-        }
-      }  // else: longer than the window, left to k_long (a.long_r[t] == r)
-    }
-    u32x4 row;
-    row.x = w0;
-    row.y = w1;
-    row.z = w2;
-    row.w = w3;
-    uint32_t* sl = slots + 4ull * r;
-    ADDR_GUARD(a.stamps, sl, a.slots, a.slots + 4ull * a.slot_cap * a.total_chunks, 3, t)
-    *(u32x4*)sl = row;
-    if (fail) atomicMin(&a.file_err[c.fi], (unsigned long long)((uint64_t)t * a.slot_cap + r));
+  if (tid == 0) {
+    if (!EXACT) a.spec[t] = s;
+    a.exit[t] = (s == kNone) ? 0 : exitv;
+    a.count[t] = n;
+    // a record that does not fit the window is hashed from HBM by k_long (only the last can)
+    a.long_r[t] = (s != kNone && exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
+  }
+  // the next chunk of the run starts where this chain left off
+  if (s != kNone) {
+    carry = exitv;
+    known = true;
+  } else {
+    known = known && !EXACT;
   }
   STAMP(2)
 }
 
-// Persistent grid, kPerCU workgroups per CU. Workgroup b works on XCD (b mod 8) under round-robin
-// placement; each XCD gets one contiguous eighth of the chunks and its workgroups stride through
-// it, so neighbouring chunks (which share halo bytes) are staged by the same XCD at about the same
-// time. Placement only affects speed: any assignment of chunks to workgroups is correct.
+// Persistent grid, kPerCU workgroups per CU; each workgroup walks a contiguous range of chunks in
+// order. Only a range's first chunk searches for its first record boundary: every later chunk
+// starts where the previous one's chain left off (the carry), so the search — a third of the
+// cycles of a speculated chunk — runs once per range. Placement only affects speed: any
+// assignment of chunks to workgroups is correct, and the validation pass checks every start.
 // EXACT (the repair re-scan) reads each chunk's known start from spec[]; the speculative kernel
 // issues no global load besides the staging loads, so the compiler's counted waits never make the
 // processing of one chunk wait for the prefetch of the next.
@@ -311,20 +388,33 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
 #else
   const FileDesc* __restrict__ files = files_r;
 #endif
-  const uint32_t x = blockIdx.x & 7, nx = gridDim.x >> 3;
+  // XCD x (= b mod 8 under round-robin placement) owns one contiguous eighth of the chunks. Its
+  // nx workgroups take runs of a.run consecutive chunks round-robin, so together they sweep the
+  // eighth front to back (a compact set of pages and DRAM rows in flight) while each run is
+  // walked in order with a carry.
+  const uint32_t x = blockIdx.x & 7, nx = gridDim.x >> 3, j = blockIdx.x >> 3;
   const uint64_t per = (a.total_chunks + 7) >> 3;
-  uint64_t t = x * per + (blockIdx.x >> 3);
-  const uint64_t tend = (x + 1) * per < a.total_chunks ? (x + 1) * per : a.total_chunks;
-  if (t >= tend) return;
-  if (threadIdx.x == 0) L.found = 0xFFFFFFFFu;
+  const uint64_t xs = x * per < a.total_chunks ? x * per : a.total_chunks;
+  const uint64_t xe = xs + per < a.total_chunks ? xs + per : a.total_chunks;
+  const uint64_t R = a.run, stride = (uint64_t)nx * R;
+  uint64_t t = xs + (uint64_t)j * R;
+  uint64_t run_end = t + R < xe ? t + R : xe;
+  if (t >= xe) return;
   Diag dg{};
+  uint64_t carry = 0;  // chain position entering chunk t, when known
+  bool known = false;  // only the first chunk of the range (and chunks after a failed search) search
   ChunkPos cur = locate<G>(files, a.nfiles, t);
   u32x4 v[G::kNL];
   stage_issue<G>(v, cur, a.stamps, t);
   for (;;) {
 #ifdef CASK_STAMPS
     const uint64_t st_top_ = __builtin_amdgcn_s_memtime();
+    if (dg.st[7] == 0) dg.st[7] = st_top_;  // first stamp: total = last - first
 #endif
+    if (threadIdx.x == 0) {  // every reader of the last chunk's values is past the end barrier
+      L.found = 0xFFFFFFFFu;
+      L.ffail = 0xFFFFFFFFu;
+    }
     stage_store<G>(L, v, cur);
     BAR();
 #ifdef CASK_STAMPS
@@ -338,12 +428,12 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
         const u32x4 g = src[i];
         const u32x4 l = ((const u32x4*)L.win)[i];
         if ((g.x != l.x || g.y != l.y || g.z != l.z || g.w != l.w) &&
-            atomicCAS(&a.stamps[8], 0ull, 9ull) == 0ull) {
-          a.stamps[9] = i;
-          a.stamps[10] = ((uint64_t)g.x << 32) | l.x;
-          a.stamps[11] = cur.n16;
-          a.stamps[12] = t;
-          a.stamps[13] = blockIdx.x | ((uint64_t)threadIdx.x << 32);
+            atomicCAS(&a.stamps[10], 0ull, 9ull) == 0ull) {
+          a.stamps[11] = i;
+          a.stamps[12] = ((uint64_t)g.x << 32) | l.x;
+          a.stamps[13] = cur.n16;
+          a.stamps[14] = t;
+          a.stamps[15] = blockIdx.x | ((uint64_t)threadIdx.x << 32);
         }
       }
       BAR();
@@ -352,19 +442,43 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
     // exact (repair) pass: the chunk's known start, loaded before the prefetch is issued so that
     // waiting for it never waits for the prefetch
     const uint64_t s_exact = EXACT ? a.spec[t] : 0;
-    const uint64_t tn = t + nx;
-    const bool more = tn < tend;
+    uint64_t tn = t + 1, next_end = run_end;
+    if (tn >= run_end) {  // next run of this workgroup
+      tn = run_end - R + stride;
+      next_end = tn + R < xe ? tn + R : xe;
+    }
+    const bool more = tn < xe;
+#ifdef CASK_STAMPS
+    const uint64_t st_pf_ = __builtin_amdgcn_s_memtime();
+#endif
     if (more) stage_issue<G>(v, locate<G>(files, a.nfiles, tn), a.stamps, tn);  // prefetch the next window
-    process_chunk<G, EXACT>(L, a, t, cur, s_exact, dg);
-    if (threadIdx.x == 0) L.found = 0xFFFFFFFFu;
+#ifdef CASK_STAMPS
+    dg.st[5] += __builtin_amdgcn_s_memtime() - st_pf_;  // phase 5: issuing the prefetch
+#endif
+#ifndef CASK_STAGE_ONLY
+    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, dg);
+#else  // diagnostic: staging and prefetch only (the memory side of the kernel in isolation)
+    if (threadIdx.x == 0 && L.win[cur.n16] == 0x12345678u) a.count[t] = 1;  // keep the staged bytes live
+#endif
+#ifdef CASK_STAMPS
+    const uint64_t st_end_ = __builtin_amdgcn_s_memtime();
+#endif
+    known = known && tn == t + 1;  // a new run searches
     BAR();
+#ifdef CASK_STAMPS
+    dg.st[6] += __builtin_amdgcn_s_memtime() - st_end_;  // phase 6: end-of-chunk barrier
+#endif
     if (!more) break;
     t = tn;
+    run_end = next_end;
     cur = locate<G>(files, a.nfiles, t);
   }
 #ifdef CASK_STAMPS
+  dg.st[7] = __builtin_amdgcn_s_memtime() - dg.st[7];
+  if (a.stamps && threadIdx.x == 0) atomicAdd(&a.stamps[7], (unsigned long long)dg.st[7]);
   if (a.stamps && threadIdx.x == 0)
-    for (int i = 0; i < 5; ++i) atomicAdd(&a.stamps[i], (unsigned long long)dg.st[i]);
+    for (int i = 0; i < 10; ++i)
+      if (i != 7) atomicAdd(&a.stamps[i], (unsigned long long)dg.st[i]);
 #endif
 }
 

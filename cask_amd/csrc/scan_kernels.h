@@ -68,7 +68,11 @@ struct ScanArgs {
   uint8_t* status;
   uint64_t row_cap;
   unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums
+  uint32_t run;                // k_scan_chunks: consecutive chunks a workgroup walks with a carry
+  uint32_t pad_;
 };
+
+constexpr uint32_t kDefaultRun = 16;
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
 struct SummaryHead {

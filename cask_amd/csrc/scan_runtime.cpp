@@ -270,6 +270,10 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.row_cap = rows->capacity;
   }
   a.stamps = nullptr;
+  {  // CASK_RUN_CHUNKS (tuning knob): chunks per workgroup run; one boundary search per run
+    static const uint32_t run = getenv("CASK_RUN_CHUNKS") ? (uint32_t)atoi(getenv("CASK_RUN_CHUNKS")) : kDefaultRun;
+    a.run = run ? run : 1;
+  }
 #ifdef CASK_STAMPS
   if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
 #endif
@@ -334,6 +338,10 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     c->dbg_count = a.count;
     c->dbg_tin = a.tin;
     c->dbg_n = total_chunks;
+    float t_k1 = 0;
+    (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
+    memset(c->last_ms, 0, sizeof(c->last_ms));
+    c->last_ms[1] = t_k1;
     return head->any_invalid ? 1 : 0;
   }
 #endif

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("CASK_LIB_PATH", os.path.join(ROOT, "cask_amd", "build", "stamps", "libcask_scan.so"))
 
-PHASES = ["search", "walk", "hash+slots"]
+PHASES = ["search", "walk", "hash+slots", "stage wait+store", "(iterations)", "prefetch issue", "end barrier", "TOTAL loop", "  rec hdr+hash", "  rec store issue"]
 
 
 def main():
@@ -38,7 +38,8 @@ def main():
     chunks = ctx.last_counters()["chunks"]
     t = ctx.last_timings()
     print(f"chunks={chunks} rows={res.count} timings={t}")
-    tot = sum(st[i] for i in range(3))
+    tot = st[7]
+    print(f"chunk iterations stamped: {st[4]}")
     for i, p in enumerate(PHASES):
         print(f"{p:14s} {st[i] / chunks:12.0f} cyc/WG  {100.0 * st[i] / max(tot, 1):5.1f}%")
 
