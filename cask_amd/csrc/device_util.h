@@ -43,34 +43,21 @@ struct Diag {
 #define DCHECK(cond, fmt, ...)
 #endif
 
-// The window is staged 16-B aligned; records start at arbitrary byte offsets. gfx950 serves
-// unaligned LDS reads (unaligned-ds-access): a memcpy from a byte address compiles to one
-// ds_read_b32/b64/b128 at that address, so no funnel shifts are needed to assemble words.
+// The window is staged 16-B aligned; records start at arbitrary byte offsets. On gfx950 an LDS
+// read whose address is not a multiple of its width is served one lane per clock (measured in
+// tools/ubench_lds.hip: ~27 ns per wave-instruction per CU against 2 ns aligned, for b32, b64 and
+// b128 alike), so every read here is of naturally aligned dwords and the bytes at an arbitrary
+// offset are funnelled out of two neighbours with v_alignbyte_b32.
+__device__ __forceinline__ uint32_t fun(uint32_t lo, uint32_t hi, uint32_t sh) {
+  return __builtin_amdgcn_alignbyte(hi, lo, sh);  // bytes sh..sh+3 of hi:lo (sh in 0..3)
+}
 __device__ __forceinline__ uint32_t lds_u32(const uint32_t* w, uint32_t x) {
-  uint32_t v;
-  __builtin_memcpy(&v, (const uint8_t*)w + x, 4);
-  return v;
-}
-__device__ __forceinline__ uint64_t lds_u64(const uint32_t* w, uint32_t x) {
-  uint64_t v;
-  __builtin_memcpy(&v, (const uint8_t*)w + x, 8);
-  return v;
-}
-__device__ __forceinline__ u32x4 lds_u128(const uint32_t* w, uint32_t x) {
-  u32x4 v;
-  __builtin_memcpy(&v, (const uint8_t*)w + x, 16);
-  return v;
+  const uint32_t i = x >> 2;
+  return fun(w[i], w[i + 1], x & 3);  // ds_read2_b32: two aligned dwords
 }
 
-// Record length at LDS byte index x: 18 + ksz + vsz_eff (data.rs:63-65; tombstone vsz = !0).
-__device__ __forceinline__ uint64_t lds_reclen(const uint32_t* w, uint32_t x) {
-  const uint64_t b = lds_u64(w, x + 12);  // ksz u16 | vsz u32 | 2 bytes of what follows
-  const uint32_t ksz = (uint32_t)b & 0xFFFFu;
-  const uint32_t vsz = (uint32_t)(b >> 16);
-  return 18ull + ksz + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
-}
-
-// The 18-byte header `xxh32 u32 | seq u64 | ksz u16 | vsz u32`, little-endian (data.rs:161-169).
+// The 18-byte header `xxh32 u32 | seq u64 | ksz u16 | vsz u32`, little-endian (data.rs:161-169),
+// from the 6 aligned dwords that cover bytes x .. x+17.
 struct Hdr {
   uint32_t stored;
   uint64_t seq;
@@ -79,68 +66,186 @@ struct Hdr {
 };
 
 __device__ __forceinline__ Hdr lds_hdr(const uint32_t* w, uint32_t x) {
-  const u32x4 d = lds_u128(w, x);          // bytes x .. x+15
-  const uint32_t e = lds_u32(w, x + 14);   // bytes x+14 .. x+17: vsz
+  const uint32_t i = x >> 2, sh = x & 3;
+  const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2], d3 = w[i + 3], d4 = w[i + 4], d5 = w[i + 5];
+  const uint32_t w3 = fun(d3, d4, sh), w4 = fun(d4, d5, sh);
   Hdr h;
-  h.stored = d.x;
-  h.seq = (uint64_t)d.y | ((uint64_t)d.z << 32);
-  h.ksz = d.w & 0xFFFFu;
-  h.vsz = e;
+  h.stored = fun(d0, d1, sh);
+  h.seq = (uint64_t)fun(d1, d2, sh) | ((uint64_t)fun(d2, d3, sh) << 32);
+  h.ksz = w3 & 0xFFFFu;
+  h.vsz = (w3 >> 16) | (w4 << 16);
   return h;
 }
 
-// XXH32 (seed 0) of LDS bytes [xs, xs + len), 16-B stripes read with unaligned ds_read_b128.
-// Two stripes are mixed per step while the next two are in flight: under load an LDS read takes
-// longer than one stripe's multiplies.
-template <bool FAKE = false>  // FAKE (diagnostic): stripes from registers, not LDS; wrong hash
+// Record length at LDS byte index x: 18 + ksz + vsz_eff (data.rs:63-65; tombstone vsz = !0),
+// from bytes x+12 .. x+17.
+__device__ __forceinline__ uint64_t lds_reclen(const uint32_t* w, uint32_t x) {
+  const uint32_t i = (x + 12) >> 2, sh = x & 3;
+  const uint32_t d0 = w[i], d1 = w[i + 1], d2 = w[i + 2];
+  const uint32_t w3 = fun(d0, d1, sh), w4 = fun(d1, d2, sh);
+  const uint32_t ksz = w3 & 0xFFFFu;
+  const uint32_t vsz = (w3 >> 16) | (w4 << 16);
+  return 18ull + ksz + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+}
+
+// XXH32 tail of `rem` (< 16) bytes at LDS byte x onto h, and the avalanche. The at most five
+// aligned dwords covering the bytes are read at once; the serial steps then run on registers.
+__device__ __forceinline__ uint32_t lds_tail_fin(const uint32_t* w, uint32_t x, uint32_t rem, uint32_t h) {
+  const uint32_t i = x >> 2, sh = x & 3;
+  const uint32_t e0 = w[i], e1 = w[i + 1], e2 = w[i + 2], e3 = w[i + 3], e4 = w[i + 4];
+  const uint32_t t0 = fun(e0, e1, sh), t1 = fun(e1, e2, sh), t2 = fun(e2, e3, sh), t3 = fun(e3, e4, sh);
+  const uint32_t nw = rem >> 2;
+  if (nw > 0) h = tail4(h, t0);
+  if (nw > 1) h = tail4(h, t1);
+  if (nw > 2) h = tail4(h, t2);
+  const uint32_t lw = nw == 0 ? t0 : nw == 1 ? t1 : nw == 2 ? t2 : t3;
+  const uint32_t nb = rem & 3;
+  if (nb > 0) h = tail1(h, lw & 0xFFu);
+  if (nb > 1) h = tail1(h, (lw >> 8) & 0xFFu);
+  if (nb > 2) h = tail1(h, (lw >> 16) & 0xFFu);
+  return avalanche(h);
+}
+
+// XXH32 (seed 0) of LDS bytes [xs, xs + len) by one lane (the boundary search's candidates).
 __device__ __forceinline__ uint32_t lds_xxh32(const uint32_t* w, uint32_t xs, uint32_t len) {
   uint32_t h;
-  const uint32_t nstr = len >> 4;
-  uint32_t x = xs;
+  const uint32_t nstr = len >> 4, sh = xs & 3;
+  uint32_t i = xs >> 2;
   if (nstr) {
     Acc a = acc_init(0);
-    auto ld = [&](uint32_t y) -> u32x4 {
-      if (!FAKE) return lds_u128(w, y);
-      u32x4 v;
-      v.x = y;
-      v.y = y ^ 0x5bd1e995u;
-      v.z = y * 3u;
-      v.w = y + 0x27d4eb2fu;
-      return v;
-    };
-    u32x4 d0 = ld(x), d1 = ld(x + 16);  // reads past the record stay in LDS
-    uint32_t s = 0;
-    for (; s + 2 <= nstr; s += 2) {
-      const u32x4 e0 = ld(x + 32), e1 = ld(x + 48);  // next pair in flight
-      __builtin_amdgcn_sched_barrier(0);  // keep them issued ahead of this pair's multiplies
-      acc_stripe(a, d0.x, d0.y, d0.z, d0.w);
-      acc_stripe(a, d1.x, d1.y, d1.z, d1.w);
-      d0 = e0;
-      d1 = e1;
-      x += 32;
-    }
-    if (s < nstr) {
-      acc_stripe(a, d0.x, d0.y, d0.z, d0.w);
-      x += 16;
+    uint32_t d0 = w[i];
+    for (uint32_t s = 0; s < nstr; ++s) {
+      const uint32_t d1 = w[i + 1], d2 = w[i + 2], d3 = w[i + 3], d4 = w[i + 4];
+      acc_stripe(a, fun(d0, d1, sh), fun(d1, d2, sh), fun(d2, d3, sh), fun(d3, d4, sh));
+      d0 = d4;
+      i += 4;
     }
     h = acc_merge(a);
   } else {
     h = P5;
   }
-  h += len;
-  uint32_t rem = len & 15;
-  while (rem >= 4) {
-    h = tail4(h, lds_u32(w, x));
-    x += 4;
-    rem -= 4;
+  return lds_tail_fin(w, xs + (nstr << 4), len & 15, h + len);
+}
+
+// Quad-lane DPP moves (quad_perm): lane a of each group of 4 receives lane perm[a]'s value.
+__device__ __forceinline__ uint32_t quad_xor1(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]
+}
+__device__ __forceinline__ uint32_t quad_xor2(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xF, 0xF, false);  // [2,3,0,1]
+}
+__device__ __forceinline__ uint32_t rotl_var(uint32_t x, uint32_t r) {
+  return __builtin_amdgcn_alignbit(x, x, 32u - r);  // r in [1, 31]
+}
+
+// XXH32 (seed 0) of LDS bytes [xs, xs + len) computed by a quad of lanes, lane a = 0..3 of the
+// quad keeping stripe accumulator v_{a+1} (XXH32's four accumulators are independent until the
+// merge). Every lane of the quad returns the hash. The four lanes must be active together and
+// call with the same xs/len. Lane a reads the two aligned dwords around its word of each stripe,
+// four stripes ahead.
+__device__ __forceinline__ uint32_t quad_xxh32(const uint32_t* w, uint32_t xs, uint32_t len, uint32_t a) {
+  uint32_t h;
+  const uint32_t nstr = len >> 4;
+  if (nstr) {
+    uint32_t v = a == 0 ? P1 + P2 : a == 1 ? P2 : a == 2 ? 0u : 0u - P1;
+    const uint32_t sh = xs & 3;
+    uint32_t i = (xs >> 2) + a;  // lane a: dwords i, i+1 of every stripe (aligned ds_read2_b32)
+    uint32_t s = 0;
+    for (; s + 4 <= nstr; s += 4) {  // 8 reads in flight, then 4 rounds
+      const uint32_t a0 = w[i], b0 = w[i + 1], a1 = w[i + 4], b1 = w[i + 5];
+      const uint32_t a2 = w[i + 8], b2 = w[i + 9], a3 = w[i + 12], b3 = w[i + 13];
+      v = xround(v, fun(a0, b0, sh));
+      v = xround(v, fun(a1, b1, sh));
+      v = xround(v, fun(a2, b2, sh));
+      v = xround(v, fun(a3, b3, sh));
+      i += 16;
+    }
+    for (; s < nstr; ++s) {
+      v = xround(v, fun(w[i], w[i + 1], sh));
+      i += 4;
+    }
+    uint32_t m = rotl_var(v, a == 0 ? 1u : a == 1 ? 7u : a == 2 ? 12u : 18u);
+    m += quad_xor1(m);
+    m += quad_xor2(m);
+    h = m;
+  } else {
+    h = P5;
   }
-  const uint8_t* b = (const uint8_t*)w;
-  while (rem) {
-    h = tail1(h, b[x]);
-    ++x;
-    --rem;
+  return lds_tail_fin(w, xs + (nstr << 4), len & 15, h + len);
+}
+
+// Two records of the same hashed length `len` (wave-uniform: the stride pass), hashed by one quad
+// at once: two independent accumulator chains per lane, and each 4-stripe block's 16 aligned
+// dwords read while the previous block is mixed. Lane a keeps accumulator a of both records; all
+// four lanes return both hashes. x0/x1 are the LDS byte offsets of the hashed bytes.
+__device__ __forceinline__ void quad_xxh32_pair(const uint32_t* w, uint32_t x0, uint32_t x1, uint32_t len, uint32_t a,
+                                                uint32_t& h0, uint32_t& h1) {
+  const uint32_t nstr = len >> 4;
+  const uint32_t sh0 = x0 & 3, sh1 = x1 & 3;
+  if (nstr) {
+    const uint32_t v_init = a == 0 ? P1 + P2 : a == 1 ? P2 : a == 2 ? 0u : 0u - P1;
+    uint32_t v0 = v_init, v1 = v_init;
+    uint32_t i0 = (x0 >> 2) + a, i1 = (x1 >> 2) + a;
+    uint32_t s = 0;
+    if (nstr >= 4) {
+      uint32_t A[8], B[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        A[2 * k] = w[i0 + 4 * k];
+        A[2 * k + 1] = w[i0 + 4 * k + 1];
+        B[2 * k] = w[i1 + 4 * k];
+        B[2 * k + 1] = w[i1 + 4 * k + 1];
+      }
+      for (; s + 8 <= nstr; s += 4) {
+        uint32_t An[8], Bn[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          An[2 * k] = w[i0 + 16 + 4 * k];
+          An[2 * k + 1] = w[i0 + 16 + 4 * k + 1];
+          Bn[2 * k] = w[i1 + 16 + 4 * k];
+          Bn[2 * k + 1] = w[i1 + 16 + 4 * k + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          v0 = xround(v0, fun(A[2 * k], A[2 * k + 1], sh0));
+          v1 = xround(v1, fun(B[2 * k], B[2 * k + 1], sh1));
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          A[k] = An[k];
+          B[k] = Bn[k];
+        }
+        i0 += 16;
+        i1 += 16;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v0 = xround(v0, fun(A[2 * k], A[2 * k + 1], sh0));
+        v1 = xround(v1, fun(B[2 * k], B[2 * k + 1], sh1));
+      }
+      i0 += 16;
+      i1 += 16;
+      s += 4;
+    }
+    for (; s < nstr; ++s) {
+      v0 = xround(v0, fun(w[i0], w[i0 + 1], sh0));
+      v1 = xround(v1, fun(w[i1], w[i1 + 1], sh1));
+      i0 += 4;
+      i1 += 4;
+    }
+    const uint32_t r = a == 0 ? 1u : a == 1 ? 7u : a == 2 ? 12u : 18u;
+    uint32_t m0 = rotl_var(v0, r), m1 = rotl_var(v1, r);
+    m0 += quad_xor1(m0);
+    m1 += quad_xor1(m1);
+    m0 += quad_xor2(m0);
+    m1 += quad_xor2(m1);
+    h0 = m0;
+    h1 = m1;
+  } else {
+    h0 = h1 = P5;
   }
-  return avalanche(h);
+  h0 = lds_tail_fin(w, x0 + (nstr << 4), len & 15, h0 + len);
+  h1 = lds_tail_fin(w, x1 + (nstr << 4), len & 15, h1 + len);
 }
 
 // Unaligned global loads: gfx950 runs in unaligned-access mode, so these memcpys become

@@ -26,9 +26,11 @@ namespace cask_dev {
 template <uint32_t CH, uint32_t HALO, uint32_t NT, uint32_t PER_CU>
 struct Geo {
   static constexpr uint32_t kCh = CH, kHaloB = HALO, kNT = NT, kWinB = CH + HALO, kPerCU = PER_CU;
+  static constexpr uint32_t kWavesPerSimd = PER_CU * NT / 256;  // 4 SIMDs of 64-lane waves per CU
   static constexpr uint32_t kMaxStartsG = CH / 18 + 2;  // every record is >= 18 bytes
+  static constexpr uint32_t kRowBuf = kMaxStartsG / 16;   // slot rows per LDS row buffer (2 in starts' space)
   static constexpr uint32_t kWinWords = (kWinB + 64) / 4;
-  static constexpr uint32_t kNL = ((kWinB + 32) / 16 + NT - 1) / NT;  // 16-B loads per thread
+  static constexpr uint32_t kNL = ((kWinB + 16) / 16 + NT - 1) / NT;  // 16-B loads per thread
 };
 
 // Records no longer than this are "short": the boundary search verifies them first.
@@ -39,8 +41,13 @@ constexpr uint32_t kShortMax = 1024;
 template <class G>
 struct __attribute__((aligned(16))) ScanLdsT {
   uint32_t win[G::kWinWords];        // staged bytes (16-B aligned base + <= 15 B shift + slop)
-  uint16_t starts[G::kMaxStartsG];   // record starts relative to the chunk start
+  union {
+    uint16_t starts[G::kMaxStartsG];  // slow path: record starts relative to the chunk start
+    u32x4 rows[2][G::kRowBuf];        // stride pass: the first kRowBuf slot rows of the chunk (parity
+                                      // buffer), flushed as 16-B stores while the next chunk runs
+  };
   uint32_t found, n;  // search result; slow path: rows of the chunk
+  uint32_t claimed;   // the run this workgroup takes after its current one
   uint32_t ffail;     // stride pass: first row whose header breaks the stride
   uint64_t exitv, lastp, lastrl;  // slow path: walk results (wave 0 -> workgroup)
 };
@@ -52,17 +59,14 @@ struct ChunkPos {
   uint32_t fi, shift, n16;
 };
 
+// The window of the chunk at byte c0 of file fi.
 template <class G>
-__device__ __forceinline__ ChunkPos locate(const FileDesc* files, uint32_t nfiles, uint64_t t) {
+__device__ __forceinline__ ChunkPos chunk_at(const uint8_t* data, uint64_t len, uint32_t fi, uint64_t c0) {
   ChunkPos c;
-  c.fi = find_file(files, nfiles, t);
-  DCHECK(c.fi < nfiles, "fi %u t %llu", c.fi, (unsigned long long)t);
-  const FileDesc fd = files[c.fi];
-  DCHECK(t >= fd.first_chunk && t < fd.first_chunk + fd.nchunks, "fi %u t %llu first %llu n %llu", c.fi,
-         (unsigned long long)t, (unsigned long long)fd.first_chunk, (unsigned long long)fd.nchunks);
-  c.data = fd.data;
-  c.len = fd.len;
-  c.c0 = (t - fd.first_chunk) * (uint64_t)G::kCh;
+  c.fi = fi;
+  c.data = data;
+  c.len = len;
+  c.c0 = c0;
   c.c1 = (c.c0 + G::kCh < c.len) ? c.c0 + G::kCh : c.len;
   c.wend = (c.c0 + G::kWinB < c.len) ? c.c0 + G::kWinB : c.len;
   const uintptr_t gstart = (uintptr_t)(c.data + c.c0);
@@ -71,6 +75,25 @@ __device__ __forceinline__ ChunkPos locate(const FileDesc* files, uint32_t nfile
   const uintptr_t aend = ((uintptr_t)(c.data + c.wend) + 15) & ~(uintptr_t)15;
   c.n16 = (uint32_t)((aend - c.a0) >> 4);
   return c;
+}
+
+template <class G>
+__device__ __forceinline__ ChunkPos locate(const FileDesc* files, uint32_t nfiles, uint64_t t) {
+  const uint32_t fi = find_file(files, nfiles, t);
+  DCHECK(fi < nfiles, "fi %u t %llu", fi, (unsigned long long)t);
+  const FileDesc fd = files[fi];
+  DCHECK(t >= fd.first_chunk && t < fd.first_chunk + fd.nchunks, "fi %u t %llu first %llu n %llu", fi,
+         (unsigned long long)t, (unsigned long long)fd.first_chunk, (unsigned long long)fd.nchunks);
+  return chunk_at<G>(fd.data, fd.len, fi, (t - fd.first_chunk) * (uint64_t)G::kCh);
+}
+
+// Chunk tn, the successor of cur's chunk t: the next chunk of the same file needs no table lookup
+// (the binary search is a chain of dependent scalar loads).
+template <class G>
+__device__ __forceinline__ ChunkPos next_chunk(const FileDesc* files, uint32_t nfiles, const ChunkPos& cur,
+                                               uint64_t t, uint64_t tn) {
+  if (tn == t + 1 && cur.c0 + G::kCh < cur.len) return chunk_at<G>(cur.data, cur.len, cur.fi, cur.c0 + G::kCh);
+  return locate<G>(files, nfiles, tn);
 }
 
 // Issue every 16-B load of a window (clamped index: no branch around a load, so all of them are
@@ -103,6 +126,11 @@ __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& 
              c.a0 >= ((uintptr_t)c.data & ~(uintptr_t)15) && c.a0 + 16ull * c.n16 <= (((uintptr_t)c.data + c.len + 15) & ~(uintptr_t)15),
          "n16 %u a0 %llx data %llx len %llu c0 %llu", c.n16, (unsigned long long)c.a0,
          (unsigned long long)(uintptr_t)c.data, (unsigned long long)c.len, (unsigned long long)c.c0);
+  if (c.n16 == G::kNL * G::kNT) {  // the whole window is inside the file: no clamping
+#pragma unroll
+    for (uint32_t j = 0; j < G::kNL; ++j) v[j] = src[threadIdx.x + j * G::kNT];
+    return;
+  }
 #pragma unroll
   for (uint32_t j = 0; j < G::kNL; ++j) {
     const uint32_t i = threadIdx.x + j * G::kNT;
@@ -115,6 +143,11 @@ __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& 
 template <class G>
 __device__ __forceinline__ void stage_store(ScanLdsT<G>& L, const u32x4 (&v)[G::kNL], const ChunkPos& c) {
   u32x4* dst = (u32x4*)L.win;
+  if (c.n16 == G::kNL * G::kNT) {
+#pragma unroll
+    for (uint32_t j = 0; j < G::kNL; ++j) dst[threadIdx.x + j * G::kNT] = v[j];
+    return;
+  }
 #pragma unroll
   for (uint32_t j = 0; j < G::kNL; ++j) {
     const uint32_t i = threadIdx.x + j * G::kNT;
@@ -122,12 +155,14 @@ __device__ __forceinline__ void stage_store(ScanLdsT<G>& L, const u32x4 (&v)[G::
   }
 }
 
-// The slot row of the record at chunk offset `off` (row r of chunk t): header fields, and the
-// checksum verified out of LDS unless the record runs past the window (then k_long does it).
-// Returns whether the row is a failure (InvalidChecksum, or the UnexpectedEof row).
+// The slot row of the record at chunk offset `off` (row r of chunk t), built by a quad of lanes
+// (lane a = 0..3 of the quad): header fields, and the checksum verified out of LDS by the quad
+// unless the record runs past the window (then k_long does it). Lane a writes dword a of the
+// 16-B row, so a wave's rows go out as contiguous 256-B stores. All four lanes return whether
+// the row is a failure (InvalidChecksum, or the UnexpectedEof row).
 template <class G>
-__device__ __forceinline__ bool record_row(const uint32_t* W, const ChunkPos& c, uint32_t* slots, uint32_t r,
-                                           uint32_t off, Diag& dg) {
+__device__ __forceinline__ bool quad_row(const uint32_t* W, const ChunkPos& c, uint32_t* slots, uint32_t r,
+                                         uint32_t off, uint32_t a, Diag& dg) {
 #ifdef CASK_STAMPS
   const uint64_t st_h0_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -147,29 +182,21 @@ __device__ __forceinline__ bool record_row(const uint32_t* W, const ChunkPos& c,
     if (p + rl > c.len) {
       fail = true;  // EOF row (data.rs:172,181)
     } else if (p + rl <= c.wend) {
-#ifndef CASK_DIAG_NO_LDS_HASH
-      if (lds_xxh32(W, x + 4, (uint32_t)rl - 4) != h.stored) {  // data.rs:193-198
-#else  // diagnostic: same instruction stream without LDS stripe reads; treated as verified
-      if (lds_xxh32<true>(W, x + 4, (uint32_t)rl - 4) == 0x9E3779B1u) {
-#endif
+      if (quad_xxh32(W, x + 4, (uint32_t)rl - 4, a) != h.stored) {  // data.rs:193-198
         w3 |= kSlotBad;
         fail = true;
       }
     }  // else: longer than the window, left to k_long
   }
-  u32x4 row;
-  row.x = w0;
-  row.y = w1;
-  row.z = w2;
-  row.w = w3;
+  const uint32_t word = a == 0 ? w0 : a == 1 ? w1 : a == 2 ? w2 : w3;
 #ifdef CASK_STAMPS
   const uint64_t st_h1_ = __builtin_amdgcn_s_memtime();
   dg.st[8] += st_h1_ - st_h0_;  // phase 8: header + hash of one record
 #endif
 #ifndef CASK_NO_SLOT_STORE
-  *(u32x4*)(slots + 4ull * r) = row;
+  slots[4ull * r + a] = word;
 #else  // diagnostic: rows computed, not stored
-  if (row.x == 0x9E3779B9u && row.y == 0x7F4A7C15u) *(u32x4*)(slots + 4ull * r) = row;
+  if (word == 0x9E3779B9u) slots[4ull * r + a] = word;
 #endif
 #ifdef CASK_STAMPS
   dg.st[9] += __builtin_amdgcn_s_memtime() - st_h1_;  // phase 9: issuing the slot store
@@ -177,11 +204,60 @@ __device__ __forceinline__ bool record_row(const uint32_t* W, const ChunkPos& c,
   return fail;
 }
 
+// ceil(a / b) for 0 < b < a <= 2^16 (wave-uniform): a float quotient, corrected to the exact one.
+__device__ __forceinline__ uint32_t ceil_div_small(uint32_t a, uint32_t b) {
+  uint32_t c = (uint32_t)__builtin_ceilf((float)a / (float)b);
+  if (c * b < a) ++c;
+  if ((c - 1) * b >= a) --c;
+  return c;
+}
+
+// Slot row of a record the stride pass settled (header in h, no EOF: it fits the file); lane a
+// of the quad writes dword a. Returns `bad`.
+// Rows below kRowBuf go to the LDS row buffer (flushed later as whole 16-B rows, a quarter of the
+// store instructions), the rest straight to the slots.
+template <class G>
+__device__ __forceinline__ bool stride_row(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t r, uint32_t off,
+                                           const Hdr& h, bool bad, uint32_t a) {
+  const uint32_t w3 = h.ksz | (off << 16) | (bad ? kSlotBad : 0u);
+  const uint32_t word = a == 0 ? (uint32_t)h.seq : a == 1 ? (uint32_t)(h.seq >> 32) : a == 2 ? h.vsz : w3;
+  if (r < G::kRowBuf) {
+    ((uint32_t*)L.rows[par])[4 * r + a] = word;
+  } else {
+#ifndef CASK_NO_SLOT_STORE
+    slots[4ull * r + a] = word;
+#else  // diagnostic: rows computed, not stored
+    if (word == 0x9E3779B9u) slots[4ull * r + a] = word;
+#endif
+  }
+  return bad;
+}
+
+// Slot rows [0, n) of a chunk from LDS row buffer `par` to its slots, one 16-B store per row.
+template <class G>
+__device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t n) {
+  u32x4* srow = (u32x4*)slots;
+  for (uint32_t r = threadIdx.x; r < n; r += G::kNT) {
+#ifndef CASK_NO_SLOT_STORE
+#ifdef CASK_NT_ROWS
+    __builtin_nontemporal_store(L.rows[par][r], &srow[r]);
+#else
+    srow[r] = L.rows[par][r];
+#endif
+#else
+    const u32x4 w = L.rows[par][r];
+    if (w.x == 0x9E3779B9u) srow[r] = w;
+#endif
+  }
+}
+
 template <class G, bool EXACT>
 __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a, uint64_t t, const ChunkPos& c,
-                                              uint64_t s_exact, uint64_t& carry, bool& known, Diag& dg) {
+                                              uint64_t s_exact, uint64_t& carry, bool& known, uint32_t par,
+                                              uint32_t& pf_n, uint32_t*& pf_slots, Diag& dg) {
   constexpr uint32_t NT = G::kNT;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr uint32_t NQ = NT / 4;  // quads: one record per quad of lanes
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, quad = tid >> 2, qa = tid & 3;
   const uint32_t* W = L.win;
   const uint64_t len = c.len, c0 = c.c0, c1 = c.c1, wend = c.wend;
   const uint32_t shift = c.shift;
@@ -235,38 +311,90 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   // length rl0 and let thread i take the record at s + i*rl0 — check its header, verify it,
   // write its row. The first i whose header breaks the stride (L.ffail) ends the run of true
   // records; rows past it are discarded. A file of equal-length records never leaves this pass.
+#if defined(CASK_SLOTS_SCRATCH)  // diagnostic (wrong rows): every chunk of a workgroup writes the same, L2-resident slots
+  uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * a.slot_cap) * 4;
+#elif !defined(CASK_DENSE_SLOTS)
   uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
+#else  // diagnostic (wrong rows): each workgroup appends its rows densely, to time the write locality
+  const uint64_t region = (a.total_chunks * a.slot_cap) / gridDim.x;
+  uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * region + (dg.st[0] % (region - a.slot_cap))) * 4;
+  dg.st[0] += 113;
+#endif
   const unsigned long long err_base = (unsigned long long)t * a.slot_cap;
   uint32_t n = 0;
   uint64_t exitv = 0, lastp = 0, lastrl = 0;
   uint32_t k = 0;  // rows settled by the stride pass
   bool slow = false;
   if (s != kNone) {
+    // Chunk-relative 32-bit offsets: every stride record starts below c1 <= c0 + CH.
+    const uint32_t srel = (uint32_t)(s - c0), span = (uint32_t)(c1 - s);
+    const uint64_t lrel64 = len - c0;
+    const uint32_t lrel = lrel64 < 0xFFFFFFFFull ? (uint32_t)lrel64 : 0xFFFFFFFFu;
+    const uint32_t wrel = (uint32_t)(wend - c0);
     uint64_t rl0 = 0;
     uint32_t cnt = 0;
     if (s + 18 <= len) {
-      rl0 = lds_reclen(W, (uint32_t)(s - c0) + shift);
-      if (s + rl0 <= len) cnt = (uint32_t)((c1 - s + rl0 - 1) / rl0);
+      rl0 = lds_reclen(W, srel + shift);
+      if (s + rl0 <= len) cnt = rl0 >= span ? 1u : ceil_div_small(span, (uint32_t)rl0);
     }
-    uint32_t failmask = 0;  // bit j: this thread's j-th record failed verification
-    for (uint32_t i = tid, j = 0; i < cnt; i += NT, ++j) {
-      const uint64_t q = s + (uint64_t)i * rl0;
-      bool ok = true;
-      if (i) {
-        ok = (q + 18 <= len);
-        if (ok) ok = (lds_reclen(W, (uint32_t)(q - c0) + shift) == rl0) && (q + rl0 <= len);
+    const uint32_t r32 = cnt > 1 ? (uint32_t)rl0 : 0u;  // stride; rl0 < span <= CH when cnt > 1
+    // Quads take records in pairs (i0, i0 + NQ), hashed together: two independent chains per lane.
+    uint32_t failmask = 0;  // bit j: this quad's record quad + j*NQ failed verification
+    const uint32_t hl = (uint32_t)rl0 - 4;
+    auto stride_ok = [&](uint32_t i, uint32_t o, const Hdr& h) -> bool {
+      if (!i) return true;  // cnt > 0: the first record fits the file
+      const uint64_t rl = 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
+      return o + 18 <= lrel && rl == rl0 && o + r32 <= lrel;  // o + r32 < 2 * CH: no wrap
+    };
+#ifdef CASK_STAMPS
+    const uint64_t st_h0_ = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint32_t i0 = quad, j = 0; i0 < cnt; i0 += 2 * NQ, j += 2) {
+      const uint32_t i1 = i0 + NQ;
+      const bool has1 = i1 < cnt;
+      const uint32_t o0 = srel + i0 * r32, o1 = srel + (has1 ? i1 : i0) * r32;
+      const Hdr h0 = lds_hdr(W, o0 + shift), h1 = lds_hdr(W, o1 + shift);  // inside the window: o < CH
+      const bool ok0 = stride_ok(i0, o0, h0), ok1 = has1 && stride_ok(i1, o1, h1);
+      const bool hs0 = ok0 && (uint64_t)o0 + rl0 <= wrel, hs1 = ok1 && (uint64_t)o1 + rl0 <= wrel;  // else k_long
+      uint32_t g0 = 0, g1 = 0;
+#ifdef CASK_DIAG_NO_HASH  // diagnostic: everything but the checksum arithmetic (rows say "verified")
+      g0 = h0.stored;
+      g1 = h1.stored;
+      if (false) {
+#else
+      if (G::kWavesPerSimd <= 4) {  // registers for two chains per lane
+#endif
+        if (hs0 || hs1)
+          quad_xxh32_pair(W, (hs0 ? o0 : o1) + shift + 4, (hs1 ? o1 : o0) + shift + 4, hl, qa, g0, g1);
+      } else {
+        if (hs0) g0 = quad_xxh32(W, o0 + shift + 4, hl, qa);
+        if (hs1) g1 = quad_xxh32(W, o1 + shift + 4, hl, qa);
       }
-      if (!ok) {
-        atomicMin(&L.ffail, i);
-      } else if (record_row<G>(W, c, slots, i, (uint32_t)(q - c0), dg)) {
+      if (!ok0) {
+        if (qa == 0) atomicMin(&L.ffail, i0);
+      } else if (stride_row<G>(L, par, slots, i0, o0, h0, hs0 && g0 != h0.stored, qa)) {  // data.rs:193-198
         failmask |= 1u << j;
       }
+      if (has1) {
+        if (!ok1) {
+          if (qa == 0) atomicMin(&L.ffail, i1);
+        } else if (stride_row<G>(L, par, slots, i1, o1, h1, hs1 && g1 != h1.stored, qa)) {
+          failmask |= 2u << j;
+        }
+      }
     }
+#ifdef CASK_STAMPS
+    dg.st[8] += __builtin_amdgcn_s_memtime() - st_h0_;  // phase 8: the stride pass's rows
+#endif
     BAR();
     k = L.ffail < cnt ? L.ffail : cnt;
-    for (uint32_t m = failmask; m; m &= m - 1) {
-      const uint32_t i = tid + (uint32_t)__builtin_ctz(m) * NT;
-      if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
+    pf_n = k < G::kRowBuf ? k : G::kRowBuf;  // buffered rows of the settled records [0, k)
+    pf_slots = slots;
+    if (qa == 0) {
+      for (uint32_t m = failmask; m; m &= m - 1) {
+        const uint32_t i = quad + (uint32_t)__builtin_ctz(m) * NQ;
+        if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
+      }
     }
     if (k == cnt && cnt) {
       n = cnt;
@@ -283,6 +411,11 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   // each step tests up to 256 equal-stride successors with one LDS round trip), then verify
   // those records, one per thread.
   if (slow) {
+    // starts[] overlays both row buffers: flush this chunk's buffered rows now (the previous chunk's
+    // were read before this chunk's barrier... and its flush loop runs before process_chunk)
+    flush_rows<G>(L, par, pf_slots, pf_n);
+    pf_n = 0;
+    BAR();
     if (wave == 0) {
       uint32_t nn = k;
       uint64_t ex = 0, lp = 0, lr = 0;
@@ -348,8 +481,8 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     exitv = L.exitv;
     lastp = L.lastp;
     lastrl = L.lastrl;
-    for (uint32_t r = k + tid; r < n; r += NT) {
-      if (record_row<G>(W, c, slots, r, L.starts[r], dg)) atomicMin(&a.file_err[c.fi], err_base + r);
+    for (uint32_t r = k + quad; r < n; r += NQ) {
+      if (quad_row<G>(W, c, slots, r, L.starts[r], qa, dg) && qa == 0) atomicMin(&a.file_err[c.fi], err_base + r);
     }
   }
   DCHECK(n <= a.slot_cap && t < a.total_chunks, "n %u t %llu", n, (unsigned long long)t);
@@ -381,26 +514,37 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 // `files` is the same table as a.files, passed as a restrict-qualified argument: the kernel never
 // writes it, so its (wave-uniform) loads go through the scalar cache.
 template <class G, bool EXACT>
-__global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDesc* __restrict__ files_r) {
+__global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanArgs a, const FileDesc* __restrict__ files_r) {
   __shared__ ScanLdsT<G> L;
 #ifdef CASK_VEC_FILES
   const FileDesc* files = a.files;
 #else
   const FileDesc* __restrict__ files = files_r;
 #endif
-  // XCD x (= b mod 8 under round-robin placement) owns one contiguous eighth of the chunks. Its
-  // nx workgroups take runs of a.run consecutive chunks round-robin, so together they sweep the
-  // eighth front to back (a compact set of pages and DRAM rows in flight) while each run is
+  // Runs of a.run consecutive chunks are handed out in order by a counter (one atomic per run, a
+  // run ahead), so workgroups that run slower take fewer runs and all finish together; each run is
   // walked in order with a carry.
-  const uint32_t x = blockIdx.x & 7, nx = gridDim.x >> 3, j = blockIdx.x >> 3;
-  const uint64_t per = (a.total_chunks + 7) >> 3;
-  const uint64_t xs = x * per < a.total_chunks ? x * per : a.total_chunks;
-  const uint64_t xe = xs + per < a.total_chunks ? xs + per : a.total_chunks;
-  const uint64_t R = a.run, stride = (uint64_t)nx * R;
-  uint64_t t = xs + (uint64_t)j * R;
-  uint64_t run_end = t + R < xe ? t + R : xe;
-  if (t >= xe) return;
+  const uint64_t R = a.run;
+  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  uint32_t my_claim = 0;  // thread 0: the run claimed for after the current one
+  bool publish = false;   // thread 0: my_claim still to be published in L.claimed
+  if (threadIdx.x == 0) {
+    L.found = atomicAdd(&a.ctr->run_next, 1u);
+    L.claimed = atomicAdd(&a.ctr->run_next, 1u);
+  }
+  BAR();
+  const uint64_t r0 = L.found;
+  if (r0 >= nruns) return;
+  uint64_t t = r0 * R;
+  uint64_t run_end = t + R < a.total_chunks ? t + R : a.total_chunks;
+  BAR();  // L.found is reset by thread 0 below
+#ifdef CASK_STAMPS
+  const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();  // 100 MHz: calibrates s_memtime, shows imbalance
+#endif
   Diag dg{};
+  uint32_t par = 0;          // row buffer of the current chunk
+  uint32_t pf_n = 0;         // rows of the previous chunk waiting in row buffer par ^ 1
+  uint32_t* pf_slots = a.slots;
   uint64_t carry = 0;  // chain position entering chunk t, when known
   bool known = false;  // only the first chunk of the range (and chunks after a failed search) search
   ChunkPos cur = locate<G>(files, a.nfiles, t);
@@ -414,6 +558,10 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
     if (threadIdx.x == 0) {  // every reader of the last chunk's values is past the end barrier
       L.found = 0xFFFFFFFFu;
       L.ffail = 0xFFFFFFFFu;
+      if (publish) {
+        L.claimed = my_claim;
+        publish = false;
+      }
     }
     stage_store<G>(L, v, cur);
     BAR();
@@ -443,22 +591,46 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
     // waiting for it never waits for the prefetch
     const uint64_t s_exact = EXACT ? a.spec[t] : 0;
     uint64_t tn = t + 1, next_end = run_end;
-    if (tn >= run_end) {  // next run of this workgroup
-      tn = run_end - R + stride;
-      next_end = tn + R < xe ? tn + R : xe;
+    if (tn >= run_end) {  // next run of this workgroup: the one claimed a run ago
+      const uint64_t rn = L.claimed;
+      tn = rn < nruns ? rn * R : a.total_chunks;
+      next_end = tn + R < a.total_chunks ? tn + R : a.total_chunks;
+      if (threadIdx.x == 0 && rn < nruns) {
+        my_claim = atomicAdd(&a.ctr->run_next, 1u);  // published at the next chunk's top
+        publish = true;
+      }
     }
-    const bool more = tn < xe;
+    const bool more = tn < a.total_chunks;
 #ifdef CASK_STAMPS
     const uint64_t st_pf_ = __builtin_amdgcn_s_memtime();
 #endif
-    if (more) stage_issue<G>(v, locate<G>(files, a.nfiles, tn), a.stamps, tn);  // prefetch the next window
+    // the previous chunk's buffered rows go out ahead of the prefetch: no vector-memory instruction
+    // is issued while the chunk is processed, and none waits behind the prefetch's loads
+    flush_rows<G>(L, par ^ 1, pf_slots, pf_n);
+    pf_n = 0;
+    ChunkPos nxt = cur;
+#ifndef CASK_LATE_PREFETCH
+    if (more) {
+      nxt = next_chunk<G>(files, a.nfiles, cur, t, tn);
+      stage_issue<G>(v, nxt, a.stamps, tn);  // prefetch the next window
+    }
+#endif
 #ifdef CASK_STAMPS
     dg.st[5] += __builtin_amdgcn_s_memtime() - st_pf_;  // phase 5: issuing the prefetch
 #endif
 #ifndef CASK_STAGE_ONLY
-    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, dg);
+    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, par, pf_n, pf_slots, dg);
+#ifdef CASK_LATE_PREFETCH  // diagnostic: the next window's loads issued after this chunk's row stores
+    if (more) {
+      nxt = next_chunk<G>(files, a.nfiles, cur, t, tn);
+      stage_issue<G>(v, nxt, a.stamps, tn);
+    }
+#endif
 #else  // diagnostic: staging and prefetch only (the memory side of the kernel in isolation)
     if (threadIdx.x == 0 && L.win[cur.n16] == 0x12345678u) a.count[t] = 1;  // keep the staged bytes live
+#ifdef CASK_STAGE_WRITES  // diagnostic: plus 113 16-B slot rows per chunk (the stride pass's write traffic)
+    if (threadIdx.x < 113) ((u32x4*)(a.slots + ((uint64_t)t * a.slot_cap) * 4))[threadIdx.x] = ((const u32x4*)L.win)[threadIdx.x];
+#endif
 #endif
 #ifdef CASK_STAMPS
     const uint64_t st_end_ = __builtin_amdgcn_s_memtime();
@@ -468,13 +640,21 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
 #ifdef CASK_STAMPS
     dg.st[6] += __builtin_amdgcn_s_memtime() - st_end_;  // phase 6: end-of-chunk barrier
 #endif
+    par ^= 1;
     if (!more) break;
     t = tn;
     run_end = next_end;
-    cur = locate<G>(files, a.nfiles, t);
+    cur = nxt;
   }
+  flush_rows<G>(L, par ^ 1, pf_slots, pf_n);  // the last chunk's rows (visible: the loop ended on a barrier)
 #ifdef CASK_STAMPS
   dg.st[7] = __builtin_amdgcn_s_memtime() - dg.st[7];
+  if (a.stamps && threadIdx.x == 0) {
+    const uint64_t rt = __builtin_amdgcn_s_memrealtime() - rt0_;
+    atomicAdd(&a.stamps[11], (unsigned long long)rt);
+    atomicMax(&a.stamps[12], (unsigned long long)rt);
+    atomicAdd(&a.stamps[13], 1ull);
+  }
   if (a.stamps && threadIdx.x == 0) atomicAdd(&a.stamps[7], (unsigned long long)dg.st[7]);
   if (a.stamps && threadIdx.x == 0)
     for (int i = 0; i < 10; ++i)
@@ -482,9 +662,9 @@ __global__ __launch_bounds__(G::kNT) void k_scan_chunks(ScanArgs a, const FileDe
 #endif
 }
 
-using GeoA = Geo<32768, 4096, 256, 4>;
-using GeoB = Geo<16384, 1536, 128, 8>;
-using GeoC = Geo<8192, 1024, 64, 16>;
+using GeoA = Geo<32768, 4080, 256, 4>;  // window + 16-B slop = 9 loads per thread
+using GeoB = Geo<16384, 2032, 128, 8>;
+using GeoC = Geo<8192, 1008, 64, 16>;
 
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
@@ -494,12 +674,15 @@ template <class G>
 static void launch_geo(const ScanArgs& a, void* stream) {
   int dev = 0, cus = 256;
   if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-  uint64_t grid = (uint64_t)cus * G::kPerCU;
+  // CASK_WG_PER_CU (diagnostic): fewer resident workgroups per CU than the LDS allows
+  static const uint32_t per_cu = getenv("CASK_WG_PER_CU") ? (uint32_t)atoi(getenv("CASK_WG_PER_CU")) : G::kPerCU;
+  uint64_t grid = (uint64_t)cus * per_cu;
   grid = (grid + 7) & ~7ull;
   const uint64_t need = (a.total_chunks + 7) & ~7ull;  // never more workgroups than chunks
   if (need < grid) grid = need;
   // CASK_LDS_PAD (diagnostic): extra dynamic LDS per workgroup, to lower workgroups per CU
   static const uint32_t pad = getenv("CASK_LDS_PAD") ? (uint32_t)atoi(getenv("CASK_LDS_PAD")) : 0u;
+  (void)hipMemsetAsync(&a.ctr->run_next, 0, sizeof(a.ctr->run_next), S(stream));
   if (a.exact)
     hipLaunchKernelGGL((k_scan_chunks<G, true>), dim3((uint32_t)grid), dim3(G::kNT), pad, S(stream), a, a.files);
   else

@@ -31,6 +31,8 @@ constexpr uint32_t kTileChunks = 1024;  // chunks per validation tile (k_pipelin
 struct Counters {
   unsigned long long nlong;      // records longer than the LDS window
   unsigned long long walk_steps; // repair walk iterations
+  unsigned int run_next;         // k_scan_chunks: next run of chunks to hand out (zeroed per launch)
+  unsigned int pad;
 };
 
 struct ScanArgs {

@@ -40,6 +40,10 @@ def main():
     print(f"chunks={chunks} rows={res.count} timings={t}")
     tot = st[7]
     print(f"chunk iterations stamped: {st[4]}")
+    if st[13]:
+        mean_ns = st[11] * 10.0 / st[13]
+        print(f"workgroups {st[13]}: mean life {mean_ns / 1e3:.1f} us, max {st[12] * 10.0 / 1e3:.1f} us "
+              f"(summed over {args.iters} calls); s_memtime units per ns {st[7] / (st[11] * 10.0):.3f}")
     for i, p in enumerate(PHASES):
         print(f"{p:14s} {st[i] / chunks:12.0f} cyc/WG  {100.0 * st[i] / max(tot, 1):5.1f}%")
 
