@@ -127,6 +127,35 @@ __device__ __forceinline__ uint32_t lds_xxh32(const uint32_t* w, uint32_t xs, ui
   return lds_tail_fin(w, xs + (nstr << 4), len & 15, h + len);
 }
 
+// XXH32 (seed 0) of LDS bytes [xs, xs + len) by one lane with its four stripe accumulators
+// interleaved (the stride pass: one record per lane). Two stripes' aligned dwords are read per step.
+__device__ __forceinline__ uint32_t lane_xxh32(const uint32_t* w, uint32_t xs, uint32_t len) {
+  uint32_t h;
+  const uint32_t nstr = len >> 4, sh = xs & 3;
+  uint32_t i = xs >> 2;
+  if (nstr) {
+    Acc a = acc_init(0);
+    uint32_t d0 = w[i];
+    uint32_t s = 0;
+    for (; s + 2 <= nstr; s += 2) {
+      const uint32_t d1 = w[i + 1], d2 = w[i + 2], d3 = w[i + 3], d4 = w[i + 4];
+      const uint32_t e1 = w[i + 5], e2 = w[i + 6], e3 = w[i + 7], e4 = w[i + 8];
+      acc_stripe(a, fun(d0, d1, sh), fun(d1, d2, sh), fun(d2, d3, sh), fun(d3, d4, sh));
+      acc_stripe(a, fun(d4, e1, sh), fun(e1, e2, sh), fun(e2, e3, sh), fun(e3, e4, sh));
+      d0 = e4;
+      i += 8;
+    }
+    if (s < nstr) {
+      const uint32_t d1 = w[i + 1], d2 = w[i + 2], d3 = w[i + 3], d4 = w[i + 4];
+      acc_stripe(a, fun(d0, d1, sh), fun(d1, d2, sh), fun(d2, d3, sh), fun(d3, d4, sh));
+    }
+    h = acc_merge(a);
+  } else {
+    h = P5;
+  }
+  return lds_tail_fin(w, xs + (nstr << 4), len & 15, h + len);
+}
+
 // Quad-lane DPP moves (quad_perm): lane a of each group of 4 receives lane perm[a]'s value.
 __device__ __forceinline__ uint32_t quad_xor1(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);  // [1,0,3,2]

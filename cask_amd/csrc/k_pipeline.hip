@@ -104,7 +104,7 @@ __global__ __launch_bounds__(256) void k_val_reduce(ScanArgs a) {
       const uint64_t g = fd.first_chunk + c;
       const unsigned long long e = chunk_exit(a, g);
       mx = mx > e ? mx : e;
-      sm += a.count[g];
+      sm += a.count[g] & kCountMask;
     }
   }
   unsigned long long em, es, tm, ts;
@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void k_val_apply(ScanArgs a) {
     if (c < fd.nchunks) {
       const uint64_t g = fd.first_chunk + c;
       e[j] = chunk_exit(a, g);
-      cn[j] = a.count[g];
+      cn[j] = a.count[g] & kCountMask;
     }
     mx = mx > e[j] ? mx : e[j];
     sm += cn[j];
@@ -240,9 +240,27 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a, const uint64_t* sum
     const uint32_t fi = find_file(a.files, a.nfiles, t);
     const FileDesc fd = a.files[fi];
     const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
-    const uint32_t n = a.count[t];
+    const uint32_t cw = a.count[t], n = cw & kCountMask;
     const uint64_t dst0 = row_off[fi] + a.base[t];
     const u32x4* src = (const u32x4*)(a.slots + (uint64_t)t * a.slot_cap * 4);
+    if (cw & kCountRegular) {  // rows from row 0: equal lengths, consecutive sequences, all Ok
+      const u32x4 w = src[0];
+      const uint64_t p0 = c0 + ((w.w >> 16) & 0x7FFFu);
+      const uint32_t ksz = w.w & 0xFFFFu;
+      const uint64_t rl = 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+      const uint64_t seq0 = (uint64_t)w.x | ((uint64_t)w.y << 32);
+      for (uint32_t r = lane; r < n; r += 64) {
+        const uint64_t d = dst0 + r;
+        if (d < a.row_cap) {
+          a.pos[d] = p0 + r * rl;
+          a.seq[d] = seq0 + r;
+          a.vsz[d] = w.z;
+          a.ksz[d] = (uint16_t)ksz;
+          a.status[d] = kRowOk;
+        }
+      }
+      continue;
+    }
     for (uint32_t r = lane; r < n; r += 64) {
       const u32x4 w = src[r];
       const uint64_t p = c0 + ((w.w >> 16) & 0x7FFFu);

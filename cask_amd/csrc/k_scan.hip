@@ -30,7 +30,16 @@ struct Geo {
   static constexpr uint32_t kMaxStartsG = CH / 18 + 2;  // every record is >= 18 bytes
   static constexpr uint32_t kRowBuf = kMaxStartsG / 16;   // slot rows per LDS row buffer (2 in starts' space)
   static constexpr uint32_t kWinWords = (kWinB + 64) / 4;
-  static constexpr uint32_t kNL = ((kWinB + 16) / 16 + NT - 1) / NT;  // 16-B loads per thread
+  // With 4+ waves, the last wave loads nothing: it issues the workgroup's stores (slot rows, chunk
+  // table, run claims), so no wave that stages the window ever waits for a store to complete.
+#ifndef CASK_NO_STORE_WAVE
+  static constexpr bool kStoreWave = NT >= 256;
+#else  // diagnostic: every wave stages; stores issued from wherever they arise
+  static constexpr bool kStoreWave = false;
+#endif
+  static constexpr uint32_t kLoadT = kStoreWave ? NT - 64 : NT;  // threads that stage the window
+  static constexpr uint32_t kMetaT = kStoreWave ? NT - 64 : 0;   // the thread that issues the stores
+  static constexpr uint32_t kNL = ((kWinB + 16) / 16 + kLoadT - 1) / kLoadT;  // 16-B loads per loader
 };
 
 // Records no longer than this are "short": the boundary search verifies them first.
@@ -49,6 +58,7 @@ struct __attribute__((aligned(16))) ScanLdsT {
   uint32_t found, n;  // search result; slow path: rows of the chunk
   uint32_t claimed;   // the run this workgroup takes after its current one
   uint32_t ffail;     // stride pass: first row whose header breaks the stride
+  uint32_t irreg;     // stride pass: some row breaks the regular-chunk pattern (kCountRegular)
   uint64_t exitv, lastp, lastrl;  // slow path: walk results (wave 0 -> workgroup)
 };
 
@@ -122,18 +132,19 @@ template <class G>
 __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& c,
                                             unsigned long long* dbg = nullptr, uint64_t t = 0) {
   const gu32x4* src = (const gu32x4*)c.a0;
-  DCHECK(c.n16 >= 1 && c.n16 <= G::kNL * G::kNT && c.n16 * 16 <= G::kWinWords * 4 &&
+  DCHECK(c.n16 >= 1 && c.n16 <= G::kNL * G::kLoadT && c.n16 * 16 <= G::kWinWords * 4 &&
              c.a0 >= ((uintptr_t)c.data & ~(uintptr_t)15) && c.a0 + 16ull * c.n16 <= (((uintptr_t)c.data + c.len + 15) & ~(uintptr_t)15),
          "n16 %u a0 %llx data %llx len %llu c0 %llu", c.n16, (unsigned long long)c.a0,
          (unsigned long long)(uintptr_t)c.data, (unsigned long long)c.len, (unsigned long long)c.c0);
-  if (c.n16 == G::kNL * G::kNT) {  // the whole window is inside the file: no clamping
+  if (G::kStoreWave && threadIdx.x >= G::kLoadT) return;
+  if (c.n16 == G::kNL * G::kLoadT) {  // the whole window is inside the file: no clamping
 #pragma unroll
-    for (uint32_t j = 0; j < G::kNL; ++j) v[j] = src[threadIdx.x + j * G::kNT];
+    for (uint32_t j = 0; j < G::kNL; ++j) v[j] = src[threadIdx.x + j * G::kLoadT];
     return;
   }
 #pragma unroll
   for (uint32_t j = 0; j < G::kNL; ++j) {
-    const uint32_t i = threadIdx.x + j * G::kNT;
+    const uint32_t i = threadIdx.x + j * G::kLoadT;
     const gu32x4* ptr = src + (i < c.n16 ? i : c.n16 - 1);
     ADDR_GUARD(dbg, ptr, (uintptr_t)c.data & ~(uintptr_t)15, (uintptr_t)c.data + c.len + 16, 1, t)
     v[j] = *ptr;
@@ -143,15 +154,19 @@ __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& 
 template <class G>
 __device__ __forceinline__ void stage_store(ScanLdsT<G>& L, const u32x4 (&v)[G::kNL], const ChunkPos& c) {
   u32x4* dst = (u32x4*)L.win;
-  if (c.n16 == G::kNL * G::kNT) {
+  if (G::kStoreWave && threadIdx.x >= G::kLoadT) return;
+  if (c.n16 == G::kNL * G::kLoadT) {
 #pragma unroll
-    for (uint32_t j = 0; j < G::kNL; ++j) dst[threadIdx.x + j * G::kNT] = v[j];
+    for (uint32_t j = 0; j < G::kNL; ++j) dst[threadIdx.x + j * G::kLoadT] = v[j];
     return;
   }
 #pragma unroll
   for (uint32_t j = 0; j < G::kNL; ++j) {
-    const uint32_t i = threadIdx.x + j * G::kNT;
-    if (i < c.n16) dst[i] = v[j];
+    const uint32_t i = threadIdx.x + j * G::kLoadT;
+    // lanes past the window loaded the last 16-B unit again (stage_issue clamps): storing that same
+    // value to it keeps every v[j] consumed on every path, so the compiler's memory-counter waits
+    // for these loads all happen here and none is left over for the next prefetch to wait on
+    dst[i < c.n16 ? i : c.n16 - 1] = v[j];
   }
 }
 
@@ -204,6 +219,13 @@ __device__ __forceinline__ bool quad_row(const uint32_t* W, const ChunkPos& c, u
   return fail;
 }
 
+// A value every lane holds equally (read from the same LDS word), moved to scalar registers so
+// that the loops and branches it controls compile to scalar control flow.
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // ceil(a / b) for 0 < b < a <= 2^16 (wave-uniform): a float quotient, corrected to the exact one.
 __device__ __forceinline__ uint32_t ceil_div_small(uint32_t a, uint32_t b) {
   uint32_t c = (uint32_t)__builtin_ceilf((float)a / (float)b);
@@ -237,7 +259,13 @@ __device__ __forceinline__ bool stride_row(ScanLdsT<G>& L, uint32_t par, uint32_
 template <class G>
 __device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t n) {
   u32x4* srow = (u32x4*)slots;
-  for (uint32_t r = threadIdx.x; r < n; r += G::kNT) {
+  if (G::kStoreWave && threadIdx.x < G::kLoadT) return;  // the store wave's job
+  const uint32_t first = G::kStoreWave ? threadIdx.x - G::kLoadT : threadIdx.x;
+  const uint32_t step = G::kStoreWave ? 64u : G::kNT;
+#ifdef CASK_DIAG_ONE_ROW  // diagnostic (wrong rows): one 16-B store per chunk instead of n
+  if (n > 1) n = 1;
+#endif
+  for (uint32_t r = first; r < n; r += step) {
 #ifndef CASK_NO_SLOT_STORE
 #ifdef CASK_NT_ROWS
     __builtin_nontemporal_store(L.rows[par][r], &srow[r]);
@@ -304,6 +332,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       }
     }
     s = found ? c0 + L.found : kNone;  // no atomicMin after the last step's barriers
+    s = uni64(s);
   }
   STAMP(0)
 
@@ -311,8 +340,8 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   // length rl0 and let thread i take the record at s + i*rl0 — check its header, verify it,
   // write its row. The first i whose header breaks the stride (L.ffail) ends the run of true
   // records; rows past it are discarded. A file of equal-length records never leaves this pass.
-#if defined(CASK_SLOTS_SCRATCH)  // diagnostic (wrong rows): every chunk of a workgroup writes the same, L2-resident slots
-  uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * a.slot_cap) * 4;
+#if defined(CASK_SLOTS_SCRATCH)  // diagnostic (wrong rows): every chunk of a workgroup writes the same 2 KiB (L2-resident)
+  uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * 128) * 4;
 #elif !defined(CASK_DENSE_SLOTS)
   uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
 #else  // diagnostic (wrong rows): each workgroup appends its rows densely, to time the write locality
@@ -324,7 +353,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   uint32_t n = 0;
   uint64_t exitv = 0, lastp = 0, lastrl = 0;
   uint32_t k = 0;  // rows settled by the stride pass
-  bool slow = false;
+  bool slow = false, regular = false;
   if (s != kNone) {
     // Chunk-relative 32-bit offsets: every stride record starts below c1 <= c0 + CH.
     const uint32_t srel = (uint32_t)(s - c0), span = (uint32_t)(c1 - s);
@@ -334,12 +363,12 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     uint64_t rl0 = 0;
     uint32_t cnt = 0;
     if (s + 18 <= len) {
-      rl0 = lds_reclen(W, srel + shift);
+      rl0 = uni64(lds_reclen(W, srel + shift));  // wave-uniform: scalar loop counts in the hash
       if (s + rl0 <= len) cnt = rl0 >= span ? 1u : ceil_div_small(span, (uint32_t)rl0);
     }
     const uint32_t r32 = cnt > 1 ? (uint32_t)rl0 : 0u;  // stride; rl0 < span <= CH when cnt > 1
-    // Quads take records in pairs (i0, i0 + NQ), hashed together: two independent chains per lane.
-    uint32_t failmask = 0;  // bit j: this quad's record quad + j*NQ failed verification
+    // One record per lane (STRIDE_QUAD: per quad of lanes, two records per quad).
+    uint32_t failmask = 0;  // bit j: this lane's (quad's) j-th record failed verification
     const uint32_t hl = (uint32_t)rl0 - 4;
     auto stride_ok = [&](uint32_t i, uint32_t o, const Hdr& h) -> bool {
       if (!i) return true;  // cnt > 0: the first record fits the file
@@ -349,6 +378,42 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 #ifdef CASK_STAMPS
     const uint64_t st_h0_ = __builtin_amdgcn_s_memtime();
 #endif
+    // the first record's header, for the regular-chunk test (one LDS broadcast)
+    const Hdr hf = cnt ? lds_hdr(W, srel + shift) : Hdr{};
+#ifndef CASK_STRIDE_QUAD
+    bool irreg = false;
+    for (uint32_t i = tid, j = 0; i < cnt; i += NT, ++j) {
+      const uint32_t o = srel + i * r32;
+      const Hdr h = lds_hdr(W, o + shift);  // inside the window: o < CH
+      const bool ok = stride_ok(i, o, h);
+      const bool hs = ok && (uint64_t)o + rl0 <= wrel;  // else k_long
+#ifdef CASK_DIAG_NO_HASH  // diagnostic: everything but the checksum arithmetic (rows say "verified")
+      const uint32_t g = h.stored;
+#else
+      const uint32_t g = hs ? lane_xxh32(W, o + shift + 4, hl) : h.stored;
+#endif
+      if (!ok) {
+        atomicMin(&L.ffail, i);
+      } else {
+        const bool bad = hs && g != h.stored;  // data.rs:193-198
+        u32x4 row;
+        row.x = (uint32_t)h.seq;
+        row.y = (uint32_t)(h.seq >> 32);
+        row.z = h.vsz;
+        row.w = h.ksz | (o << 16) | (bad ? kSlotBad : 0u);
+        if (i < G::kRowBuf) {
+          L.rows[par][i] = row;
+        } else {
+#ifndef CASK_NO_SLOT_STORE
+          ((u32x4*)slots)[i] = row;
+#endif
+        }
+        if (bad) failmask |= 1u << j;
+        irreg |= bad || !hs || h.ksz != hf.ksz || h.vsz != hf.vsz || h.seq != hf.seq + i;
+      }
+    }
+    if (__ballot(irreg) && lane == 0) atomicOr(&L.irreg, 1u);
+#else
     for (uint32_t i0 = quad, j = 0; i0 < cnt; i0 += 2 * NQ, j += 2) {
       const uint32_t i1 = i0 + NQ;
       const bool has1 = i1 < cnt;
@@ -383,6 +448,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
         }
       }
     }
+#endif
 #ifdef CASK_STAMPS
     dg.st[8] += __builtin_amdgcn_s_memtime() - st_h0_;  // phase 8: the stride pass's rows
 #endif
@@ -390,12 +456,23 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     k = L.ffail < cnt ? L.ffail : cnt;
     pf_n = k < G::kRowBuf ? k : G::kRowBuf;  // buffered rows of the settled records [0, k)
     pf_slots = slots;
+#ifndef CASK_STRIDE_QUAD
+    regular = a.regular_ok && k == cnt && cnt && !L.irreg;
+    if (regular) pf_n = 1;  // row 0 describes them all (kCountRegular)
+#endif
+#ifndef CASK_STRIDE_QUAD
+    for (uint32_t m = failmask; m; m &= m - 1) {
+      const uint32_t i = tid + (uint32_t)__builtin_ctz(m) * NT;
+      if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
+    }
+#else
     if (qa == 0) {
       for (uint32_t m = failmask; m; m &= m - 1) {
         const uint32_t i = quad + (uint32_t)__builtin_ctz(m) * NQ;
         if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
       }
     }
+#endif
     if (k == cnt && cnt) {
       n = cnt;
       lastp = s + (uint64_t)(cnt - 1) * rl0;
@@ -486,10 +563,10 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     }
   }
   DCHECK(n <= a.slot_cap && t < a.total_chunks, "n %u t %llu", n, (unsigned long long)t);
-  if (tid == 0) {
+  if (tid == G::kMetaT) {
     if (!EXACT) a.spec[t] = s;
     a.exit[t] = (s == kNone) ? 0 : exitv;
-    a.count[t] = n;
+    a.count[t] = n | (regular ? kCountRegular : 0u);
     // a record that does not fit the window is hashed from HBM by k_long (only the last can)
     a.long_r[t] = (s != kNone && exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
   }
@@ -526,9 +603,9 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   // walked in order with a carry.
   const uint64_t R = a.run;
   const uint64_t nruns = (a.total_chunks + R - 1) / R;
-  uint32_t my_claim = 0;  // thread 0: the run claimed for after the current one
-  bool publish = false;   // thread 0: my_claim still to be published in L.claimed
-  if (threadIdx.x == 0) {
+  uint32_t my_claim = 0;  // thread kMetaT: the run claimed for after the current one
+  bool publish = false;   // thread kMetaT: my_claim still to be published in L.claimed
+  if (threadIdx.x == G::kMetaT) {
     L.found = atomicAdd(&a.ctr->run_next, 1u);
     L.claimed = atomicAdd(&a.ctr->run_next, 1u);
   }
@@ -558,10 +635,11 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
     if (threadIdx.x == 0) {  // every reader of the last chunk's values is past the end barrier
       L.found = 0xFFFFFFFFu;
       L.ffail = 0xFFFFFFFFu;
-      if (publish) {
-        L.claimed = my_claim;
-        publish = false;
-      }
+      L.irreg = 0u;
+    }
+    if (threadIdx.x == G::kMetaT && publish) {
+      L.claimed = my_claim;
+      publish = false;
     }
     stage_store<G>(L, v, cur);
     BAR();
@@ -595,7 +673,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
       const uint64_t rn = L.claimed;
       tn = rn < nruns ? rn * R : a.total_chunks;
       next_end = tn + R < a.total_chunks ? tn + R : a.total_chunks;
-      if (threadIdx.x == 0 && rn < nruns) {
+      if (threadIdx.x == G::kMetaT && rn < nruns) {
         my_claim = atomicAdd(&a.ctr->run_next, 1u);  // published at the next chunk's top
         publish = true;
       }
@@ -606,8 +684,10 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #endif
     // the previous chunk's buffered rows go out ahead of the prefetch: no vector-memory instruction
     // is issued while the chunk is processed, and none waits behind the prefetch's loads
+#ifndef CASK_FLUSH_LATE
     flush_rows<G>(L, par ^ 1, pf_slots, pf_n);
     pf_n = 0;
+#endif
     ChunkPos nxt = cur;
 #ifndef CASK_LATE_PREFETCH
     if (more) {
@@ -617,6 +697,10 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #endif
 #ifdef CASK_STAMPS
     dg.st[5] += __builtin_amdgcn_s_memtime() - st_pf_;  // phase 5: issuing the prefetch
+#endif
+#ifdef CASK_FLUSH_LATE  // diagnostic: the flush behind the prefetch's loads
+    flush_rows<G>(L, par ^ 1, pf_slots, pf_n);
+    pf_n = 0;
 #endif
 #ifndef CASK_STAGE_ONLY
     process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, par, pf_n, pf_slots, dg);
@@ -662,7 +746,10 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #endif
 }
 
-using GeoA = Geo<32768, 4080, 256, 4>;  // window + 16-B slop = 9 loads per thread
+#ifndef CASK_HALO_A
+#define CASK_HALO_A 4080
+#endif
+using GeoA = Geo<32768, CASK_HALO_A, 256, 4>;  // window + 16-B slop = 9 loads per thread
 using GeoB = Geo<16384, 2032, 128, 8>;
 using GeoC = Geo<8192, 1008, 64, 16>;
 

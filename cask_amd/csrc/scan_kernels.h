@@ -17,6 +17,14 @@ enum : uint8_t { kRowOk = 0, kRowChecksum = 1, kRowEof = 2 };
 // Status is implied: EOF if the record runs past the file end, else bad bit ? CHECKSUM : OK.
 constexpr uint32_t kSlotBad = 0x80000000u;
 
+// count[c] flag: the chunk is regular — its n rows are records of one length rl, all verified Ok
+// and inside the window, with key size, value size and sequence step of one from its slot row 0
+// (row r = pos0 + r*rl, seq0 + r, vsz0, ksz0). Only row 0 is stored; k_compact expands the rest.
+// Set only when the dense output is requested (ScanArgs.regular_ok); the segmented output keeps
+// every row.
+constexpr uint32_t kCountRegular = 0x80000000u;
+constexpr uint32_t kCountMask = 0x7FFFFFFFu;
+
 struct FileDesc {
   const uint8_t* data;   // device pointer to the file's bytes
   uint64_t len;
@@ -71,7 +79,7 @@ struct ScanArgs {
   uint64_t row_cap;
   unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums
   uint32_t run;                // k_scan_chunks: consecutive chunks a workgroup walks with a carry
-  uint32_t pad_;
+  uint32_t regular_ok;         // 1: a regular chunk may keep only its first slot row (kCountRegular)
 };
 
 constexpr uint32_t kDefaultRun = 16;

@@ -201,7 +201,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
 
   // file table
   const uint32_t chunk = geometry_chunk(c->geo);
-  const uint32_t slot_cap = chunk / 18 + 2;
+  // slot rows per chunk, rounded to 8 rows: every chunk's rows start on a 128-B line, so the
+  // scan's 1-KiB row stores cover whole lines and need no fill from HBM
+  const uint32_t slot_cap = ((chunk / 18 + 2) + 7) & ~7u;
   uint64_t total_chunks = 0, total_tiles = 0;
   const size_t head_words = sizeof(SummaryHead) / 8;
   const size_t sum_words = head_words + (nfiles + 1) + 4ull * nfiles;
@@ -274,6 +276,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     static const uint32_t run = getenv("CASK_RUN_CHUNKS") ? (uint32_t)atoi(getenv("CASK_RUN_CHUNKS")) : kDefaultRun;
     a.run = run ? run : 1;
   }
+  // regular chunks keep only their first slot row when the rows go to the dense output (k_compact
+  // expands them); the segmented output hands the slots to the caller, so every row is written
+  a.regular_ok = (rows && !getenv("CASK_NO_REGULAR")) ? 1u : 0u;
 #ifdef CASK_STAMPS
   if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
 #endif
