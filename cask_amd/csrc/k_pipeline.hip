@@ -243,8 +243,8 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a, const uint64_t* sum
     const uint32_t cw = a.count[t], n = cw & kCountMask;
     const uint64_t dst0 = row_off[fi] + a.base[t];
     const u32x4* src = (const u32x4*)(a.slots + (uint64_t)t * a.slot_cap * 4);
-    if (cw & kCountRegular) {  // rows from row 0: equal lengths, consecutive sequences, all Ok
-      const u32x4 w = src[0];
+    if (cw & kCountRegular) {  // rows from the first: equal lengths, consecutive sequences, all Ok
+      const u32x4 w = ((const u32x4*)a.desc)[t];
       const uint64_t p0 = c0 + ((w.w >> 16) & 0x7FFFu);
       const uint32_t ksz = w.w & 0xFFFFu;
       const uint64_t rl = 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);

@@ -255,6 +255,15 @@ __device__ __forceinline__ bool stride_row(ScanLdsT<G>& L, uint32_t par, uint32_
   return bad;
 }
 
+// A chunk's entries in the chunk table (wave-uniform): written by the store wave for a whole run
+// of chunks at once (consecutive entries: a few full-line stores instead of five scattered ones
+// per chunk), or straight away where there is no store wave.
+struct Meta {
+  uint64_t spec, exit;
+  uint32_t count, long_r;
+  u32x4 desc;  // first row of a regular chunk
+};
+
 // Slot rows [0, n) of a chunk from LDS row buffer `par` to its slots, one 16-B store per row.
 template <class G>
 __device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t n) {
@@ -282,7 +291,7 @@ __device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_
 template <class G, bool EXACT>
 __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a, uint64_t t, const ChunkPos& c,
                                               uint64_t s_exact, uint64_t& carry, bool& known, uint32_t par,
-                                              uint32_t& pf_n, uint32_t*& pf_slots, Diag& dg) {
+                                              uint32_t& pf_n, uint32_t*& pf_slots, Meta& m, Diag& dg) {
   constexpr uint32_t NT = G::kNT;
   constexpr uint32_t NQ = NT / 4;  // quads: one record per quad of lanes
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, quad = tid >> 2, qa = tid & 3;
@@ -458,7 +467,13 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     pf_slots = slots;
 #ifndef CASK_STRIDE_QUAD
     regular = a.regular_ok && k == cnt && cnt && !L.irreg;
-    if (regular) pf_n = 1;  // row 0 describes them all (kCountRegular)
+    if (regular) {  // the first row describes them all (kCountRegular): it goes to desc[t]
+      pf_n = 0;
+      m.desc.x = (uint32_t)hf.seq;
+      m.desc.y = (uint32_t)(hf.seq >> 32);
+      m.desc.z = hf.vsz;
+      m.desc.w = hf.ksz | (srel << 16);
+    }
 #endif
 #ifndef CASK_STRIDE_QUAD
     for (uint32_t m = failmask; m; m &= m - 1) {
@@ -563,12 +578,17 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     }
   }
   DCHECK(n <= a.slot_cap && t < a.total_chunks, "n %u t %llu", n, (unsigned long long)t);
-  if (tid == G::kMetaT) {
-    if (!EXACT) a.spec[t] = s;
-    a.exit[t] = (s == kNone) ? 0 : exitv;
-    a.count[t] = n | (regular ? kCountRegular : 0u);
-    // a record that does not fit the window is hashed from HBM by k_long (only the last can)
-    a.long_r[t] = (s != kNone && exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
+  m.spec = s;
+  m.exit = (s == kNone) ? 0 : exitv;
+  m.count = n | (regular ? kCountRegular : 0u);
+  // a record that does not fit the window is hashed from HBM by k_long (only the last can)
+  m.long_r = (s != kNone && exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
+  if (!G::kStoreWave && tid == G::kMetaT) {
+    if (!EXACT) a.spec[t] = m.spec;
+    a.exit[t] = m.exit;
+    a.count[t] = m.count;
+    a.long_r[t] = m.long_r;
+    if (regular) ((u32x4*)a.desc)[t] = m.desc;
   }
   // the next chunk of the run starts where this chain left off
   if (s != kNone) {
@@ -614,6 +634,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   if (r0 >= nruns) return;
   uint64_t t = r0 * R;
   uint64_t run_end = t + R < a.total_chunks ? t + R : a.total_chunks;
+  uint64_t run_first = t;  // first chunk of the current run (its chunk-table entries go out together)
   BAR();  // L.found is reset by thread 0 below
 #ifdef CASK_STAMPS
   const uint64_t rt0_ = __builtin_amdgcn_s_memrealtime();  // 100 MHz: calibrates s_memtime, shows imbalance
@@ -703,7 +724,30 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
     pf_n = 0;
 #endif
 #ifndef CASK_STAGE_ONLY
-    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, par, pf_n, pf_slots, dg);
+    Meta m;
+    m.desc = u32x4{0u, 0u, 0u, 0u};
+    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, par, pf_n, pf_slots, m, dg);
+    if (G::kStoreWave && threadIdx.x >= G::kLoadT) {
+      // store wave: lane (t - run_first) keeps chunk t's entries in the staging registers this wave
+      // never loads into; the run's entries go out when the run ends
+      const uint32_t li = (uint32_t)(t - run_first), sl = threadIdx.x & 63;
+      if (sl == li) {
+        v[0] = u32x4{(uint32_t)m.spec, (uint32_t)(m.spec >> 32), (uint32_t)m.exit, (uint32_t)(m.exit >> 32)};
+        v[1] = u32x4{m.count, m.long_r, 0u, 0u};
+        v[2] = m.desc;
+      }
+      if (tn != t + 1 || !more || li == 63) {  // run ends (or a wave's worth of entries)
+        if (sl <= li) {
+          const uint64_t g = run_first + sl;
+          if (!EXACT) a.spec[g] = (uint64_t)v[0].x | ((uint64_t)v[0].y << 32);
+          a.exit[g] = (uint64_t)v[0].z | ((uint64_t)v[0].w << 32);
+          a.count[g] = v[1].x;
+          a.long_r[g] = v[1].y;
+          if (v[1].x & kCountRegular) ((u32x4*)a.desc)[g] = v[2];
+        }
+        run_first = tn;
+      }
+    }
 #ifdef CASK_LATE_PREFETCH  // diagnostic: the next window's loads issued after this chunk's row stores
     if (more) {
       nxt = next_chunk<G>(files, a.nfiles, cur, t, tn);

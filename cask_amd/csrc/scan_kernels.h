@@ -18,8 +18,9 @@ enum : uint8_t { kRowOk = 0, kRowChecksum = 1, kRowEof = 2 };
 constexpr uint32_t kSlotBad = 0x80000000u;
 
 // count[c] flag: the chunk is regular — its n rows are records of one length rl, all verified Ok
-// and inside the window, with key size, value size and sequence step of one from its slot row 0
-// (row r = pos0 + r*rl, seq0 + r, vsz0, ksz0). Only row 0 is stored; k_compact expands the rest.
+// and inside the window, with key size, value size and sequence step of one from its first row
+// (row r = pos0 + r*rl, seq0 + r, vsz0, ksz0). Only that row is stored, in desc[c] (slot-row
+// format); k_compact expands the rest.
 // Set only when the dense output is requested (ScanArgs.regular_ok); the segmented output keeps
 // every row.
 constexpr uint32_t kCountRegular = 0x80000000u;
@@ -70,6 +71,7 @@ struct ScanArgs {
   // global
   Counters* ctr;
   uint32_t* long_r;            // per chunk: row of its record longer than the window, or !0
+  uint32_t* desc;              // per chunk, 4 words: the first row of a regular chunk (kCountRegular)
   // dense rows (compaction output, device)
   uint64_t* pos;
   uint64_t* seq;

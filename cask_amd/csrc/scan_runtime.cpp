@@ -224,7 +224,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   const size_t pf_bytes = align_up(8ull * (nfiles + 1), 256);
   const size_t sum_bytes = align_up(sum_words * 8, 256);
   if (!c->filebuf.ensure(fd_bytes + 3 * pf_bytes + sum_bytes)) return CASK_E_NOMEM;
-  if (!c->chunk.ensure((total_chunks + 1) * (4 * 8 + 4 + 4) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
+  if (!c->chunk.ensure((total_chunks + 1) * (4 * 8 + 4 + 4 + 16) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
   if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
@@ -252,6 +252,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     uint64_t* tb = cb + 4 * C + (C + 1) / 2 + 1;
     const uint64_t TT = total_tiles + 1;
     a.long_r = (uint32_t*)(tb + 4 * TT);
+    uint64_t doff = (uint64_t)(tb - cb) + 4 * TT + (C + 1) / 2 + 2;  // after long_r, 16-B aligned
+    doff = (doff + 1) & ~1ull;
+    a.desc = (uint32_t*)(cb + doff);
     a.total_tiles = total_tiles;
     a.tile_max = tb;
     a.tile_sum = tb + TT;

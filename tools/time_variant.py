@@ -1,5 +1,6 @@
 """Diagnostic: best-of chunk-scan time of the library at $CASK_LIB_PATH on the configs[1] files
-(segmented output, repair off), to compare kernel variants built with `make variant`."""
+(dense output as bench.py, or segmented with CASK_TV_SEGMENTED=1; repair off), to compare kernel
+variants built with `make variant`."""
 import os
 import sys
 
@@ -15,10 +16,12 @@ def main():
     files = cfg2_files(ctx, nfiles=8)
     views = [(f.file_id, f.data) for f in files]
     total = sum(f.data.numel() for f in files)
+    seg = bool(os.environ.get("CASK_TV_SEGMENTED"))
+    rows = None if seg else ctx.alloc_rows(sum(f.nrec for f in files))
     ms = []
     for it in range(8):
         try:
-            ctx.scan_device_segmented(views)
+            ctx.scan_device_segmented(views) if seg else ctx.scan_device(views, rows)
         except Exception as e:  # diagnostic builds produce wrong rows; only the timing matters
             if it == 0:
                 print(f"  ({type(e).__name__}: {str(e)[:120]})")
