@@ -37,6 +37,8 @@ def parse():
     ap.add_argument("--cpu-sample-files", type=int, default=1, help="files timed by the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (H2D+D2H) measurement")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-segmented", action="store_true",
+                    help="skip the segmented-output measurement (profiling runs: dense-path launches only)")
     return ap.parse_args()
 
 
@@ -180,14 +182,15 @@ def main():
 
     extra = {"pipeline_breakdown_ms": ctx.last_timings()}
     counters = ctx.last_counters()
-    # segmented output (no dense compaction), same files, same clock discipline
-    ctx.scan_device_segmented(views)
-    barrier()
-    ts = time.perf_counter()
-    for _ in range(args.steps):
+    # segmented output (no dense compaction; every slot row written), same files, same clock
+    if not args.no_segmented:
         ctx.scan_device_segmented(views)
-    barrier()
-    extra["segmented_gibps"] = bytes_per_step * world * args.steps / (time.perf_counter() - ts) / 2 ** 30
+        barrier()
+        ts = time.perf_counter()
+        for _ in range(args.steps):
+            ctx.scan_device_segmented(views)
+        barrier()
+        extra["segmented_gibps"] = bytes_per_step * world * args.steps / (time.perf_counter() - ts) / 2 ** 30
     # scan + gather of keydir rows to rank 0 (reported separately from the metric)
     if dist is not None and not args.no_gather:
         from cask_amd.distributed import gather_rows
