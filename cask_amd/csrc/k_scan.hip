@@ -5,18 +5,19 @@
 // reading the 18-byte header `xxh32 u32 | seq u64 | ksz u16 | vsz u32` (LE), the key, the value
 // (absent for a tombstone, vsz == 0xFFFFFFFF) and checking XXH32(header[4..] ‖ key ‖ value).
 //
-// Here every file is cut into fixed-size chunks and a persistent grid streams through them.
-// Per chunk, one workgroup:
-//   1. has the chunk (+ halo) staged into LDS: the 16-B loads for chunk i+1 are issued into
-//      registers before chunk i is processed, so HBM latency hides behind the work;
-//   2. finds the chunk's first record boundary speculatively: the lowest offset whose header gives
-//      a record that fits the window and whose XXH32 matches its stored checksum (short records
-//      first, so long false candidates are rarely hashed);
-//   3. walks the boundary chain inside LDS (a wave tests 64 equal-stride successors per step);
-//   4. hashes one record per lane out of LDS and writes one 16-B slot row per record into the
-//      chunk's own slot range.
-// No workgroup ever waits on another: boundary speculation is checked afterwards (k_validate)
-// and rows are ordered by a later pass (k_compact), both in k_pipeline.hip.
+// Here every file is cut into fixed-size chunks and a persistent grid streams through them, in
+// runs of consecutive chunks claimed from a counter. Per chunk, one workgroup:
+//   1. has the chunk (+ halo) staged into LDS by its loader waves: the 16-B loads for the next
+//      chunk are issued into registers before this one is processed;
+//   2. takes the chunk's first record boundary from the previous chunk of the run (the carry) or,
+//      for a run's first chunk, finds it speculatively: the lowest offset whose header gives a
+//      record that fits and whose XXH32 matches its stored checksum;
+//   3. stride pass: one record per lane at the first record's length, header checked, XXH32 out of
+//      LDS (aligned dwords only); the rows go to an LDS row buffer that the store wave flushes
+//      during the next chunk — or, for a regular chunk, only its first row is kept (kCountRegular);
+//   4. slow path when the stride breaks: walk the chain, hash one record per quad of lanes.
+// No workgroup ever waits on another: boundary speculation is checked afterwards (k_val_*) and
+// rows are ordered by a later pass (k_compact), both in k_pipeline.hip.
 #include "device_util.h"
 
 #include <stdlib.h>
@@ -139,7 +140,13 @@ __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& 
   if (G::kStoreWave && threadIdx.x >= G::kLoadT) return;
   if (c.n16 == G::kNL * G::kLoadT) {  // the whole window is inside the file: no clamping
 #pragma unroll
-    for (uint32_t j = 0; j < G::kNL; ++j) v[j] = src[threadIdx.x + j * G::kLoadT];
+    for (uint32_t j = 0; j < G::kNL; ++j) {
+#ifdef CASK_NT_LOADS  // streaming (non-temporal) policy on the window loads
+      v[j] = __builtin_nontemporal_load(src + threadIdx.x + j * G::kLoadT);
+#else
+      v[j] = src[threadIdx.x + j * G::kLoadT];
+#endif
+    }
     return;
   }
 #pragma unroll
@@ -276,11 +283,7 @@ __device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_
 #endif
   for (uint32_t r = first; r < n; r += step) {
 #ifndef CASK_NO_SLOT_STORE
-#ifdef CASK_NT_ROWS
-    __builtin_nontemporal_store(L.rows[par][r], &srow[r]);
-#else
     srow[r] = L.rows[par][r];
-#endif
 #else
     const u32x4 w = L.rows[par][r];
     if (w.x == 0x9E3779B9u) srow[r] = w;
@@ -351,12 +354,8 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   // records; rows past it are discarded. A file of equal-length records never leaves this pass.
 #if defined(CASK_SLOTS_SCRATCH)  // diagnostic (wrong rows): every chunk of a workgroup writes the same 2 KiB (L2-resident)
   uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * 128) * 4;
-#elif !defined(CASK_DENSE_SLOTS)
+#else
   uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
-#else  // diagnostic (wrong rows): each workgroup appends its rows densely, to time the write locality
-  const uint64_t region = (a.total_chunks * a.slot_cap) / gridDim.x;
-  uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * region + (dg.st[0] % (region - a.slot_cap))) * 4;
-  dg.st[0] += 113;
 #endif
   const unsigned long long err_base = (unsigned long long)t * a.slot_cap;
   uint32_t n = 0;
@@ -705,23 +704,15 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #endif
     // the previous chunk's buffered rows go out ahead of the prefetch: no vector-memory instruction
     // is issued while the chunk is processed, and none waits behind the prefetch's loads
-#ifndef CASK_FLUSH_LATE
     flush_rows<G>(L, par ^ 1, pf_slots, pf_n);
     pf_n = 0;
-#endif
     ChunkPos nxt = cur;
-#ifndef CASK_LATE_PREFETCH
     if (more) {
       nxt = next_chunk<G>(files, a.nfiles, cur, t, tn);
       stage_issue<G>(v, nxt, a.stamps, tn);  // prefetch the next window
     }
-#endif
 #ifdef CASK_STAMPS
     dg.st[5] += __builtin_amdgcn_s_memtime() - st_pf_;  // phase 5: issuing the prefetch
-#endif
-#ifdef CASK_FLUSH_LATE  // diagnostic: the flush behind the prefetch's loads
-    flush_rows<G>(L, par ^ 1, pf_slots, pf_n);
-    pf_n = 0;
 #endif
 #ifndef CASK_STAGE_ONLY
     Meta m;
@@ -748,17 +739,8 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
         run_first = tn;
       }
     }
-#ifdef CASK_LATE_PREFETCH  // diagnostic: the next window's loads issued after this chunk's row stores
-    if (more) {
-      nxt = next_chunk<G>(files, a.nfiles, cur, t, tn);
-      stage_issue<G>(v, nxt, a.stamps, tn);
-    }
-#endif
 #else  // diagnostic: staging and prefetch only (the memory side of the kernel in isolation)
     if (threadIdx.x == 0 && L.win[cur.n16] == 0x12345678u) a.count[t] = 1;  // keep the staged bytes live
-#ifdef CASK_STAGE_WRITES  // diagnostic: plus 113 16-B slot rows per chunk (the stride pass's write traffic)
-    if (threadIdx.x < 113) ((u32x4*)(a.slots + ((uint64_t)t * a.slot_cap) * 4))[threadIdx.x] = ((const u32x4*)L.win)[threadIdx.x];
-#endif
 #endif
 #ifdef CASK_STAMPS
     const uint64_t st_end_ = __builtin_amdgcn_s_memtime();
