@@ -377,8 +377,10 @@ void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream) {
 }
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream) {
   if (!a.total_chunks) return;
+  // one wave per chunk where possible: each chunk's rows wait on a chain of dependent table loads
+  // (file, count, base, descriptor), so the launch needs many chunks in flight
   uint64_t g = (a.total_chunks + 3) / 4;
-  if (g > 4096) g = 4096;
+  if (g > 65536) g = 65536;
   hipLaunchKernelGGL(k_compact, dim3((uint32_t)g), dim3(256), 0, S(stream), a, summary);
 }
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream) {
