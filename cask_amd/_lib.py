@@ -51,6 +51,19 @@ class OpenError(C.Structure):
                 ("found", C.c_uint32)]
 
 
+class CompactOptions(C.Structure):
+    _fields_ = [("fragmentation_trigger", C.c_double), ("dead_bytes_trigger", C.c_uint64),
+                ("fragmentation_threshold", C.c_double), ("dead_bytes_threshold", C.c_uint64),
+                ("small_file_threshold", C.c_uint64)]
+
+
+class CompactResult(C.Structure):
+    _fields_ = [("n_compacted", C.c_uint32), ("n_new", C.c_uint32), ("n_tomb_only", C.c_uint32),
+                ("pad", C.c_uint32), ("live_records", C.c_uint64), ("tombstones", C.c_uint64),
+                ("bytes_in", C.c_uint64), ("bytes_out", C.c_uint64), ("ms", C.c_double * 5),
+                ("ms_total", C.c_double)]
+
+
 class IndexEntry(C.Structure):
     _fields_ = [("file_id", C.c_uint32), ("pad", C.c_uint32), ("entry_pos", C.c_uint64),
                 ("entry_size", C.c_uint64), ("sequence", C.c_uint64)]
@@ -106,6 +119,13 @@ SIGNATURES = [
     ("cask_db_current_sequence", C.c_uint64, [C.c_void_p]),
     ("cask_db_files", C.c_uint64, [C.c_void_p, c_u32p, C.c_uint64]),
     ("cask_db_open_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    ("cask_gather_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, c_u32p, c_u64p, c_u64p, c_u32p,
+                                     C.c_uint64, C.c_void_p]),
+    ("cask_compact_options_default", None, [C.POINTER(CompactOptions)]),
+    ("cask_db_compact_files", C.c_int, [C.c_void_p, c_u32p, C.c_uint64, C.POINTER(CompactResult),
+                                        C.POINTER(OpenError)]),
+    ("cask_db_compact", C.c_int64, [C.c_void_p, C.POINTER(CompactOptions), C.POINTER(CompactResult),
+                                    C.POINTER(OpenError)]),
 ]
 
 _lib = None

@@ -3,7 +3,9 @@
 `CaskOptions` keeps the builder of cask.rs:194-331 (same names, same defaults); `open()` runs the
 Cask::open replay (cask.rs:335-382) in the native engine, with every data file that lacks a valid
 hint file scanned on the GPU. Only the keydir/stats/sequence the replay builds are exposed here;
-get/put/delete and the background sync/compaction threads are outside this path.
+`compact()` / `compact_files()` run the compaction merge (cask.rs:451-642) with the live records
+verified and copied on the GPU. get/put/delete and the background sync/compaction threads are
+outside this path.
 """
 from __future__ import annotations
 
@@ -122,9 +124,10 @@ class CaskOptions:
 class Cask:
     """Handle to a replayed database (cask.rs:171-177)."""
 
-    def __init__(self, handle, path: str):
+    def __init__(self, handle, path: str, options: "CaskOptions | None" = None):
         self._h = handle
         self.path = path
+        self.options = options or CaskOptions()
 
     @staticmethod
     def open(path: str, options: CaskOptions | None = None) -> "Cask":
@@ -141,7 +144,7 @@ class Cask:
         h = lib.cask_db_open(path.encode(), C.byref(opts), C.byref(err))
         if not h:
             raise_status(err.status, err.file_id, err.pos, err.expected, err.found, what=path)
-        return Cask(h, path)
+        return Cask(h, path, o)
 
     def _handle(self):
         if not self._h:
@@ -229,6 +232,44 @@ class Cask:
     def file_stats(self) -> list[tuple[int, float, int]]:
         """Stats::file_stats (stats.rs:56-67): (file_id, dead/entries, dead_bytes)."""
         return [(f, (d / e) if e else float("nan"), b) for f, (e, d, b) in sorted(self.stats().items())]
+
+    def _compact_opts(self) -> "L.CompactOptions":
+        o = self.options
+        c = L.CompactOptions()
+        c.fragmentation_trigger = o._fragmentation_trigger
+        c.dead_bytes_trigger = o._dead_bytes_trigger
+        c.fragmentation_threshold = o._fragmentation_threshold
+        c.dead_bytes_threshold = o._dead_bytes_threshold
+        c.small_file_threshold = o._small_file_threshold
+        return c
+
+    @staticmethod
+    def _compact_report(r: "L.CompactResult") -> dict:
+        return {"compacted": int(r.n_compacted), "new_files": int(r.n_new), "tombstone_only_files": int(r.n_tomb_only),
+                "live_records": int(r.live_records), "tombstones": int(r.tombstones), "bytes_in": int(r.bytes_in),
+                "bytes_out": int(r.bytes_out), "hints_ms": r.ms[0], "verify_ms": r.ms[1], "gather_ms": r.ms[2],
+                "write_ms": r.ms[3], "swap_ms": r.ms[4], "total_ms": r.ms_total}
+
+    def compact_files(self, files) -> dict:
+        """Cask::compact_files (cask.rs:525-560): compact the given data files (ascending, once
+        each) into new ones. Returns a report of what was done; raises like the reference."""
+        ids = sorted(set(int(f) for f in files))
+        arr = (C.c_uint32 * max(len(ids), 1))(*ids)
+        res, err = L.CompactResult(), L.OpenError()
+        st = L.lib().cask_db_compact_files(self._handle(), arr, len(ids), C.byref(res), C.byref(err))
+        if st != L.OK:
+            raise_status(st, err.file_id, err.pos, err.expected, err.found, what=self.path)
+        return self._compact_report(res)
+
+    def compact(self) -> dict | None:
+        """Cask::compact (cask.rs:563-642) with this Cask's CaskOptions thresholds. Returns the
+        report, or None when no trigger fired."""
+        opts = self._compact_opts()
+        res, err = L.CompactResult(), L.OpenError()
+        n = L.lib().cask_db_compact(self._handle(), C.byref(opts), C.byref(res), C.byref(err))
+        if n < 0:
+            raise_status(int(n), err.file_id, err.pos, err.expected, err.found, what=self.path)
+        return self._compact_report(res) if n > 0 else None
 
     def open_timings(self) -> dict[str, float]:
         t = (C.c_double * 5)()

@@ -3,6 +3,8 @@
 // fast path (log.rs:121-135, 432-447, 512-539; data.rs:258-276), hint recreation
 // (log.rs:137-148, 367-395, 449-471), and the keydir fold Index::update + Stats
 // (cask.rs:28-95; stats.rs:6-67). The scan itself is cask_scan_host (scan_runtime.cpp).
+// Also the compaction merge (cask.rs:451-640): liveness against the keydir on the host, the
+// live records verified by the device scan and copied into the new data files on the device.
 #include <dirent.h>
 #include <fcntl.h>
 #include <sys/file.h>
@@ -19,6 +21,8 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "../../include/cask_scan.h"
 #include "xxh32.h"
@@ -95,6 +99,11 @@ class KeyDir {
       slots[i] = s;
       ++used;
     }
+  }
+
+  const cask_index_entry* get(const uint8_t* k, uint32_t n) const {  // Index::get (cask.rs:41-43)
+    const int64_t f = find(k, n, hash_key(k, n));
+    return f >= 0 ? &slots[(uint64_t)f].e : nullptr;
   }
 
   // Stats::add_entry / remove_entry (stats.rs:23-48)
@@ -218,6 +227,23 @@ bool write_file(const std::string& p, const std::vector<uint8_t>& body, uint32_t
   return true;
 }
 
+bool write_raw(const std::string& p, const uint8_t* b, size_t n) {
+  int fd = open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return false;
+  size_t off = 0;
+  while (off < n) {
+    ssize_t w = write(fd, b + off, n - off);
+    if (w < 0) {
+      if (errno == EINTR) continue;
+      close(fd);
+      return false;
+    }
+    off += (size_t)w;
+  }
+  close(fd);
+  return true;
+}
+
 // find_data_files (log.rs:483-510): regex "(\d+).cask.data$" (unescaped '.', unanchored),
 // regular files only (DirEntry::metadata does not follow symlinks), u32 parse, ascending.
 bool find_data_files(const std::string& dir, std::vector<uint32_t>& out) {
@@ -262,6 +288,7 @@ struct cask_db {
   std::vector<uint32_t> files;
   KeyDir index;
   uint64_t sequence = 0;
+  uint32_t file_seq = 0;  // Log::file_id_seq: the last data file id at open (log.rs:63-69)
   double timings[5] = {0, 0, 0, 0, 0};
   ~cask_db() {
     if (lock_fd >= 0) {
@@ -342,6 +369,7 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     set_err(err, CASK_E_IO);
     return nullptr;
   }
+  db->file_seq = db->files.empty() ? 0u : db->files.back();
 
   // Which files have a valid hint file (log.rs:121-135, 512-539)?
   const size_t nf = db->files.size();
@@ -509,6 +537,388 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   db->timings[3] = t_fold;
   db->timings[4] = ms_since(t0);
   return db;
+}
+
+void cask_compact_options_default(cask_compact_options* o) {  // cask.rs:229-234
+  if (!o) return;
+  o->fragmentation_trigger = 0.6;
+  o->dead_bytes_trigger = 512ull * 1024 * 1024;
+  o->fragmentation_threshold = 0.4;
+  o->dead_bytes_threshold = 128ull * 1024 * 1024;
+  o->small_file_threshold = 10ull * 1024 * 1024;
+}
+
+// Cask::compact_files_aux + compact_files (cask.rs:451-560). The hint pass and the liveness test
+// run on the host against the keydir; the live records' checksums are verified by the device scan
+// of their files (Log::read_entry -> Entry::from_read, log.rs:150-166) and their bytes are copied
+// into the new data files by the device gather. LogWriter rollover (log.rs:282-306) and the
+// EntryWriter/HintWriter output (log.rs:317-395) are restated on the host.
+int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
+                          cask_open_error* err) {
+  set_err(err, CASK_OK);
+  if (!db || (nfiles && !files_in)) return CASK_E_INVALID_ARG;
+  cask_compact_result R{};
+  auto t0 = std::chrono::steady_clock::now();
+  const std::string& path = db->path;
+  // BTreeSet<u32> order (cask.rs:574, 639-640); only files of this Log
+  std::vector<uint32_t> files(files_in, files_in + nfiles);
+  std::sort(files.begin(), files.end());
+  files.erase(std::unique(files.begin(), files.end()), files.end());
+  files.erase(std::remove_if(files.begin(), files.end(),
+                             [&](uint32_t f) { return !std::binary_search(db->files.begin(), db->files.end(), f); }),
+              files.end());
+
+  // 1. hints of each file with a valid hint file (files without one are skipped: cask.rs:456-468)
+  struct Ins {
+    uint32_t src;  // index into `srcs`
+    uint64_t pos;
+  };
+  std::vector<uint32_t> compacted, srcs;      // srcs: compacted files with live records
+  std::vector<Ins> ins;
+  std::vector<std::string> del_keys;           // the tombstone tail, in first-seen order
+  std::vector<uint64_t> del_seq;
+  std::unordered_map<std::string, size_t> del_at;
+  for (uint32_t fid : files) {
+    std::vector<uint8_t> hb;
+    const std::string hp = hint_path(path, fid);
+    if (!is_file_follow(hp) || !read_file(hp, hb) || hb.size() < 4 ||
+        cask_xxh::xxh32(hb.data(), hb.size() - 4, 0) != rd32(hb.data() + hb.size() - 4))
+      continue;
+    const uint64_t body = hb.size() - 4;
+    const uint32_t si = (uint32_t)srcs.size();
+    bool any = false;
+    for (uint64_t p = 0; p < body;) {  // Hints::next (log.rs:437-447); `hint?` aborts (cask.rs:483)
+      if (body - p < 22 || body - p - 22 < rd16(hb.data() + p + 8)) {
+        set_err(err, CASK_E_EOF, fid, p);
+        return CASK_E_EOF;
+      }
+      const uint8_t* h = hb.data() + p;
+      const uint64_t seq = rd64(h);
+      const uint16_t k = rd16(h + 8);
+      const uint32_t v = rd32(h + 10);
+      const uint64_t epos = rd64(h + 14);
+      const cask_index_entry* ie = db->index.get(h + 22, k);
+      if (v == CASK_ENTRY_TOMBSTONE) {  // cask.rs:487-499
+        if (!ie) {
+          std::string key((const char*)h + 22, k);
+          auto it = del_at.find(key);
+          if (it == del_at.end()) {
+            del_at.emplace(key, del_keys.size());
+            del_keys.push_back(std::move(key));
+            del_seq.push_back(seq);
+          } else if (del_seq[it->second] < seq) {
+            del_seq[it->second] = seq;
+          }
+        }
+      } else if (ie && ie->sequence == seq) {  // cask.rs:500-502
+        ins.push_back(Ins{si, epos});
+        any = true;
+      }
+      p += 22ull + k;
+    }
+    compacted.push_back(fid);
+    if (any) srcs.push_back(fid);
+  }
+  R.ms[0] = ms_since(t0);
+
+  // 2. the live records: read_entry at each hint position, verified by the device scan
+  auto t1 = std::chrono::steady_clock::now();
+  const size_t ns = srcs.size();
+  std::vector<std::vector<uint8_t>> data(ns);
+  std::vector<uint8_t*> dsrc(ns, nullptr);
+  cask_ctx* ctx = nullptr;
+  auto cleanup = [&]() {
+    for (uint8_t* p : dsrc)
+      if (p) (void)hipFree(p);
+    if (ctx) cask_ctx_destroy(ctx);
+  };
+  struct Rec {
+    uint32_t src, ksz, vsz;
+    uint64_t pos, seq, len;
+  };
+  std::vector<Rec> recs(ins.size());
+  if (!ins.empty()) {
+    int st = CASK_OK;
+    ctx = cask_ctx_create(db->opts.device, &st);
+    if (!ctx) return CASK_E_DEVICE;
+    std::vector<cask_file_view> views(ns);
+    for (size_t i = 0; i < ns; ++i) {
+      if (!read_file(data_path(path, srcs[i]), data[i])) {
+        cleanup();
+        set_err(err, CASK_E_IO, srcs[i]);
+        return CASK_E_IO;
+      }
+      R.bytes_in += data[i].size();
+      if (hipMalloc(&dsrc[i], data[i].size() + 16) != hipSuccess ||
+          hipMemcpy(dsrc[i], data[i].data(), data[i].size(), hipMemcpyHostToDevice) != hipSuccess) {
+        cleanup();
+        return CASK_E_DEVICE;
+      }
+      views[i] = cask_file_view{srcs[i], CASK_VIEW_DEVICE, dsrc[i], data[i].size()};
+    }
+    const uint64_t bound = cask_rows_bound(views.data(), (uint32_t)ns);
+    void* drow = nullptr;
+    if (hipMalloc(&drow, bound * 23 + 64) != hipSuccess) {
+      cleanup();
+      return CASK_E_DEVICE;
+    }
+    cask_rows rows{};
+    rows.capacity = bound;
+    rows.pos = (uint64_t*)drow;
+    rows.seq = rows.pos + bound;
+    rows.vsz = (uint32_t*)(rows.seq + bound);
+    rows.ksz = (uint16_t*)(rows.vsz + bound);
+    rows.status = (uint8_t*)(rows.ksz + bound);
+    std::vector<uint64_t> row_off(ns + 1);
+    cask_scan_error se{};
+    st = cask_scan_device(ctx, views.data(), (uint32_t)ns, &rows, row_off.data(), &se);
+    std::vector<uint64_t> pos(rows.count), seq(rows.count);
+    std::vector<uint32_t> vsz(rows.count);
+    std::vector<uint16_t> ksz(rows.count);
+    std::vector<uint8_t> stat(rows.count);
+    if (st == CASK_OK && rows.count &&
+        (hipMemcpy(pos.data(), rows.pos, 8 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(seq.data(), rows.seq, 8 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(vsz.data(), rows.vsz, 4 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(ksz.data(), rows.ksz, 2 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
+         hipMemcpy(stat.data(), rows.status, rows.count, hipMemcpyDeviceToHost) != hipSuccess))
+      st = CASK_E_DEVICE;
+    (void)hipFree(drow);
+    if (st != CASK_OK) {
+      cleanup();
+      return st;
+    }
+    for (size_t k = 0; k < ins.size(); ++k) {  // in write order: the first failure is the reference's
+      const Ins& in = ins[k];
+      const std::vector<uint8_t>& buf = data[in.src];
+      const uint64_t n = buf.size(), p = in.pos;
+      Rec& rc = recs[k];
+      rc.src = in.src;
+      rc.pos = p;
+      const uint64_t* b = pos.data() + row_off[in.src];
+      const uint64_t* e = pos.data() + row_off[in.src + 1];
+      const uint64_t* f = std::lower_bound(b, e, p);
+      bool ok;
+      if (f != e && *f == p) {  // the record lies on the file's chain: the scan verified it
+        const uint64_t r = (uint64_t)(f - pos.data());
+        ok = stat[r] == CASK_ROW_OK;
+        rc.ksz = ksz[r];
+        rc.vsz = vsz[r];
+        rc.seq = seq[r];
+      } else {  // off the chain (a stale hint): Entry::from_read at p on the host
+        ok = p + 18 <= n;
+        if (ok) {
+          rc.seq = rd64(buf.data() + p + 4);
+          rc.ksz = rd16(buf.data() + p + 12);
+          rc.vsz = rd32(buf.data() + p + 14);
+        }
+      }
+      const uint64_t rl = ok || p + 18 <= n ? 18ull + rc.ksz + (rc.vsz == CASK_ENTRY_TOMBSTONE ? 0ull : (uint64_t)rc.vsz) : 0;
+      if (p + 18 > n || p + rl > n) {  // data.rs:163,172,181
+        cleanup();
+        set_err(err, CASK_E_EOF, srcs[in.src], p);
+        return CASK_E_EOF;
+      }
+      const uint32_t stored = rd32(buf.data() + p);
+      const uint32_t found = ok ? stored : cask_xxh::xxh32(buf.data() + p + 4, rl - 4, 0);
+      if (found != stored) {  // data.rs:193-198
+        cleanup();
+        set_err(err, CASK_E_CHECKSUM, srcs[in.src], p, stored, found);
+        return CASK_E_CHECKSUM;
+      }
+      rc.len = rl;
+    }
+  }
+  R.ms[1] = ms_since(t1);
+
+  // 3. LogWriter rollover (log.rs:282-306): live records in order, then the tombstone tail
+  struct Out {
+    uint32_t file_id;
+    uint64_t pos;
+  };
+  const size_t nt = del_keys.size();
+  std::vector<Out> place(ins.size() + nt);
+  std::vector<uint32_t> new_files, tomb_files, out_files;
+  std::vector<uint64_t> out_len;
+  {
+    uint64_t cur = 0;
+    bool have = false;
+    for (size_t k = 0; k < place.size(); ++k) {
+      const uint64_t size = k < ins.size() ? recs[k].len : 18ull + del_keys[k - ins.size()].size();
+      if (!have || cur + size > db->opts.max_file_size) {
+        const uint32_t fid = ++db->file_seq;  // Sequence::increment (util.rs:62-64)
+        (k < ins.size() ? new_files : tomb_files).push_back(fid);  // cask.rs:510-512, 518-520
+        out_files.push_back(fid);
+        out_len.push_back(0);
+        cur = 0;
+        have = true;
+      }
+      place[k] = Out{out_files.back(), cur};
+      cur += size;
+      out_len.back() = cur;
+    }
+  }
+
+  // 4. live bytes gathered on the device into one buffer laid out file after file
+  auto t2 = std::chrono::steady_clock::now();
+  std::vector<uint64_t> file_base(out_files.size() + 1, 0);
+  for (size_t i = 0; i < out_files.size(); ++i) file_base[i + 1] = file_base[i] + out_len[i];
+  std::vector<uint8_t> out(file_base.back());
+  if (!ins.empty()) {
+    std::vector<uint32_t> g_src(ins.size()), g_len(ins.size());
+    std::vector<uint64_t> g_pos(ins.size()), g_dst(ins.size());
+    uint64_t live_bytes = 0;
+    size_t fi = 0;
+    for (size_t k = 0; k < ins.size(); ++k) {
+      while (out_files[fi] != place[k].file_id) ++fi;
+      g_src[k] = recs[k].src;
+      g_pos[k] = recs[k].pos;
+      g_len[k] = (uint32_t)recs[k].len;
+      g_dst[k] = file_base[fi] + place[k].pos;
+      live_bytes = g_dst[k] + recs[k].len;
+    }
+    uint8_t* dout = nullptr;
+    int st = CASK_OK;
+    if (hipMalloc(&dout, live_bytes + 16) != hipSuccess) st = CASK_E_DEVICE;
+    if (st == CASK_OK)
+      st = cask_gather_device(ctx, (const uint8_t* const*)dsrc.data(), (uint32_t)ns, g_src.data(), g_pos.data(),
+                              g_dst.data(), g_len.data(), ins.size(), dout);
+    if (st == CASK_OK && hipMemcpy(out.data(), dout, live_bytes, hipMemcpyDeviceToHost) != hipSuccess)
+      st = CASK_E_DEVICE;
+    if (dout) (void)hipFree(dout);
+    if (st != CASK_OK) {
+      cleanup();
+      return st;
+    }
+  }
+  R.ms[2] = ms_since(t2);
+
+  // 5. data and hint files (EntryWriter::write, HintWriter, log.rs:343-395)
+  auto t3 = std::chrono::steady_clock::now();
+  std::vector<std::vector<uint8_t>> hints(out_files.size());
+  {
+    size_t fi = 0;
+    for (size_t k = 0; k < place.size(); ++k) {
+      while (out_files[fi] != place[k].file_id) ++fi;
+      uint8_t* o = out.data() + file_base[fi] + place[k].pos;
+      uint8_t h[22];
+      const uint8_t* key;
+      uint32_t klen;
+      if (k < ins.size()) {
+        const Rec& rc = recs[k];
+        key = data[rc.src].data() + rc.pos + 18;
+        klen = rc.ksz;
+        wr64(h, rc.seq);
+        wr32(h + 10, rc.vsz == CASK_ENTRY_TOMBSTONE ? CASK_ENTRY_TOMBSTONE : rc.vsz);
+      } else {  // Entry::deleted(sequence, key).write_bytes (data.rs:90-121)
+        const std::string& kk = del_keys[k - ins.size()];
+        key = (const uint8_t*)kk.data();
+        klen = (uint32_t)kk.size();
+        wr64(o + 4, del_seq[k - ins.size()]);
+        wr16(o + 12, (uint16_t)klen);
+        wr32(o + 14, CASK_ENTRY_TOMBSTONE);
+        memcpy(o + 18, key, klen);
+        wr32(o, cask_xxh::xxh32(o + 4, 14ull + klen, 0));
+        wr64(h, del_seq[k - ins.size()]);
+        wr32(h + 10, CASK_ENTRY_TOMBSTONE);
+      }
+      wr16(h + 8, (uint16_t)klen);
+      wr64(h + 14, place[k].pos);  // Hint::new(entry, entry_pos) (data.rs:218-226)
+      hints[fi].insert(hints[fi].end(), h, h + 22);
+      hints[fi].insert(hints[fi].end(), key, key + klen);
+    }
+  }
+  for (size_t i = 0; i < out_files.size(); ++i) {
+    const uint32_t fid = out_files[i];
+    if (!write_raw(data_path(path, fid), out.data() + file_base[i], out_len[i]) ||
+        !write_file(hint_path(path, fid), hints[i], cask_xxh::xxh32(hints[i].data(), hints[i].size(), 0))) {
+      cleanup();
+      set_err(err, CASK_E_IO, fid);
+      return CASK_E_IO;
+    }
+  }
+  R.ms[3] = ms_since(t3);
+  cleanup();
+
+  // 6. compact_files (cask.rs:528-550): index the new files from their hints, drop the compacted
+  // files' stats, swap the file sets
+  auto t4 = std::chrono::steady_clock::now();
+  for (uint32_t fid : new_files) {
+    const size_t i = (size_t)(std::find(out_files.begin(), out_files.end(), fid) - out_files.begin());
+    const std::vector<uint8_t>& hb = hints[i];
+    for (uint64_t p = 0; p < hb.size();) {
+      const uint8_t* h = hb.data() + p;
+      const uint16_t k = rd16(h + 8);
+      db->index.update(h + 22, k, fid, rd64(h + 14), rd32(h + 10), rd64(h));
+      p += 22ull + k;
+    }
+  }
+  for (uint32_t fid : compacted) db->index.stats.erase(fid);  // Stats::remove_files (stats.rs:50-54)
+  for (uint32_t fid : compacted) {  // Log::swap_files (log.rs:198-217)
+    db->files.erase(std::lower_bound(db->files.begin(), db->files.end(), fid));
+    if (unlink(data_path(path, fid).c_str()) != 0) {
+      set_err(err, CASK_E_IO, fid);
+      return CASK_E_IO;
+    }
+    (void)unlink(hint_path(path, fid).c_str());
+  }
+  db->files.insert(db->files.end(), new_files.begin(), new_files.end());
+  std::sort(db->files.begin(), db->files.end());
+  R.ms[4] = ms_since(t4);
+
+  R.n_compacted = (uint32_t)compacted.size();
+  R.n_new = (uint32_t)new_files.size();
+  R.n_tomb_only = (uint32_t)tomb_files.size();
+  R.live_records = ins.size();
+  R.tombstones = nt;
+  R.bytes_out = out.size();
+  R.ms_total = ms_since(t0);
+  if (res) *res = R;
+  return CASK_OK;
+}
+
+// Cask::compact (cask.rs:563-642): pick the files by the stats and their sizes; compact them if
+// a trigger fired. Returns the number of files compacted (0: no trigger), or a negative status.
+int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts_in, cask_compact_result* res,
+                        cask_open_error* err) {
+  set_err(err, CASK_OK);
+  if (!db) return CASK_E_INVALID_ARG;
+  cask_compact_options o;
+  if (opts_in) o = *opts_in; else cask_compact_options_default(&o);
+  std::vector<uint32_t> sel;
+  bool triggered = false;
+  std::vector<uint32_t> ids;
+  for (const auto& kv : db->index.stats) ids.push_back(kv.first);
+  std::sort(ids.begin(), ids.end());  // the reference iterates a HashMap; the selected set is order-free
+  for (uint32_t fid : ids) {
+    const StatsEntry& se = db->index.stats[fid];
+    const double frag = (double)se.dead_entries / (double)se.entries;  // stats.rs:56-67
+    const uint64_t dead = se.dead_bytes;
+    auto has = [&](uint32_t f) { return std::find(sel.begin(), sel.end(), f) != sel.end(); };
+    if (!triggered) {
+      if (frag >= o.fragmentation_trigger) {
+        triggered = true;
+        sel.push_back(fid);
+      } else if (dead >= o.dead_bytes_trigger && !has(fid)) {
+        triggered = true;
+        sel.push_back(fid);
+      }
+    }
+    if (frag >= o.fragmentation_threshold && !has(fid)) {
+      sel.push_back(fid);
+    } else if (dead >= o.dead_bytes_threshold && !has(fid)) {
+      sel.push_back(fid);
+    }
+    if (!has(fid)) {
+      struct stat st;
+      if (stat(data_path(db->path, fid).c_str(), &st) == 0 && (uint64_t)st.st_size <= o.small_file_threshold)
+        sel.push_back(fid);
+    }
+  }
+  if (res) *res = cask_compact_result{};
+  if (!triggered) return 0;
+  const int st = cask_db_compact_files(db, sel.data(), sel.size(), res, err);
+  return st == CASK_OK ? (int64_t)sel.size() : (int64_t)st;
 }
 
 void cask_db_close(cask_db* db) { delete db; }

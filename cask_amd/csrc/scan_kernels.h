@@ -97,7 +97,14 @@ struct SummaryHead {
 };
 // followed by row_off[nfiles+1], then per file: first_bad, bad_T, err_row, err_slot
 
+// One record of a compaction rewrite: len bytes from src file `src` at `pos` to output byte `dst`.
+struct GatherRec {
+  uint64_t pos, dst;
+  uint32_t src, len;
+};
+
 // Host-callable launchers (defined in scan_kernels.hip).
+void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src, uint8_t* dst, void* stream);
 uint32_t geometry_chunk(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
 void launch_long(const ScanArgs& a, void* stream);

@@ -80,6 +80,7 @@ struct cask_ctx {
   DevBuf ctr;        // Counters
   DevBuf filebuf;    // FileDesc[] | file_err[] | first_bad[] | file_total[] | summary
   DevBuf err2;       // error detail words
+  DevBuf gather;     // compaction rewrite: GatherRec[] | source pointers
   DevBuf stamps;     // diagnostic builds (-DCASK_STAMPS) only
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
@@ -141,6 +142,7 @@ void cask_ctx_destroy(cask_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   c->chunk.release();
   c->slots.release();
+  c->gather.release();
   c->ctr.release();
   c->filebuf.release();
   c->err2.release();
@@ -515,6 +517,29 @@ extern "C" int cask_encode_device(cask_ctx* c, uint64_t nrec, const uint64_t* of
   if (set_dev(c)) return CASK_E_DEVICE;
   launch_encode(nrec, off, seq, ksz, vsz_raw, keys, key_off, vals, val_off, out, c->stream);
   launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
+  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+  return CASK_OK;
+}
+
+extern "C" int cask_gather_device(cask_ctx* c, const uint8_t* const* srcs, uint32_t nsrc, const uint32_t* src,
+                                  const uint64_t* pos, const uint64_t* dst_off, const uint32_t* len, uint64_t nrec,
+                                  uint8_t* dst) {
+  if (!c || (nrec && (!srcs || !src || !pos || !dst_off || !len || !dst))) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (!nrec) return CASK_OK;
+  std::vector<GatherRec> recs(nrec);
+  for (uint64_t r = 0; r < nrec; ++r) {
+    if (src[r] >= nsrc) return CASK_E_INVALID_ARG;
+    recs[r] = GatherRec{pos[r], dst_off[r], src[r], len[r]};
+  }
+  const size_t rb = align_up(sizeof(GatherRec) * nrec, 256);
+  if (!c->gather.ensure(rb + sizeof(void*) * nsrc)) return CASK_E_NOMEM;
+  uint8_t* base = c->gather.as<uint8_t>();
+  if (hipMemcpyAsync(base, recs.data(), sizeof(GatherRec) * nrec, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(base + rb, srcs, sizeof(void*) * nsrc, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+    return CASK_E_DEVICE;
+  launch_gather((const GatherRec*)base, nrec, (const uint8_t* const*)(base + rb), dst, c->stream);
   if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
   return CASK_OK;
 }

@@ -163,6 +163,14 @@ int cask_encode_device(cask_ctx* ctx, uint64_t nrec, const uint64_t* off, const 
                        const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
                        uint8_t* out);
 
+/* Compaction rewrite (Cask::compact_files_aux, cask.rs:505-513; LogWriter::write, log.rs:282-306):
+ * nrec records copied byte for byte into dst (device memory). Record r is len[r] bytes of source
+ * file src[r] (device pointer srcs[src[r]]) from byte pos[r], written at dst[dst_off[r]]. The
+ * record arrays and srcs are host memory. Synchronous. */
+int cask_gather_device(cask_ctx* ctx, const uint8_t* const* srcs, uint32_t nsrc, const uint32_t* src,
+                       const uint64_t* pos, const uint64_t* dst_off, const uint32_t* len, uint64_t nrec,
+                       uint8_t* dst);
+
 /* XXH32 seed 0 on the host (util.rs:37-41) — convenience for bindings. */
 uint32_t cask_xxh32(const uint8_t* data, uint64_t len);
 
@@ -223,6 +231,51 @@ uint64_t cask_db_files(const cask_db* db, uint32_t* ids, uint64_t cap);
 /* Timing of the replay phases (ms): [0] discover+read, [1] device scan, [2] hint write,
  * [3] keydir fold, [4] total. */
 int cask_db_open_timings(const cask_db* db, double* ms5);
+
+/* ------------------------------------------------------------------------------------------ */
+/* Compaction merge (Cask::compact / compact_files / compact_files_aux, cask.rs:451-642).      */
+/* ------------------------------------------------------------------------------------------ */
+/* The CaskOptions compaction thresholds (cask.rs:229-234). */
+typedef struct cask_compact_options {
+  double fragmentation_trigger;    /* 0.6 */
+  uint64_t dead_bytes_trigger;     /* 512 MiB */
+  double fragmentation_threshold;  /* 0.4 */
+  uint64_t dead_bytes_threshold;   /* 128 MiB */
+  uint64_t small_file_threshold;   /* 10 MiB */
+} cask_compact_options;
+
+void cask_compact_options_default(cask_compact_options* o);
+
+typedef struct cask_compact_result {
+  uint32_t n_compacted;   /* files compacted (those with a valid hint file) */
+  uint32_t n_new;         /* files created by live records (the reference's new_files) */
+  uint32_t n_tomb_only;   /* files created by the tombstone tail alone (not in new_files,
+                             cask.rs:518-520: on disk, not indexed, found at the next open) */
+  uint32_t pad;
+  uint64_t live_records;
+  uint64_t tombstones;
+  uint64_t bytes_in;      /* data bytes of the compacted files with live records (to the device) */
+  uint64_t bytes_out;     /* bytes written to new data files */
+  double ms[5];           /* [0] hints + liveness, [1] device verify, [2] device gather,
+                             [3] file writes, [4] keydir update + file swap */
+  double ms_total;
+} cask_compact_result;
+
+/* Cask::compact_files(files) (cask.rs:525-560 over compact_files_aux 451-523): files are taken
+ * as a set in ascending order; ids that are not data files of this db are ignored. Live records
+ * (index sequence == hint sequence) are verified (Log::read_entry, log.rs:150-166) and rewritten
+ * byte for byte through the LogWriter rollover; tombstones of keys absent from the index follow,
+ * one per key with its highest sequence, in the order the keys were first seen (the reference
+ * iterates a HashMap: its order is unspecified). On an error nothing is written and the
+ * reference's error is returned (the reference may have written part of the output by then). */
+int cask_db_compact_files(cask_db* db, const uint32_t* files, uint64_t nfiles, cask_compact_result* res,
+                          cask_open_error* err);
+
+/* Cask::compact (cask.rs:563-642): selects files by fragmentation, dead bytes and size, and
+ * compacts them if a trigger fired. Returns the number of files compacted (0: not triggered) or
+ * a negative status. */
+int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts, cask_compact_result* res,
+                        cask_open_error* err);
 
 #ifdef __cplusplus
 }

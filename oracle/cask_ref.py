@@ -300,6 +300,7 @@ class ReplayResult:
     sequence: int              # max over all hints (cask.rs:350-352)
     files: list[int] = field(default_factory=list)
     error: CaskError | None = None
+    file_id_seq: int = 0       # Log::file_id_seq: the last data file id at open (log.rs:63-69)
 
     @property
     def current_sequence(self) -> int:  # cask.rs:379
@@ -312,6 +313,7 @@ def replay(path: str, write_hints: bool = True) -> ReplayResult:
     (log.rs:137-148, 449-471). The first Err aborts open(); hint files already written stay."""
     index = Index()
     res = ReplayResult(index=index, sequence=0, files=find_data_files(path))
+    res.file_id_seq = res.files[-1] if res.files else 0
     for file_id in res.files:
         hp = hint_file_path(path, file_id)
         hb = None
@@ -376,3 +378,155 @@ def write_log(path: str, entries: list[Entry], max_file_size: int, first_file_id
         pos += e.size()
     close()
     return files
+
+
+# ----------------------------------------------------------------------------- compaction
+def read_entry(path: str, file_id: int, entry_pos: int) -> Entry:
+    """Log::read_entry (log.rs:150-166) = seek + Entry::from_read (data.rs:161-206): a short read
+    is Io(UnexpectedEof), a hash mismatch InvalidChecksum{expected: stored, found: computed}."""
+    with open(data_file_path(path, file_id), "rb") as f:
+        f.seek(entry_pos)
+        hdr = f.read(ENTRY_STATIC_SIZE)
+        if len(hdr) < ENTRY_STATIC_SIZE:
+            raise CaskError("eof", file_id, entry_pos)
+        stored, seq, ksz, vsz = struct.unpack("<IQHI", hdr)
+        deleted = vsz == ENTRY_TOMBSTONE
+        key = f.read(ksz)
+        value = b"" if deleted else f.read(vsz)
+        if len(key) < ksz or len(value) < (0 if deleted else vsz):
+            raise CaskError("eof", file_id, entry_pos)
+    found = xxhash32(hdr[4:] + key + value)
+    if found != stored:
+        raise CaskError("checksum", file_id, entry_pos, stored, found)
+    return Entry(key, value, seq, deleted)
+
+
+class LogWriter:
+    """LogWriter::write rollover (log.rs:245-306) with EntryWriter + HintWriter (log.rs:317-395):
+    a new file (id = file_id_seq.increment(), util.rs:62-64) when there is no writer or
+    pos + entry.size() > max_file_size. Files are flushed on close (the writers' Drop)."""
+
+    def __init__(self, path: str, max_file_size: int, file_id_seq: int):
+        self.path, self.max_file_size, self.file_id_seq = path, max_file_size, file_id_seq
+        self.cur = None  # [file_id, [record bytes], [hint bytes], pos]
+
+    def _flush(self):
+        if self.cur is not None:
+            fid, recs, hints, _ = self.cur
+            with open(data_file_path(self.path, fid), "wb") as f:
+                f.write(b"".join(recs))
+            body = b"".join(hints)
+            with open(hint_file_path(self.path, fid), "wb") as f:
+                f.write(body + struct.pack("<I", xxhash32(body)))
+
+    def write(self, e: Entry):
+        """Returns ("new", file_id) or ("ok", entry_pos) like LogWrite (log.rs:260-263)."""
+        new = self.cur is None or self.cur[3] + e.size() > self.max_file_size
+        if new:
+            self._flush()
+            self.file_id_seq += 1
+            self.cur = [self.file_id_seq, [], [], 0]
+        pos = self.cur[3]
+        self.cur[1].append(e.write_bytes())
+        self.cur[2].append(hint_bytes(e.sequence, e.key, len(e.value), e.deleted, pos))
+        self.cur[3] += e.size()
+        return ("new", self.cur[0]) if new else ("ok", pos)
+
+    def close(self):
+        self._flush()
+        self.cur = None
+
+
+def _valid_hints(path: str, file_id: int):
+    """Log::hints (log.rs:121-135): the hint rows if the hint file is valid, else None."""
+    hp = hint_file_path(path, file_id)
+    if not os.path.isfile(hp):
+        return None
+    with open(hp, "rb") as f:
+        hb = f.read()
+    return hb[:-4] if is_valid_hint_bytes(hb) else None
+
+
+def compact_files(path: str, db: ReplayResult, files, max_file_size: int):
+    """Cask::compact_files (cask.rs:525-560) over compact_files_aux (cask.rs:451-523). Mutates db
+    (index, stats, files, file_id_seq). Per file in the given order: hints of files with a valid
+    hint file (others are skipped and stay), live = index[key].sequence == hint.sequence, then
+    read_entry + LogWriter.write of each live entry. The tombstones of keys absent from the index
+    (highest sequence per key) are written last; the reference iterates a HashMap there, the
+    restatement uses first-seen order (the engine's documented choice). Files created only by
+    tombstone writes are not in new_files (cask.rs:518-520). Raises CaskError on the first
+    failure, leaving what was written so far (as the reference does)."""
+    compacted, new_files = [], []
+    deletes: dict[bytes, int] = {}
+    w = LogWriter(path, max_file_size, db.file_id_seq)
+    try:
+        for fid in files:
+            body = _valid_hints(path, fid)
+            if body is None:
+                continue
+            inserts = []
+            try:
+                hints = list(parse_hints(body))
+            except EOFError:
+                raise CaskError("eof", fid)
+            for h in hints:
+                ie = db.index.map.get(h.key)
+                if h.deleted:
+                    if ie is None and deletes.get(h.key, -1) < h.seq:
+                        deletes[h.key] = h.seq
+                elif ie is not None and ie.sequence == h.seq:
+                    inserts.append(h)
+            for h in inserts:
+                kind, v = w.write(read_entry(path, fid, h.pos))
+                if kind == "new":
+                    new_files.append(v)
+            compacted.append(fid)
+        for key, seq in deletes.items():
+            w.write(entry_deleted(seq, key))
+    finally:
+        w.close()
+        db.file_id_seq = w.file_id_seq
+    for fid in new_files:
+        for h in parse_hints(_valid_hints(path, fid)):
+            db.index.update(h, fid)
+    db.index.stats.remove_files(compacted)
+    for fid in compacted:  # Log::swap_files (log.rs:198-217)
+        db.files.remove(fid)
+        os.remove(data_file_path(path, fid))
+        try:
+            os.remove(hint_file_path(path, fid))
+        except FileNotFoundError:
+            pass
+    db.files = sorted(db.files + new_files)
+    return compacted, new_files
+
+
+def compact_select(path: str, db: ReplayResult, fragmentation_trigger=0.6, dead_bytes_trigger=512 << 20,
+                   fragmentation_threshold=0.4, dead_bytes_threshold=128 << 20,
+                   small_file_threshold=10 << 20):
+    """Cask::compact's file choice (cask.rs:563-642), stats rows visited in ascending file id
+    (the reference visits a HashMap; with trigger >= threshold the chosen set is the same).
+    Returns (triggered, sorted files)."""
+    files: set[int] = set()
+    triggered = False
+    for fid in sorted(db.index.stats.map):
+        e, d, b = db.index.stats.map[fid]
+        frag = d / e
+        if not triggered:
+            if frag >= fragmentation_trigger:
+                triggered = True
+                files.add(fid)
+            elif b >= dead_bytes_trigger and fid not in files:
+                triggered = True
+                files.add(fid)
+        if frag >= fragmentation_threshold and fid not in files:
+            files.add(fid)
+        elif b >= dead_bytes_threshold and fid not in files:
+            files.add(fid)
+        if fid not in files:
+            try:
+                if os.path.getsize(data_file_path(path, fid)) <= small_file_threshold:
+                    files.add(fid)
+            except OSError:
+                pass
+    return triggered, sorted(files)
