@@ -176,7 +176,16 @@ __global__ __launch_bounds__(256) void k_val_apply(ScanArgs a) {
       if (c == 0) ok = true;
       else if (sp != kNone) ok = (sp == run_max);
       else ok = (run_max >= c1);
-      if (!ok) atomicMin((unsigned long long*)&a.first_bad[f], (unsigned long long)c);
+      if (!ok) {
+        atomicMin((unsigned long long*)&a.first_bad[f], (unsigned long long)c);
+        // local repair: T[c] is the chain's true entry into chunk c whenever every earlier chunk
+        // is valid, so the next exact pass starts chunk c there (or skips it: T[c] past its
+        // end). A T[c] behind the chunk comes from a stale earlier exit: keep the old start.
+        if (a.respec) {
+          if (run_max >= c1) a.spec[g] = kNone;
+          else if (run_max >= c0) a.spec[g] = run_max;
+        }
+      }
     }
     run_max = run_max > e[j] ? run_max : e[j];
     run_sum += cn[j];

@@ -305,13 +305,15 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 
   // 2. the chunk's first record boundary
   uint64_t s;
-  if (EXACT) {
-    s = s_exact;
-  } else if (c0 == 0) {
+  if (c0 == 0) {
     s = 0;  // a file's first record starts at 0 (log.rs:116)
   } else if (known) {
-    // the previous chunk of this range ended its chain at `carry` (>= c0): no search needed
+    // the previous chunk of this range ended its chain at `carry` (>= c0): no search needed. In
+    // the exact pass too: the run's first start is exact, so the carry is, and a stretch of
+    // chunks whose stale starts came from the speculative pass is settled in this one pass.
     s = (carry == kTerm || carry >= c1) ? kNone : carry;
+  } else if (EXACT) {
+    s = s_exact;
   } else {
     const uint32_t span = (uint32_t)(c1 - c0);
     // pass A: short records starting in the first kShortMax bytes; pass B: everything, in order.
@@ -583,7 +585,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   // a record that does not fit the window is hashed from HBM by k_long (only the last can)
   m.long_r = (s != kNone && exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
   if (!G::kStoreWave && tid == G::kMetaT) {
-    if (!EXACT) a.spec[t] = m.spec;
+    a.spec[t] = m.spec;  // the exact pass too: the start it used (the carry may replace spec[t])
     a.exit[t] = m.exit;
     a.count[t] = m.count;
     a.long_r[t] = m.long_r;
@@ -593,9 +595,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   if (s != kNone) {
     carry = exitv;
     known = true;
-  } else {
-    known = known && !EXACT;
-  }
+  }  // else: a known chain skips this chunk and stays known; an unknown one stays unknown
   STAMP(2)
 }
 
@@ -604,7 +604,8 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 // starts where the previous one's chain left off (the carry), so the search — a third of the
 // cycles of a speculated chunk — runs once per range. Placement only affects speed: any
 // assignment of chunks to workgroups is correct, and the validation pass checks every start.
-// EXACT (the repair re-scan) reads each chunk's known start from spec[]; the speculative kernel
+// EXACT (the repair re-scan) reads each run's first start from spec[] (later chunks of the run take
+// the carry) and writes back the start it used; the speculative kernel
 // issues no global load besides the staging loads, so the compiler's counted waits never make the
 // processing of one chunk wait for the prefetch of the next.
 // `files` is the same table as a.files, passed as a restrict-qualified argument: the kernel never
@@ -730,7 +731,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
       if (tn != t + 1 || !more || li == 63) {  // run ends (or a wave's worth of entries)
         if (sl <= li) {
           const uint64_t g = run_first + sl;
-          if (!EXACT) a.spec[g] = (uint64_t)v[0].x | ((uint64_t)v[0].y << 32);
+          a.spec[g] = (uint64_t)v[0].x | ((uint64_t)v[0].y << 32);
           a.exit[g] = (uint64_t)v[0].z | ((uint64_t)v[0].w << 32);
           a.count[g] = v[1].x;
           a.long_r[g] = v[1].y;

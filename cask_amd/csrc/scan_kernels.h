@@ -82,6 +82,8 @@ struct ScanArgs {
   unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums
   uint32_t run;                // k_scan_chunks: consecutive chunks a workgroup walks with a carry
   uint32_t regular_ok;         // 1: a regular chunk may keep only its first slot row (kCountRegular)
+  uint32_t respec;             // 1: validation rewrites an invalid chunk's start from T[c] (local repair)
+  uint32_t pad_;
 };
 
 constexpr uint32_t kDefaultRun = 16;

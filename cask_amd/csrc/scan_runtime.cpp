@@ -95,7 +95,7 @@ struct cask_ctx {
   int geo = 0;       // k_scan_chunks geometry (CASK_SCAN_GEOMETRY overrides the default)
   hipEvent_t ev[7] = {};
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
-  uint64_t last_counters[3] = {0, 0, 0};
+  uint64_t last_counters[5] = {0, 0, 0, 0, 0};
   std::mutex mu;
   char last_error[256] = {0};
 };
@@ -181,9 +181,9 @@ int cask_last_timings(const cask_ctx* c, float* ms6) {
   return CASK_OK;
 }
 
-int cask_last_counters(const cask_ctx* c, uint64_t* c3) {
-  if (!c || !c3) return CASK_E_INVALID_ARG;
-  memcpy(c3, c->last_counters, sizeof(c->last_counters));
+int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
+  if (!c || !c5) return CASK_E_INVALID_ARG;
+  memcpy(c5, c->last_counters, sizeof(c->last_counters));
   return CASK_OK;
 }
 
@@ -284,6 +284,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // regular chunks keep only their first slot row when the rows go to the dense output (k_compact
   // expands them); the segmented output hands the slots to the caller, so every row is written
   a.regular_ok = (rows && !getenv("CASK_NO_REGULAR")) ? 1u : 0u;
+  a.respec = getenv("CASK_NO_LOCAL_REPAIR") ? 0u : 1u;
 #ifdef CASK_STAMPS
   if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
 #endif
@@ -355,16 +356,29 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     return head->any_invalid ? 1 : 0;
   }
 #endif
+  uint64_t local_passes = 0, walked = 0;
   if (head->any_invalid) {
-    // Repair: exact boundary walk from each file's first invalid chunk, then a full re-scan
-    // with known starts (exact=1). Chunks before the first invalid one keep their (validated)
-    // speculative starts.
+    // Repair. First, local: validation has already moved every invalid chunk's start to T[c]
+    // (a.respec), which is exact for the first invalid chunk of each stretch, so exact re-scans
+    // (exact=1, no search) settle isolated misses — e.g. a record longer than the window whose
+    // start the search cannot verify — in one or two passes. If that does not converge, the
+    // exact boundary walk from each file's first invalid chunk, then one more exact re-scan.
+    // Chunks before the first invalid one keep their (validated) speculative starts.
     invalid_chunks = head->invalid_chunks;
-    launch_walk(a, d_sum, st);
-    L("k_walk");
     a.exact = 1;
-    pass(false);
-    if (!ok) return CASK_E_DEVICE;
+    const int max_local = getenv("CASK_LOCAL_REPAIRS") ? atoi(getenv("CASK_LOCAL_REPAIRS")) : 3;
+    for (int it = 0; it < max_local && head->any_invalid; ++it) {
+      pass(false);
+      if (!ok) return CASK_E_DEVICE;
+      ++local_passes;
+    }
+    if (head->any_invalid) {
+      walked = 1;
+      launch_walk(a, d_sum, st);
+      L("k_walk");
+      pass(false);
+      if (!ok) return CASK_E_DEVICE;
+    }
     if (head->any_invalid) {  // the exact pass must validate
       snprintf(c->last_error, sizeof(c->last_error), "exact re-scan did not validate");
       return CASK_E_DEVICE;
@@ -386,6 +400,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   c->last_counters[0] = total_chunks;
   c->last_counters[1] = head->nlong;
   c->last_counters[2] = invalid_chunks;
+  c->last_counters[3] = local_passes;
+  c->last_counters[4] = walked;
 
   const uint64_t* row_off = hs + head_words;
   const uint64_t* ferr_row = row_off + nfiles + 1 + 2ull * nfiles;

@@ -192,9 +192,10 @@ class ScanContext:
                 "repair_ms": t[4], "compact_ms": t[5]}
 
     def last_counters(self) -> dict[str, int]:
-        c = (C.c_uint64 * 3)()
+        c = (C.c_uint64 * 5)()
         self.lib.cask_last_counters(self._h, c)
-        return {"chunks": int(c[0]), "long_records": int(c[1]), "repaired_chunks": int(c[2])}
+        return {"chunks": int(c[0]), "long_records": int(c[1]), "repaired_chunks": int(c[2]),
+                "local_repair_passes": int(c[3]), "walked": int(c[4])}
 
     # -- encoder ------------------------------------------------------------------------------
     def encode_synthetic(self, off, seq, ksz, vsz_raw, key_id, value_seed: int, out):

@@ -141,8 +141,10 @@ int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
  * [0] whole device pipeline, [1] chunk-scan kernel, [2] long-record kernel,
  * [3] validate + summary kernels, [4] repair (0 when speculation held), [5] compaction. */
 int cask_last_timings(const cask_ctx* ctx, float* ms6);
-/* Counters of the last call: [0] chunks, [1] long records, [2] invalid chunks repaired. */
-int cask_last_counters(const cask_ctx* ctx, uint64_t* c3);
+/* Counters of the last call: [0] chunks, [1] long records, [2] chunks from each file's first
+ * invalid one on (0: speculation held), [3] local exact re-scans, [4] 1 if the serial boundary
+ * walk ran. */
+int cask_last_counters(const cask_ctx* ctx, uint64_t* c5);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Batched record encoder (Entry::write_bytes, data.rs:90-121) — the bulk write path and the   */

@@ -169,6 +169,42 @@ def test_variable_sizes_with_long_records(gpu_ctx):
     assert gpu_ctx.last_counters()["long_records"] > 0
 
 
+def _zipf_vsz(rng, s=1.1, kmax=4096):
+    """vsz = 16·k, k ~ Zipf(s) truncated to [1, kmax] (BASELINE configs[2] shape)."""
+    w = [k ** -s for k in range(1, kmax + 1)]
+    tot = sum(w)
+    cdf, acc = [], 0.0
+    for x in w:
+        acc += x / tot
+        cdf.append(acc)
+    import bisect
+
+    def f(r):
+        return 16 * (min(bisect.bisect_left(cdf, r.random()), kmax - 1) + 1)
+    return f
+
+
+@pytest.mark.parametrize("seed", [41, 42])
+def test_zipf_sizes_long_records(gpu_ctx, seed):
+    """configs[2] record shape (16 B keys, Zipf value sizes up to 64 KiB): most bytes sit in
+    records longer than the window, whose starts the speculative search cannot verify; the local
+    repair (exact re-scans from T[c]) must settle them without the serial walk."""
+    rng = random.Random(seed)
+    buf = make_records(rng, 4000, lambda r: 16, _zipf_vsz(rng), tomb_p=0.02)
+    check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 3]], device=True)
+    cnt = gpu_ctx.last_counters()
+    assert cnt["long_records"] > 0
+    assert cnt["walked"] == 0, cnt
+
+
+def test_zipf_sizes_corrupt(gpu_ctx):
+    rng = random.Random(43)
+    buf = bytearray(make_records(rng, 3000, lambda r: 16, _zipf_vsz(rng)))
+    for _ in range(3):
+        buf[rng.randrange(len(buf))] ^= 1 << rng.randrange(8)
+    check_against_oracle(gpu_ctx, [bytes(buf)], device=True)
+
+
 def test_many_files_empty_and_tiny(gpu_ctx):
     rng = random.Random(4)
     bufs = []
@@ -196,6 +232,21 @@ def test_adversarial_embedded_records_repair(gpu_ctx):
         out.append(R.entry_new(i + 1, b"outer%d" % i, v).write_bytes())
     check_against_oracle(gpu_ctx, [b"".join(out)])
     assert gpu_ctx.last_counters()["repaired_chunks"] > 0
+
+
+def test_adversarial_repair_by_walk_only(gpu_ctx):
+    """The same input with the local repair disabled: the exact boundary walk alone repairs it."""
+    rng = random.Random(5)
+    inner = [R.entry_new(10_000 + i, rng.randbytes(8), rng.randbytes(rng.randrange(0, 40))).write_bytes()
+             for i in range(64)]
+    out = [R.entry_new(i + 1, b"outer%d" % i, b"".join(rng.choice(inner) for _ in range(rng.randrange(1, 30))))
+           .write_bytes() for i in range(3000)]
+    os.environ["CASK_LOCAL_REPAIRS"] = "0"
+    try:
+        check_against_oracle(gpu_ctx, [b"".join(out)])
+        assert gpu_ctx.last_counters()["walked"] == 1
+    finally:
+        del os.environ["CASK_LOCAL_REPAIRS"]
 
 
 def test_all_zero_file(gpu_ctx):
