@@ -180,6 +180,27 @@ __device__ __forceinline__ uint32_t quad_xxh32(const uint32_t* w, uint32_t xs, u
     const uint32_t sh = xs & 3;
     uint32_t i = (xs >> 2) + a;  // lane a: dwords i, i+1 of every stripe (aligned ds_read2_b32)
     uint32_t s = 0;
+    if (nstr >= 8) {  // double-buffered: the next block's 8 reads are in flight while this one mixes
+      uint32_t A[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        A[2 * k] = w[i + 4 * k];
+        A[2 * k + 1] = w[i + 4 * k + 1];
+      }
+      for (; s + 8 <= nstr; s += 4) {
+        uint32_t An[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          An[2 * k] = w[i + 16 + 4 * k];
+          An[2 * k + 1] = w[i + 16 + 4 * k + 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v = xround(v, fun(A[2 * k], A[2 * k + 1], sh));
+#pragma unroll
+        for (int k = 0; k < 8; ++k) A[k] = An[k];
+        i += 16;
+      }
+    }
     for (; s + 4 <= nstr; s += 4) {  // 8 reads in flight, then 4 rounds
       const uint32_t a0 = w[i], b0 = w[i + 1], a1 = w[i + 4], b1 = w[i + 5];
       const uint32_t a2 = w[i + 8], b2 = w[i + 9], a3 = w[i + 12], b3 = w[i + 13];
@@ -297,7 +318,27 @@ __device__ __forceinline__ uint32_t gbl_xxh32(const uint8_t* p, uint64_t len) {
   if (len >= 16) {
     Acc a = acc_init(0);
     const uint64_t nstr = len >> 4;
-    for (uint64_t s = 0; s < nstr; ++s) {
+    uint64_t s = 0;
+    if (nstr >= 8) {  // double-buffered: the next 128 B are in flight while these 128 B mix
+      u32x4 A[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) A[k] = gld16(p + 16 * k);
+      for (; s + 16 <= nstr; s += 8) {
+        u32x4 B[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) B[k] = gld16(p + 128 + 16 * k);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) acc_stripe(a, A[k].x, A[k].y, A[k].z, A[k].w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) A[k] = B[k];
+        p += 128;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc_stripe(a, A[k].x, A[k].y, A[k].z, A[k].w);
+      p += 128;
+      s += 8;
+    }
+    for (; s < nstr; ++s) {
       const u32x4 v = gld16(p);
       acc_stripe(a, v.x, v.y, v.z, v.w);
       p += 16;
@@ -307,14 +348,23 @@ __device__ __forceinline__ uint32_t gbl_xxh32(const uint8_t* p, uint64_t len) {
     h = P5;
   }
   h += (uint32_t)len;
-  while (p + 4 <= end) {
-    h = tail4(h, gld4(p));
-    p += 4;
-  }
-  while (p < end) {
-    h = tail1(h, *p);
-    ++p;
-  }
+  // the last < 16 bytes: loaded at once (no load waits on another), then folded in order
+  const uint32_t nt = (uint32_t)(end - p);
+  uint32_t t4[3] = {0u, 0u, 0u};
+  uint8_t t1[3] = {0, 0, 0};
+  const uint32_t n4 = nt >> 2, n1 = nt & 3;
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n4) t4[k] = gld4(p + 4 * k);
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n1) t1[k] = p[4 * n4 + k];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n4) h = tail4(h, t4[k]);
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n1) h = tail1(h, t1[k]);
   return avalanche(h);
 }
 

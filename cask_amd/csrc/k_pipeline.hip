@@ -6,27 +6,38 @@
 namespace cask_dev {
 
 // ------------------------------------------------------------------------------------------
-// K_long: records longer than the LDS window, one lane each, straight from HBM.
+// K_long: the records the chunk scan did not hash out of LDS — those that run past the window, or
+// are longer than ScanArgs::big — hashed straight from HBM, one lane per chunk over rows
+// long_r[t] .. count-1 (the same rule picks them: lds_hashed()). EOF rows have already failed.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_long(ScanArgs a) {
+  uint32_t nl = 0;
   for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < a.total_chunks;
        t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t r = a.long_r[t];
-    if (r == 0xFFFFFFFFu) continue;
-    atomicAdd(&a.ctr->nlong, 1ull);
+    const uint32_t r0 = a.long_r[t];
+    if (r0 == 0xFFFFFFFFu) continue;
+    const uint32_t n = a.count[t] & kCountMask;
     const uint32_t fi = find_file(a.files, a.nfiles, t);
     const FileDesc fd = a.files[fi];
-    const uint64_t slot = t * a.slot_cap + r;
-    uint32_t* w = a.slots + slot * 4;
-    const uint64_t p = (t - fd.first_chunk) * (uint64_t)a.chunk + ((w[3] >> 16) & 0x7FFFu);
-    const uint32_t vsz = w[2];
-    const uint64_t rl = 18ull + (w[3] & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
-    const uint32_t stored = gld4(fd.data + p);
-    if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {
-      w[3] |= kSlotBad;
-      atomicMin(&a.file_err[fi], (unsigned long long)slot);
+    const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+    const uint64_t wend = c0 + a.win < fd.len ? c0 + a.win : fd.len;
+    for (uint32_t r = r0; r < n; ++r) {
+      const uint64_t slot = t * a.slot_cap + r;
+      uint32_t* w = a.slots + slot * 4;
+      const uint32_t w3 = w[3], vsz = w[2];
+      const uint64_t p = c0 + ((w3 >> 16) & 0x7FFFu);
+      const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+      if (p + rl > fd.len || lds_hashed(p, rl, wend, a.big)) continue;  // EOF row, or done in LDS
+      ++nl;
+      const uint32_t stored = gld4(fd.data + p);
+      if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {
+        w[3] = w3 | kSlotBad;
+        atomicMin(&a.file_err[fi], (unsigned long long)slot);
+      }
     }
   }
+  for (int o = 32; o; o >>= 1) nl += __shfl_xor(nl, o, 64);  // one counter update per wave
+  if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&a.ctr->nlong, (unsigned long long)nl);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -372,7 +383,9 @@ static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
 void launch_long(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
-  hipLaunchKernelGGL(k_long, dim3(1024), dim3(256), 0, S(stream), a);
+  uint64_t blocks = (a.total_chunks + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_long, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
 }
 void launch_validate(const ScanArgs& a, void* stream) {
   if (!a.nfiles) return;

@@ -59,6 +59,7 @@ struct __attribute__((aligned(16))) ScanLdsT {
   uint32_t found, n;  // search result; slow path: rows of the chunk
   uint32_t claimed;   // the run this workgroup takes after its current one
   uint32_t ffail;     // stride pass: first row whose header breaks the stride
+  uint32_t ldefer;    // slow path: first row left to k_long (longer than ScanArgs::big)
   uint32_t irreg;     // stride pass: some row breaks the regular-chunk pattern (kCountRegular)
   uint64_t exitv, lastp, lastrl;  // slow path: walk results (wave 0 -> workgroup)
 };
@@ -184,7 +185,7 @@ __device__ __forceinline__ void stage_store(ScanLdsT<G>& L, const u32x4 (&v)[G::
 // the row is a failure (InvalidChecksum, or the UnexpectedEof row).
 template <class G>
 __device__ __forceinline__ bool quad_row(const uint32_t* W, const ChunkPos& c, uint32_t* slots, uint32_t r,
-                                         uint32_t off, uint32_t a, Diag& dg) {
+                                         uint32_t off, uint32_t a, uint32_t big, Diag& dg) {
 #ifdef CASK_STAMPS
   const uint64_t st_h0_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -203,12 +204,12 @@ __device__ __forceinline__ bool quad_row(const uint32_t* W, const ChunkPos& c, u
     const uint64_t rl = 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
     if (p + rl > c.len) {
       fail = true;  // EOF row (data.rs:172,181)
-    } else if (p + rl <= c.wend) {
+    } else if (lds_hashed(p, rl, c.wend, big)) {
       if (quad_xxh32(W, x + 4, (uint32_t)rl - 4, a) != h.stored) {  // data.rs:193-198
         w3 |= kSlotBad;
         fail = true;
       }
-    }  // else: longer than the window, left to k_long
+    }  // else: left to k_long (hashed from HBM)
   }
   const uint32_t word = a == 0 ? w0 : a == 1 ? w1 : a == 2 ? w2 : w3;
 #ifdef CASK_STAMPS
@@ -362,6 +363,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   const unsigned long long err_base = (unsigned long long)t * a.slot_cap;
   uint32_t n = 0;
   uint64_t exitv = 0, lastp = 0, lastrl = 0;
+  bool rl0_big = false;  // the stride rows' records are longer than a.big (k_long hashes them)
   uint32_t k = 0;  // rows settled by the stride pass
   bool slow = false, regular = false;
   if (s != kNone) {
@@ -376,6 +378,19 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       rl0 = uni64(lds_reclen(W, srel + shift));  // wave-uniform: scalar loop counts in the hash
       if (s + rl0 <= len) cnt = rl0 >= span ? 1u : ceil_div_small(span, (uint32_t)rl0);
     }
+    // Records 1..3 at the stride (uniform reads, one LDS round trip): if one breaks it, the chunk's
+    // records vary in length and the slow path takes them all — otherwise the stride pass would
+    // hash cnt strided stretches of bytes that are not records.
+    if (cnt > 1) {
+      bool brk = false;
+#pragma unroll
+      for (uint32_t j = 1; j <= 3; ++j) {
+        const uint64_t q = s + j * rl0;
+        if (j < cnt && q + 18 <= len) brk |= lds_reclen(W, (uint32_t)(q - c0) + shift) != rl0;
+      }
+      if (brk) cnt = 0;
+    }
+    rl0_big = rl0 > a.big;
     const uint32_t r32 = cnt > 1 ? (uint32_t)rl0 : 0u;  // stride; rl0 < span <= CH when cnt > 1
     // One record per lane (STRIDE_QUAD: per quad of lanes, two records per quad).
     uint32_t failmask = 0;  // bit j: this lane's (quad's) j-th record failed verification
@@ -396,7 +411,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       const uint32_t o = srel + i * r32;
       const Hdr h = lds_hdr(W, o + shift);  // inside the window: o < CH
       const bool ok = stride_ok(i, o, h);
-      const bool hs = ok && (uint64_t)o + rl0 <= wrel;  // else k_long
+      const bool hs = ok && lds_hashed(c0 + o, rl0, wend, a.big);  // else k_long
 #ifdef CASK_DIAG_NO_HASH  // diagnostic: everything but the checksum arithmetic (rows say "verified")
       const uint32_t g = h.stored;
 #else
@@ -430,7 +445,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       const uint32_t o0 = srel + i0 * r32, o1 = srel + (has1 ? i1 : i0) * r32;
       const Hdr h0 = lds_hdr(W, o0 + shift), h1 = lds_hdr(W, o1 + shift);  // inside the window: o < CH
       const bool ok0 = stride_ok(i0, o0, h0), ok1 = has1 && stride_ok(i1, o1, h1);
-      const bool hs0 = ok0 && (uint64_t)o0 + rl0 <= wrel, hs1 = ok1 && (uint64_t)o1 + rl0 <= wrel;  // else k_long
+      const bool hs0 = ok0 && lds_hashed(c0 + o0, rl0, wend, a.big), hs1 = ok1 && lds_hashed(c0 + o1, rl0, wend, a.big);
       uint32_t g0 = 0, g1 = 0;
 #ifdef CASK_DIAG_NO_HASH  // diagnostic: everything but the checksum arithmetic (rows say "verified")
       g0 = h0.stored;
@@ -510,7 +525,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     pf_n = 0;
     BAR();
     if (wave == 0) {
-      uint32_t nn = k;
+      uint32_t nn = k, ld = 0xFFFFFFFFu;  // ld: first walked row longer than a.big
       uint64_t ex = 0, lp = 0, lr = 0;
       uint64_t p = s + (k ? (uint64_t)k * lds_reclen(W, (uint32_t)(s - c0) + shift) : 0ull);
       for (;;) {
@@ -531,6 +546,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
           ex = kTerm;
           break;
         }
+        if (rl > a.big && ld == 0xFFFFFFFFu) ld = nn;
         const uint64_t span = c1 - p;
         const uint32_t M = span > 192ull * rl ? 4u : span > 128ull * rl ? 3u : span > 64ull * rl ? 2u : 1u;
         bool vj[4];
@@ -564,6 +580,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       }
       if (lane == 0) {
         L.n = nn;
+        L.ldefer = ld;
         L.exitv = ex;
         L.lastp = lp;
         L.lastrl = lr;
@@ -575,7 +592,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     lastp = L.lastp;
     lastrl = L.lastrl;
     for (uint32_t r = k + quad; r < n; r += NQ) {
-      if (quad_row<G>(W, c, slots, r, L.starts[r], qa, dg) && qa == 0) atomicMin(&a.file_err[c.fi], err_base + r);
+      if (quad_row<G>(W, c, slots, r, L.starts[r], qa, a.big, dg) && qa == 0) atomicMin(&a.file_err[c.fi], err_base + r);
     }
   }
   DCHECK(n <= a.slot_cap && t < a.total_chunks, "n %u t %llu", n, (unsigned long long)t);
@@ -583,7 +600,13 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   m.exit = (s == kNone) ? 0 : exitv;
   m.count = n | (regular ? kCountRegular : 0u);
   // a record that does not fit the window is hashed from HBM by k_long (only the last can)
-  m.long_r = (s != kNone && exitv != kTerm && n && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
+  // k_long hashes, from row long_r on, the rows lds_hashed() rejects: from 0 when the stride rows
+  // are longer than a.big; else the slow path's first such row; else the last row when it runs
+  // past the window
+  m.long_r = (s == kNone || !n) ? 0xFFFFFFFFu
+             : (k && rl0_big) ? 0u
+             : (L.ldefer != 0xFFFFFFFFu) ? L.ldefer
+             : (exitv != kTerm && lastp + lastrl > wend) ? n - 1 : 0xFFFFFFFFu;
   if (!G::kStoreWave && tid == G::kMetaT) {
     a.spec[t] = m.spec;  // the exact pass too: the start it used (the carry may replace spec[t])
     a.exit[t] = m.exit;
@@ -657,6 +680,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
       L.found = 0xFFFFFFFFu;
       L.ffail = 0xFFFFFFFFu;
       L.irreg = 0u;
+      L.ldefer = 0xFFFFFFFFu;
     }
     if (threadIdx.x == G::kMetaT && publish) {
       L.claimed = my_claim;
@@ -783,6 +807,7 @@ using GeoC = Geo<8192, 1008, 64, 16>;
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
 uint32_t geometry_chunk(int geo) { return geo == 1 ? GeoB::kCh : geo == 2 ? GeoC::kCh : GeoA::kCh; }
+uint32_t geometry_halo(int geo) { return geo == 1 ? GeoB::kHaloB : geo == 2 ? GeoC::kHaloB : GeoA::kHaloB; }
 
 template <class G>
 static void launch_geo(const ScanArgs& a, void* stream) {

@@ -83,8 +83,18 @@ struct ScanArgs {
   uint32_t run;                // k_scan_chunks: consecutive chunks a workgroup walks with a carry
   uint32_t regular_ok;         // 1: a regular chunk may keep only its first slot row (kCountRegular)
   uint32_t respec;             // 1: validation rewrites an invalid chunk's start from T[c] (local repair)
-  uint32_t pad_;
+  uint32_t big;                // records longer than this are hashed by k_long from HBM, not in LDS
+  uint32_t win;                // bytes staged per chunk (chunk + halo): the LDS window
 };
+
+// Default ScanArgs::big: no limit — the chunk scan hashes every record that fits its window.
+constexpr uint32_t kBigRec = 0xFFFFFFFFu;
+
+// Whether the chunk scan hashes the record [p, p + rl) of a chunk whose window ends at wend out of
+// LDS (the same rule in k_scan_chunks and k_long): it fits the window and is at most `big` long.
+__host__ __device__ __forceinline__ bool lds_hashed(uint64_t p, uint64_t rl, uint64_t wend, uint32_t big) {
+  return p + rl <= wend && rl <= big;
+}
 
 constexpr uint32_t kDefaultRun = 16;
 
@@ -108,6 +118,7 @@ struct GatherRec {
 // Host-callable launchers (defined in scan_kernels.hip).
 void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src, uint8_t* dst, void* stream);
 uint32_t geometry_chunk(int geo);
+uint32_t geometry_halo(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
 void launch_long(const ScanArgs& a, void* stream);
 void launch_validate(const ScanArgs& a, void* stream);

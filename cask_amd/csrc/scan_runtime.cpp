@@ -285,6 +285,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // expands them); the segmented output hands the slots to the caller, so every row is written
   a.regular_ok = (rows && !getenv("CASK_NO_REGULAR")) ? 1u : 0u;
   a.respec = getenv("CASK_NO_LOCAL_REPAIR") ? 0u : 1u;
+  // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
+  a.big = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
+  a.win = chunk + geometry_halo(c->geo);
 #ifdef CASK_STAMPS
   if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
 #endif

@@ -23,7 +23,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def cfg3(ctx, torch, steps, total_gib, max_file):
+def zipf_files(ctx, torch, total_gib, max_file):
+    """configs[2] files on the device: [(DataFile, record indices)], the value sizes, n, rec lens."""
     from cask_amd.workloads import variable_file, zipf_sizes
     dev = torch.device("cuda", ctx.device)
     target = int(total_gib * 2 ** 30)
@@ -45,6 +46,12 @@ def cfg3(ctx, torch, steps, total_gib, max_file):
         r0 = r1
     del cum
     torch.cuda.synchronize(dev)
+    return files, vsz, n, rl
+
+
+def cfg3(ctx, torch, steps, total_gib, max_file):
+    dev = torch.device("cuda", ctx.device)
+    files, vsz, n, rl = zipf_files(ctx, torch, total_gib, max_file)
     views = [(f.file_id, f.data) for f, _ in files]
     nbytes = sum(f.data.numel() for f, _ in files)
     rows = ctx.alloc_rows(n + 16)

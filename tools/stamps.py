@@ -20,6 +20,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--files", type=int, default=2)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--zipf-gib", type=float, default=0.0, help="configs[2]-shaped files instead of configs[1]")
     args = ap.parse_args()
     import torch
     import cask_amd
@@ -28,9 +29,14 @@ def main():
     L.cask_debug_stamps.restype = C.c_int
     L.cask_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     ctx = cask_amd.ScanContext(0)
-    files = cfg2_files(ctx, nfiles=args.files)
+    if args.zipf_gib > 0:
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from bench_configs import zipf_files
+        files = [f for f, _ in zipf_files(ctx, torch, args.zipf_gib, 2 ** 31)[0]]
+    else:
+        files = cfg2_files(ctx, nfiles=args.files)
     views = [(f.file_id, f.data) for f in files]
-    rows = ctx.alloc_rows(sum(f.nrec for f in files))
+    rows = ctx.alloc_rows(sum(f.nrec for f in files) + 16)
     for _ in range(args.iters):
         res = ctx.scan_device(views, rows)
     st = (C.c_uint64 * 16)()
