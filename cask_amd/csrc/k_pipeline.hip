@@ -18,6 +18,7 @@ __global__ __launch_bounds__(256) void k_long(ScanArgs a) {
     if (r0 == 0xFFFFFFFFu) continue;
     const uint32_t n = a.count[t] & kCountMask;
     const uint32_t fi = find_file(a.files, a.nfiles, t);
+    if (a.first_bad[fi] != kNone) continue;  // invalid: the repair pass re-scans this file
     const FileDesc fd = a.files[fi];
     const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint64_t wend = c0 + a.win < fd.len ? c0 + a.win : fd.len;
@@ -258,6 +259,7 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a, const uint64_t* sum
   const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
   for (uint64_t t = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); t < a.total_chunks; t += nw) {
     const uint32_t fi = find_file(a.files, a.nfiles, t);
+    if (a.first_bad[fi] != kNone) continue;  // invalid: the repair pass re-scans this file
     const FileDesc fd = a.files[fi];
     const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint32_t cw = a.count[t], n = cw & kCountMask;

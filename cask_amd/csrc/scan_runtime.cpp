@@ -318,11 +318,12 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_scan_chunks(a, c->geo, st);
     L("k_scan_chunks");
     if (timed) H(hipEventRecord(c->ev[2], st));
-    launch_long(a, st);
-    L("k_long");
-    if (timed) H(hipEventRecord(c->ev[3], st));
+    // validation before k_long: k_long skips the files a repair pass is about to re-scan
     launch_validate(a, st);
     L("k_val");
+    if (timed) H(hipEventRecord(c->ev[3], st));
+    launch_long(a, st);
+    L("k_long");
     launch_summary(a, d_sum, st);
     L("k_summary");
     if (timed) H(hipEventRecord(c->ev[4], st));
@@ -390,8 +391,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
   float t_all = 0, t_k1 = 0, t_long = 0, t_val = 0, t_cmp = 0;
   (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
-  (void)hipEventElapsedTime(&t_long, c->ev[2], c->ev[3]);
-  (void)hipEventElapsedTime(&t_val, c->ev[3], c->ev[4]);
+  (void)hipEventElapsedTime(&t_val, c->ev[2], c->ev[3]);
+  (void)hipEventElapsedTime(&t_long, c->ev[3], c->ev[4]);  // with the summary (a few us)
   (void)hipEventElapsedTime(&t_cmp, c->ev[4], c->ev[5]);
   (void)hipEventElapsedTime(&t_all, c->ev[0], c->ev[5]);
   c->last_ms[0] = t_all + repair_ms;

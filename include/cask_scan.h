@@ -138,8 +138,8 @@ int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
                    cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);
 
 /* Timing of the last cask_scan_* call on the context's stream (HIP events, milliseconds):
- * [0] whole device pipeline, [1] chunk-scan kernel, [2] long-record kernel,
- * [3] validate + summary kernels, [4] repair (0 when speculation held), [5] compaction. */
+ * [0] whole device pipeline, [1] chunk-scan kernel, [2] long-record + summary kernels,
+ * [3] validation kernels, [4] repair (0 when speculation held), [5] compaction. */
 int cask_last_timings(const cask_ctx* ctx, float* ms6);
 /* Counters of the last call: [0] chunks, [1] long records, [2] chunks from each file's first
  * invalid one on (0: speculation held), [3] local exact re-scans, [4] 1 if the serial boundary
