@@ -147,6 +147,8 @@ def lib():
             pass
         L = C.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            if os.environ.get("CASK_LIB_PATH") and not hasattr(L, name):
+                continue  # a diagnostic or older build (A/B timing): bind what it has
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -294,7 +294,7 @@ __device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_
 
 template <class G, bool EXACT>
 __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a, uint64_t t, const ChunkPos& c,
-                                              uint64_t s_exact, uint64_t& carry, bool& known, uint32_t par,
+                                              uint64_t s_exact, uint64_t& carry, bool& known, bool& strided, uint32_t par,
                                               uint32_t& pf_n, uint32_t*& pf_slots, Meta& m, Diag& dg) {
   constexpr uint32_t NT = G::kNT;
   constexpr uint32_t NQ = NT / 4;  // quads: one record per quad of lanes
@@ -381,7 +381,9 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     // Records 1..3 at the stride (uniform reads, one LDS round trip): if one breaks it, the chunk's
     // records vary in length and the slow path takes them all — otherwise the stride pass would
     // hash cnt strided stretches of bytes that are not records.
-    if (cnt > 1) {
+    // Skipped after a chunk the stride pass settled whole (uniform logs: the next chunk almost
+    // always is too, and the pass itself finds a break).
+    if (cnt > 1 && !strided) {
       bool brk = false;
 #pragma unroll
       for (uint32_t j = 1; j <= 3; ++j) {
@@ -619,6 +621,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     carry = exitv;
     known = true;
   }  // else: a known chain skips this chunk and stays known; an unknown one stays unknown
+  strided = s != kNone && !slow;
   STAMP(2)
 }
 
@@ -668,6 +671,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   uint32_t* pf_slots = a.slots;
   uint64_t carry = 0;  // chain position entering chunk t, when known
   bool known = false;  // only the first chunk of the range (and chunks after a failed search) search
+  bool strided = false;  // the previous chunk's records were all settled by the stride pass
   ChunkPos cur = locate<G>(files, a.nfiles, t);
   u32x4 v[G::kNL];
   stage_issue<G>(v, cur, a.stamps, t);
@@ -742,7 +746,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #ifndef CASK_STAGE_ONLY
     Meta m;
     m.desc = u32x4{0u, 0u, 0u, 0u};
-    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, par, pf_n, pf_slots, m, dg);
+    process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, strided, par, pf_n, pf_slots, m, dg);
     if (G::kStoreWave && threadIdx.x >= G::kLoadT) {
       // store wave: lane (t - run_first) keeps chunk t's entries in the staging registers this wave
       // never loads into; the run's entries go out when the run ends
