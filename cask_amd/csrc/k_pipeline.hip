@@ -19,6 +19,7 @@ __global__ __launch_bounds__(256) void k_long(ScanArgs a) {
     const uint32_t n = a.count[t] & kCountMask;
     const uint32_t fi = find_file(a.files, a.nfiles, t);
     if (a.first_bad[fi] != kNone) continue;  // invalid: the repair pass re-scans this file
+    if (a.long_skip && a.long_skip[fi]) continue;  // hashed by an earlier pass (valid then, not re-scanned since)
     const FileDesc fd = a.files[fi];
     const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint64_t wend = c0 + a.win < fd.len ? c0 + a.win : fd.len;
@@ -33,6 +34,7 @@ __global__ __launch_bounds__(256) void k_long(ScanArgs a) {
       const uint32_t stored = gld4(fd.data + p);
       if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {
         w[3] = w3 | kSlotBad;
+        atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
         atomicMin(&a.file_err[fi], (unsigned long long)slot);
       }
     }
@@ -188,6 +190,9 @@ __global__ __launch_bounds__(256) void k_val_apply(ScanArgs a) {
       if (c == 0) ok = true;
       else if (sp != kNone) ok = (sp == run_max);
       else ok = (run_max >= c1);
+      a.redo[g] = ok ? 0 : 1;  // a repair pass re-scans the chunks flagged here
+      const uint32_t ce = a.cerr[g];
+      if (ce != 0xFFFFFFFFu) atomicMin(&a.file_err[f], (unsigned long long)(g * a.slot_cap + ce));
       if (!ok) {
         atomicMin((unsigned long long*)&a.first_bad[f], (unsigned long long)c);
         // local repair: T[c] is the chain's true entry into chunk c whenever every earlier chunk

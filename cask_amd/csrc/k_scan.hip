@@ -61,6 +61,8 @@ struct __attribute__((aligned(16))) ScanLdsT {
   uint32_t ffail;     // stride pass: first row whose header breaks the stride
   uint32_t ldefer;    // slow path: first row left to k_long (longer than ScanArgs::big)
   uint32_t irreg;     // stride pass: some row breaks the regular-chunk pattern (kCountRegular)
+  uint32_t cerr_s;    // stride pass: lowest failing row (rows past the stride break included)
+  uint32_t cerr_w;    // slow path: lowest failing row
   uint64_t exitv, lastp, lastrl;  // slow path: walk results (wave 0 -> workgroup)
 };
 
@@ -269,6 +271,7 @@ __device__ __forceinline__ bool stride_row(ScanLdsT<G>& L, uint32_t par, uint32_
 struct Meta {
   uint64_t spec, exit;
   uint32_t count, long_r;
+  uint32_t cerr;  // first failing row (!0: none): ScanArgs::cerr
   u32x4 desc;  // first row of a regular chunk
 };
 
@@ -360,8 +363,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 #else
   uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
 #endif
-  const unsigned long long err_base = (unsigned long long)t * a.slot_cap;
-  uint32_t n = 0;
+  uint32_t n = 0, cerr = 0xFFFFFFFFu;  // cerr: the chunk's first failing row
   uint64_t exitv = 0, lastp = 0, lastrl = 0;
   bool rl0_big = false;  // the stride rows' records are longer than a.big (k_long hashes them)
   uint32_t k = 0;  // rows settled by the stride pass
@@ -371,7 +373,6 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     const uint32_t srel = (uint32_t)(s - c0), span = (uint32_t)(c1 - s);
     const uint64_t lrel64 = len - c0;
     const uint32_t lrel = lrel64 < 0xFFFFFFFFull ? (uint32_t)lrel64 : 0xFFFFFFFFu;
-    const uint32_t wrel = (uint32_t)(wend - c0);
     uint64_t rl0 = 0;
     uint32_t cnt = 0;
     if (s + 18 <= len) {
@@ -395,7 +396,6 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     rl0_big = rl0 > a.big;
     const uint32_t r32 = cnt > 1 ? (uint32_t)rl0 : 0u;  // stride; rl0 < span <= CH when cnt > 1
     // One record per lane (STRIDE_QUAD: per quad of lanes, two records per quad).
-    uint32_t failmask = 0;  // bit j: this lane's (quad's) j-th record failed verification
     const uint32_t hl = (uint32_t)rl0 - 4;
     auto stride_ok = [&](uint32_t i, uint32_t o, const Hdr& h) -> bool {
       if (!i) return true;  // cnt > 0: the first record fits the file
@@ -409,7 +409,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     const Hdr hf = cnt ? lds_hdr(W, srel + shift) : Hdr{};
 #ifndef CASK_STRIDE_QUAD
     bool irreg = false;
-    for (uint32_t i = tid, j = 0; i < cnt; i += NT, ++j) {
+    for (uint32_t i = tid; i < cnt; i += NT) {
       const uint32_t o = srel + i * r32;
       const Hdr h = lds_hdr(W, o + shift);  // inside the window: o < CH
       const bool ok = stride_ok(i, o, h);
@@ -435,13 +435,13 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
           ((u32x4*)slots)[i] = row;
 #endif
         }
-        if (bad) failmask |= 1u << j;
+        if (bad) atomicMin(&L.cerr_s, i);
         irreg |= bad || !hs || h.ksz != hf.ksz || h.vsz != hf.vsz || h.seq != hf.seq + i;
       }
     }
     if (__ballot(irreg) && lane == 0) atomicOr(&L.irreg, 1u);
 #else
-    for (uint32_t i0 = quad, j = 0; i0 < cnt; i0 += 2 * NQ, j += 2) {
+    for (uint32_t i0 = quad; i0 < cnt; i0 += 2 * NQ) {
       const uint32_t i1 = i0 + NQ;
       const bool has1 = i1 < cnt;
       const uint32_t o0 = srel + i0 * r32, o1 = srel + (has1 ? i1 : i0) * r32;
@@ -465,13 +465,13 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       if (!ok0) {
         if (qa == 0) atomicMin(&L.ffail, i0);
       } else if (stride_row<G>(L, par, slots, i0, o0, h0, hs0 && g0 != h0.stored, qa)) {  // data.rs:193-198
-        failmask |= 1u << j;
+        if (qa == 0) atomicMin(&L.cerr_s, i0);
       }
       if (has1) {
         if (!ok1) {
           if (qa == 0) atomicMin(&L.ffail, i1);
         } else if (stride_row<G>(L, par, slots, i1, o1, h1, hs1 && g1 != h1.stored, qa)) {
-          failmask |= 2u << j;
+          if (qa == 0) atomicMin(&L.cerr_s, i1);
         }
       }
     }
@@ -493,19 +493,8 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       m.desc.w = hf.ksz | (srel << 16);
     }
 #endif
-#ifndef CASK_STRIDE_QUAD
-    for (uint32_t m = failmask; m; m &= m - 1) {
-      const uint32_t i = tid + (uint32_t)__builtin_ctz(m) * NT;
-      if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
-    }
-#else
-    if (qa == 0) {
-      for (uint32_t m = failmask; m; m &= m - 1) {
-        const uint32_t i = quad + (uint32_t)__builtin_ctz(m) * NQ;
-        if (i < k) atomicMin(&a.file_err[c.fi], err_base + i);
-      }
-    }
-#endif
+    // the lowest failing row counts only if it lies before the stride break (then it is the first)
+    cerr = L.cerr_s < k ? L.cerr_s : 0xFFFFFFFFu;
     if (k == cnt && cnt) {
       n = cnt;
       lastp = s + (uint64_t)(cnt - 1) * rl0;
@@ -594,13 +583,16 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     lastp = L.lastp;
     lastrl = L.lastrl;
     for (uint32_t r = k + quad; r < n; r += NQ) {
-      if (quad_row<G>(W, c, slots, r, L.starts[r], qa, a.big, dg) && qa == 0) atomicMin(&a.file_err[c.fi], err_base + r);
+      if (quad_row<G>(W, c, slots, r, L.starts[r], qa, a.big, dg) && qa == 0) atomicMin(&L.cerr_w, r);
     }
+    BAR();  // every slow-path row's verdict is in L.cerr_w
+    cerr = cerr < L.cerr_w ? cerr : L.cerr_w;
   }
   DCHECK(n <= a.slot_cap && t < a.total_chunks, "n %u t %llu", n, (unsigned long long)t);
   m.spec = s;
   m.exit = (s == kNone) ? 0 : exitv;
   m.count = n | (regular ? kCountRegular : 0u);
+  m.cerr = cerr;
   // a record that does not fit the window is hashed from HBM by k_long (only the last can)
   // k_long hashes, from row long_r on, the rows lds_hashed() rejects: from 0 when the stride rows
   // are longer than a.big; else the slow path's first such row; else the last row when it runs
@@ -614,6 +606,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     a.exit[t] = m.exit;
     a.count[t] = m.count;
     a.long_r[t] = m.long_r;
+    a.cerr[t] = m.cerr;
     if (regular) ((u32x4*)a.desc)[t] = m.desc;
   }
   // the next chunk of the run starts where this chain left off
@@ -647,8 +640,18 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   // Runs of a.run consecutive chunks are handed out in order by a counter (one atomic per run, a
   // run ahead), so workgroups that run slower take fewer runs and all finish together; each run is
   // walked in order with a carry.
+  // A repair pass re-scans only the stretches listed in a.runs (each one walked like a run).
   const uint64_t R = a.run;
-  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  const uint64_t nruns = a.runs ? a.nruns_list : (a.total_chunks + R - 1) / R;
+  auto run_at = [&](uint64_t r, uint64_t& first, uint64_t& end) {
+    if (a.runs) {
+      first = a.runs[2 * r];
+      end = a.runs[2 * r + 1];
+    } else {
+      first = r * R;
+      end = first + R < a.total_chunks ? first + R : a.total_chunks;
+    }
+  };
   uint32_t my_claim = 0;  // thread kMetaT: the run claimed for after the current one
   bool publish = false;   // thread kMetaT: my_claim still to be published in L.claimed
   if (threadIdx.x == G::kMetaT) {
@@ -658,8 +661,8 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   BAR();
   const uint64_t r0 = L.found;
   if (r0 >= nruns) return;
-  uint64_t t = r0 * R;
-  uint64_t run_end = t + R < a.total_chunks ? t + R : a.total_chunks;
+  uint64_t t, run_end;
+  run_at(r0, t, run_end);
   uint64_t run_first = t;  // first chunk of the current run (its chunk-table entries go out together)
   BAR();  // L.found is reset by thread 0 below
 #ifdef CASK_STAMPS
@@ -685,6 +688,8 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
       L.ffail = 0xFFFFFFFFu;
       L.irreg = 0u;
       L.ldefer = 0xFFFFFFFFu;
+      L.cerr_s = 0xFFFFFFFFu;
+      L.cerr_w = 0xFFFFFFFFu;
     }
     if (threadIdx.x == G::kMetaT && publish) {
       L.claimed = my_claim;
@@ -720,8 +725,12 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
     uint64_t tn = t + 1, next_end = run_end;
     if (tn >= run_end) {  // next run of this workgroup: the one claimed a run ago
       const uint64_t rn = L.claimed;
-      tn = rn < nruns ? rn * R : a.total_chunks;
-      next_end = tn + R < a.total_chunks ? tn + R : a.total_chunks;
+      if (rn < nruns) {
+        run_at(rn, tn, next_end);
+      } else {
+        tn = a.total_chunks;
+        next_end = tn;
+      }
       if (threadIdx.x == G::kMetaT && rn < nruns) {
         my_claim = atomicAdd(&a.ctr->run_next, 1u);  // published at the next chunk's top
         publish = true;
@@ -753,7 +762,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
       const uint32_t li = (uint32_t)(t - run_first), sl = threadIdx.x & 63;
       if (sl == li) {
         v[0] = u32x4{(uint32_t)m.spec, (uint32_t)(m.spec >> 32), (uint32_t)m.exit, (uint32_t)(m.exit >> 32)};
-        v[1] = u32x4{m.count, m.long_r, 0u, 0u};
+        v[1] = u32x4{m.count, m.long_r, m.cerr, 0u};
         v[2] = m.desc;
       }
       if (tn != t + 1 || !more || li == 63) {  // run ends (or a wave's worth of entries)
@@ -763,6 +772,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
           a.exit[g] = (uint64_t)v[0].z | ((uint64_t)v[0].w << 32);
           a.count[g] = v[1].x;
           a.long_r[g] = v[1].y;
+          a.cerr[g] = v[1].z;
           if (v[1].x & kCountRegular) ((u32x4*)a.desc)[g] = v[2];
         }
         run_first = tn;

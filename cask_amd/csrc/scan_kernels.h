@@ -85,6 +85,12 @@ struct ScanArgs {
   uint32_t respec;             // 1: validation rewrites an invalid chunk's start from T[c] (local repair)
   uint32_t big;                // records longer than this are hashed by k_long from HBM, not in LDS
   uint32_t win;                // bytes staged per chunk (chunk + halo): the LDS window
+  // sparse repair: chunk errors that outlive a pass, and the chunks a repair pass re-scans
+  uint32_t* cerr;              // per chunk: first failing row (!0: none), written by every scan of it
+  uint8_t* redo;               // per chunk: 1 if the last validation found its start wrong
+  const uint64_t* runs;        // repair pass: [first, end) chunk stretches to re-scan (null: all)
+  uint64_t nruns_list;         // stretches in runs[]
+  const uint8_t* long_skip;    // per file: 1 if k_long has already hashed its long records
 };
 
 // Default ScanArgs::big: no limit — the chunk scan hashes every record that fits its window.

@@ -82,6 +82,7 @@ struct cask_ctx {
   DevBuf err2;       // error detail words
   DevBuf gather;     // compaction rewrite: GatherRec[] | source pointers
   DevBuf stamps;     // diagnostic builds (-DCASK_STAMPS) only
+  DevBuf repair;     // runs (u64 x 2 per chunk) | cerr (u32) | redo (u8) | long_skip (u8 per file)
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
   uint64_t* dbg_tin = nullptr;
@@ -228,6 +229,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   if (!c->filebuf.ensure(fd_bytes + 3 * pf_bytes + sum_bytes)) return CASK_E_NOMEM;
   if (!c->chunk.ensure((total_chunks + 1) * (4 * 8 + 4 + 4 + 16) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
   if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
+  const size_t runs_bytes = align_up(16ull * (total_chunks + 1), 256), cerr_bytes = align_up(4ull * (total_chunks + 1), 256),
+               redo_bytes = align_up(total_chunks + 1, 256);
+  if (!c->repair.ensure(runs_bytes + cerr_bytes + redo_bytes + nfiles + 1)) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
@@ -268,6 +272,14 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.file_err = d_ferr;
   a.first_bad = d_fbad;
   a.ctr = c->ctr.as<Counters>();
+  uint8_t* rb = c->repair.as<uint8_t>();
+  uint64_t* d_runs = (uint64_t*)rb;
+  a.cerr = (uint32_t*)(rb + runs_bytes);
+  a.redo = rb + runs_bytes + cerr_bytes;
+  uint8_t* d_skip = rb + runs_bytes + cerr_bytes + redo_bytes;
+  a.runs = nullptr;
+  a.nruns_list = 0;
+  a.long_skip = nullptr;
   if (rows) {
     a.pos = rows->pos;
     a.seq = rows->seq;
@@ -361,6 +373,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
 #endif
   uint64_t local_passes = 0, walked = 0;
+  std::vector<uint8_t> redo, skip;
+  std::vector<uint64_t> runs;
   if (head->any_invalid) {
     // Repair. First, local: validation has already moved every invalid chunk's start to T[c]
     // (a.respec), which is exact for the first invalid chunk of each stretch, so exact re-scans
@@ -368,16 +382,53 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // start the search cannot verify — in one or two passes. If that does not converge, the
     // exact boundary walk from each file's first invalid chunk, then one more exact re-scan.
     // Chunks before the first invalid one keep their (validated) speculative starts.
-    invalid_chunks = head->invalid_chunks;
+    // A local pass re-scans only the chunks validation flagged (redo), as maximal stretches of
+    // consecutive flagged chunks walked with a carry; files that were valid keep their chunk
+    // table, rows and per-chunk errors (cerr), and k_long skips the files it has already hashed.
     a.exact = 1;
+    static const bool sparse = getenv("CASK_FULL_REPAIR") == nullptr;  // diagnostic: re-scan everything
     const int max_local = getenv("CASK_LOCAL_REPAIRS") ? atoi(getenv("CASK_LOCAL_REPAIRS")) : 3;
+    if (sparse) {
+      redo.resize(total_chunks);
+      skip.assign(nfiles, 0);
+    }
     for (int it = 0; it < max_local && head->any_invalid; ++it) {
+      if (sparse) {
+        H(hipMemcpyAsync(redo.data(), a.redo, total_chunks, hipMemcpyDeviceToHost, st), "redo D2H");
+        H(hipStreamSynchronize(st), "redo sync");
+        if (!ok) return CASK_E_DEVICE;
+        const uint64_t* fbad = hs + head_words + nfiles + 1;
+        for (size_t f = 0; f < nfiles; ++f) skip[f] |= fbad[f] == kNone ? 1 : 0;
+        runs.clear();
+        for (uint64_t g = 0; g < total_chunks;) {
+          if (!redo[g]) {
+            ++g;
+            continue;
+          }
+          const uint64_t g0 = g;
+          while (g < total_chunks && redo[g]) ++g;
+          runs.push_back(g0);
+          runs.push_back(g);
+          invalid_chunks += g - g0;
+        }
+        H(hipMemcpyAsync(d_runs, runs.data(), runs.size() * 8, hipMemcpyHostToDevice, st), "runs H2D");
+        H(hipMemcpyAsync(d_skip, skip.data(), nfiles, hipMemcpyHostToDevice, st), "long_skip H2D");
+        a.runs = d_runs;
+        a.nruns_list = runs.size() / 2;
+        a.long_skip = d_skip;
+      } else {
+        invalid_chunks += head->invalid_chunks;
+      }
       pass(false);
       if (!ok) return CASK_E_DEVICE;
       ++local_passes;
     }
     if (head->any_invalid) {
       walked = 1;
+      invalid_chunks += total_chunks;
+      a.runs = nullptr;  // the walk rewrites every start from each file's first bad chunk: re-scan all
+      a.nruns_list = 0;
+      a.long_skip = nullptr;
       launch_walk(a, d_sum, st);
       L("k_walk");
       pass(false);
