@@ -7,39 +7,112 @@ namespace cask_dev {
 
 // ------------------------------------------------------------------------------------------
 // K_long: the records the chunk scan did not hash out of LDS — those that run past the window, or
-// are longer than ScanArgs::big — hashed straight from HBM, one lane per chunk over rows
-// long_r[t] .. count-1 (the same rule picks them: lds_hashed()). EOF rows have already failed.
+// are longer than ScanArgs::big — hashed straight from HBM (the same rule picks them:
+// lds_hashed()). EOF rows have already failed.
+//  * k_long_enqueue, one lane per chunk not yet queued since its last scan (long_done): rows
+//    long_r[t] .. count-1 go to the queue region of their length class;
+//  * k_long_hash, one lane per queued record, longest class first: the lanes of a wave hash
+//    records of similar length, so a wave's lifetime is not set by one 64-KiB record among 1-KiB
+//    ones. Each lane keeps 128 B of its record in flight while it mixes the previous 128 B.
+// Chunks are queued whatever their file's validity: a repair pass re-scans only flagged chunks,
+// and re-scanning one clears long_done, so every chunk's long records are hashed once per scan.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_long(ScanArgs a) {
+__device__ __forceinline__ void long_verify(const ScanArgs& a, uint64_t slot, uint32_t& nl) {
+  const uint64_t t = slot / a.slot_cap;
+  const uint32_t r = (uint32_t)(slot % a.slot_cap);
+  const uint32_t fi = find_file(a.files, a.nfiles, t);
+  const FileDesc fd = a.files[fi];
+  const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+  uint32_t* w = a.slots + slot * 4;
+  const uint32_t w3 = w[3], vsz = w[2];
+  const uint64_t p = c0 + ((w3 >> 16) & 0x7FFFu);
+  const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+  ++nl;
+  const uint32_t stored = gld4(fd.data + p);
+  if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {  // data.rs:193-198
+    w[3] = w3 | kSlotBad;
+    atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
+    atomicMin(&a.file_err[fi], (unsigned long long)slot);
+  }
+}
+
+// The rows of chunk t that k_long hashes, with their length class (f(slot, class) per row).
+template <class F>
+__device__ __forceinline__ void long_rows(const ScanArgs& a, uint64_t t, F f) {
+  const uint32_t r0 = a.long_r[t];
+  const uint32_t n = a.count[t] & kCountMask;
+  const uint32_t fi = find_file(a.files, a.nfiles, t);
+  const FileDesc fd = a.files[fi];
+  const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+  const uint64_t wend = c0 + a.win < fd.len ? c0 + a.win : fd.len;
+  for (uint32_t r = r0; r < n; ++r) {
+    const uint64_t slot = t * a.slot_cap + r;
+    const uint32_t* w = a.slots + slot * 4;
+    const uint32_t w3 = w[3], vsz = w[2];
+    const uint64_t p = c0 + ((w3 >> 16) & 0x7FFFu);
+    const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+    if (p + rl > fd.len || lds_hashed(p, rl, wend, a.big)) continue;  // EOF row, or done in LDS
+    uint32_t b = 63u - (uint32_t)__builtin_clzll(rl);
+    b = b < kLqMinLog ? kLqMinLog : b > 31u ? 31u : b;
+    f(slot, b - kLqMinLog);
+  }
+}
+
+// Each block queues the long records of 256 consecutive chunks at a time (8 MiB of log with the
+// default geometry) as one contiguous piece per length class, so a wave of k_long_hash reads a
+// few neighbouring stretches of HBM rather than 64 pages spread over every file.
+__global__ __launch_bounds__(256) void k_long_enqueue(ScanArgs a) {
+  __shared__ uint32_t cnt1[kLqClasses], cnt2[kLqClasses];
+  __shared__ uint64_t gb[kLqClasses];
   uint32_t nl = 0;
-  for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < a.total_chunks;
-       t += (uint64_t)gridDim.x * blockDim.x) {
-    const uint32_t r0 = a.long_r[t];
-    if (r0 == 0xFFFFFFFFu) continue;
-    const uint32_t n = a.count[t] & kCountMask;
-    const uint32_t fi = find_file(a.files, a.nfiles, t);
-    if (a.first_bad[fi] != kNone) continue;  // invalid: the repair pass re-scans this file
-    if (a.long_skip && a.long_skip[fi]) continue;  // hashed by an earlier pass (valid then, not re-scanned since)
-    const FileDesc fd = a.files[fi];
-    const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
-    const uint64_t wend = c0 + a.win < fd.len ? c0 + a.win : fd.len;
-    for (uint32_t r = r0; r < n; ++r) {
-      const uint64_t slot = t * a.slot_cap + r;
-      uint32_t* w = a.slots + slot * 4;
-      const uint32_t w3 = w[3], vsz = w[2];
-      const uint64_t p = c0 + ((w3 >> 16) & 0x7FFFu);
-      const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
-      if (p + rl > fd.len || lds_hashed(p, rl, wend, a.big)) continue;  // EOF row, or done in LDS
-      ++nl;
-      const uint32_t stored = gld4(fd.data + p);
-      if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {
-        w[3] = w3 | kSlotBad;
-        atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
-        atomicMin(&a.file_err[fi], (unsigned long long)slot);
-      }
+  for (uint64_t base = blockIdx.x * 256ull; base < a.total_chunks; base += (uint64_t)gridDim.x * 256ull) {
+    if (threadIdx.x < kLqClasses) cnt1[threadIdx.x] = cnt2[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t t = base + threadIdx.x;
+    const bool act = t < a.total_chunks && a.long_r[t] != 0xFFFFFFFFu && !a.long_done[t];
+    if (act) long_rows(a, t, [&](uint64_t, uint32_t c) { atomicAdd(&cnt1[c], 1u); });
+    __syncthreads();
+    if (threadIdx.x < kLqClasses && cnt1[threadIdx.x])
+      gb[threadIdx.x] = atomicAdd(&a.ctr->lq_cnt[threadIdx.x], cnt1[threadIdx.x]);
+    __syncthreads();
+    if (act) {
+      a.long_done[t] = 1;
+      long_rows(a, t, [&](uint64_t slot, uint32_t c) {
+        const uint64_t k = gb[c] + atomicAdd(&cnt2[c], 1u);
+        const uint32_t b = c + kLqMinLog;
+        if (k < lq_region_cap(a.total_chunks, a.chunk, b)) {
+          a.lq[lq_region_base(a.total_chunks, a.chunk, b) + k] = slot;
+        } else {
+          long_verify(a, slot, nl);  // cannot happen (region bound); hashed here rather than lost
+        }
+      });
     }
+    __syncthreads();  // cnt1/cnt2/gb are reused by the next stretch
   }
   for (int o = 32; o; o >>= 1) nl += __shfl_xor(nl, o, 64);  // one counter update per wave
+  if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&a.ctr->nlong, (unsigned long long)nl);
+}
+
+__global__ __launch_bounds__(256) void k_long_hash(ScanArgs a) {
+  __shared__ uint64_t cnt[kLqClasses], base[kLqClasses];
+  if (threadIdx.x < kLqClasses) {
+    const uint32_t b = kLqMinLog + threadIdx.x;
+    const uint64_t cap = lq_region_cap(a.total_chunks, a.chunk, b);
+    const uint64_t c = a.ctr->lq_cnt[threadIdx.x];
+    cnt[threadIdx.x] = c < cap ? c : cap;
+    base[threadIdx.x] = lq_region_base(a.total_chunks, a.chunk, b);
+  }
+  __syncthreads();
+  uint64_t total = 0;
+  for (uint32_t j = 0; j < kLqClasses; ++j) total += cnt[j];
+  uint32_t nl = 0;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = i;
+    uint32_t j = kLqClasses - 1;  // longest class first
+    while (k >= cnt[j]) k -= cnt[j--];
+    long_verify(a, a.lq[base[j] + k], nl);
+  }
+  for (int o = 32; o; o >>= 1) nl += __shfl_xor(nl, o, 64);
   if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&a.ctr->nlong, (unsigned long long)nl);
 }
 
@@ -392,7 +465,10 @@ void launch_long(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
   uint64_t blocks = (a.total_chunks + 255) / 256;
   if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_long, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
+  hipLaunchKernelGGL(k_long_enqueue, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
+  int dev = 0, cus = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipLaunchKernelGGL(k_long_hash, dim3((uint32_t)cus * 8u), dim3(256), 0, S(stream), a);
 }
 void launch_validate(const ScanArgs& a, void* stream) {
   if (!a.nfiles) return;

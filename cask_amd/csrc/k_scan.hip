@@ -607,6 +607,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     a.count[t] = m.count;
     a.long_r[t] = m.long_r;
     a.cerr[t] = m.cerr;
+    a.long_done[t] = 0;
     if (regular) ((u32x4*)a.desc)[t] = m.desc;
   }
   // the next chunk of the run starts where this chain left off
@@ -773,6 +774,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
           a.count[g] = v[1].x;
           a.long_r[g] = v[1].y;
           a.cerr[g] = v[1].z;
+          a.long_done[g] = 0;  // its long records (if any) are queued again by k_long_enqueue
           if (v[1].x & kCountRegular) ((u32x4*)a.desc)[g] = v[2];
         }
         run_first = tn;

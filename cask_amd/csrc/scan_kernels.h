@@ -42,7 +42,24 @@ struct Counters {
   unsigned long long walk_steps; // repair walk iterations
   unsigned int run_next;         // k_scan_chunks: next run of chunks to hand out (zeroed per launch)
   unsigned int pad;
+  unsigned int lq_cnt[22];       // long-record queue: entries per length class 2^10 .. 2^31+
+  unsigned int pad2[2];
 };
+
+// Long-record queue (k_long_enqueue -> k_long_hash): slot indices of the records hashed from HBM,
+// one region per length class b (record length in [2^b, 2^(b+1)), b = 10..31, the last open-ended),
+// so that the lanes of a wave hash records of similar length. Region b holds at most
+// (chunk >> b) + 1 records per chunk: records do not overlap, and those of a chunk start within it.
+constexpr uint32_t kLqMinLog = 10, kLqClasses = 22;
+constexpr uint32_t kMinBigRec = 1u << kLqMinLog;  // ScanArgs::big is never below this
+__host__ __device__ __forceinline__ uint64_t lq_region_cap(uint64_t chunks, uint32_t chunk, uint32_t b) {
+  return chunks * ((uint64_t)(chunk >> b) + 1);
+}
+__host__ __device__ __forceinline__ uint64_t lq_region_base(uint64_t chunks, uint32_t chunk, uint32_t b) {
+  uint64_t o = 0;
+  for (uint32_t j = kLqMinLog; j < b; ++j) o += lq_region_cap(chunks, chunk, j);
+  return o;
+}
 
 struct ScanArgs {
   const FileDesc* files;
@@ -90,11 +107,15 @@ struct ScanArgs {
   uint8_t* redo;               // per chunk: 1 if the last validation found its start wrong
   const uint64_t* runs;        // repair pass: [first, end) chunk stretches to re-scan (null: all)
   uint64_t nruns_list;         // stretches in runs[]
-  const uint8_t* long_skip;    // per file: 1 if k_long has already hashed its long records
+  uint8_t* long_done;          // per chunk: 1 once k_long_enqueue has queued its long records
+                               // (every scan of the chunk clears it)
+  uint64_t* lq;                // long-record queue: slot indices by length class (lq_region_base)
 };
 
-// Default ScanArgs::big: no limit — the chunk scan hashes every record that fits its window.
-constexpr uint32_t kBigRec = 0xFFFFFFFFu;
+// Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
+// instead of by one quad of the chunk's workgroup while the rest of it waits (configs[2]: 32 GiB of
+// Zipf-length records, 841 -> 1,002 GiB/s; fixed 290-B records never reach it).
+constexpr uint32_t kBigRec = 2048u;
 
 // Whether the chunk scan hashes the record [p, p + rl) of a chunk whose window ends at wend out of
 // LDS (the same rule in k_scan_chunks and k_long): it fits the window and is at most `big` long.
@@ -126,7 +147,7 @@ void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src,
 uint32_t geometry_chunk(int geo);
 uint32_t geometry_halo(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
-void launch_long(const ScanArgs& a, void* stream);
+void launch_long(const ScanArgs& a, void* stream);  // k_long_enqueue + k_long_hash
 void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);

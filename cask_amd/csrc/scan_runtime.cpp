@@ -82,7 +82,8 @@ struct cask_ctx {
   DevBuf err2;       // error detail words
   DevBuf gather;     // compaction rewrite: GatherRec[] | source pointers
   DevBuf stamps;     // diagnostic builds (-DCASK_STAMPS) only
-  DevBuf repair;     // runs (u64 x 2 per chunk) | cerr (u32) | redo (u8) | long_skip (u8 per file)
+  DevBuf repair;     // runs (u64 x 2 per chunk) | cerr (u32) | redo (u8) | long_done (u8)
+  DevBuf lq;         // long-record queue (slot indices by length class)
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
   uint64_t* dbg_tin = nullptr;
@@ -231,7 +232,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
   const size_t runs_bytes = align_up(16ull * (total_chunks + 1), 256), cerr_bytes = align_up(4ull * (total_chunks + 1), 256),
                redo_bytes = align_up(total_chunks + 1, 256);
-  if (!c->repair.ensure(runs_bytes + cerr_bytes + redo_bytes + nfiles + 1)) return CASK_E_NOMEM;
+  if (!c->repair.ensure(runs_bytes + cerr_bytes + 2 * redo_bytes)) return CASK_E_NOMEM;
+  if (!c->lq.ensure(8 * (lq_region_base(total_chunks, chunk, 32) + 1))) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
@@ -276,10 +278,10 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   uint64_t* d_runs = (uint64_t*)rb;
   a.cerr = (uint32_t*)(rb + runs_bytes);
   a.redo = rb + runs_bytes + cerr_bytes;
-  uint8_t* d_skip = rb + runs_bytes + cerr_bytes + redo_bytes;
+  a.long_done = rb + runs_bytes + cerr_bytes + redo_bytes;
+  a.lq = c->lq.as<uint64_t>();
   a.runs = nullptr;
   a.nruns_list = 0;
-  a.long_skip = nullptr;
   if (rows) {
     a.pos = rows->pos;
     a.seq = rows->seq;
@@ -299,6 +301,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.respec = getenv("CASK_NO_LOCAL_REPAIR") ? 0u : 1u;
   // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
   a.big = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
+  if (a.big < kMinBigRec) a.big = kMinBigRec;  // the long-record queue's smallest length class
   a.win = chunk + geometry_halo(c->geo);
 #ifdef CASK_STAMPS
   if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
@@ -373,7 +376,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
 #endif
   uint64_t local_passes = 0, walked = 0;
-  std::vector<uint8_t> redo, skip;
+  std::vector<uint8_t> redo;
   std::vector<uint64_t> runs;
   if (head->any_invalid) {
     // Repair. First, local: validation has already moved every invalid chunk's start to T[c]
@@ -384,25 +387,24 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // Chunks before the first invalid one keep their (validated) speculative starts.
     // A local pass re-scans only the chunks validation flagged (redo), as maximal stretches of
     // consecutive flagged chunks walked with a carry; files that were valid keep their chunk
-    // table, rows and per-chunk errors (cerr), and k_long skips the files it has already hashed.
+    // table, rows and per-chunk errors (cerr), and k_long queues only chunks scanned since it last ran.
     a.exact = 1;
     static const bool sparse = getenv("CASK_FULL_REPAIR") == nullptr;  // diagnostic: re-scan everything
     const int max_local = getenv("CASK_LOCAL_REPAIRS") ? atoi(getenv("CASK_LOCAL_REPAIRS")) : 3;
     if (sparse) {
       redo.resize(total_chunks);
-      skip.assign(nfiles, 0);
     }
     for (int it = 0; it < max_local && head->any_invalid; ++it) {
       if (sparse) {
         H(hipMemcpyAsync(redo.data(), a.redo, total_chunks, hipMemcpyDeviceToHost, st), "redo D2H");
         H(hipStreamSynchronize(st), "redo sync");
         if (!ok) return CASK_E_DEVICE;
-        const uint64_t* fbad = hs + head_words + nfiles + 1;
-        for (size_t f = 0; f < nfiles; ++f) skip[f] |= fbad[f] == kNone ? 1 : 0;
         runs.clear();
         for (uint64_t g = 0; g < total_chunks;) {
-          if (!redo[g]) {
-            ++g;
+          if (!redo[g]) {  // skip unflagged chunks 8 at a time
+            uint64_t w;
+            if (!(g & 7) && g + 8 <= total_chunks && (memcpy(&w, &redo[g], 8), w == 0)) g += 8;
+            else ++g;
             continue;
           }
           const uint64_t g0 = g;
@@ -412,10 +414,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
           invalid_chunks += g - g0;
         }
         H(hipMemcpyAsync(d_runs, runs.data(), runs.size() * 8, hipMemcpyHostToDevice, st), "runs H2D");
-        H(hipMemcpyAsync(d_skip, skip.data(), nfiles, hipMemcpyHostToDevice, st), "long_skip H2D");
         a.runs = d_runs;
         a.nruns_list = runs.size() / 2;
-        a.long_skip = d_skip;
       } else {
         invalid_chunks += head->invalid_chunks;
       }
@@ -428,7 +428,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       invalid_chunks += total_chunks;
       a.runs = nullptr;  // the walk rewrites every start from each file's first bad chunk: re-scan all
       a.nruns_list = 0;
-      a.long_skip = nullptr;
       launch_walk(a, d_sum, st);
       L("k_walk");
       pass(false);
