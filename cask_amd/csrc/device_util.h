@@ -368,6 +368,90 @@ __device__ __forceinline__ uint32_t gbl_xxh32(const uint8_t* p, uint64_t len) {
   return avalanche(h);
 }
 
+// 4x4 transpose across a quad: lane q enters with stripe q of a 4-stripe block (words 0..3) and
+// leaves with word q of stripes 0..3, in order (two butterfly stages of quad DPP moves).
+__device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
+  const bool b1 = q & 2, b0 = q & 1;
+  uint32_t r0 = quad_xor2(b1 ? v.x : v.z), r1 = quad_xor2(b1 ? v.y : v.w);  // swap off-diagonal 2x2 blocks
+  if (b1) { v.x = r0; v.y = r1; } else { v.z = r0; v.w = r1; }
+  r0 = quad_xor1(b0 ? v.x : v.y);  // transpose within the 2x2 blocks
+  r1 = quad_xor1(b0 ? v.z : v.w);
+  if (b0) { v.x = r0; v.z = r1; } else { v.y = r0; v.w = r1; }
+}
+
+// XXH32 (seed 0) of global bytes [p, p+len) by a quad of lanes (q = lane & 3), lane q keeping stripe
+// accumulator v_{q+1}. Lane q loads stripe q of each 64-B block (one 16-B load: the quad reads 64
+// contiguous bytes per instruction, 4 blocks ahead), quad_transpose hands every lane its word of
+// the block's four stripes. The four lanes must be active together and call with the same p/len;
+// all four return the hash.
+__device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t len, uint32_t q) {
+  const uint64_t nstr = len >> 4;
+  uint32_t h;
+  if (nstr) {
+    uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
+    const uint64_t nblk = nstr >> 2;
+    if (nblk) {
+      constexpr uint32_t D = 4;  // blocks in flight per quad (256 B)
+      const uint8_t* lp = p + 16 * q;
+      u32x4 A[D];
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) A[d] = gld16(lp + 64 * (d < nblk ? d : nblk - 1));
+      for (uint64_t k = 0; k < nblk; k += D) {
+        u32x4 B[D];
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+          const uint64_t kb = k + D + d;
+          B[d] = gld16(lp + 64 * (kb < nblk ? kb : nblk - 1));  // clamped: no branch around a load
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) {
+          if (k + d < nblk) {
+            quad_transpose(A[d], q);
+            v = xround(v, A[d].x);
+            v = xround(v, A[d].y);
+            v = xround(v, A[d].z);
+            v = xround(v, A[d].w);
+          }
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) A[d] = B[d];
+      }
+    }
+    const uint32_t rem = (uint32_t)(nstr & 3);
+    if (rem) {  // the last 1-3 stripes: lanes q < rem load one each
+      u32x4 R = gld16(p + 64 * nblk + 16 * (q < rem ? q : 0));
+      quad_transpose(R, q);
+      v = xround(v, R.x);
+      if (rem > 1) v = xround(v, R.y);
+      if (rem > 2) v = xround(v, R.z);
+    }
+    uint32_t m = rotl_var(v, q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u);
+    m += quad_xor1(m);
+    m += quad_xor2(m);
+    h = m;
+  } else {
+    h = P5;
+  }
+  h += (uint32_t)len;
+  const uint8_t* t = p + 16 * nstr;
+  const uint32_t nt = (uint32_t)(len & 15), n4 = nt >> 2, n1 = nt & 3;
+  uint32_t t4[3] = {0u, 0u, 0u};
+  uint8_t t1[3] = {0, 0, 0};
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n4) t4[k] = gld4(t + 4 * k);
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n1) t1[k] = t[4 * n4 + k];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n4) h = tail4(h, t4[k]);
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < n1) h = tail1(h, t1[k]);
+  return avalanche(h);
+}
+
 __device__ __forceinline__ uint64_t g_reclen(const uint8_t* hdr) {
   const uint32_t b3 = gld4(hdr + 12);
   const uint32_t b4 = (uint32_t)hdr[16] | ((uint32_t)hdr[17] << 8);

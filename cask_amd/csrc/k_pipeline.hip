@@ -93,6 +93,30 @@ __global__ __launch_bounds__(256) void k_long_enqueue(ScanArgs a) {
   if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&a.ctr->nlong, (unsigned long long)nl);
 }
 
+// long_verify by a quad of lanes (the same slot in all four, all four active): quad_gbl_xxh32.
+__device__ __forceinline__ void long_verify_quad(const ScanArgs& a, uint64_t slot, uint32_t q, uint32_t& nl) {
+  const uint64_t t = slot / a.slot_cap;
+  const uint32_t r = (uint32_t)(slot % a.slot_cap);
+  const uint32_t fi = find_file(a.files, a.nfiles, t);
+  const FileDesc fd = a.files[fi];
+  const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+  uint32_t* w = a.slots + slot * 4;
+  const uint32_t w3 = w[3], vsz = w[2];
+  const uint64_t p = c0 + ((w3 >> 16) & 0x7FFFu);
+  const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+  const uint32_t stored = gld4(fd.data + p);
+  const uint32_t got = quad_gbl_xxh32(fd.data + p + 4, rl - 4, q);
+  if (q == 0) {
+    ++nl;
+    if (got != stored) {  // data.rs:193-198
+      w[3] = w3 | kSlotBad;
+      atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
+      atomicMin(&a.file_err[fi], (unsigned long long)slot);
+    }
+  }
+}
+
+// One quad of lanes per queued record, longest length class first.
 __global__ __launch_bounds__(256) void k_long_hash(ScanArgs a) {
   __shared__ uint64_t cnt[kLqClasses], base[kLqClasses];
   if (threadIdx.x < kLqClasses) {
@@ -106,11 +130,13 @@ __global__ __launch_bounds__(256) void k_long_hash(ScanArgs a) {
   uint64_t total = 0;
   for (uint32_t j = 0; j < kLqClasses; ++j) total += cnt[j];
   uint32_t nl = 0;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+  const uint32_t q = threadIdx.x & 3;
+  const uint64_t nq = (uint64_t)gridDim.x * (blockDim.x >> 2);
+  for (uint64_t i = blockIdx.x * (uint64_t)(blockDim.x >> 2) + (threadIdx.x >> 2); i < total; i += nq) {
     uint64_t k = i;
     uint32_t j = kLqClasses - 1;  // longest class first
     while (k >= cnt[j]) k -= cnt[j--];
-    long_verify(a, a.lq[base[j] + k], nl);
+    long_verify_quad(a, a.lq[base[j] + k], q, nl);
   }
   for (int o = 32; o; o >>= 1) nl += __shfl_xor(nl, o, 64);
   if ((threadIdx.x & 63) == 0 && nl) atomicAdd(&a.ctr->nlong, (unsigned long long)nl);

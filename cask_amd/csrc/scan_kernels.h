@@ -114,7 +114,8 @@ struct ScanArgs {
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
 // instead of by one quad of the chunk's workgroup while the rest of it waits (configs[2]: 32 GiB of
-// Zipf-length records, 841 -> 1,002 GiB/s; fixed 290-B records never reach it).
+// Zipf-length records, 841 -> 1,005 GiB/s with per-lane hashing, 1,337 with quads; fixed
+// 290-B records never reach it).
 constexpr uint32_t kBigRec = 2048u;
 
 // Whether the chunk scan hashes the record [p, p + rl) of a chunk whose window ends at wend out of

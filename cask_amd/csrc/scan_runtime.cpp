@@ -327,6 +327,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     if (sync_each) H(hipStreamSynchronize(st), what);
   };
   // one pass of the pipeline; events 1..4 bracket scan / long / validate+summary / compact
+  uint64_t nlong_total = 0;  // records hashed by k_long over all passes (each pass queues only chunks it scanned)
   auto pass = [&](bool timed) {
     reset();
     if (timed) H(hipEventRecord(c->ev[1], st));
@@ -349,6 +350,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipEventRecord(timed ? c->ev[5] : c->ev[6], st));
     H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st), "summary D2H");
     H(hipStreamSynchronize(st), "stream sync");
+    if (ok) nlong_total += ((const SummaryHead*)c->hsum.p)->nlong;
   };
   H(hipEventRecord(c->ev[0], st));
   H(hipMemcpyAsync(d_files, fd, sizeof(FileDesc) * (nfiles ? nfiles : 1), hipMemcpyHostToDevice, st));
@@ -452,7 +454,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   c->last_ms[4] = repair_ms;
   c->last_ms[5] = t_cmp;
   c->last_counters[0] = total_chunks;
-  c->last_counters[1] = head->nlong;
+  c->last_counters[1] = nlong_total;
   c->last_counters[2] = invalid_chunks;
   c->last_counters[3] = local_passes;
   c->last_counters[4] = walked;

@@ -205,6 +205,24 @@ def test_zipf_sizes_corrupt(gpu_ctx):
     check_against_oracle(gpu_ctx, [bytes(buf)], device=True)
 
 
+def test_long_record_hash_every_length_residue(gpu_ctx):
+    """Records past ScanArgs::big (2 KiB) are hashed from HBM by quads of lanes (k_long_hash): every
+    hashed length mod 64 (full 4-stripe blocks, 1-3 trailing stripes, 0-15 tail bytes), with value
+    bytes flipped in a third of them, must give the oracle's statuses row for row."""
+    rng = random.Random(47)
+    recs, seq = [], 1
+    for vsz in list(range(2020, 2150)) + [rng.randrange(4096, 70000) for _ in range(12)]:
+        rec = bytearray(R.entry_new(seq, rng.randbytes(16), rng.randbytes(vsz)).write_bytes())
+        if rng.random() < 0.33:
+            rec[18 + 16 + rng.randrange(vsz)] ^= 1 << rng.randrange(8)
+        recs.append(bytes(rec))
+        seq += 1
+    buf = b"".join(recs)
+    res = check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 2]], device=True)
+    assert gpu_ctx.last_counters()["long_records"] > 0
+    assert res.error is not None
+
+
 def test_many_files_empty_and_tiny(gpu_ctx):
     rng = random.Random(4)
     bufs = []
