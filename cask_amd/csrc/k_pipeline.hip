@@ -487,13 +487,24 @@ __global__ void k_err_detail(ScanArgs a, uint32_t fi, uint64_t slot, uint32_t* o
 // ------------------------------------------------------------------------------------------
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
+int device_cus() {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (!cached[dev]) {
+    int cus = 256;
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    cached[dev] = cus > 0 ? cus : 256;
+  }
+  return cached[dev];
+}
+
 void launch_long(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
   uint64_t blocks = (a.total_chunks + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(k_long_enqueue, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
-  int dev = 0, cus = 256;
-  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  const int cus = device_cus();
   hipLaunchKernelGGL(k_long_hash, dim3((uint32_t)cus * 8u), dim3(256), 0, S(stream), a);
 }
 void launch_validate(const ScanArgs& a, void* stream) {

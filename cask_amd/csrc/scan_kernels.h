@@ -124,7 +124,7 @@ __host__ __device__ __forceinline__ bool lds_hashed(uint64_t p, uint64_t rl, uin
   return p + rl <= wend && rl <= big;
 }
 
-constexpr uint32_t kDefaultRun = 16;
+constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
 struct SummaryHead {
@@ -148,6 +148,7 @@ void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src,
 uint32_t geometry_chunk(int geo);
 uint32_t geometry_halo(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
+int device_cus();  // compute units of the current device (cached per device)
 void launch_long(const ScanArgs& a, void* stream);  // k_long_enqueue + k_long_hash
 void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);

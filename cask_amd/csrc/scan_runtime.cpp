@@ -291,9 +291,18 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.row_cap = rows->capacity;
   }
   a.stamps = nullptr;
-  {  // CASK_RUN_CHUNKS (tuning knob): chunks per workgroup run; one boundary search per run
-    static const uint32_t run = getenv("CASK_RUN_CHUNKS") ? (uint32_t)atoi(getenv("CASK_RUN_CHUNKS")) : kDefaultRun;
-    a.run = run ? run : 1;
+  {  // CASK_RUN_CHUNKS (tuning knob): chunks per workgroup run; one boundary search per run.
+    // Default: about 16 runs per resident workgroup (the counter's balance), at least kDefaultRun and
+    // at most kMaxRun chunks — longer runs search less often, which is what variable-length logs
+    // pay for (a search that lands inside a record longer than the window scans the whole chunk).
+    static const uint32_t run = getenv("CASK_RUN_CHUNKS") ? (uint32_t)atoi(getenv("CASK_RUN_CHUNKS")) : 0u;
+    if (run) {
+      a.run = run;
+    } else {
+      const int cus = device_cus();
+      const uint64_t per_wg = total_chunks / ((uint64_t)cus * 4u * 16u);
+      a.run = (uint32_t)std::min<uint64_t>(kMaxRun, std::max<uint64_t>(kDefaultRun, per_wg));
+    }
   }
   // regular chunks keep only their first slot row when the rows go to the dense output (k_compact
   // expands them); the segmented output hands the slots to the caller, so every row is written

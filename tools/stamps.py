@@ -37,14 +37,21 @@ def main():
         files = cfg2_files(ctx, nfiles=args.files)
     views = [(f.file_id, f.data) for f in files]
     rows = ctx.alloc_rows(sum(f.nrec for f in files) + 16)
+    res = None
     for _ in range(args.iters):
-        res = ctx.scan_device(views, rows)
+        try:
+            res = ctx.scan_device(views, rows)
+        except Exception as e:  # CASK_NO_REPAIR: an unrepaired speculative pass reports status 1
+            if not os.environ.get("CASK_NO_REPAIR"):
+                raise
+            print("unrepaired pass:", e)
     st = (C.c_uint64 * 16)()
     L.cask_debug_stamps(ctx._h, st)
-    chunks = ctx.last_counters()["chunks"]
+    chunks = ctx.last_counters()["chunks"] or None
     t = ctx.last_timings()
-    print(f"chunks={chunks} rows={res.count} timings={t}")
+    print(f"chunks={chunks} rows={res.count if res else '-'} timings={t}")
     tot = st[7]
+    chunks = chunks or max(st[4], 1)
     print(f"chunk iterations stamped: {st[4]}")
     if st[13]:
         mean_ns = st[11] * 10.0 / st[13]
