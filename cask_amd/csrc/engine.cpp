@@ -18,6 +18,7 @@
 #include <cstring>
 #include <new>
 #include <regex>
+#include <thread>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -115,8 +116,38 @@ class KeyDir {
     it->second.dead_bytes += size;
   }
 
+  // Room for n keys without growing.
+  void reserve(uint64_t n) {
+    uint64_t cap = 1024;
+    while (cap * 3 < (n + 1) * 4) cap *= 2;
+    if (cap > slots.size()) {
+      std::vector<Slot> old;
+      old.swap(slots);
+      slots.assign(cap, Slot{});
+      used = 0;
+      for (const Slot& s : old)
+        if (s.state == 1) insert_new(s);
+    }
+  }
+  // A key known to be absent (a live slot of another table).
+  void insert_new(const Slot& s0, const uint8_t* key = nullptr) {
+    const uint64_t m = slots.size() - 1;
+    uint64_t i = s0.hash & m;
+    while (slots[i].state) i = (i + 1) & m;
+    slots[i] = s0;
+    if (key) {
+      slots[i].key_off = arena.size();
+      arena.insert(arena.end(), key, key + s0.ksz);
+    }
+    ++used;
+  }
+
   // Index::update (cask.rs:60-90). vsz_raw is the hint's value_size field.
   void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+    update_h(key, ksz, file_id, pos, vsz_raw, seq, hash_key(key, ksz));
+  }
+  void update_h(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq,
+                uint64_t h) {
     const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
     cask_index_entry ie{};
     ie.file_id = file_id;
@@ -124,7 +155,6 @@ class KeyDir {
     ie.entry_size = 18ull + ksz + (deleted ? 0ull : (uint64_t)vsz_raw);  // data.rs:238-240
     ie.sequence = seq;
     if ((used + 1) * 4 > slots.size() * 3) grow();
-    const uint64_t h = hash_key(key, ksz);
     int64_t f = find(key, ksz, h);
     if (f >= 0) {  // Occupied
       Slot& s = slots[f];
@@ -280,6 +310,82 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 }
 
 }  // namespace
+
+// One record of the replay fold (a hint, or an Ok row of a scanned file), in replay order.
+struct FoldRec {
+  const uint8_t* key;
+  uint64_t pos, seq, hash;
+  uint32_t file_id, vsz_raw;
+  uint32_t ksz;
+};
+
+// The replay fold of Cask::open (cask.rs:346-382) over every file's records at once, sharded by
+// key hash over threads. Index::update's outcome for a key depends only on that key's records in
+// order, and every shard sees its keys' records in replay order; Stats rows are per-file counters
+// (order-free sums), and during open every remove_entry follows an add_entry of the same key and
+// file, so no shard drops a remove the single fold would count. The shards' live keys and stats
+// rows then merge into `out`. Small replays fold on the calling thread.
+void parallel_fold(std::vector<FoldRec>& recs, KeyDir& out) {
+  const char* mv = getenv("CASK_PAR_FOLD_MIN");  // tuning/test knob: smallest replay folded in parallel
+  const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
+  unsigned nt = std::thread::hardware_concurrency();
+  nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;
+  if (recs.size() < min_par || nt == 1 || out.live || !out.stats.empty()) {
+    for (const FoldRec& r : recs) out.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq);
+    return;
+  }
+  const uint64_t n = recs.size();
+  // 1. hashes, and per (range, shard) lists of record indices, ranges in replay order
+  std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(nt));
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+      for (auto& l : lists[t]) l.reserve((hi - lo) / nt + 16);
+      for (uint64_t i = lo; i < hi; ++i) {
+        FoldRec& r = recs[i];
+        r.hash = hash_key(r.key, r.ksz);
+        lists[t][(r.hash >> 40) % nt].push_back((uint32_t)(i - lo));
+      }
+    });
+  for (auto& x : th) x.join();
+  th.clear();
+  // 2. each shard folds its keys in replay order
+  std::vector<KeyDir> shard(nt);
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      uint64_t cnt = 0;
+      for (unsigned g = 0; g < nt; ++g) cnt += lists[g][t].size();
+      shard[t].reserve(cnt / 2);
+      for (unsigned g = 0; g < nt; ++g) {
+        const uint64_t lo = n * g / nt;
+        for (uint32_t j : lists[g][t]) {
+          const FoldRec& r = recs[lo + j];
+          shard[t].update_h(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash);
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  // 3. merge: disjoint key sets
+  uint64_t live = 0, keyb = 0;
+  for (const KeyDir& k : shard) {
+    live += k.live;
+    keyb += k.arena.size();
+  }
+  out.reserve(out.live + live);
+  out.arena.reserve(out.arena.size() + keyb);
+  for (const KeyDir& k : shard) {
+    for (const auto& sl : k.slots)
+      if (sl.state == 1) out.insert_new(sl, k.key_of(sl));
+    out.live += k.live;
+    for (const auto& kv : k.stats) {
+      StatsEntry& e = out.stats[kv.first];
+      e.entries += kv.second.entries;
+      e.dead_entries += kv.second.dead_entries;
+      e.dead_bytes += kv.second.dead_bytes;
+    }
+  }
+}
 
 struct cask_db {
   std::string path;
@@ -447,6 +553,7 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
 
   // Replay in ascending file order (cask.rs:348-369); the first Err aborts open().
   double t_hint = 0, t_fold = 0;
+  std::vector<FoldRec> recs;  // the replay's fold, in order (parallel_fold)
   for (size_t i = 0; i < nf; ++i) {
     const uint32_t fid = db->files[i];
     if (use_hint[i]) {
@@ -472,7 +579,7 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
           return nullptr;
         }
         if (s > db->sequence) db->sequence = s;
-        db->index.update(h + 22, k, fid, epos, v == CASK_ENTRY_TOMBSTONE ? CASK_ENTRY_TOMBSTONE : v, s);
+        recs.push_back(FoldRec{h + 22, epos, s, 0, fid, v, k});
         p += 22ull + k;
       }
       t_fold += ms_since(tf);
@@ -528,10 +635,14 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
         return nullptr;
       }
       if (seq[r] > db->sequence) db->sequence = seq[r];
-      db->index.update(buf + pos[r] + 18, ksz[r], fid, pos[r], vsz[r], seq[r]);
+      recs.push_back(FoldRec{buf + pos[r] + 18, pos[r], seq[r], 0, fid, vsz[r], ksz[r]});
     }
     t_fold += ms_since(tf);
-    std::vector<uint8_t>().swap(data[i]);
+  }
+  {  // Index::update + Stats over every record (the keys stay in data[] / hints[] until here)
+    auto tf = std::chrono::steady_clock::now();
+    parallel_fold(recs, db->index);
+    t_fold += ms_since(tf);
   }
   db->timings[2] = t_hint;
   db->timings[3] = t_fold;

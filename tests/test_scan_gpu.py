@@ -103,10 +103,13 @@ def test_golden_rows_device(gpu_ctx, case):
     check_against_oracle(gpu_ctx, bufs, device=True)
 
 
+@pytest.mark.parametrize("par_fold", [False, True], ids=["fold", "sharded_fold"])
 @pytest.mark.parametrize("case", golden_cases())
-def test_golden_engine_open(native, case, tmp_path):
-    """Cask::open on the fixture directory: keydir, stats, sequence or error, hint files."""
+def test_golden_engine_open(native, case, tmp_path, monkeypatch, par_fold):
+    """Cask::open on the fixture directory: keydir, stats, sequence or error, hint files — with the
+    fold on one thread and sharded by key hash over threads (CASK_PAR_FOLD_MIN=0 forces it)."""
     from cask_amd import CaskOptions, errors
+    monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if par_fold else str(1 << 62))
     exp = _expected(case)
     rep = exp["replay"]
     d = tmp_path / case
@@ -140,6 +143,39 @@ def make_records(rng, n, ksz_fn, vsz_fn, seq0=1, tomb_p=0.0):
         else:
             out.append(R.entry_new(seq0 + i, k, rng.randbytes(vsz_fn(rng))).write_bytes())
     return b"".join(out)
+
+
+def test_sharded_fold_matches_single_thread(native, tmp_path, monkeypatch):
+    """Many files of overwrites, stale and live tombstones and out-of-order sequences: the sharded
+    fold must give the single-thread fold's keydir, stats and sequence (Index::update, Stats)."""
+    from cask_amd import CaskOptions
+    rng = random.Random(53)
+    keys = [rng.randbytes(rng.randrange(0, 24)) for _ in range(700)]
+    d = tmp_path / "db"
+    d.mkdir()
+    seq = 1
+    for fid in range(1, 7):
+        recs = []
+        for _ in range(2500):
+            k = rng.choice(keys)
+            s = seq if rng.random() < 0.9 else max(1, seq - rng.randrange(1, 3000))  # some stale sequences
+            seq += 1
+            if rng.random() < 0.15:
+                recs.append(R.entry_deleted(s, k).write_bytes())
+            else:
+                recs.append(R.entry_new(s, k, rng.randbytes(rng.randrange(0, 300))).write_bytes())
+        with open(R.data_file_path(str(d), fid), "wb") as f:
+            f.write(b"".join(recs))
+    got = []
+    for par in (False, True):
+        for h in d.glob("*.cask.hint"):
+            h.unlink()  # both opens take the scan path
+        monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if par else str(1 << 62))
+        with CaskOptions().open(str(d)) as db:
+            got.append((sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence] for k, e in db.index().items()),
+                        sorted([f, *st] for f, st in db.stats().items()), db.current_sequence))
+    assert got[0] == got[1]
+    assert len(got[0][0]) > 100
 
 
 def test_uniform_290(gpu_ctx):
