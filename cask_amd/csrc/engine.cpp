@@ -698,34 +698,54 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
     const uint64_t body = hb.size() - 4;
     const uint32_t si = (uint32_t)srcs.size();
     bool any = false;
-    for (uint64_t p = 0; p < body;) {  // Hints::next (log.rs:437-447); `hint?` aborts (cask.rs:483)
+    // Hints::next (log.rs:437-447): record offsets first (`hint?` aborts, cask.rs:483), then the
+    // keydir lookups on threads (read-only), then the tail and the live list in hint order.
+    std::vector<uint64_t> offs;
+    for (uint64_t p = 0; p < body;) {
       if (body - p < 22 || body - p - 22 < rd16(hb.data() + p + 8)) {
         set_err(err, CASK_E_EOF, fid, p);
         return CASK_E_EOF;
       }
-      const uint8_t* h = hb.data() + p;
+      offs.push_back(p);
+      p += 22ull + rd16(hb.data() + p + 8);
+    }
+    std::vector<uint8_t> kind(offs.size());  // 1: live (cask.rs:500-502); 2: tombstone of an absent key (:487-499)
+    auto classify = [&](uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i) {
+        const uint8_t* h = hb.data() + offs[i];
+        const cask_index_entry* ie = db->index.get(h + 22, rd16(h + 8));
+        kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
+      }
+    };
+    unsigned nt = std::thread::hardware_concurrency();
+    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;
+    const char* mv = getenv("CASK_PAR_FOLD_MIN");  // the same knob as parallel_fold
+    if (offs.size() < (mv ? strtoull(mv, nullptr, 10) : (1ull << 16))) nt = 1;
+    {
+      std::vector<std::thread> th;
+      for (unsigned t = 1; t < nt; ++t) th.emplace_back(classify, offs.size() * t / nt, offs.size() * (t + 1) / nt);
+      classify(0, offs.size() / nt);
+      for (auto& x : th) x.join();
+    }
+    for (uint64_t i = 0; i < offs.size(); ++i) {
+      if (!kind[i]) continue;
+      const uint8_t* h = hb.data() + offs[i];
       const uint64_t seq = rd64(h);
       const uint16_t k = rd16(h + 8);
-      const uint32_t v = rd32(h + 10);
-      const uint64_t epos = rd64(h + 14);
-      const cask_index_entry* ie = db->index.get(h + 22, k);
-      if (v == CASK_ENTRY_TOMBSTONE) {  // cask.rs:487-499
-        if (!ie) {
-          std::string key((const char*)h + 22, k);
-          auto it = del_at.find(key);
-          if (it == del_at.end()) {
-            del_at.emplace(key, del_keys.size());
-            del_keys.push_back(std::move(key));
-            del_seq.push_back(seq);
-          } else if (del_seq[it->second] < seq) {
-            del_seq[it->second] = seq;
-          }
+      if (kind[i] == 2) {
+        std::string key((const char*)h + 22, k);
+        auto it = del_at.find(key);
+        if (it == del_at.end()) {
+          del_at.emplace(key, del_keys.size());
+          del_keys.push_back(std::move(key));
+          del_seq.push_back(seq);
+        } else if (del_seq[it->second] < seq) {
+          del_seq[it->second] = seq;
         }
-      } else if (ie && ie->sequence == seq) {  // cask.rs:500-502
-        ins.push_back(Ins{si, epos});
+      } else {
+        ins.push_back(Ins{si, rd64(h + 14)});
         any = true;
       }
-      p += 22ull + k;
     }
     compacted.push_back(fid);
     if (any) srcs.push_back(fid);
