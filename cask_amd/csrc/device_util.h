@@ -391,7 +391,10 @@ __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t le
     uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
     const uint64_t nblk = nstr >> 2;
     if (nblk) {
-      constexpr uint32_t D = 4;  // blocks in flight per quad (256 B)
+#ifndef CASK_LQ_DEPTH
+#define CASK_LQ_DEPTH 8
+#endif
+      constexpr uint32_t D = CASK_LQ_DEPTH;  // blocks in flight per quad (64 B each)
       const uint8_t* lp = p + 16 * q;
       u32x4 A[D];
 #pragma unroll
