@@ -128,8 +128,16 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
 
+    import hashlib
+    import cask_amd
     from cask_amd import ScanContext
     from cask_amd.workloads import CFG2_KSZ, CFG2_VSZ, fixed_file
+    # only the in-tree product build is ever timed (no environment variable selects another)
+    lib_path = cask_amd._lib.loaded_path()
+    if lib_path != cask_amd.LIB_PATH:
+        raise SystemExit(f"bench.py times only {cask_amd.LIB_PATH}, not {lib_path}")
+    with open(lib_path, "rb") as fh:
+        lib_sha = hashlib.sha256(fh.read()).hexdigest()
 
     ctx = ScanContext(dev.index)
     rpf = args.records_per_file
@@ -257,6 +265,7 @@ def main():
             },
             "cpu_baseline": cpu,
             "counters": counters,
+            "library": {"path": os.path.relpath(lib_path, ROOT), "sha256": lib_sha},
         }
         line.update(extra)
         print(json.dumps(line), flush=True)

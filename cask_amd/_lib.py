@@ -9,8 +9,11 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# CASK_LIB_PATH selects a diagnostic build (e.g. build/stamps/libcask_scan.so) for profiling tools.
-LIB_PATH = os.environ.get("CASK_LIB_PATH") or os.path.join(_HERE, "libcask_scan.so")
+# The in-tree product build. No environment variable selects another library: diagnostic builds
+# (make -C cask_amd stamps) are loaded only by tools that call use_library() explicitly, and
+# bench.py refuses to time anything but this file.
+LIB_PATH = os.path.join(_HERE, "libcask_scan.so")
+_path = LIB_PATH
 
 c_u8p = C.POINTER(C.c_uint8)
 c_u16p = C.POINTER(C.c_uint16)
@@ -91,6 +94,7 @@ SIGNATURES = [
     ("cask_ctx_destroy", None, [C.c_void_p]),
     ("cask_ctx_set_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("cask_ctx_stream", C.c_void_p, [C.c_void_p]),
+    ("cask_ctx_wait_stream", C.c_int, [C.c_void_p, C.c_void_p]),
     ("cask_ctx_device", C.c_int, [C.c_void_p]),
     ("cask_ctx_last_error", C.c_char_p, [C.c_void_p]),
     ("cask_scan_chunk_bytes", C.c_uint32, []),
@@ -103,6 +107,7 @@ SIGNATURES = [
                                  C.POINTER(ScanError)]),
     ("cask_last_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     ("cask_last_counters", C.c_int, [C.c_void_p, c_u64p]),
+    ("cask_last_dense", C.c_int, [C.c_void_p]),
     ("cask_encode_synthetic_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
     ("cask_encode_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -131,13 +136,27 @@ SIGNATURES = [
 _lib = None
 
 
+def use_library(path: str) -> None:
+    """Tools only: load `path` (a diagnostic build) instead of the product library. Must run
+    before the first lib() call; symbols the build lacks are left unbound."""
+    global _path
+    if _lib is not None:
+        raise RuntimeError("libcask_scan.so is already loaded")
+    _path = os.path.abspath(path)
+
+
+def loaded_path() -> str:
+    """Path of the shared object lib() loaded (or will load)."""
+    return _path
+
+
 def lib():
     """Load libcask_scan.so once and bind every signature. Raises if it is absent."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        if not os.path.exists(_path):
             raise NativeLibraryMissing(
-                f"{LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+                f"{_path} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
         # torch (device-memory plumbing) bundles its own libamdhip64.so.7; whichever copy loads
         # first serves the whole process. Load torch's first so torch and this library share one
         # HIP runtime; loading ours first leaves torch with "No HIP GPUs are available".
@@ -145,10 +164,10 @@ def lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(_path)
         for name, res, args in SIGNATURES:
-            if os.environ.get("CASK_LIB_PATH") and not hasattr(L, name):
-                continue  # a diagnostic or older build (A/B timing): bind what it has
+            if _path != LIB_PATH and not hasattr(L, name):
+                continue  # a diagnostic or older build (tools' A/B timing): bind what it has
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -224,80 +224,6 @@ __device__ __forceinline__ uint32_t quad_xxh32(const uint32_t* w, uint32_t xs, u
   return lds_tail_fin(w, xs + (nstr << 4), len & 15, h + len);
 }
 
-// Two records of the same hashed length `len` (wave-uniform: the stride pass), hashed by one quad
-// at once: two independent accumulator chains per lane, and each 4-stripe block's 16 aligned
-// dwords read while the previous block is mixed. Lane a keeps accumulator a of both records; all
-// four lanes return both hashes. x0/x1 are the LDS byte offsets of the hashed bytes.
-__device__ __forceinline__ void quad_xxh32_pair(const uint32_t* w, uint32_t x0, uint32_t x1, uint32_t len, uint32_t a,
-                                                uint32_t& h0, uint32_t& h1) {
-  const uint32_t nstr = len >> 4;
-  const uint32_t sh0 = x0 & 3, sh1 = x1 & 3;
-  if (nstr) {
-    const uint32_t v_init = a == 0 ? P1 + P2 : a == 1 ? P2 : a == 2 ? 0u : 0u - P1;
-    uint32_t v0 = v_init, v1 = v_init;
-    uint32_t i0 = (x0 >> 2) + a, i1 = (x1 >> 2) + a;
-    uint32_t s = 0;
-    if (nstr >= 4) {
-      uint32_t A[8], B[8];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        A[2 * k] = w[i0 + 4 * k];
-        A[2 * k + 1] = w[i0 + 4 * k + 1];
-        B[2 * k] = w[i1 + 4 * k];
-        B[2 * k + 1] = w[i1 + 4 * k + 1];
-      }
-      for (; s + 8 <= nstr; s += 4) {
-        uint32_t An[8], Bn[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          An[2 * k] = w[i0 + 16 + 4 * k];
-          An[2 * k + 1] = w[i0 + 16 + 4 * k + 1];
-          Bn[2 * k] = w[i1 + 16 + 4 * k];
-          Bn[2 * k + 1] = w[i1 + 16 + 4 * k + 1];
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          v0 = xround(v0, fun(A[2 * k], A[2 * k + 1], sh0));
-          v1 = xround(v1, fun(B[2 * k], B[2 * k + 1], sh1));
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          A[k] = An[k];
-          B[k] = Bn[k];
-        }
-        i0 += 16;
-        i1 += 16;
-      }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v0 = xround(v0, fun(A[2 * k], A[2 * k + 1], sh0));
-        v1 = xround(v1, fun(B[2 * k], B[2 * k + 1], sh1));
-      }
-      i0 += 16;
-      i1 += 16;
-      s += 4;
-    }
-    for (; s < nstr; ++s) {
-      v0 = xround(v0, fun(w[i0], w[i0 + 1], sh0));
-      v1 = xround(v1, fun(w[i1], w[i1 + 1], sh1));
-      i0 += 4;
-      i1 += 4;
-    }
-    const uint32_t r = a == 0 ? 1u : a == 1 ? 7u : a == 2 ? 12u : 18u;
-    uint32_t m0 = rotl_var(v0, r), m1 = rotl_var(v1, r);
-    m0 += quad_xor1(m0);
-    m1 += quad_xor1(m1);
-    m0 += quad_xor2(m0);
-    m1 += quad_xor2(m1);
-    h0 = m0;
-    h1 = m1;
-  } else {
-    h0 = h1 = P5;
-  }
-  h0 = lds_tail_fin(w, x0 + (nstr << 4), len & 15, h0 + len);
-  h1 = lds_tail_fin(w, x1 + (nstr << 4), len & 15, h1 + len);
-}
-
 // Unaligned global loads: gfx950 runs in unaligned-access mode, so these memcpys become
 // global_load_dwordx4 / global_load_dword at any byte address.
 __device__ __forceinline__ u32x4 gld16(const uint8_t* p) {
@@ -391,10 +317,7 @@ __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t le
     uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
     const uint64_t nblk = nstr >> 2;
     if (nblk) {
-#ifndef CASK_LQ_DEPTH
-#define CASK_LQ_DEPTH 8
-#endif
-      constexpr uint32_t D = CASK_LQ_DEPTH;  // blocks in flight per quad (64 B each)
+      constexpr uint32_t D = 8;  // blocks in flight per quad (64 B each; 4 / 8 / 16: 7.0 / 6.26 / 6.2 ms on configs[2])
       const uint8_t* lp = p + 16 * q;
       u32x4 A[D];
 #pragma unroll
@@ -461,6 +384,122 @@ __device__ __forceinline__ uint64_t g_reclen(const uint8_t* hdr) {
   const uint32_t ksz = b3 & 0xFFFFu;
   const uint32_t vsz = (b3 >> 16) | (b4 << 16);
   return 18ull + ksz + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+}
+
+// ------------------------------------------------------------------------------------------
+// Decoupled look-back (single-pass prefix scan over elements handed out in order): the dense row
+// numbering and the chunk-start validation of k_finish (tiles) and of the dense k_scan_chunks
+// (runs) are a prefix over every earlier chunk of (row count, max chain exit within the file).
+// ------------------------------------------------------------------------------------------
+struct SegAgg {  // prefix aggregate: rows, and the max exit within the last file seen
+  uint64_t rows, mx;
+  uint32_t fl;     // file of the last chunk (0xFFFFFFFF: empty)
+  uint32_t hs;     // the aggregate contains file fl's first chunk (T restarts there)
+};
+
+// a, then b. An aggregate of no chunks (fl = 0xFFFFFFFF: a tile's lanes past the last chunk, the
+// prefix of tile 0) is the identity on either side.
+__device__ __forceinline__ SegAgg seg_combine(const SegAgg& a, const SegAgg& b) {
+  SegAgg r;
+  if (b.fl == 0xFFFFFFFFu) {
+    r = a;
+    r.rows += b.rows;
+    return r;
+  }
+  if (a.fl == 0xFFFFFFFFu) {
+    r = b;
+    r.rows += a.rows;
+    return r;
+  }
+  r.rows = a.rows + b.rows;
+  r.fl = b.fl;
+  if (b.hs || a.fl != b.fl) {
+    r.mx = b.mx;
+    r.hs = b.hs;
+  } else {
+    r.mx = a.mx > b.mx ? a.mx : b.mx;
+    r.hs = a.hs;
+  }
+  return r;
+}
+
+// Look-back granules: 8-B words written once per call by one relaxed agent-scope atomic store and
+// polled the same way (untorn, no ordering needed), each tagged with the call's epoch in its top
+// byte so that no memset is needed between calls. Per tile: aggregate (rows, mx, fl|hs) at 0..2,
+// inclusive prefix at 3..5.
+constexpr uint64_t kPay = (1ull << 56) - 1;
+__device__ __forceinline__ void gran_put(uint64_t* p, uint32_t epoch, uint64_t v) {
+  __hip_atomic_store(p, ((uint64_t)epoch << 56) | (v & kPay), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool gran_get(const uint64_t* p, uint32_t epoch, uint64_t& v) {
+  const uint64_t g = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  v = g & kPay;
+  return (uint32_t)(g >> 56) == epoch;
+}
+__device__ __forceinline__ void agg_put(uint64_t* p, uint32_t epoch, const SegAgg& x) {
+  gran_put(p, epoch, x.rows);
+  gran_put(p + 1, epoch, x.mx > kPay ? kPay : x.mx);  // kTerm (the chain ended) -> kPay
+  gran_put(p + 2, epoch, ((uint64_t)x.hs << 32) | x.fl);
+}
+__device__ __forceinline__ bool agg_get(const uint64_t* p, uint32_t epoch, SegAgg& x) {
+  uint64_t a, b, c;
+  const int ok = (int)gran_get(p, epoch, a) & (int)gran_get(p + 1, epoch, b) & (int)gran_get(p + 2, epoch, c);
+  x.rows = a;
+  x.mx = b == kPay ? kTerm : b;
+  x.fl = (uint32_t)c;
+  x.hs = (uint32_t)(c >> 32) & 1u;
+  return ok != 0;
+}
+
+// Exclusive prefix of element `idx` (> 0: a tile of k_finish, a run of k_scan_chunks) by one whole
+// wave: lane l reads element idx - 1 - l (its inclusive prefix if published, else its aggregate);
+// the nearest inclusive prefix ends the walk. An element with neither has not finished yet
+// (elements are handed out in order, so it is being worked on and will publish): with `block` the
+// wave polls it, without it returns false and the caller tries again later. A blocking walk gives up
+// (returns false) after about a quarter of a second of polling, so that a protocol fault ends in the
+// repair path rather than in a hung kernel; the caller then flags the call invalid.
+__device__ bool lookback(const uint64_t* state, uint32_t epoch, uint64_t idx, bool block, SegAgg& out) {
+  const uint32_t lane = threadIdx.x & 63;
+  SegAgg acc{0, 0, 0xFFFFFFFFu, 0};  // combined (older) ... (newer) of the elements walked so far
+  int64_t top = (int64_t)idx - 1;   // newest element of the current window (lane 0)
+  uint32_t polls = 0;
+  for (;;) {
+    const int64_t j = top - (int64_t)lane;
+    SegAgg x{0, 0, 0xFFFFFFFFu, 0};
+    uint32_t st = 2;  // 2: inclusive, 1: aggregate, 0: nothing yet
+    if (j >= 0) {
+      const uint64_t* g = state + 8ull * (uint64_t)j;
+      if (agg_get(g + 3, epoch, x)) st = 2;
+      else if (agg_get(g, epoch, x)) st = 1;
+      else st = 0;
+    }
+    const unsigned long long m_inc = __ballot(st == 2), m_none = __ballot(st == 0);
+    const uint32_t f_inc = m_inc ? (uint32_t)__builtin_ctzll(m_inc) : 64u;
+    const uint32_t f_none = m_none ? (uint32_t)__builtin_ctzll(m_none) : 64u;
+    if (f_none < f_inc) {  // an element before the nearest inclusive one has not published yet
+      if (!block || ++polls > (1u << 20)) return false;
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    const uint32_t last = f_inc < 64u ? f_inc : 63u;  // lanes last .. 0, oldest first
+    SegAgg w{0, 0, 0xFFFFFFFFu, 0};
+    for (int l = (int)last; l >= 0; --l) {
+      SegAgg y;
+      y.rows = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x.rows >> 32), l) << 32) |
+               __builtin_amdgcn_readlane((uint32_t)x.rows, l);
+      y.mx = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x.mx >> 32), l) << 32) |
+             __builtin_amdgcn_readlane((uint32_t)x.mx, l);
+      y.fl = __builtin_amdgcn_readlane(x.fl, l);
+      y.hs = __builtin_amdgcn_readlane(x.hs, l);
+      w = seg_combine(w, y);
+    }
+    acc = seg_combine(w, acc);
+    if (f_inc < 64u) {
+      out = acc;
+      return true;
+    }
+    top -= 64;
+  }
 }
 
 // Last file with first_chunk <= t (empty files share first_chunk with their successor). Call it

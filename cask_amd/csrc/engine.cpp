@@ -7,6 +7,7 @@
 // live records verified by the device scan and copied into the new data files on the device.
 #include <dirent.h>
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/file.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -305,6 +306,41 @@ bool find_data_files(const std::string& dir, std::vector<uint32_t>& out) {
   return true;
 }
 
+// Host threads for the fold and the compaction lookups: the CPUs this process may run on
+// (sched_getaffinity, so cgroup/affinity limits count), at most 16. CASK_HOST_THREADS (test and
+// tuning knob) sets the count, e.g. to force the threaded paths on a one-CPU machine.
+unsigned host_threads() {
+  if (const char* e = getenv("CASK_HOST_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return (unsigned)std::min(v, 64);
+  }
+  unsigned k = 0;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) k = (unsigned)CPU_COUNT(&set);
+  if (!k) k = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(k, 16u));
+}
+
+// fn(t) for t in [0, nt): t = 1.. on threads of their own, t = 0 on the caller. A thread that cannot
+// be created (std::system_error) has its share run on the calling thread: no exception leaves the
+// C ABI, and the result does not depend on how many threads actually ran.
+template <class F>
+void parallel_for(unsigned nt, F fn) {
+  std::vector<std::thread> th;
+  std::vector<unsigned> here;
+  for (unsigned t = 1; t < nt; ++t) {
+    try {
+      th.emplace_back(fn, t);
+    } catch (...) {
+      here.push_back(t);
+    }
+  }
+  fn(0u);
+  for (unsigned t : here) fn(t);
+  for (auto& x : th) x.join();
+}
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -328,8 +364,7 @@ struct FoldRec {
 void parallel_fold(std::vector<FoldRec>& recs, KeyDir& out) {
   const char* mv = getenv("CASK_PAR_FOLD_MIN");  // tuning/test knob: smallest replay folded in parallel
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
-  unsigned nt = std::thread::hardware_concurrency();
-  nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;
+  const unsigned nt = host_threads();
   if (recs.size() < min_par || nt == 1 || out.live || !out.stats.empty()) {
     for (const FoldRec& r : recs) out.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq);
     return;
@@ -337,35 +372,29 @@ void parallel_fold(std::vector<FoldRec>& recs, KeyDir& out) {
   const uint64_t n = recs.size();
   // 1. hashes, and per (range, shard) lists of record indices, ranges in replay order
   std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(nt));
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
-      for (auto& l : lists[t]) l.reserve((hi - lo) / nt + 16);
-      for (uint64_t i = lo; i < hi; ++i) {
-        FoldRec& r = recs[i];
-        r.hash = hash_key(r.key, r.ksz);
-        lists[t][(r.hash >> 40) % nt].push_back((uint32_t)(i - lo));
-      }
-    });
-  for (auto& x : th) x.join();
-  th.clear();
+  parallel_for(nt, [&](unsigned t) {
+    const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    for (auto& l : lists[t]) l.reserve((hi - lo) / nt + 16);
+    for (uint64_t i = lo; i < hi; ++i) {
+      FoldRec& r = recs[i];
+      r.hash = hash_key(r.key, r.ksz);
+      lists[t][(r.hash >> 40) % nt].push_back((uint32_t)(i - lo));
+    }
+  });
   // 2. each shard folds its keys in replay order
   std::vector<KeyDir> shard(nt);
-  for (unsigned t = 0; t < nt; ++t)
-    th.emplace_back([&, t] {
-      uint64_t cnt = 0;
-      for (unsigned g = 0; g < nt; ++g) cnt += lists[g][t].size();
-      shard[t].reserve(cnt / 2);
-      for (unsigned g = 0; g < nt; ++g) {
-        const uint64_t lo = n * g / nt;
-        for (uint32_t j : lists[g][t]) {
-          const FoldRec& r = recs[lo + j];
-          shard[t].update_h(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash);
-        }
+  parallel_for(nt, [&](unsigned t) {
+    uint64_t cnt = 0;
+    for (unsigned g = 0; g < nt; ++g) cnt += lists[g][t].size();
+    shard[t].reserve(cnt / 2);
+    for (unsigned g = 0; g < nt; ++g) {
+      const uint64_t lo = n * g / nt;
+      for (uint32_t j : lists[g][t]) {
+        const FoldRec& r = recs[lo + j];
+        shard[t].update_h(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash);
       }
-    });
-  for (auto& x : th) x.join();
+    }
+  });
   // 3. merge: disjoint key sets
   uint64_t live = 0, keyb = 0;
   for (const KeyDir& k : shard) {
@@ -717,16 +746,10 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
         kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
       }
     };
-    unsigned nt = std::thread::hardware_concurrency();
-    nt = nt < 1 ? 1 : nt > 16 ? 16 : nt;
+    unsigned nt = host_threads();
     const char* mv = getenv("CASK_PAR_FOLD_MIN");  // the same knob as parallel_fold
     if (offs.size() < (mv ? strtoull(mv, nullptr, 10) : (1ull << 16))) nt = 1;
-    {
-      std::vector<std::thread> th;
-      for (unsigned t = 1; t < nt; ++t) th.emplace_back(classify, offs.size() * t / nt, offs.size() * (t + 1) / nt);
-      classify(0, offs.size() / nt);
-      for (auto& x : th) x.join();
-    }
+    parallel_for(nt, [&](unsigned t) { classify(offs.size() * t / nt, offs.size() * (t + 1) / nt); });
     for (uint64_t i = 0; i < offs.size(); ++i) {
       if (!kind[i]) continue;
       const uint8_t* h = hb.data() + offs[i];

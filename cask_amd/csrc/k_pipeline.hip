@@ -17,6 +17,21 @@ namespace cask_dev {
 // Chunks are queued whatever their file's validity: a repair pass re-scans only flagged chunks,
 // and re-scanning one clears long_done, so every chunk's long records are hashed once per scan.
 // ------------------------------------------------------------------------------------------
+// A long record failed its checksum: mark its slot row and chunk (the repair/compaction path reads
+// those), and when k_finish has already written the dense rows, its dense row and the file's first
+// failing row too.
+__device__ __forceinline__ void long_failed(const ScanArgs& a, uint64_t slot, uint64_t t, uint32_t r, uint32_t fi,
+                                            uint32_t w3) {
+  a.slots[slot * 4 + 3] = w3 | kSlotBad;
+  atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
+  atomicMin(&a.file_err[fi], (unsigned long long)slot);
+  if (a.dense) {
+    const uint64_t d = a.gbase[t] + r;
+    if (d < a.row_cap) a.status[d] = kRowChecksum;
+    atomicMax(&a.err_inv[fi], ~(unsigned long long)d);
+  }
+}
+
 __device__ __forceinline__ void long_verify(const ScanArgs& a, uint64_t slot, uint32_t& nl) {
   const uint64_t t = slot / a.slot_cap;
   const uint32_t r = (uint32_t)(slot % a.slot_cap);
@@ -29,11 +44,7 @@ __device__ __forceinline__ void long_verify(const ScanArgs& a, uint64_t slot, ui
   const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
   ++nl;
   const uint32_t stored = gld4(fd.data + p);
-  if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) {  // data.rs:193-198
-    w[3] = w3 | kSlotBad;
-    atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
-    atomicMin(&a.file_err[fi], (unsigned long long)slot);
-  }
+  if (gbl_xxh32(fd.data + p + 4, rl - 4) != stored) long_failed(a, slot, t, r, fi, w3);  // data.rs:193-198
 }
 
 // The rows of chunk t that k_long hashes, with their length class (f(slot, class) per row).
@@ -108,11 +119,7 @@ __device__ __forceinline__ void long_verify_quad(const ScanArgs& a, uint64_t slo
   const uint32_t got = quad_gbl_xxh32(fd.data + p + 4, rl - 4, q);
   if (q == 0) {
     ++nl;
-    if (got != stored) {  // data.rs:193-198
-      w[3] = w3 | kSlotBad;
-      atomicMin(&a.cerr[t], r);  // outlives the pass: validation rebuilds file_err from cerr
-      atomicMin(&a.file_err[fi], (unsigned long long)slot);
-    }
+    if (got != stored) long_failed(a, slot, t, r, fi, w3);  // data.rs:193-198
   }
 }
 
@@ -356,6 +363,215 @@ __global__ void k_summary(ScanArgs a, uint64_t* out) {
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K_finish (dense path): one launch after k_scan_chunks that validates every speculated chunk
+// start, numbers the rows and writes them dense, in (file, pos) order, into the caller's arrays.
+// It replaces the three validation launches, the summary and k_compact of the repair path.
+//
+// Chunks are taken in tiles of kFinTile (one per thread), tiles in order from a counter. A tile's
+// chunks give (rows, exit) pairs; the exclusive prefix over all earlier chunks — row count
+// (global: files are consecutive chunk ranges, so the dense row index is a global prefix) and the
+// maximum exit within the current file, T[c], the chain position entering chunk c as long as
+// every earlier chunk of the file is valid — comes from a decoupled look-back over the earlier
+// tiles' published aggregates (north_star's prefix scan). Chunk c is valid iff its start equals
+// T[c] (or it found none and T[c] is past its end); any invalid chunk sends the call to the
+// repair path, which rewrites every row (k_compact). Rows are then expanded from the chunk table:
+// a regular chunk from its first row, the others from their slot rows; each thread writes four
+// consecutive rows with 16-B (pos, seq, vsz), 8-B (ksz) and 4-B (status) stores.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
+  constexpr uint32_t TC = kFinTile;
+  __shared__ uint32_t s_tile;
+  __shared__ SegAgg s_wave[4];
+  __shared__ SegAgg s_prefix;
+  __shared__ uint32_t s_base[TC + 1];      // row base of each chunk of the tile, relative to the tile
+  __shared__ u32x4 s_desc[TC];            // regular chunk: first row; else slot row of the chunk
+  __shared__ uint64_t s_c0[TC], s_len[TC];
+  __shared__ uint32_t s_reg[TC];          // regular flag
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(&a.ctr->tile_next, 1u);
+  __syncthreads();
+  const uint64_t tile = s_tile;
+  const uint64_t c = tile * TC + tid;
+  const bool act = c < a.total_chunks;
+  // the chunk's table entries
+  uint32_t n = 0, cw = 0, fi = 0, cerr = 0xFFFFFFFFu, lr = 0xFFFFFFFFu;
+  uint64_t e = 0, spec = kNone, c0 = 0, c1 = 0, len = 0;
+  bool head = false;
+  if (act) {
+    cw = a.count[c];
+    n = cw & kCountMask;
+    spec = a.spec[c];
+    e = spec == kNone ? 0ull : a.exit[c];
+    cerr = a.cerr[c];
+    lr = a.long_r[c];
+    fi = find_file(a.files, a.nfiles, c);
+    const FileDesc fd = a.files[fi];
+    c0 = (c - fd.first_chunk) * (uint64_t)a.chunk;
+    c1 = (c0 + a.chunk < fd.len) ? c0 + a.chunk : fd.len;
+    len = fd.len;
+    head = c0 == 0;
+  }
+  // in-tile inclusive scan of (rows, segmented max exit), by wave then across the 4 waves
+  SegAgg v{n, e, act ? fi : 0xFFFFFFFFu, head ? 1u : 0u};
+  SegAgg inc = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    SegAgg u;
+    u.rows = __shfl_up(inc.rows, o, 64);
+    u.mx = __shfl_up(inc.mx, o, 64);
+    u.fl = __shfl_up(inc.fl, o, 64);
+    u.hs = __shfl_up(inc.hs, o, 64);
+    if ((int)lane >= o) inc = seg_combine(u, inc);
+  }
+  if (lane == 63) s_wave[wave] = inc;
+  __syncthreads();
+  SegAgg wpre{0, 0, 0xFFFFFFFFu, 0};
+  for (uint32_t k = 0; k < wave; ++k) wpre = seg_combine(wpre, s_wave[k]);
+  inc = seg_combine(wpre, inc);
+  SegAgg total = seg_combine(seg_combine(seg_combine(s_wave[0], s_wave[1]), s_wave[2]), s_wave[3]);
+  // publish the tile's aggregate, then find the prefix of the earlier tiles
+  uint64_t* g = a.tstate + 8ull * tile;
+  if (tid == 0) {
+    if (tile == 0) agg_put(g + 3, a.epoch, total);
+    else agg_put(g, a.epoch, total);
+  }
+  if (wave == 0) {
+    SegAgg P{0, 0, 0xFFFFFFFFu, 0};
+    if (tile > 0) {
+      if (lookback(a.tstate, a.epoch, tile, true, P)) {
+        if (lane == 0) agg_put(g + 3, a.epoch, seg_combine(P, total));
+      } else if (lane == 0) {
+        atomicOr(&a.ctr->any_invalid, 1u);  // gave up waiting: the repair path redoes the call
+      }
+    }
+    if (lane == 0) s_prefix = P;
+  }
+  __syncthreads();
+  const SegAgg P = s_prefix;
+  const SegAgg full = seg_combine(P, inc);  // inclusive prefix through this chunk
+  const uint64_t base = full.rows - n;      // this chunk's first dense row
+  // T[c]: max exit of the earlier chunks of this file. The lane before holds the tile's inclusive
+  // prefix through c - 1 (lane 0: the earlier waves' total).
+  SegAgg prev;
+  prev.rows = __shfl_up(inc.rows, 1, 64);
+  prev.mx = __shfl_up(inc.mx, 1, 64);
+  prev.fl = __shfl_up(inc.fl, 1, 64);
+  prev.hs = __shfl_up(inc.hs, 1, 64);
+  if (lane == 0) prev = wpre;
+  const SegAgg pf = seg_combine(P, prev);
+  if (act) {
+    const uint64_t T = (pf.fl == fi) ? pf.mx : 0ull;
+    const bool ok = head || (spec != kNone ? spec == T : T >= c1);
+    if (!ok) atomicOr(&a.ctr->any_invalid, 1u);
+    a.gbase[c] = base;
+    if (head) a.row_off[fi] = base;
+    if (cerr != 0xFFFFFFFFu) atomicMax(&a.err_inv[fi], ~(unsigned long long)(base + cerr));
+    if (c + 1 == a.total_chunks) a.ctr->total_rows = base + n;
+  }
+  if (__ballot(act && lr != 0xFFFFFFFFu) && lane == 0) atomicOr(&a.ctr->long_pending, 1u);
+  // rows of the tile: [tile_lo, tile_lo + tile_rows)
+  const uint64_t tile_lo = P.rows, tile_rows = total.rows;
+  s_base[tid] = (uint32_t)(base - tile_lo);
+  if (tid == TC - 1) s_base[TC] = (uint32_t)tile_rows;
+  s_reg[tid] = act && (cw & kCountRegular);
+  s_c0[tid] = c0;
+  s_len[tid] = len;
+  if (act && (cw & kCountRegular)) s_desc[tid] = ((const u32x4*)a.desc)[c];
+  __syncthreads();
+  if (!tile_rows) return;
+  const uint64_t cap = a.row_cap;
+  const uint64_t g0 = tile_lo >> 2, g1 = (tile_lo + tile_rows + 3) >> 2;
+  const uint32_t nch = (uint32_t)((a.total_chunks - tile * TC) < TC ? (a.total_chunks - tile * TC) : TC);
+  for (uint64_t grp = g0 + tid; grp < g1; grp += TC) {
+    const uint64_t d0 = grp << 2;
+    // chunk of the group's first row in the tile: last j with s_base[j] <= rel
+    const uint64_t rel0 = d0 > tile_lo ? d0 - tile_lo : 0;
+    uint32_t lo = 0, hi = nch;  // s_base[lo] <= rel0 < s_base[hi]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_base[mid] <= rel0) lo = mid; else hi = mid;
+    }
+    uint32_t j = lo;
+    uint64_t P4[4], S4[4];
+    uint32_t V4[4], K4[4], T4[4];
+    bool inr[4];
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+      const uint64_t d = d0 + q;
+      inr[q] = d >= tile_lo && d < tile_lo + tile_rows;
+      P4[q] = 0; S4[q] = 0; V4[q] = 0; K4[q] = 0; T4[q] = 0;
+      if (!inr[q]) continue;
+      const uint32_t rel = (uint32_t)(d - tile_lo);
+      while (j + 1 < nch && s_base[j + 1] <= rel) ++j;
+      // skip chunks with no rows: s_base[j + 1] == s_base[j]
+      const uint32_t r = rel - s_base[j];
+      const uint64_t cc0 = s_c0[j];
+      if (s_reg[j]) {
+        const u32x4 w = s_desc[j];
+        const uint32_t ksz = w.w & 0xFFFFu;
+        const uint64_t rl = 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+        P4[q] = cc0 + ((w.w >> 16) & 0x7FFFu) + (uint64_t)r * rl;
+        S4[q] = (((uint64_t)w.y << 32) | w.x) + r;
+        V4[q] = w.z;
+        K4[q] = ksz;
+        T4[q] = kRowOk;
+      } else {
+        const u32x4 w = *(const u32x4*)(a.slots + ((tile * TC + j) * (uint64_t)a.slot_cap + r) * 4);
+        const uint32_t ksz = w.w & 0xFFFFu;
+        const uint64_t p = cc0 + ((w.w >> 16) & 0x7FFFu);
+        const uint64_t end = p + 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+        const uint64_t fl = s_len[j];
+        P4[q] = p;
+        S4[q] = ((uint64_t)w.y << 32) | w.x;
+        V4[q] = w.z;
+        K4[q] = ksz;
+        T4[q] = (p + 18 > fl || end > fl) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
+      }
+    }
+    if (a.vec_ok && inr[0] && inr[3] && d0 + 3 < cap) {
+      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+      *(u64x2*)(a.pos + d0) = u64x2{P4[0], P4[1]};
+      *(u64x2*)(a.pos + d0 + 2) = u64x2{P4[2], P4[3]};
+      *(u64x2*)(a.seq + d0) = u64x2{S4[0], S4[1]};
+      *(u64x2*)(a.seq + d0 + 2) = u64x2{S4[2], S4[3]};
+      *(u32x4*)(a.vsz + d0) = u32x4{V4[0], V4[1], V4[2], V4[3]};
+      *(uint64_t*)(a.ksz + d0) = (uint64_t)(K4[0] & 0xFFFFu) | ((uint64_t)(K4[1] & 0xFFFFu) << 16) |
+                                 ((uint64_t)(K4[2] & 0xFFFFu) << 32) | ((uint64_t)(K4[3] & 0xFFFFu) << 48);
+      *(uint32_t*)(a.status + d0) = T4[0] | (T4[1] << 8) | (T4[2] << 16) | (T4[3] << 24);
+    } else {
+#pragma unroll
+      for (uint32_t q = 0; q < 4; ++q) {
+        const uint64_t d = d0 + q;
+        if (!inr[q] || d >= cap) continue;
+        a.pos[d] = P4[q];
+        a.seq[d] = S4[q];
+        a.vsz[d] = V4[q];
+        a.ksz[d] = (uint16_t)K4[q];
+        a.status[d] = (uint8_t)T4[q];
+      }
+    }
+  }
+}
+
+// Error detail of the first failing dense row `row` of file fi (error path only): out[0] stored
+// checksum, out[1] computed XXH32, out[2] row status, out[3..4] pos.
+__global__ void k_err_dense(ScanArgs a, uint32_t fi, uint64_t row, uint32_t* out) {
+  if (threadIdx.x || blockIdx.x) return;
+  const FileDesc fd = a.files[fi];
+  const uint64_t p = a.pos[row];
+  out[0] = 0;
+  out[1] = 0;
+  out[2] = a.status[row];
+  out[3] = (uint32_t)p;
+  out[4] = (uint32_t)(p >> 32);
+  if (p + 18 > fd.len) return;
+  const uint8_t* hp = fd.data + p;
+  const uint64_t rl = g_reclen(hp);
+  out[0] = gld4(hp);
+  if (p + rl > fd.len) return;
+  out[1] = gbl_xxh32(hp + 4, rl - 4);
+}
+
 // K_compact: slot rows -> dense SoA rows in (file, pos) order. One wave per chunk.
 __global__ __launch_bounds__(256) void k_compact(ScanArgs a, const uint64_t* summary) {
   const uint64_t* row_off = summary + sizeof(SummaryHead) / 8;
@@ -554,6 +770,14 @@ void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream) {
   uint64_t g = (a.total_chunks + 3) / 4;
   if (g > 65536) g = 65536;
   hipLaunchKernelGGL(k_compact, dim3((uint32_t)g), dim3(256), 0, S(stream), a, summary);
+}
+void launch_finish(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t tiles = (a.total_chunks + kFinTile - 1) / kFinTile;
+  hipLaunchKernelGGL(k_finish, dim3((uint32_t)tiles), dim3(kFinTile), 0, S(stream), a);
+}
+void launch_err_dense(const ScanArgs& a, uint32_t fi, uint64_t row, uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(k_err_dense, dim3(1), dim3(64), 0, S(stream), a, fi, row, out);
 }
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream) {
   if (!a.nfiles) return;

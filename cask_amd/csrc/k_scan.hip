@@ -33,11 +33,7 @@ struct Geo {
   static constexpr uint32_t kWinWords = (kWinB + 64) / 4;
   // With 4+ waves, the last wave loads nothing: it issues the workgroup's stores (slot rows, chunk
   // table, run claims), so no wave that stages the window ever waits for a store to complete.
-#ifndef CASK_NO_STORE_WAVE
   static constexpr bool kStoreWave = NT >= 256;
-#else  // diagnostic: every wave stages; stores issued from wherever they arise
-  static constexpr bool kStoreWave = false;
-#endif
   static constexpr uint32_t kLoadT = kStoreWave ? NT - 64 : NT;  // threads that stage the window
   static constexpr uint32_t kMetaT = kStoreWave ? NT - 64 : 0;   // the thread that issues the stores
   static constexpr uint32_t kNL = ((kWinB + 16) / 16 + kLoadT - 1) / kLoadT;  // 16-B loads per loader
@@ -45,11 +41,8 @@ struct Geo {
 
 // Records no longer than this are "short": the boundary search verifies them first.
 constexpr uint32_t kShortMax = 1024;
-// Offsets each thread tests per step of the boundary search.
-#ifndef CASK_SEARCH_PER
-#define CASK_SEARCH_PER 1
-#endif
-constexpr uint32_t kSearchPer = CASK_SEARCH_PER;
+// Offsets each thread tests per step of the boundary search (1: measured no slower than 4).
+constexpr uint32_t kSearchPer = 1;
 
 #define BAR() __syncthreads()
 
@@ -122,21 +115,6 @@ __device__ __forceinline__ ChunkPos next_chunk(const FileDesc* files, uint32_t n
 // walk could then be satisfied by a prefetch load instead of its own read.
 typedef __attribute__((address_space(1))) const u32x4 gu32x4;
 
-// Diagnostic (-DCASK_ADDR_GUARD, stamps builds): an address outside [lo, hi) is recorded in
-// stamps[10..15] and replaced by lo instead of being accessed.
-#ifdef CASK_ADDR_GUARD
-#define ADDR_GUARD(stamps, ptr, lo, hi, tag, t)                                                      \
-  if ((uintptr_t)(ptr) < (uintptr_t)(lo) || (uintptr_t)(ptr) >= (uintptr_t)(hi)) {                  \
-    if ((stamps) && atomicCAS(&(stamps)[10], 0ull, (unsigned long long)(tag)) == 0ull) {            \
-      (stamps)[11] = (uintptr_t)(ptr); (stamps)[12] = (uintptr_t)(lo); (stamps)[13] = (uintptr_t)(hi); \
-      (stamps)[14] = (t); (stamps)[15] = blockIdx.x | ((uint64_t)threadIdx.x << 32);                \
-    }                                                                                                \
-    (ptr) = (decltype(ptr))(lo);                                                                     \
-  }
-#else
-#define ADDR_GUARD(stamps, ptr, lo, hi, tag, t)
-#endif
-
 template <class G>
 __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& c,
                                             unsigned long long* dbg = nullptr, uint64_t t = 0) {
@@ -149,20 +127,14 @@ __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& 
   if (c.n16 == G::kNL * G::kLoadT) {  // the whole window is inside the file: no clamping
 #pragma unroll
     for (uint32_t j = 0; j < G::kNL; ++j) {
-#ifdef CASK_NT_LOADS  // streaming (non-temporal) policy on the window loads
-      v[j] = __builtin_nontemporal_load(src + threadIdx.x + j * G::kLoadT);
-#else
       v[j] = src[threadIdx.x + j * G::kLoadT];
-#endif
     }
     return;
   }
 #pragma unroll
   for (uint32_t j = 0; j < G::kNL; ++j) {
     const uint32_t i = threadIdx.x + j * G::kLoadT;
-    const gu32x4* ptr = src + (i < c.n16 ? i : c.n16 - 1);
-    ADDR_GUARD(dbg, ptr, (uintptr_t)c.data & ~(uintptr_t)15, (uintptr_t)c.data + c.len + 16, 1, t)
-    v[j] = *ptr;
+    v[j] = src[i < c.n16 ? i : c.n16 - 1];
   }
 }
 
@@ -223,11 +195,7 @@ __device__ __forceinline__ bool quad_row(const uint32_t* W, const ChunkPos& c, u
   const uint64_t st_h1_ = __builtin_amdgcn_s_memtime();
   dg.st[8] += st_h1_ - st_h0_;  // phase 8: header + hash of one record
 #endif
-#ifndef CASK_NO_SLOT_STORE
   slots[4ull * r + a] = word;
-#else  // diagnostic: rows computed, not stored
-  if (word == 0x9E3779B9u) slots[4ull * r + a] = word;
-#endif
 #ifdef CASK_STAMPS
   dg.st[9] += __builtin_amdgcn_s_memtime() - st_h1_;  // phase 9: issuing the slot store
 #endif
@@ -249,27 +217,6 @@ __device__ __forceinline__ uint32_t ceil_div_small(uint32_t a, uint32_t b) {
   return c;
 }
 
-// Slot row of a record the stride pass settled (header in h, no EOF: it fits the file); lane a
-// of the quad writes dword a. Returns `bad`.
-// Rows below kRowBuf go to the LDS row buffer (flushed later as whole 16-B rows, a quarter of the
-// store instructions), the rest straight to the slots.
-template <class G>
-__device__ __forceinline__ bool stride_row(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t r, uint32_t off,
-                                           const Hdr& h, bool bad, uint32_t a) {
-  const uint32_t w3 = h.ksz | (off << 16) | (bad ? kSlotBad : 0u);
-  const uint32_t word = a == 0 ? (uint32_t)h.seq : a == 1 ? (uint32_t)(h.seq >> 32) : a == 2 ? h.vsz : w3;
-  if (r < G::kRowBuf) {
-    ((uint32_t*)L.rows[par])[4 * r + a] = word;
-  } else {
-#ifndef CASK_NO_SLOT_STORE
-    slots[4ull * r + a] = word;
-#else  // diagnostic: rows computed, not stored
-    if (word == 0x9E3779B9u) slots[4ull * r + a] = word;
-#endif
-  }
-  return bad;
-}
-
 // A chunk's entries in the chunk table (wave-uniform): written by the store wave for a whole run
 // of chunks at once (consecutive entries: a few full-line stores instead of five scattered ones
 // per chunk), or straight away where there is no store wave.
@@ -287,17 +234,7 @@ __device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_
   if (G::kStoreWave && threadIdx.x < G::kLoadT) return;  // the store wave's job
   const uint32_t first = G::kStoreWave ? threadIdx.x - G::kLoadT : threadIdx.x;
   const uint32_t step = G::kStoreWave ? 64u : G::kNT;
-#ifdef CASK_DIAG_ONE_ROW  // diagnostic (wrong rows): one 16-B store per chunk instead of n
-  if (n > 1) n = 1;
-#endif
-  for (uint32_t r = first; r < n; r += step) {
-#ifndef CASK_NO_SLOT_STORE
-    srow[r] = L.rows[par][r];
-#else
-    const u32x4 w = L.rows[par][r];
-    if (w.x == 0x9E3779B9u) srow[r] = w;
-#endif
-  }
+  for (uint32_t r = first; r < n; r += step) srow[r] = L.rows[par][r];
 }
 
 template <class G, bool EXACT>
@@ -368,11 +305,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   // length rl0 and let thread i take the record at s + i*rl0 — check its header, verify it,
   // write its row. The first i whose header breaks the stride (L.ffail) ends the run of true
   // records; rows past it are discarded. A file of equal-length records never leaves this pass.
-#if defined(CASK_SLOTS_SCRATCH)  // diagnostic (wrong rows): every chunk of a workgroup writes the same 2 KiB (L2-resident)
-  uint32_t* slots = a.slots + ((uint64_t)blockIdx.x * 128) * 4;
-#else
   uint32_t* slots = a.slots + ((uint64_t)t * a.slot_cap) * 4;
-#endif
   uint32_t n = 0, cerr = 0xFFFFFFFFu;  // cerr: the chunk's first failing row
   uint64_t exitv = 0, lastp = 0, lastrl = 0;
   bool rl0_big = false;  // the stride rows' records are longer than a.big (k_long hashes them)
@@ -405,7 +338,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     }
     rl0_big = rl0 > a.big;
     const uint32_t r32 = cnt > 1 ? (uint32_t)rl0 : 0u;  // stride; rl0 < span <= CH when cnt > 1
-    // One record per lane (STRIDE_QUAD: per quad of lanes, two records per quad).
+    // One record per lane, its four XXH32 accumulators interleaved.
     const uint32_t hl = (uint32_t)rl0 - 4;
     auto stride_ok = [&](uint32_t i, uint32_t o, const Hdr& h) -> bool {
       if (!i) return true;  // cnt > 0: the first record fits the file
@@ -417,18 +350,13 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 #endif
     // the first record's header, for the regular-chunk test (one LDS broadcast)
     const Hdr hf = cnt ? lds_hdr(W, srel + shift) : Hdr{};
-#ifndef CASK_STRIDE_QUAD
     bool irreg = false;
     for (uint32_t i = tid; i < cnt; i += NT) {
       const uint32_t o = srel + i * r32;
       const Hdr h = lds_hdr(W, o + shift);  // inside the window: o < CH
       const bool ok = stride_ok(i, o, h);
       const bool hs = ok && lds_hashed(c0 + o, rl0, wend, a.big);  // else k_long
-#ifdef CASK_DIAG_NO_HASH  // diagnostic: everything but the checksum arithmetic (rows say "verified")
-      const uint32_t g = h.stored;
-#else
       const uint32_t g = hs ? lane_xxh32(W, o + shift + 4, hl) : h.stored;
-#endif
       if (!ok) {
         atomicMin(&L.ffail, i);
       } else {
@@ -438,54 +366,13 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
         row.y = (uint32_t)(h.seq >> 32);
         row.z = h.vsz;
         row.w = h.ksz | (o << 16) | (bad ? kSlotBad : 0u);
-        if (i < G::kRowBuf) {
-          L.rows[par][i] = row;
-        } else {
-#ifndef CASK_NO_SLOT_STORE
-          ((u32x4*)slots)[i] = row;
-#endif
-        }
+        if (i < G::kRowBuf) L.rows[par][i] = row;
+        else ((u32x4*)slots)[i] = row;
         if (bad) atomicMin(&L.cerr_s, i);
         irreg |= bad || !hs || h.ksz != hf.ksz || h.vsz != hf.vsz || h.seq != hf.seq + i;
       }
     }
     if (__ballot(irreg) && lane == 0) atomicOr(&L.irreg, 1u);
-#else
-    for (uint32_t i0 = quad; i0 < cnt; i0 += 2 * NQ) {
-      const uint32_t i1 = i0 + NQ;
-      const bool has1 = i1 < cnt;
-      const uint32_t o0 = srel + i0 * r32, o1 = srel + (has1 ? i1 : i0) * r32;
-      const Hdr h0 = lds_hdr(W, o0 + shift), h1 = lds_hdr(W, o1 + shift);  // inside the window: o < CH
-      const bool ok0 = stride_ok(i0, o0, h0), ok1 = has1 && stride_ok(i1, o1, h1);
-      const bool hs0 = ok0 && lds_hashed(c0 + o0, rl0, wend, a.big), hs1 = ok1 && lds_hashed(c0 + o1, rl0, wend, a.big);
-      uint32_t g0 = 0, g1 = 0;
-#ifdef CASK_DIAG_NO_HASH  // diagnostic: everything but the checksum arithmetic (rows say "verified")
-      g0 = h0.stored;
-      g1 = h1.stored;
-      if (false) {
-#else
-      if (G::kWavesPerSimd <= 4) {  // registers for two chains per lane
-#endif
-        if (hs0 || hs1)
-          quad_xxh32_pair(W, (hs0 ? o0 : o1) + shift + 4, (hs1 ? o1 : o0) + shift + 4, hl, qa, g0, g1);
-      } else {
-        if (hs0) g0 = quad_xxh32(W, o0 + shift + 4, hl, qa);
-        if (hs1) g1 = quad_xxh32(W, o1 + shift + 4, hl, qa);
-      }
-      if (!ok0) {
-        if (qa == 0) atomicMin(&L.ffail, i0);
-      } else if (stride_row<G>(L, par, slots, i0, o0, h0, hs0 && g0 != h0.stored, qa)) {  // data.rs:193-198
-        if (qa == 0) atomicMin(&L.cerr_s, i0);
-      }
-      if (has1) {
-        if (!ok1) {
-          if (qa == 0) atomicMin(&L.ffail, i1);
-        } else if (stride_row<G>(L, par, slots, i1, o1, h1, hs1 && g1 != h1.stored, qa)) {
-          if (qa == 0) atomicMin(&L.cerr_s, i1);
-        }
-      }
-    }
-#endif
 #ifdef CASK_STAMPS
     dg.st[8] += __builtin_amdgcn_s_memtime() - st_h0_;  // phase 8: the stride pass's rows
 #endif
@@ -493,7 +380,6 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
     k = L.ffail < cnt ? L.ffail : cnt;
     pf_n = k < G::kRowBuf ? k : G::kRowBuf;  // buffered rows of the settled records [0, k)
     pf_slots = slots;
-#ifndef CASK_STRIDE_QUAD
     regular = a.regular_ok && k == cnt && cnt && !L.irreg;
     if (regular) {  // the first row describes them all (kCountRegular): it goes to desc[t]
       pf_n = 0;
@@ -502,7 +388,6 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
       m.desc.z = hf.vsz;
       m.desc.w = hf.ksz | (srel << 16);
     }
-#endif
     // the lowest failing row counts only if it lies before the stride break (then it is the first)
     cerr = L.cerr_s < k ? L.cerr_s : 0xFFFFFFFFu;
     if (k == cnt && cnt) {
@@ -643,11 +528,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
 template <class G, bool EXACT>
 __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanArgs a, const FileDesc* __restrict__ files_r) {
   __shared__ ScanLdsT<G> L;
-#ifdef CASK_VEC_FILES
-  const FileDesc* files = a.files;
-#else
   const FileDesc* __restrict__ files = files_r;
-#endif
   // Runs of a.run consecutive chunks are handed out in order by a counter (one atomic per run, a
   // run ahead), so workgroups that run slower take fewer runs and all finish together; each run is
   // walked in order with a carry.
@@ -712,24 +593,6 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
     dg.st[3] += __builtin_amdgcn_s_memtime() - st_top_;  // phase 3: window wait + LDS store
     dg.st[4] += 1;
 #endif
-#ifdef CASK_VERIFY_LDS
-    if (a.stamps) {  // diagnostic: the staged window must equal HBM
-      const volatile gu32x4* src = (const volatile gu32x4*)cur.a0;
-      for (uint32_t i = threadIdx.x; i < cur.n16; i += G::kNT) {
-        const u32x4 g = src[i];
-        const u32x4 l = ((const u32x4*)L.win)[i];
-        if ((g.x != l.x || g.y != l.y || g.z != l.z || g.w != l.w) &&
-            atomicCAS(&a.stamps[10], 0ull, 9ull) == 0ull) {
-          a.stamps[11] = i;
-          a.stamps[12] = ((uint64_t)g.x << 32) | l.x;
-          a.stamps[13] = cur.n16;
-          a.stamps[14] = t;
-          a.stamps[15] = blockIdx.x | ((uint64_t)threadIdx.x << 32);
-        }
-      }
-      BAR();
-    }
-#endif
     // exact (repair) pass: the chunk's known start, loaded before the prefetch is issued so that
     // waiting for it never waits for the prefetch
     const uint64_t s_exact = EXACT ? a.spec[t] : 0;
@@ -763,7 +626,6 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #ifdef CASK_STAMPS
     dg.st[5] += __builtin_amdgcn_s_memtime() - st_pf_;  // phase 5: issuing the prefetch
 #endif
-#ifndef CASK_STAGE_ONLY
     Meta m;
     m.desc = u32x4{0u, 0u, 0u, 0u};
     process_chunk<G, EXACT>(L, a, t, cur, s_exact, carry, known, strided, par, pf_n, pf_slots, m, dg);
@@ -776,7 +638,8 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
         v[1] = u32x4{m.count, m.long_r, m.cerr, 0u};
         v[2] = m.desc;
       }
-      if (tn != t + 1 || !more || li == 63) {  // run ends (or a wave's worth of entries)
+      const bool run_ends = tn != t + 1 || !more || li == 63;  // (a run is at most 64 chunks)
+      if (run_ends) {  // run ends (or a wave's worth of entries)
         if (sl <= li) {
           const uint64_t g = run_first + sl;
           a.spec[g] = (uint64_t)v[0].x | ((uint64_t)v[0].y << 32);
@@ -790,9 +653,6 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
         run_first = tn;
       }
     }
-#else  // diagnostic: staging and prefetch only (the memory side of the kernel in isolation)
-    if (threadIdx.x == 0 && L.win[cur.n16] == 0x12345678u) a.count[t] = 1;  // keep the staged bytes live
-#endif
 #ifdef CASK_STAMPS
     const uint64_t st_end_ = __builtin_amdgcn_s_memtime();
 #endif
@@ -846,7 +706,7 @@ static void launch_geo(const ScanArgs& a, void* stream) {
   if (need < grid) grid = need;
   // CASK_LDS_PAD (diagnostic): extra dynamic LDS per workgroup, to lower workgroups per CU
   static const uint32_t pad = getenv("CASK_LDS_PAD") ? (uint32_t)atoi(getenv("CASK_LDS_PAD")) : 0u;
-  (void)hipMemsetAsync(&a.ctr->run_next, 0, sizeof(a.ctr->run_next), S(stream));
+  // a.ctr->run_next is zero: every launch follows a fresh call block or the repair path's reset
   if (a.exact)
     hipLaunchKernelGGL((k_scan_chunks<G, true>), dim3((uint32_t)grid), dim3(G::kNT), pad, S(stream), a, a.files);
   else

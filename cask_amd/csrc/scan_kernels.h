@@ -37,14 +37,27 @@ struct FileDesc {
 
 constexpr uint32_t kTileChunks = 1024;  // chunks per validation tile (k_pipeline.hip kTile)
 
+// Per-call counters and flags, at the head of the call block (zeroed by one memset per call and
+// read back by the host in one copy, with the per-file arrays that follow it: see CallLayout).
 struct Counters {
   unsigned long long nlong;      // records longer than the LDS window
   unsigned long long walk_steps; // repair walk iterations
-  unsigned int run_next;         // k_scan_chunks: next run of chunks to hand out (zeroed per launch)
-  unsigned int pad;
+  unsigned long long total_rows; // k_finish: rows of the call
+  unsigned int run_next;         // k_scan_chunks: next run of chunks to hand out
+  unsigned int tile_next;        // k_finish: next tile of chunks to hand out
+  unsigned int any_invalid;      // k_finish: some chunk's speculated start is wrong (repair path)
+  unsigned int long_pending;     // k_finish: some chunk has rows for k_long
   unsigned int lq_cnt[22];       // long-record queue: entries per length class 2^10 .. 2^31+
-  unsigned int pad2[2];
 };
+
+// Layout of the call block: Counters, then row_off[nfiles + 1] (each file's first dense row,
+// written by k_finish at the file's first chunk), then err_inv[nfiles] (~ the file's first failing
+// dense row, by atomicMax: 0 = none).
+struct CallLayout {
+  static constexpr uint64_t kHead = 256;  // bytes reserved for Counters
+  static uint64_t bytes(uint32_t nfiles) { return kHead + 8ull * (nfiles + 1) + 8ull * nfiles; }
+};
+static_assert(sizeof(Counters) <= CallLayout::kHead, "Counters outgrew the call block head");
 
 // Long-record queue (k_long_enqueue -> k_long_hash): slot indices of the records hashed from HBM,
 // one region per length class b (record length in [2^b, 2^(b+1)), b = 10..31, the last open-ended),
@@ -110,6 +123,15 @@ struct ScanArgs {
   uint8_t* long_done;          // per chunk: 1 once k_long_enqueue has queued its long records
                                // (every scan of the chunk clears it)
   uint64_t* lq;                // long-record queue: slot indices by length class (lq_region_base)
+  // dense path (k_finish): rows go straight from the chunk table to the caller's arrays
+  uint32_t dense;              // 1: k_finish validated every chunk; k_long also fixes dense rows
+  uint32_t epoch;              // tag of this call's lookback granules (1..255)
+  uint64_t* tstate;            // k_finish lookback: 8 granules per tile
+  uint64_t* gbase;             // per chunk: its first dense row (k_finish)
+  uint64_t* row_off;           // call block: per file first dense row
+  unsigned long long* err_inv; // call block: per file ~first failing dense row (0: none)
+  uint32_t vec_ok;             // dense arrays aligned for the 4-row vector stores of k_finish
+  uint32_t pad_;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -153,6 +175,9 @@ void launch_long(const ScanArgs& a, void* stream);  // k_long_enqueue + k_long_h
 void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);
+constexpr uint32_t kFinTile = 256;  // chunks per k_finish tile (one per thread)
+void launch_finish(const ScanArgs& a, void* stream);
+void launch_err_dense(const ScanArgs& a, uint32_t fi, uint64_t row, uint32_t* out, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

@@ -19,20 +19,27 @@ using namespace cask_dev;
 
 namespace {
 
+// Device scratch that only grows. Owned by a context; freed by its destructor (cask_ctx_destroy),
+// so no buffer outlives its context.
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
-  bool ensure(size_t bytes) {
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  // Returns false on allocation failure; `fresh` (optional) is set when the buffer was reallocated.
+  bool ensure(size_t bytes, bool* fresh = nullptr) {
+    if (fresh) *fresh = false;
     if (bytes <= cap) return true;
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     size_t want = bytes + bytes / 4 + 256;
     if (hipMalloc(&p, want) != hipSuccess) {
       p = nullptr;
       return false;
     }
     cap = want;
+    if (fresh) *fresh = true;
     return true;
   }
   void release() {
@@ -47,11 +54,13 @@ struct DevBuf {
 struct HostPinned {
   void* p = nullptr;
   size_t cap = 0;
+  HostPinned() = default;
+  HostPinned(const HostPinned&) = delete;
+  HostPinned& operator=(const HostPinned&) = delete;
+  ~HostPinned() { release(); }
   bool ensure(size_t bytes) {
     if (bytes <= cap) return true;
-    if (p) (void)hipHostFree(p);
-    p = nullptr;
-    cap = 0;
+    release();
     size_t want = bytes + bytes / 4 + 256;
     if (hipHostMalloc(&p, want, hipHostMallocDefault) != hipSuccess) {
       p = nullptr;
@@ -75,15 +84,17 @@ struct cask_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  DevBuf chunk;      // spec | exit | base | tin (u64 x4) | count (u32)
+  // Members are destroyed in reverse order: every buffer is freed before the context goes.
+  DevBuf chunk;      // spec | exit | base | tin (u64 x4) | count (u32) | tiles | long_r | desc | gbase
   DevBuf slots;      // 16-B slot rows, slot_cap per chunk
-  DevBuf ctr;        // Counters
-  DevBuf filebuf;    // FileDesc[] | file_err[] | first_bad[] | file_total[] | summary
+  DevBuf filebuf;    // FileDesc[] | call block (CallLayout) | file_err[] | first_bad[] | file_total[] | summary
   DevBuf err2;       // error detail words
   DevBuf gather;     // compaction rewrite: GatherRec[] | source pointers
   DevBuf stamps;     // diagnostic builds (-DCASK_STAMPS) only
   DevBuf repair;     // runs (u64 x 2 per chunk) | cerr (u32) | redo (u8) | long_done (u8)
   DevBuf lq;         // long-record queue (slot indices by length class)
+  DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
+  uint32_t epoch = 0;
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
   uint64_t* dbg_tin = nullptr;
@@ -91,15 +102,26 @@ struct cask_ctx {
   uint64_t dbg_n = 0;
   HostPinned hfiles;
   HostPinned hsum;
+  HostPinned hcall;
   // host-scan staging
   DevBuf stage_data;
   DevBuf stage_rows;
   int geo = 0;       // k_scan_chunks geometry (CASK_SCAN_GEOMETRY overrides the default)
-  hipEvent_t ev[7] = {};
+  hipEvent_t ev[8] = {};
+  hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
+  int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
   std::mutex mu;
   char last_error[256] = {0};
+  ~cask_ctx() {
+    (void)hipSetDevice(device);
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    if (evw) (void)hipEventDestroy(evw);
+    if (own) (void)hipStreamDestroy(own);
+  }
 };
 
 static int set_dev(const cask_ctx* c) {
@@ -129,7 +151,8 @@ cask_ctx* cask_ctx_create(int device, int* status) {
   c->geo = kDefaultGeometry;
   if (const char* g = getenv("CASK_SCAN_GEOMETRY")) c->geo = atoi(g);
   for (auto& e : c->ev) (void)hipEventCreate(&e);
-  if (!c->ctr.ensure(sizeof(Counters)) || !c->err2.ensure(64)) {
+  (void)hipEventCreateWithFlags(&c->evw, hipEventDisableTiming);
+  if (!c->err2.ensure(64)) {
     cask_ctx_destroy(c);
     if (status) *status = CASK_E_NOMEM;
     return nullptr;
@@ -139,28 +162,23 @@ cask_ctx* cask_ctx_create(int device, int* status) {
 }
 
 void cask_ctx_destroy(cask_ctx* c) {
-  if (!c) return;
-  (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
-  c->chunk.release();
-  c->slots.release();
-  c->gather.release();
-  c->ctr.release();
-  c->filebuf.release();
-  c->err2.release();
-  c->stage_data.release();
-  c->stage_rows.release();
-  c->hfiles.release();
-  c->hsum.release();
-  for (auto& e : c->ev)
-    if (e) (void)hipEventDestroy(e);
-  if (c->own) (void)hipStreamDestroy(c->own);
-  delete c;
+  delete c;  // ~cask_ctx waits for the stream, then every DevBuf/HostPinned frees its memory
 }
 
 int cask_ctx_set_stream(cask_ctx* c, void* s) {
   if (!c) return CASK_E_INVALID_ARG;
   c->stream = s ? (hipStream_t)s : c->own;
+  return CASK_OK;
+}
+
+int cask_ctx_wait_stream(cask_ctx* c, void* other) {
+  if (!c) return CASK_E_INVALID_ARG;
+  if ((hipStream_t)other == c->stream) return CASK_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (hipEventRecord(c->evw, (hipStream_t)other) != hipSuccess ||
+      hipStreamWaitEvent(c->stream, c->evw, 0) != hipSuccess)
+    return CASK_E_DEVICE;
   return CASK_OK;
 }
 
@@ -183,6 +201,8 @@ int cask_last_timings(const cask_ctx* c, float* ms6) {
   return CASK_OK;
 }
 
+int cask_last_dense(const cask_ctx* c) { return c ? c->last_dense : 0; }
+
 int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
   if (!c || !c5) return CASK_E_INVALID_ARG;
   memcpy(c5, c->last_counters, sizeof(c->last_counters));
@@ -192,7 +212,13 @@ int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
 }  // extern "C"
 
 // Core pipeline on device-resident files. rows == nullptr: segmented output only (slots + chunk
-// table, owned by the context); otherwise dense SoA rows are compacted into the caller's arrays.
+// table, owned by the context); otherwise dense SoA rows in the caller's arrays.
+//
+// Dense path (the common case): k_scan_chunks, then k_finish validates every speculated chunk
+// start and writes the dense rows; one copy of the call block tells the host whether every start
+// held and whether records longer than the window wait for k_long. Two kernels when the log has
+// no long records. If some start was wrong the repair path takes over (validate, exact re-scans,
+// k_compact), as does the segmented output.
 static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
                             cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err) {
   if (nfiles && !files) return CASK_E_INVALID_ARG;
@@ -211,7 +237,12 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   uint64_t total_chunks = 0, total_tiles = 0;
   const size_t head_words = sizeof(SummaryHead) / 8;
   const size_t sum_words = head_words + (nfiles + 1) + 4ull * nfiles;
-  if (!c->hfiles.ensure(sizeof(FileDesc) * (nfiles + 1)) || !c->hsum.ensure(sum_words * 8)) return CASK_E_NOMEM;
+  const size_t call_bytes = CallLayout::bytes(nfiles);
+  // the file table and the zeroed call block go to the device in one copy: [FileDesc | call block]
+  const size_t fd_bytes = align_up(sizeof(FileDesc) * (nfiles + 1), 256);
+  if (!c->hfiles.ensure(fd_bytes + call_bytes) || !c->hsum.ensure(sum_words * 8) || !c->hcall.ensure(call_bytes))
+    return CASK_E_NOMEM;
+  memset((uint8_t*)c->hfiles.p + fd_bytes, 0, call_bytes);
   FileDesc* fd = (FileDesc*)c->hfiles.p;
   for (uint32_t i = 0; i < nfiles; ++i) {
     fd[i].data = files[i].data;
@@ -223,27 +254,31 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     total_chunks += fd[i].nchunks;
     total_tiles += (fd[i].nchunks + kTileChunks - 1) / kTileChunks;
   }
+  const uint64_t fin_tiles = (total_chunks + kFinTile - 1) / kFinTile;
   // device scratch
-  const size_t fd_bytes = align_up(sizeof(FileDesc) * (nfiles + 1), 256);
   const size_t pf_bytes = align_up(8ull * (nfiles + 1), 256);
   const size_t sum_bytes = align_up(sum_words * 8, 256);
-  if (!c->filebuf.ensure(fd_bytes + 3 * pf_bytes + sum_bytes)) return CASK_E_NOMEM;
-  if (!c->chunk.ensure((total_chunks + 1) * (4 * 8 + 4 + 4 + 16) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
+  const size_t callb = align_up(call_bytes, 256);
+  const uint64_t C = total_chunks + 1;
+  if (!c->filebuf.ensure(fd_bytes + callb + 3 * pf_bytes + sum_bytes)) return CASK_E_NOMEM;
+  if (!c->chunk.ensure(C * (4 * 8 + 4 + 4 + 16 + 8) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
   if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
   const size_t runs_bytes = align_up(16ull * (total_chunks + 1), 256), cerr_bytes = align_up(4ull * (total_chunks + 1), 256),
                redo_bytes = align_up(total_chunks + 1, 256);
   if (!c->repair.ensure(runs_bytes + cerr_bytes + 2 * redo_bytes)) return CASK_E_NOMEM;
   if (!c->lq.ensure(8 * (lq_region_base(total_chunks, chunk, 32) + 1))) return CASK_E_NOMEM;
+  bool fresh = false;  // k_finish look-back granules, 8 per tile
+  if (!c->tstate.ensure(64ull * (fin_tiles + 1), &fresh)) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
-  unsigned long long* d_ferr = (unsigned long long*)(fbase + fd_bytes);
-  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + pf_bytes);
-  uint64_t* d_ftot = (uint64_t*)(fbase + fd_bytes + 2 * pf_bytes);
-  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + 3 * pf_bytes);
+  uint8_t* callp = fbase + fd_bytes;
+  unsigned long long* d_ferr = (unsigned long long*)(fbase + fd_bytes + callb);
+  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + callb + pf_bytes);
+  uint64_t* d_ftot = (uint64_t*)(fbase + fd_bytes + callb + 2 * pf_bytes);
+  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + callb + 3 * pf_bytes);
 
   uint64_t* cb = c->chunk.as<uint64_t>();
-  const uint64_t C = total_chunks + 1;
   ScanArgs a{};
   a.files = d_files;
   a.nfiles = nfiles;
@@ -263,6 +298,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     uint64_t doff = (uint64_t)(tb - cb) + 4 * TT + (C + 1) / 2 + 2;  // after long_r, 16-B aligned
     doff = (doff + 1) & ~1ull;
     a.desc = (uint32_t*)(cb + doff);
+    a.gbase = cb + doff + 2 * C;  // after desc (16 B per chunk)
     a.total_tiles = total_tiles;
     a.tile_max = tb;
     a.tile_sum = tb + TT;
@@ -273,7 +309,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.file_total = d_ftot;
   a.file_err = d_ferr;
   a.first_bad = d_fbad;
-  a.ctr = c->ctr.as<Counters>();
+  a.ctr = (Counters*)callp;
+  a.row_off = (uint64_t*)(callp + CallLayout::kHead);
+  a.err_inv = (unsigned long long*)(a.row_off + nfiles + 1);
   uint8_t* rb = c->repair.as<uint8_t>();
   uint64_t* d_runs = (uint64_t*)rb;
   a.cerr = (uint32_t*)(rb + runs_bytes);
@@ -282,6 +320,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.lq = c->lq.as<uint64_t>();
   a.runs = nullptr;
   a.nruns_list = 0;
+  a.tstate = c->tstate.as<uint64_t>();
   if (rows) {
     a.pos = rows->pos;
     a.seq = rows->seq;
@@ -289,6 +328,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.ksz = rows->ksz;
     a.status = rows->status;
     a.row_cap = rows->capacity;
+    a.vec_ok = ((uintptr_t)rows->pos % 16 == 0 && (uintptr_t)rows->seq % 16 == 0 && (uintptr_t)rows->vsz % 16 == 0 &&
+                (uintptr_t)rows->ksz % 8 == 0 && (uintptr_t)rows->status % 4 == 0) ? 1u : 0u;
   }
   a.stamps = nullptr;
   {  // CASK_RUN_CHUNKS (tuning knob): chunks per workgroup run; one boundary search per run.
@@ -304,14 +345,25 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       a.run = (uint32_t)std::min<uint64_t>(kMaxRun, std::max<uint64_t>(kDefaultRun, per_wg));
     }
   }
-  // regular chunks keep only their first slot row when the rows go to the dense output (k_compact
-  // expands them); the segmented output hands the slots to the caller, so every row is written
-  a.regular_ok = (rows && !getenv("CASK_NO_REGULAR")) ? 1u : 0u;
-  a.respec = getenv("CASK_NO_LOCAL_REPAIR") ? 0u : 1u;
+  // regular chunks keep only their first slot row when the rows go to the dense output (k_finish
+  // and k_compact expand them); the segmented output hands the slots to the caller
+  a.regular_ok = rows ? 1u : 0u;
+  a.respec = 1u;
   // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
   a.big = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
   if (a.big < kMinBigRec) a.big = kMinBigRec;  // the long-record queue's smallest length class
   a.win = chunk + geometry_halo(c->geo);
+  // the dense path: CASK_DENSE=0 (tuning knob) sends every call through the repair path's k_compact
+  static const bool dense_on = !(getenv("CASK_DENSE") && atoi(getenv("CASK_DENSE")) == 0);
+  const bool dense = rows != nullptr && dense_on && total_chunks > 0;
+  a.dense = 0;  // k_long fixes dense rows only once they are validated
+
+  // look-back granules carry the call's epoch: no memset between calls, one when the tag wraps
+  if (fresh || c->epoch >= 255) {
+    if (hipMemsetAsync(a.tstate, 0, c->tstate.cap, st) != hipSuccess) return CASK_E_DEVICE;
+    c->epoch = 0;
+  }
+  a.epoch = ++c->epoch;
 #ifdef CASK_STAMPS
   if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
 #endif
@@ -323,27 +375,102 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       snprintf(c->last_error, sizeof(c->last_error), "%s: %s", what, hipGetErrorString(e));
     }
   };
-  auto reset = [&]() {
-    H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
-    H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
-    H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
-    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 16 * 8, st));
-  };
   // CASK_SYNC_EACH=1 (diagnostic): synchronise after every launch so a fault names its kernel
   static const bool sync_each = getenv("CASK_SYNC_EACH") != nullptr;
   auto L = [&](const char* what) {
     H(hipGetLastError(), what);
     if (sync_each) H(hipStreamSynchronize(st), what);
   };
-  // one pass of the pipeline; events 1..4 bracket scan / long / validate+summary / compact
+  const Counters* hc = (const Counters*)c->hcall.p;
+  const uint64_t* h_rowoff = (const uint64_t*)((const uint8_t*)c->hcall.p + CallLayout::kHead);
+  const unsigned long long* h_errinv = (const unsigned long long*)(h_rowoff + nfiles + 1);
+  auto read_call = [&]() {
+    H(hipMemcpyAsync(c->hcall.p, callp, call_bytes, hipMemcpyDeviceToHost, st), "call block D2H");
+    H(hipStreamSynchronize(st), "stream sync");
+  };
+
+  c->last_error[0] = 0;
+  (void)hipGetLastError();  // drop any stale error another library left on this thread
+  H(hipMemcpyAsync(d_files, fd, fd_bytes + call_bytes, hipMemcpyHostToDevice, st), "file table H2D");
+  H(hipEventRecord(c->ev[1], st));
+  launch_scan_chunks(a, c->geo, st);
+  L("k_scan_chunks");
+  H(hipEventRecord(c->ev[2], st));
+  if (dense) {
+    launch_finish(a, st);
+    L("k_finish");
+    H(hipEventRecord(c->ev[3], st));
+    read_call();
+    if (!ok) return CASK_E_DEVICE;
+  }
+
+  c->last_dense = 0;
+  if (dense && !hc->any_invalid) {
+    // every speculated start held: the rows are final but for the long records' checksums
+    a.dense = 1;
+    c->last_dense = 1;
+    if (hc->long_pending) {
+      launch_long(a, st);
+      L("k_long");
+    }
+    H(hipEventRecord(c->ev[4], st));
+    if (hc->long_pending) read_call();
+    else H(hipEventSynchronize(c->ev[4]), "event sync");
+    if (!ok) return CASK_E_DEVICE;
+    float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0;
+    (void)hipEventElapsedTime(&t_all, c->ev[1], c->ev[4]);
+    (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
+    (void)hipEventElapsedTime(&t_fin, c->ev[2], c->ev[3]);
+    (void)hipEventElapsedTime(&t_long, c->ev[3], c->ev[4]);
+    c->last_ms[0] = t_all;
+    c->last_ms[1] = t_k1;
+    c->last_ms[2] = t_long;
+    c->last_ms[3] = t_fin;
+    c->last_ms[4] = 0.f;
+    c->last_ms[5] = 0.f;
+    c->last_counters[0] = total_chunks;
+    c->last_counters[1] = hc->nlong;
+    c->last_counters[2] = c->last_counters[3] = c->last_counters[4] = 0;
+    const uint64_t total = hc->total_rows;
+    if (file_row_offset) {  // empty files have no chunk: they start where the next file does
+      file_row_offset[nfiles] = total;
+      for (uint32_t f = nfiles; f-- > 0;)
+        file_row_offset[f] = fd[f].nchunks ? h_rowoff[f] : file_row_offset[f + 1];
+    }
+    rows->count = total;
+    if (total > rows->capacity) return CASK_E_CAPACITY;
+    if (err) {
+      memset(err, 0, sizeof(*err));
+      for (uint32_t f = 0; f < nfiles; ++f) {
+        if (!h_errinv[f]) continue;
+        const uint64_t d = ~(uint64_t)h_errinv[f];
+        uint32_t e5[6] = {0, 0, 0, 0, 0, 0};
+        launch_err_dense(a, f, d, c->err2.as<uint32_t>(), st);
+        H(hipMemcpyAsync(e5, c->err2.p, 24, hipMemcpyDeviceToHost, st));
+        H(hipStreamSynchronize(st));
+        if (!ok) return CASK_E_DEVICE;
+        err->kind = (int32_t)e5[2];
+        err->file_id = files[f].file_id;
+        err->pos = (uint64_t)e5[3] | ((uint64_t)e5[4] << 32);
+        err->row = d;
+        err->expected = e5[0];
+        err->found = e5[2] == CASK_ROW_CHECKSUM ? e5[1] : 0;
+        break;
+      }
+    }
+    return CASK_OK;
+  }
+
+  // ---- repair path (and the segmented output) --------------------------------------------------
+  auto reset = [&]() {
+    H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
+    H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
+    H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
+    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 16 * 8, st));
+  };
   uint64_t nlong_total = 0;  // records hashed by k_long over all passes (each pass queues only chunks it scanned)
-  auto pass = [&](bool timed) {
-    reset();
-    if (timed) H(hipEventRecord(c->ev[1], st));
-    launch_scan_chunks(a, c->geo, st);
-    L("k_scan_chunks");
-    if (timed) H(hipEventRecord(c->ev[2], st));
-    // validation before k_long: k_long skips the files a repair pass is about to re-scan
+  // validation, long records and summary after a scan of the chunks (events 2..4 when timed)
+  auto post = [&](bool timed) {
     launch_validate(a, st);
     L("k_val");
     if (timed) H(hipEventRecord(c->ev[3], st));
@@ -352,20 +479,22 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_summary(a, d_sum, st);
     L("k_summary");
     if (timed) H(hipEventRecord(c->ev[4], st));
-    if (rows) {
-      launch_compact(a, d_sum, st);
-      L("k_compact");
-    }
-    H(hipEventRecord(timed ? c->ev[5] : c->ev[6], st));
     H(hipMemcpyAsync(c->hsum.p, d_sum, sum_words * 8, hipMemcpyDeviceToHost, st), "summary D2H");
     H(hipStreamSynchronize(st), "stream sync");
     if (ok) nlong_total += ((const SummaryHead*)c->hsum.p)->nlong;
   };
-  H(hipEventRecord(c->ev[0], st));
-  H(hipMemcpyAsync(d_files, fd, sizeof(FileDesc) * (nfiles ? nfiles : 1), hipMemcpyHostToDevice, st));
-  c->last_error[0] = 0;
-  (void)hipGetLastError();  // drop any stale error another library left on this thread
-  pass(true);
+  auto pass = [&]() {
+    reset();
+    launch_scan_chunks(a, c->geo, st);
+    L("k_scan_chunks");
+    post(false);
+  };
+  // the first scan has run (its counters are in the call block): keep its run counter's effects,
+  // clear the per-file error state the validation builds
+  H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
+  H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
+  H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
+  post(true);
   if (!ok) return CASK_E_DEVICE;
 
   uint64_t* hs = (uint64_t*)c->hsum.p;
@@ -389,6 +518,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   uint64_t local_passes = 0, walked = 0;
   std::vector<uint8_t> redo;
   std::vector<uint64_t> runs;
+  H(hipEventRecord(c->ev[5], st));
   if (head->any_invalid) {
     // Repair. First, local: validation has already moved every invalid chunk's start to T[c]
     // (a.respec), which is exact for the first invalid chunk of each stretch, so exact re-scans
@@ -402,9 +532,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.exact = 1;
     static const bool sparse = getenv("CASK_FULL_REPAIR") == nullptr;  // diagnostic: re-scan everything
     const int max_local = getenv("CASK_LOCAL_REPAIRS") ? atoi(getenv("CASK_LOCAL_REPAIRS")) : 3;
-    if (sparse) {
-      redo.resize(total_chunks);
-    }
+    if (sparse) redo.resize(total_chunks);
     for (int it = 0; it < max_local && head->any_invalid; ++it) {
       if (sparse) {
         H(hipMemcpyAsync(redo.data(), a.redo, total_chunks, hipMemcpyDeviceToHost, st), "redo D2H");
@@ -430,7 +558,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       } else {
         invalid_chunks += head->invalid_chunks;
       }
-      pass(false);
+      pass();
       if (!ok) return CASK_E_DEVICE;
       ++local_passes;
     }
@@ -441,22 +569,30 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       a.nruns_list = 0;
       launch_walk(a, d_sum, st);
       L("k_walk");
-      pass(false);
+      pass();
       if (!ok) return CASK_E_DEVICE;
     }
     if (head->any_invalid) {  // the exact pass must validate
       snprintf(c->last_error, sizeof(c->last_error), "exact re-scan did not validate");
       return CASK_E_DEVICE;
     }
-    (void)hipEventElapsedTime(&repair_ms, c->ev[5], c->ev[6]);
   }
+  H(hipEventRecord(c->ev[6], st));
+  if (rows) {
+    launch_compact(a, d_sum, st);
+    L("k_compact");
+  }
+  H(hipEventRecord(c->ev[7], st));
+  H(hipStreamSynchronize(st), "stream sync");
+  if (!ok) return CASK_E_DEVICE;
   float t_all = 0, t_k1 = 0, t_long = 0, t_val = 0, t_cmp = 0;
   (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
-  (void)hipEventElapsedTime(&t_val, c->ev[2], c->ev[3]);
+  (void)hipEventElapsedTime(&t_val, c->ev[2], c->ev[3]);  // with k_finish's time on a dense attempt
   (void)hipEventElapsedTime(&t_long, c->ev[3], c->ev[4]);  // with the summary (a few us)
-  (void)hipEventElapsedTime(&t_cmp, c->ev[4], c->ev[5]);
-  (void)hipEventElapsedTime(&t_all, c->ev[0], c->ev[5]);
-  c->last_ms[0] = t_all + repair_ms;
+  (void)hipEventElapsedTime(&repair_ms, c->ev[5], c->ev[6]);
+  (void)hipEventElapsedTime(&t_cmp, c->ev[6], c->ev[7]);
+  (void)hipEventElapsedTime(&t_all, c->ev[1], c->ev[7]);
+  c->last_ms[0] = t_all;
   c->last_ms[1] = t_k1;
   c->last_ms[2] = t_long;
   c->last_ms[3] = t_val;

@@ -72,9 +72,12 @@ class ScanContext:
 
     def _inputs_ready(self):
         """The context runs on its own non-blocking HIP stream, which does not wait for torch's
-        stream: tensors torch is still producing must be complete before the library reads them."""
+        stream by itself: tensors torch is still producing must be complete before the library
+        reads them. The context's stream waits for torch's on the device (an event), the host does
+        not block."""
         import torch
-        torch.cuda.current_stream(self.device).synchronize()
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        raise_status(self.lib.cask_ctx_wait_stream(self._h, C.c_void_p(s or None)), what="cask_ctx_wait_stream")
 
     def set_stream(self, stream_ptr: int | None):
         self.lib.cask_ctx_set_stream(self._h, C.c_void_p(stream_ptr or 0))
@@ -188,6 +191,8 @@ class ScanContext:
     def last_timings(self) -> dict[str, float]:
         t = (C.c_float * 6)()
         self.lib.cask_last_timings(self._h, t)
+        # validate_ms: k_finish on the dense path (validation + dense rows; compact_ms is then 0),
+        # the three validation launches on the repair path
         return {"pipeline_ms": t[0], "chunk_scan_ms": t[1], "long_ms": t[2], "validate_ms": t[3],
                 "repair_ms": t[4], "compact_ms": t[5]}
 
@@ -195,7 +200,8 @@ class ScanContext:
         c = (C.c_uint64 * 5)()
         self.lib.cask_last_counters(self._h, c)
         return {"chunks": int(c[0]), "long_records": int(c[1]), "repaired_chunks": int(c[2]),
-                "local_repair_passes": int(c[3]), "walked": int(c[4])}
+                "local_repair_passes": int(c[3]), "walked": int(c[4]),
+                "dense_path": int(self.lib.cask_last_dense(self._h))}
 
     # -- encoder ------------------------------------------------------------------------------
     def encode_synthetic(self, off, seq, ksz, vsz_raw, key_id, value_seed: int, out):

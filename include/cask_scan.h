@@ -59,6 +59,10 @@ void cask_ctx_destroy(cask_ctx* ctx);
  * set here) before a call reads them. */
 int cask_ctx_set_stream(cask_ctx* ctx, void* hip_stream);
 void* cask_ctx_stream(cask_ctx* ctx);
+/* Make the context's stream wait, on the device and without blocking the host, for the work queued
+ * so far on another stream (hipStream_t as void*; NULL = the null stream) — how a caller hands over
+ * inputs another library is still producing. */
+int cask_ctx_wait_stream(cask_ctx* ctx, void* hip_stream);
 int cask_ctx_device(const cask_ctx* ctx);
 /* Human-readable cause of the last CASK_E_DEVICE returned on this context ("" if none). */
 const char* cask_ctx_last_error(const cask_ctx* ctx);
@@ -145,6 +149,9 @@ int cask_last_timings(const cask_ctx* ctx, float* ms6);
  * invalid one on (0: speculation held), [3] local exact re-scans, [4] 1 if the serial boundary
  * walk ran. */
 int cask_last_counters(const cask_ctx* ctx, uint64_t* c5);
+/* 1 if the last cask_scan_device / cask_scan_host call took the two-kernel dense path (k_scan_chunks
+ * + k_finish: every speculated chunk start held), 0 if it went through the repair path. */
+int cask_last_dense(const cask_ctx* ctx);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Batched record encoder (Entry::write_bytes, data.rs:90-121) — the bulk write path and the   */

@@ -182,7 +182,8 @@ def test_uniform_290(gpu_ctx):
     rng = random.Random(1)
     buf = make_records(rng, 20000, lambda r: 16, lambda r: 256)
     res = check_against_oracle(gpu_ctx, [buf])
-    assert gpu_ctx.last_counters()["repaired_chunks"] == 0
+    cnt = gpu_ctx.last_counters()
+    assert cnt["repaired_chunks"] == 0 and cnt["dense_path"] == 1, cnt
 
 
 def test_uniform_82_device(gpu_ctx):
@@ -285,7 +286,8 @@ def test_adversarial_embedded_records_repair(gpu_ctx):
         v = b"".join(rng.choice(inner) for _ in range(rng.randrange(1, 30)))
         out.append(R.entry_new(i + 1, b"outer%d" % i, v).write_bytes())
     check_against_oracle(gpu_ctx, [b"".join(out)])
-    assert gpu_ctx.last_counters()["repaired_chunks"] > 0
+    cnt = gpu_ctx.last_counters()
+    assert cnt["repaired_chunks"] > 0 and cnt["dense_path"] == 0, cnt
 
 
 def test_adversarial_repair_by_walk_only(gpu_ctx):
@@ -417,9 +419,16 @@ def test_cfg2_full_size_properties(gpu_ctx):
         assert torch.equal(res.seq[sl], idx + f.seq0)
     assert int((res.ksz[:res.count] != 16).sum().item()) == 0
     assert int((res.vsz[:res.count] != 256).sum().item()) == 0
-    assert gpu_ctx.last_counters()["repaired_chunks"] == 0
+    cnt = gpu_ctx.last_counters()
+    assert cnt["repaired_chunks"] == 0 and cnt["dense_path"] == 1, cnt
+    # a 64 MiB slice of file 1 against the oracle, all five row fields
     sl_bytes = (64 << 20) // 290 * 290
     host = files[0].data[:sl_bytes].cpu().numpy()
     want = O.scan(host)
-    assert len(want) == sl_bytes // 290 and (want["status"] == 0).all()
-    assert np.array_equal(want["seq"], res.seq[:len(want)].cpu().numpy().astype(np.uint64))
+    m = len(want)
+    assert m == sl_bytes // 290 and (want["status"] == 0).all()
+    assert np.array_equal(want["pos"], res.pos[:m].cpu().numpy().astype(np.uint64))
+    assert np.array_equal(want["seq"], res.seq[:m].cpu().numpy().astype(np.uint64))
+    assert np.array_equal(want["ksz"].astype(np.uint16), res.ksz[:m].cpu().numpy().view(np.uint16))
+    assert np.array_equal(want["vsz_raw"].astype(np.uint32), res.vsz[:m].cpu().numpy().view(np.uint32))
+    assert np.array_equal(want["status"].astype(np.uint8), res.status[:m].cpu().numpy())

@@ -1,0 +1,69 @@
+"""A/B timing of library builds on one box (tools only; bench.py always times the product build).
+
+  python tools/ab.py [--rounds 3] [--steps 20] NAME=PATH [NAME=PATH ...]
+
+Each build runs in its own process (the library is picked with cask_amd._lib.use_library, never by
+an environment variable the package reads); the builds alternate `--rounds` times so box drift
+hits them alike. Prints the headline loop's GiB/s and the chunk-scan kernel time per run.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def child(path, steps, files):
+    sys.path.insert(0, ROOT)
+    import torch
+    import cask_amd
+    if path != "product":
+        cask_amd._lib.use_library(path)
+    from cask_amd.workloads import cfg2_files
+    ctx = cask_amd.ScanContext(0)
+    fs = cfg2_files(ctx, nfiles=files)
+    views = [(f.file_id, f.data) for f in fs]
+    rows = ctx.alloc_rows(sum(f.nrec for f in fs))
+    nbytes = sum(f.data.numel() for f in fs)
+    for _ in range(3):
+        ctx.scan_device(views, rows)
+    torch.cuda.synchronize()
+    k = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        ctx.scan_device(views, rows)
+        k.append(ctx.last_timings()["chunk_scan_ms"])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    print(json.dumps({"gibps": nbytes * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps,
+                      "k_scan_ms": sum(k) / len(k), "timings": ctx.last_timings()}))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--files", type=int, default=8)
+    ap.add_argument("--child", default="")
+    ap.add_argument("libs", nargs="*")
+    a = ap.parse_args()
+    if a.child:
+        return child(a.child, a.steps, a.files)
+    for r in range(a.rounds):
+        for spec in a.libs:
+            name, path = spec.split("=", 1)
+            out = subprocess.run([sys.executable, __file__, "--child", path, "--steps", str(a.steps),
+                                  "--files", str(a.files)], capture_output=True, text=True, timeout=300)
+            if out.returncode != 0:
+                print(name, "FAILED", out.stderr[-2000:])
+                sys.exit(1)
+            d = json.loads(out.stdout.strip().splitlines()[-1])
+            print(f"round {r} {name}: {d['gibps']:.1f} GiB/s  {d['ms_per_step']:.4f} ms/step  "
+                  f"k_scan {d['k_scan_ms']:.4f} ms  {json.dumps(d['timings'])}", flush=True)
+
+
+if __name__ == "__main__":
+    main()

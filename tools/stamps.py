@@ -1,6 +1,6 @@
 """Phase breakdown of k_scan_chunks from the diagnostic build (make -C cask_amd stamps).
 
-CASK_LIB_PATH=cask_amd/build/stamps/libcask_scan.so python tools/stamps.py [--files N]
+python tools/stamps.py [--files N]   (after make -C cask_amd stamps)
 Prints the average s_memtime cycles per workgroup spent in each phase (shares, not wall time:
 the stamps serialise what the real kernel overlaps).
 """
@@ -11,7 +11,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("CASK_LIB_PATH", os.path.join(ROOT, "cask_amd", "build", "stamps", "libcask_scan.so"))
+STAMPS_LIB = os.path.join(ROOT, "cask_amd", "build", "stamps", "libcask_scan.so")
 
 PHASES = ["search", "walk", "hash+slots", "stage wait+store", "(iterations)", "prefetch issue", "end barrier", "TOTAL loop", "  rec hdr+hash", "  rec store issue"]
 
@@ -24,6 +24,7 @@ def main():
     args = ap.parse_args()
     import torch
     import cask_amd
+    cask_amd._lib.use_library(STAMPS_LIB)
     from cask_amd.workloads import cfg2_files
     L = cask_amd.lib()
     L.cask_debug_stamps.restype = C.c_int
