@@ -37,6 +37,10 @@ def parse():
     ap.add_argument("--cpu-sample-files", type=int, default=1, help="files timed by the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (H2D+D2H) measurement")
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="rehearsal only: gloo (blocks gathered through host memory)")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal only: every rank on cuda:0 (a one-GPU box)")
     ap.add_argument("--no-segmented", action="store_true",
                     help="skip the segmented-output measurement (profiling runs: dense-path launches only)")
     return ap.parse_args()
@@ -120,10 +124,15 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    if args.same_device:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.dist_backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", local if world > 1 else 0)
@@ -161,6 +170,7 @@ def main():
         ctx.scan_device(views, rows)
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize(dev)
@@ -177,7 +187,7 @@ def main():
     barrier()
     elapsed = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     ms_per_step = elapsed * 1e3 / args.steps
@@ -199,15 +209,29 @@ def main():
             ctx.scan_device_segmented(views)
         barrier()
         extra["segmented_gibps"] = bytes_per_step * world * args.steps / (time.perf_counter() - ts) / 2 ** 30
-    # scan + gather of keydir rows to rank 0 (reported separately from the metric)
+    # keydir block of this rank's files, and the blocks gathered on rank 0 over RCCL,
+    # reported separately from the metric; any failure here is reported, not fatal to the line
     if dist is not None and not args.no_gather:
-        from cask_amd.distributed import gather_rows
-        barrier()
-        tg = time.perf_counter()
-        gather_rows(rows, res.count)
-        barrier()
-        extra["gather_rows_ms"] = (time.perf_counter() - tg) * 1e3
-        extra["gather_rows_per_rank"] = res.count
+        try:
+            from cask_amd.distributed import gather_blocks
+            from cask_amd.keydir import shard_keydir
+            res = ctx.scan_device(views, rows)
+            barrier()
+            tb = time.perf_counter()
+            blk = shard_keydir(ctx, views, rows, res.count, res.file_row_offset)
+            barrier()
+            tg = time.perf_counter()
+            got = gather_blocks(blk if args.dist_backend == "nccl" else blk.cpu(), dst=0)
+            barrier()
+            te = time.perf_counter()
+            extra["keydir_block_ms"] = (tg - tb) * 1e3
+            extra["keydir_gather_ms"] = (te - tg) * 1e3
+            extra["keydir_block_bytes_per_rank"] = int(blk.numel())
+            if rank == 0:
+                extra["keydir_gathered_bytes"] = int(sum(b.numel() for b in got))
+            del blk, got
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            extra["keydir_gather_error"] = f"{type(e).__name__}: {e}"[:300]
 
     # end-to-end: host-resident files -> H2D -> scan -> rows D2H (cask_scan_host)
     if rank == 0 and not args.no_e2e:

@@ -131,6 +131,14 @@ SIGNATURES = [
                                         C.POINTER(OpenError)]),
     ("cask_db_compact", C.c_int64, [C.c_void_p, C.POINTER(CompactOptions), C.POINTER(CompactResult),
                                     C.POINTER(OpenError)]),
+    ("cask_shard_keydir", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
+                                    C.POINTER(C.c_void_p), c_u64p]),
+    ("cask_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_keydir_new", C.c_void_p, []),
+    ("cask_keydir_merge", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_keydir_finish", C.c_int, [C.c_void_p]),
+    ("cask_db_open_multi", C.c_void_p, [C.c_char_p, C.POINTER(Options), C.POINTER(C.c_int), C.c_int,
+                                        C.POINTER(OpenError)]),
 ]
 
 _lib = None

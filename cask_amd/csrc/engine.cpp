@@ -27,6 +27,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/cask_scan.h"
+#include "keydir_format.h"
 #include "xxh32.h"
 
 namespace {
@@ -140,6 +141,37 @@ class KeyDir {
       slots[i].key_off = arena.size();
       arena.insert(arena.end(), key, key + s0.ksz);
     }
+    ++used;
+  }
+
+  // Index::update's effect on the keydir alone (cask.rs:60-90 without the Stats calls): the fold of
+  // the sharded replay, whose stats come from per-file counts (cask_keydir_finish).
+  void update_kd(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+    const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
+    const uint64_t h = hash_key(key, ksz);
+    if ((used + 1) * 4 > slots.size() * 3) grow();
+    const int64_t f = find(key, ksz, h);
+    if (f >= 0) {
+      Slot& s = slots[f];
+      if (s.e.sequence <= seq) {
+        if (deleted) {
+          s.state = 2;
+          --live;
+        } else {
+          s.e = cask_index_entry{file_id, 0, pos, 18ull + ksz + vsz_raw, seq};
+        }
+      }
+      return;
+    }
+    if (deleted) return;
+    Slot& s = slots[(uint64_t)(-f - 1)];
+    s.hash = h;
+    s.key_off = arena.size();
+    s.ksz = ksz;
+    s.state = 1;
+    s.e = cask_index_entry{file_id, 0, pos, 18ull + ksz + vsz_raw, seq};
+    arena.insert(arena.end(), key, key + ksz);
+    ++live;
     ++used;
   }
 
@@ -425,6 +457,13 @@ struct cask_db {
   uint64_t sequence = 0;
   uint32_t file_seq = 0;  // Log::file_id_seq: the last data file id at open (log.rs:63-69)
   double timings[5] = {0, 0, 0, 0, 0};
+  // sharded replay (cask_keydir_merge): per-file order-free stats terms, summed over shards
+  struct ShardTerms {
+    uint64_t puts = 0, put_bytes = 0, stale = 0, stale_bytes = 0;
+  };
+  std::unordered_map<uint32_t, ShardTerms> terms;
+  bool merging = false;
+  uint32_t shards = 0;
   ~cask_db() {
     if (lock_fd >= 0) {
       flock(lock_fd, LOCK_UN);  // Drop for Log (log.rs:225-229)
@@ -454,13 +493,14 @@ static void set_err(cask_open_error* err, int status, uint32_t fid = 0, uint64_t
   err->found = f;
 }
 
-cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
+// Log::open (log.rs:36-85): path checks, the lock file, the data files in id order. Returns the
+// handle (no keydir yet) or NULL with *err set.
+static cask_db* open_log(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
   set_err(err, CASK_OK);
   if (!path_c) {
     set_err(err, CASK_E_INVALID_ARG);
     return nullptr;
   }
-  auto t0 = std::chrono::steady_clock::now();
   cask_options opts;
   if (opts_in) opts = *opts_in; else cask_options_default(&opts);
   std::string path = path_c;
@@ -505,6 +545,15 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     return nullptr;
   }
   db->file_seq = db->files.empty() ? 0u : db->files.back();
+  return db;
+}
+
+cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
+  auto t0 = std::chrono::steady_clock::now();
+  cask_db* db = open_log(path_c, opts_in, err);
+  if (!db) return nullptr;
+  const cask_options opts = db->opts;
+  const std::string path = db->path;
 
   // Which files have a valid hint file (log.rs:121-135, 512-539)?
   const size_t nf = db->files.size();
@@ -1073,6 +1122,240 @@ int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts_in, cask_c
   if (!triggered) return 0;
   const int st = cask_db_compact_files(db, sel.data(), sel.size(), res, err);
   return st == CASK_OK ? (int64_t)sel.size() : (int64_t)st;
+}
+
+// ------------------------------------------------------------------------------------------
+// Sharded replay: rank 0 folds the shards' keydir blocks (keydir_format.h) in
+// rank order — the replay order, since shards are contiguous file-id ranges.
+// ------------------------------------------------------------------------------------------
+cask_db* cask_keydir_new(void) {
+  cask_db* db = new (std::nothrow) cask_db();
+  if (db) db->merging = true;
+  return db;
+}
+
+int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
+  using namespace cask_kd;
+  if (!db || !db->merging || (bytes && !blk) || bytes < sizeof(ShardHeader)) return CASK_E_INVALID_ARG;
+  ShardHeader hd;
+  memcpy(&hd, blk, sizeof(hd));
+  const uint64_t rec_at = sizeof(ShardHeader), fst_at = rec_at + sizeof(ShardRec) * hd.nrec,
+                 key_at = fst_at + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
+  if (hd.magic != kMagic || hd.version != kVersion || hd.bytes > bytes || key_at + hd.key_bytes > hd.bytes)
+    return CASK_E_INVALID_ARG;
+  const ShardRec* rec = (const ShardRec*)(blk + rec_at);
+  const uint8_t* keys = blk + key_at;
+  auto stale = [&](uint32_t fid, uint32_t ksz) {  // Stats add + remove of a stale tombstone
+    cask_db::ShardTerms& t = db->terms[fid];
+    t.stale += 1;
+    t.stale_bytes += 18ull + ksz;
+  };
+  // 1. thresholds, against the keydir entering the shard
+  uint64_t ko = 0;
+  for (uint64_t i = 0; i < hd.nrec; ++i) {
+    const ShardRec& r = rec[i];
+    if (ko + r.ksz > hd.key_bytes) return CASK_E_INVALID_ARG;
+    if (r.kind == kCond) {
+      const cask_index_entry* e = db->index.get(keys + ko, r.ksz);
+      if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+    }
+    ko += r.ksz;
+  }
+  // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
+  ko = 0;
+  for (uint64_t i = 0; i < hd.nrec; ++i) {
+    const ShardRec& r = rec[i];
+    const uint8_t* k = keys + ko;
+    ko += r.ksz;
+    if (r.kind == kCond) continue;
+    if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
+      const cask_index_entry* e = db->index.get(k, r.ksz);
+      if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+    }
+    db->index.update_kd(k, r.ksz, r.file_id, r.pos, r.vsz, r.seq);
+  }
+  const ShardFileStat* fs = (const ShardFileStat*)(blk + fst_at);
+  for (uint32_t f = 0; f < hd.nfiles; ++f) {
+    cask_db::ShardTerms& t = db->terms[fs[f].file_id];
+    t.puts += fs[f].puts;
+    t.put_bytes += fs[f].put_bytes;
+    t.stale += fs[f].stale;
+    t.stale_bytes += fs[f].stale_bytes;
+    db->files.push_back(fs[f].file_id);
+  }
+  if (hd.max_seq_p1 && hd.max_seq_p1 - 1 > db->sequence) db->sequence = hd.max_seq_p1 - 1;
+  ++db->shards;
+  return CASK_OK;
+}
+
+// Stats after the last shard: per file, entries = puts + stale tombstones, dead = puts that are not
+// the key's final entry + stale tombstones (stats.rs:23-48 summed over Index::update's cases).
+int cask_keydir_finish(cask_db* db) {
+  if (!db || !db->merging) return CASK_E_INVALID_ARG;
+  std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> live;  // file -> (entries, bytes)
+  for (const auto& sl : db->index.slots)
+    if (sl.state == 1) {
+      auto& l = live[sl.e.file_id];
+      l.first += 1;
+      l.second += sl.e.entry_size;
+    }
+  db->index.stats.clear();
+  for (const auto& kv : db->terms) {
+    const cask_db::ShardTerms& t = kv.second;
+    if (!t.puts && !t.stale) continue;  // no Stats::add_entry for this file
+    const auto it = live.find(kv.first);
+    const uint64_t le = it == live.end() ? 0 : it->second.first, lb = it == live.end() ? 0 : it->second.second;
+    StatsEntry& e = db->index.stats[kv.first];
+    e.entries = t.puts + t.stale;
+    e.dead_entries = t.puts - le + t.stale;
+    e.dead_bytes = t.put_bytes - lb + t.stale_bytes;
+  }
+  std::sort(db->files.begin(), db->files.end());
+  db->files.erase(std::unique(db->files.begin(), db->files.end()), db->files.end());
+  db->file_seq = db->files.empty() ? 0u : db->files.back();
+  db->merging = false;
+  return CASK_OK;
+}
+
+// Cask::open over several GPUs of this process: contiguous file-id ranges, one per devices[] entry;
+// each range is read, scanned and reduced to its keydir block on its device (one host thread per
+// distinct device, its ranges one after another), and the blocks are folded here in range order.
+cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, const int* devices, int ndev,
+                            cask_open_error* err) {
+  set_err(err, CASK_OK);
+  if (!devices || ndev < 1) {
+    set_err(err, CASK_E_INVALID_ARG);
+    return nullptr;
+  }
+  auto t0 = std::chrono::steady_clock::now();
+  cask_db* db = open_log(path_c, opts_in, err);
+  if (!db) return nullptr;
+  const std::string path = db->path;
+  const size_t nf = db->files.size();
+  struct Shard {
+    size_t lo = 0, hi = 0;
+    std::vector<uint8_t> block;
+    cask_open_error e{};
+    double ms_read = 0, ms_scan = 0;
+  };
+  std::vector<Shard> sh((size_t)ndev);
+  for (int r = 0; r < ndev; ++r) {
+    sh[r].lo = nf * (size_t)r / (size_t)ndev;
+    sh[r].hi = nf * (size_t)(r + 1) / (size_t)ndev;
+  }
+  auto run_shard = [&](int r) {
+    Shard& s = sh[r];
+    if (s.lo == s.hi) return;
+    auto fail = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
+      s.e = cask_open_error{st, fid, pos, e, f};
+    };
+    auto tr = std::chrono::steady_clock::now();
+    const size_t n = s.hi - s.lo;
+    std::vector<std::vector<uint8_t>> data(n);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (!read_file(data_path(path, db->files[s.lo + i]), data[i])) return fail(CASK_E_IO, db->files[s.lo + i]);
+      total += (data[i].size() + 255) & ~255ull;
+    }
+    s.ms_read = ms_since(tr);
+    auto ts = std::chrono::steady_clock::now();
+    int st = CASK_OK;
+    cask_ctx* ctx = cask_ctx_create(devices[r], &st);
+    if (!ctx) return fail(st);
+    uint8_t* dbuf = nullptr;
+    void* drows = nullptr;
+    auto done = [&]() {
+      if (dbuf) (void)hipFree(dbuf);
+      if (drows) (void)hipFree(drows);
+      cask_ctx_destroy(ctx);
+    };
+    if (hipSetDevice(devices[r]) != hipSuccess || hipMalloc(&dbuf, total + 256) != hipSuccess) {
+      done();
+      return fail(CASK_E_DEVICE);
+    }
+    std::vector<cask_file_view> views(n);
+    uint64_t off = 0;
+    for (size_t i = 0; i < n; ++i) {
+      if (!data[i].empty() && hipMemcpy(dbuf + off, data[i].data(), data[i].size(), hipMemcpyHostToDevice) != hipSuccess) {
+        done();
+        return fail(CASK_E_DEVICE);
+      }
+      views[i] = cask_file_view{db->files[s.lo + i], CASK_VIEW_DEVICE, dbuf + off, data[i].size()};
+      off += (data[i].size() + 255) & ~255ull;
+    }
+    const uint64_t bound = cask_rows_bound(views.data(), (uint32_t)n);
+    const uint64_t a8 = (bound * 8 + 255) & ~255ull, a4 = (bound * 4 + 255) & ~255ull, a2 = (bound * 2 + 255) & ~255ull;
+    if (hipMalloc(&drows, 2 * a8 + a4 + a2 + bound + 256) != hipSuccess) {
+      done();
+      return fail(CASK_E_DEVICE);
+    }
+    uint8_t* rb = (uint8_t*)drows;
+    cask_rows rows{};
+    rows.capacity = bound;
+    rows.pos = (uint64_t*)rb;
+    rows.seq = (uint64_t*)(rb + a8);
+    rows.vsz = (uint32_t*)(rb + 2 * a8);
+    rows.ksz = (uint16_t*)(rb + 2 * a8 + a4);
+    rows.status = rb + 2 * a8 + a4 + a2;
+    std::vector<uint64_t> roff(n + 1);
+    cask_scan_error se{};
+    st = cask_scan_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
+    if (st != CASK_OK) {
+      done();
+      return fail(st);
+    }
+    if (se.kind) {  // the shard's first failing record: Cask::open's `?` (cask.rs:360,365)
+      done();
+      return fail(se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF, se.file_id, se.pos, se.expected, se.found);
+    }
+    const void* blk = nullptr;
+    uint64_t nb = 0;
+    st = cask_shard_keydir(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb);
+    if (st == CASK_OK) {
+      s.block.resize(nb);
+      if (hipMemcpy(s.block.data(), blk, nb, hipMemcpyDeviceToHost) != hipSuccess) st = CASK_E_DEVICE;
+    }
+    done();
+    if (st != CASK_OK) return fail(st);
+    s.ms_scan = ms_since(ts);
+  };
+  // one thread per distinct device; a device's shards run in order on its thread
+  std::vector<int> devs;
+  for (int r = 0; r < ndev; ++r)
+    if (std::find(devs.begin(), devs.end(), devices[r]) == devs.end()) devs.push_back(devices[r]);
+  parallel_for((unsigned)devs.size(), [&](unsigned t) {
+    for (int r = 0; r < ndev; ++r)
+      if (devices[r] == devs[t]) run_shard(r);
+  });
+  for (int r = 0; r < ndev; ++r)  // the first failure in replay order
+    if (sh[r].e.status != CASK_OK) {
+      if (err) *err = sh[r].e;
+      delete db;
+      return nullptr;
+    }
+  double rd = 0, sc = 0;
+  for (const Shard& s : sh) {
+    rd = std::max(rd, s.ms_read);
+    sc = std::max(sc, s.ms_scan);
+  }
+  auto tf = std::chrono::steady_clock::now();
+  db->merging = true;
+  for (int r = 0; r < ndev; ++r) {
+    if (sh[r].block.empty()) continue;
+    const int st = cask_keydir_merge(db, sh[r].block.data(), sh[r].block.size());
+    if (st != CASK_OK) {
+      set_err(err, st);
+      delete db;
+      return nullptr;
+    }
+  }
+  cask_keydir_finish(db);
+  db->timings[0] = rd;
+  db->timings[1] = sc;
+  db->timings[2] = 0;
+  db->timings[3] = ms_since(tf);
+  db->timings[4] = ms_since(t0);
+  return db;
 }
 
 void cask_db_close(cask_db* db) { delete db; }

@@ -1,0 +1,421 @@
+// Keydir rows of one shard for the multi-GPU replay (Cask::open, cask.rs:346-382 with
+// Index::update, cask.rs:60-90, folded per key).
+//
+// A rank scans a contiguous range of data files. Its rows are grouped by key on the device: a
+// 64-bit hash of the key bytes per row, a stable radix sort of (hash, row) and segments of equal
+// hash. Per key (one thread walks a segment):
+//  * keydir: only the suffix-strict maxima of the key's records in the shard — records with a
+//    larger sequence than every later record of the key — can decide the keydir after the whole
+//    replay, so only they are sent (kKept). With unique keys every row is one.
+//  * stats (stats.rs): Index::update adds one entry per put and removes each put that is not the
+//    key's final entry, so per file entries = puts and dead = puts - live (live from the final
+//    keydir, on rank 0): the shard sends per-file put counts and bytes. What is left are stale
+//    tombstones (an occupant with a larger sequence: add + remove of the tombstone itself). Whether a
+//    tombstone is stale depends on the key's entry when it arrives, a function of the entry
+//    entering the shard; composing the per-record maps (put a: S -> max(S, a); tombstone b:
+//    S -> S > b ? S : vacant) gives, per tombstone, "stale always" (counted here) or "stale iff
+//    the entering entry's sequence is > T" (kCond, resolved on rank 0 against its keydir).
+//  * keys whose hash collides with another key's are sent whole (kRaw) and folded record by record.
+// The result is exact, keydir and stats, whatever the distribution of keys over shards.
+#include <hipcub/hipcub.hpp>
+
+#include "device_util.h"
+#include "keydir_format.h"
+
+namespace cask_dev {
+
+using namespace cask_kd;
+
+struct KdArgs {
+  const FileDesc* files;
+  const uint32_t* file_ids;
+  const uint64_t* row_off;  // nfiles + 1: first dense row of each file
+  uint32_t nfiles;
+  uint32_t pad;
+  const uint64_t* pos;
+  const uint64_t* seq;
+  const uint32_t* vsz;
+  const uint16_t* ksz;
+  uint64_t n;
+  uint64_t* h;        // key hash per row
+  uint32_t* idx;      // row index
+  uint32_t* fidx;     // file index per row
+  uint64_t* hs;       // sorted hashes
+  uint32_t* is;       // rows in sorted order
+  uint8_t* head;      // sorted position starts a segment
+  uint8_t* kind;      // per sorted position: bit 0 kKept, bit 1 kCond, bit 2 kRaw
+  uint64_t* tval;     // per sorted position: kCond threshold + 1
+  uint64_t* ecnt;     // per sorted position: records emitted
+  uint64_t* ekey;     // ... and their key bytes
+  uint64_t* eoff;     // exclusive sums
+  uint64_t* koff;
+  uint32_t* seg;      // segment starts
+  uint32_t* nseg;
+  uint64_t* fstat;    // per file: puts, put_bytes, stale, stale_bytes
+  unsigned long long* tot;  // [0] max seq + 1, [1] records, [2] key bytes
+  uint8_t* out;       // the block
+  uint64_t rec_at, key_at;
+};
+
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+// 64-bit hash of a key (any bytes, any length up to 65535); only speed depends on its quality.
+__device__ __forceinline__ uint64_t key_hash(const uint8_t* k, uint32_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xD6E8FEB86659FD93ull);
+  uint32_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    __builtin_memcpy(&w, k + i, 8);
+    h = mix64(h ^ w);
+  }
+  uint64_t t = 0;
+  for (uint32_t j = 0; i + j < n; ++j) t |= (uint64_t)k[i + j] << (8 * j);
+  return mix64(h ^ t ^ 0xA0761D6478BD642Full);
+}
+
+__device__ __forceinline__ uint32_t row_file(const KdArgs& a, uint64_t d) {
+  uint32_t lo = 0, hi = a.nfiles;  // last f with row_off[f] <= d
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.row_off[mid] <= d) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ const uint8_t* row_key(const KdArgs& a, uint64_t d, uint32_t f) {
+  return a.files[f].data + a.pos[d] + 18;
+}
+
+// Hash every row's key; per-file put counts and bytes, max sequence.
+__global__ __launch_bounds__(256) void k_kd_hash(KdArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  unsigned long long mx = 0;
+  for (uint64_t d0 = blockIdx.x * 256ull; d0 < a.n; d0 += (uint64_t)gridDim.x * 256ull) {
+    const uint64_t d = d0 + threadIdx.x;
+    const bool in = d < a.n;
+    uint32_t f = 0;
+    unsigned long long put = 0, pb = 0;
+    if (in) {
+      f = row_file(a, d);
+      const uint32_t k = a.ksz[d], v = a.vsz[d];
+      a.h[d] = key_hash(row_key(a, d, f), k);
+      a.idx[d] = (uint32_t)d;
+      a.fidx[d] = f;
+      const unsigned long long s1 = (unsigned long long)a.seq[d] + 1;
+      mx = mx > s1 ? mx : s1;
+      if (v != 0xFFFFFFFFu) {
+        put = 1;
+        pb = 18ull + k + v;
+      }
+    }
+    // per-file sums: one atomic per wave when the wave's rows are all of one file (rows are in file order)
+    const uint32_t f0 = __shfl(f, 0, 64);
+    if (__all(!in || f == f0)) {
+      for (int o = 32; o; o >>= 1) {
+        put += __shfl_xor(put, o, 64);
+        pb += __shfl_xor(pb, o, 64);
+      }
+      if (lane == 0 && put) {
+        atomicAdd((unsigned long long*)&a.fstat[4ull * f0], put);
+        atomicAdd((unsigned long long*)&a.fstat[4ull * f0 + 1], pb);
+      }
+    } else if (put) {
+      atomicAdd((unsigned long long*)&a.fstat[4ull * f], put);
+      atomicAdd((unsigned long long*)&a.fstat[4ull * f + 1], pb);
+    }
+  }
+  for (int o = 32; o; o >>= 1) {
+    const unsigned long long y = __shfl_xor(mx, o, 64);
+    mx = mx > y ? mx : y;
+  }
+  if (lane == 0 && mx) atomicMax(&a.tot[0], mx);
+}
+
+__global__ __launch_bounds__(256) void k_kd_heads(KdArgs a) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256ull)
+    a.head[i] = (i == 0 || a.hs[i] != a.hs[i - 1]) ? 1 : 0;
+}
+
+__device__ __forceinline__ bool same_key(const KdArgs& a, uint64_t d0, uint32_t f0, uint64_t d1, uint32_t f1) {
+  const uint32_t k = a.ksz[d0];
+  if (a.ksz[d1] != k) return false;
+  const uint8_t* x = row_key(a, d0, f0);
+  const uint8_t* y = row_key(a, d1, f1);
+  for (uint32_t i = 0; i < k; ++i)
+    if (x[i] != y[i]) return false;
+  return true;
+}
+
+// One thread per segment (records of one key hash, in replay order): what each record emits.
+__global__ __launch_bounds__(256) void k_kd_segs(KdArgs a) {
+  const uint32_t ns = *a.nseg;
+  for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < ns; j += (uint64_t)gridDim.x * 256ull) {
+    const uint64_t s = a.seg[j], e = (j + 1 < ns) ? a.seg[j + 1] : a.n;
+    const uint64_t d0 = a.is[s];
+    const uint32_t f0 = a.fidx[d0];
+    bool raw = false;
+    for (uint64_t i = s + 1; i < e && !raw; ++i) raw = !same_key(a, d0, f0, a.is[i], a.fidx[a.is[i]]);
+    if (raw) {  // a 64-bit collision between different keys: every record, folded one by one
+      for (uint64_t i = s; i < e; ++i) {
+        const uint64_t d = a.is[i];
+        a.kind[i] = 4;
+        a.ecnt[i] = 1;
+        a.ekey[i] = a.ksz[d];
+      }
+      continue;
+    }
+    // keydir: suffix-strict maxima (sequence + 1 > every later record's)
+    unsigned long long later = 0;
+    for (uint64_t i = e; i-- > s;) {
+      const unsigned long long q = (unsigned long long)a.seq[a.is[i]] + 1;
+      a.kind[i] = q > later ? 1 : 0;
+      later = later > q ? later : q;
+    }
+    // stats: the key's entry after the records so far, as a function of the entry x entering the
+    // shard (sequence + 1, 0 = vacant): x > L ? max(x, A) : C
+    unsigned long long L = 0, A = 0, C = 0;
+    for (uint64_t i = s; i < e; ++i) {
+      const uint64_t d = a.is[i];
+      const unsigned long long q = (unsigned long long)a.seq[d] + 1;
+      uint8_t kd = a.kind[i];
+      if (a.vsz[d] != 0xFFFFFFFFu) {
+        A = A > q ? A : q;
+        C = C > q ? C : q;
+      } else {
+        if (C > q) {  // stale whatever entered the shard
+          const uint32_t f = a.fidx[d];
+          atomicAdd((unsigned long long*)&a.fstat[4ull * f + 2], 1ull);
+          atomicAdd((unsigned long long*)&a.fstat[4ull * f + 3], 18ull + a.ksz[d]);
+        } else {      // stale iff x > T
+          kd |= 2;
+          a.tval[i] = A > q ? L : (L > q ? L : q);
+        }
+        if (A > q) C = C > q ? C : 0;
+        else {
+          L = L > q ? L : q;
+          C = 0;
+        }
+      }
+      a.kind[i] = kd;
+      const uint32_t m = (kd & 1) + ((kd >> 1) & 1);
+      a.ecnt[i] = m;
+      a.ekey[i] = (uint64_t)m * a.ksz[d];
+    }
+  }
+}
+
+__global__ void k_kd_totals(KdArgs a) {
+  if (threadIdx.x || blockIdx.x || !a.n) return;
+  a.tot[1] = a.eoff[a.n - 1] + a.ecnt[a.n - 1];
+  a.tot[2] = a.koff[a.n - 1] + a.ekey[a.n - 1];
+}
+
+__device__ __forceinline__ void kd_emit(const KdArgs& a, uint64_t r, uint64_t ko, uint64_t d, uint32_t f, uint8_t kind,
+                                        uint64_t seq) {
+  ShardRec* rec = (ShardRec*)(a.out + a.rec_at) + r;
+  ShardRec x;
+  x.pos = a.pos[d];
+  x.seq = seq;
+  x.file_id = a.file_ids[f];
+  x.vsz = a.vsz[d];
+  x.ksz = a.ksz[d];
+  x.kind = kind;
+  x.pad0 = 0;
+  x.pad1 = 0;
+  *rec = x;
+  const uint8_t* k = row_key(a, d, f);
+  uint8_t* o = a.out + a.key_at + ko;
+  for (uint32_t i = 0; i < x.ksz; ++i) o[i] = k[i];
+}
+
+__global__ __launch_bounds__(256) void k_kd_write(KdArgs a) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256ull) {
+    const uint8_t kd = a.kind[i];
+    if (!kd) continue;
+    const uint64_t d = a.is[i];
+    const uint32_t f = a.fidx[d];
+    uint64_t r = a.eoff[i], ko = a.koff[i];
+    if (kd & 4) {
+      kd_emit(a, r, ko, d, f, kRaw, a.seq[d]);
+      continue;
+    }
+    if (kd & 2) {  // the threshold first: rank 0 resolves it before it folds the shard's rows
+      kd_emit(a, r, ko, d, f, kCond, a.tval[i]);
+      ++r;
+      ko += a.ksz[d];
+    }
+    if (kd & 1) kd_emit(a, r, ko, d, f, kKept, a.seq[d]);
+  }
+}
+
+// Header and per-file stats into the block.
+__global__ void k_kd_header(KdArgs a, uint64_t rows_in, uint64_t fstat_at, uint64_t bytes) {
+  if (blockIdx.x) return;
+  if (threadIdx.x == 0) {
+    ShardHeader hd{};
+    hd.magic = kMagic;
+    hd.version = kVersion;
+    hd.nrec = a.n ? a.tot[1] : 0;
+    hd.key_bytes = a.n ? a.tot[2] : 0;
+    hd.nfiles = a.nfiles;
+    hd.max_seq_p1 = a.tot[0];
+    hd.rows_in = rows_in;
+    hd.bytes = bytes;
+    *(ShardHeader*)a.out = hd;
+  }
+  for (uint32_t f = threadIdx.x; f < a.nfiles; f += blockDim.x) {
+    ShardFileStat st{};
+    st.file_id = a.file_ids[f];
+    st.puts = a.fstat[4ull * f];
+    st.put_bytes = a.fstat[4ull * f + 1];
+    st.stale = a.fstat[4ull * f + 2];
+    st.stale_bytes = a.fstat[4ull * f + 3];
+    ((ShardFileStat*)(a.out + fstat_at))[f] = st;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Host side of the pipeline (called from scan_runtime.cpp with the context's scratch).
+// ------------------------------------------------------------------------------------------
+static inline hipStream_t S(void* s) { return (hipStream_t)s; }
+static inline uint64_t al(uint64_t x) { return (x + 255) & ~255ull; }
+
+struct KdScratch {
+  void* p = nullptr;
+  size_t cap = 0;
+  void* out = nullptr;
+  size_t out_cap = 0;
+  ~KdScratch() {
+    if (p) (void)hipFree(p);
+    if (out) (void)hipFree(out);
+  }
+  bool ensure(size_t b) {
+    if (b <= cap) return true;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, b + b / 4 + 256) != hipSuccess) return false;
+    cap = b + b / 4 + 256;
+    return true;
+  }
+  bool ensure_out(size_t b) {
+    if (b <= out_cap) return true;
+    if (out) (void)hipFree(out);
+    out = nullptr;
+    out_cap = 0;
+    if (hipMalloc(&out, b + b / 8 + 256) != hipSuccess) return false;
+    out_cap = b + b / 8 + 256;
+    return true;
+  }
+};
+
+void* kd_scratch_create() { return new (std::nothrow) KdScratch(); }
+void kd_scratch_destroy(void* s) { delete (KdScratch*)s; }
+
+// Returns 0, or a negative cask_status; *out / *bytes: the block in device memory (owned by the
+// scratch, valid until the next call).
+int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids_host, uint32_t nfiles,
+             const uint64_t* row_off_host, const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz,
+             const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes) {
+  KdScratch& S_ = *(KdScratch*)scratch;
+  hipStream_t st = S(stream);
+  if (n >= (1ull << 32)) return -10;  // row indices are 32-bit per shard
+  // temp storage sizes of the hipCUB calls
+  size_t t_sort = 0, t_sel = 0, t_scan = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
+                                          (uint32_t*)nullptr, (int)std::max<uint64_t>(n, 1), 0, 64, st) != hipSuccess ||
+      hipcub::DeviceSelect::Flagged(nullptr, t_sel, hipcub::CountingInputIterator<uint32_t>(0), (uint8_t*)nullptr,
+                                    (uint32_t*)nullptr, (uint32_t*)nullptr, (int)std::max<uint64_t>(n, 1), st) != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                       (int)std::max<uint64_t>(n, 1), st) != hipSuccess)
+    return -11;
+  const size_t tmp = std::max(t_sort, std::max(t_sel, t_scan));
+  // layout of the scratch
+  uint64_t o = 0;
+  auto take = [&](uint64_t b) { const uint64_t r = o; o = al(o + b); return r; };
+  const uint64_t n1 = n ? n : 1;
+  const uint64_t o_fd = take(sizeof(FileDesc) * (nfiles + 1)), o_files = take(4ull * (nfiles + 1)), o_rowoff = take(8ull * (nfiles + 1)), o_h = take(8 * n1),
+                 o_idx = take(4 * n1), o_fidx = take(4 * n1), o_hs = take(8 * n1), o_is = take(4 * n1),
+                 o_head = take(n1), o_kind = take(n1), o_tval = take(8 * n1), o_ecnt = take(8 * n1),
+                 o_ekey = take(8 * n1), o_eoff = take(8 * n1), o_koff = take(8 * n1), o_seg = take(4 * n1),
+                 o_nseg = take(8), o_fstat = take(32ull * (nfiles + 1)), o_tot = take(64), o_tmp = take(tmp);
+  if (!S_.ensure(o)) return -13;
+  uint8_t* b = (uint8_t*)S_.p;
+  KdArgs a{};
+  a.files = (const FileDesc*)(b + o_fd);
+  a.file_ids = (const uint32_t*)(b + o_files);
+  a.row_off = (const uint64_t*)(b + o_rowoff);
+  a.nfiles = nfiles;
+  a.pos = pos;
+  a.seq = seq;
+  a.vsz = vsz;
+  a.ksz = ksz;
+  a.n = n;
+  a.h = (uint64_t*)(b + o_h);
+  a.idx = (uint32_t*)(b + o_idx);
+  a.fidx = (uint32_t*)(b + o_fidx);
+  a.hs = (uint64_t*)(b + o_hs);
+  a.is = (uint32_t*)(b + o_is);
+  a.head = b + o_head;
+  a.kind = b + o_kind;
+  a.tval = (uint64_t*)(b + o_tval);
+  a.ecnt = (uint64_t*)(b + o_ecnt);
+  a.ekey = (uint64_t*)(b + o_ekey);
+  a.eoff = (uint64_t*)(b + o_eoff);
+  a.koff = (uint64_t*)(b + o_koff);
+  a.seg = (uint32_t*)(b + o_seg);
+  a.nseg = (uint32_t*)(b + o_nseg);
+  a.fstat = (uint64_t*)(b + o_fstat);
+  a.tot = (unsigned long long*)(b + o_tot);
+  void* tmpp = b + o_tmp;
+  bool ok = true;
+  auto H = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+  H(hipMemcpyAsync((void*)a.files, files_host, sizeof(FileDesc) * nfiles, hipMemcpyHostToDevice, st));
+  H(hipMemcpyAsync((void*)a.file_ids, file_ids_host, 4ull * nfiles, hipMemcpyHostToDevice, st));
+  H(hipMemcpyAsync((void*)a.row_off, row_off_host, 8ull * (nfiles + 1), hipMemcpyHostToDevice, st));
+  H(hipMemsetAsync(a.fstat, 0, 32ull * (nfiles + 1), st));
+  H(hipMemsetAsync(a.tot, 0, 64, st));
+  const int cus = device_cus();
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)cus * 16);
+  if (n) {
+    hipLaunchKernelGGL(k_kd_hash, dim3(grid), dim3(256), 0, st, a);
+    size_t tb = tmp;
+    H(hipcub::DeviceRadixSort::SortPairs(tmpp, tb, a.h, a.hs, a.idx, a.is, (int)n, 0, 64, st));
+    hipLaunchKernelGGL(k_kd_heads, dim3(grid), dim3(256), 0, st, a);
+    tb = tmp;
+    H(hipcub::DeviceSelect::Flagged(tmpp, tb, hipcub::CountingInputIterator<uint32_t>(0), a.head, a.seg, a.nseg,
+                                     (int)n, st));
+    hipLaunchKernelGGL(k_kd_segs, dim3(grid), dim3(256), 0, st, a);
+    tb = tmp;
+    H(hipcub::DeviceScan::ExclusiveSum(tmpp, tb, a.ecnt, a.eoff, (int)n, st));
+    tb = tmp;
+    H(hipcub::DeviceScan::ExclusiveSum(tmpp, tb, a.ekey, a.koff, (int)n, st));
+    hipLaunchKernelGGL(k_kd_totals, dim3(1), dim3(64), 0, st, a);
+  }
+  unsigned long long tot[3] = {0, 0, 0};
+  H(hipMemcpyAsync(tot, a.tot, sizeof(tot), hipMemcpyDeviceToHost, st));
+  H(hipStreamSynchronize(st));
+  H(hipGetLastError());
+  if (!ok) return -11;
+  const uint64_t nrec = n ? tot[1] : 0, kb = n ? tot[2] : 0;
+  a.rec_at = sizeof(ShardHeader);
+  const uint64_t fstat_at = a.rec_at + sizeof(ShardRec) * nrec;
+  a.key_at = fstat_at + sizeof(ShardFileStat) * nfiles;
+  const uint64_t total = (a.key_at + kb + 7) & ~7ull;
+  if (!S_.ensure_out(total)) return -13;
+  a.out = (uint8_t*)S_.out;
+  if (n && nrec) hipLaunchKernelGGL(k_kd_write, dim3(grid), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_kd_header, dim3(1), dim3(256), 0, st, a, n, fstat_at, total);
+  H(hipStreamSynchronize(st));
+  H(hipGetLastError());
+  if (!ok) return -11;
+  *out = S_.out;
+  *bytes = total;
+  return 0;
+}
+
+}  // namespace cask_dev

@@ -178,6 +178,12 @@ void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);
 constexpr uint32_t kFinTile = 256;  // chunks per k_finish tile (one per thread)
 void launch_finish(const ScanArgs& a, void* stream);
 void launch_err_dense(const ScanArgs& a, uint32_t fi, uint64_t row, uint32_t* out, void* stream);
+// k_keydir.hip: a shard's keydir block (keydir_format.h) from its dense rows
+void* kd_scratch_create();
+void kd_scratch_destroy(void* s);
+int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids_host, uint32_t nfiles,
+             const uint64_t* row_off_host, const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz,
+             const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

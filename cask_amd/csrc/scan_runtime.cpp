@@ -109,6 +109,7 @@ struct cask_ctx {
   int geo = 0;       // k_scan_chunks geometry (CASK_SCAN_GEOMETRY overrides the default)
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
+  void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
   int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
@@ -120,6 +121,7 @@ struct cask_ctx {
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (evw) (void)hipEventDestroy(evw);
+    if (kd) kd_scratch_destroy(kd);
     if (own) (void)hipStreamDestroy(own);
   }
 };
@@ -711,6 +713,45 @@ extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t
   }
   H(hipStreamSynchronize(st));
   return ok ? CASK_OK : CASK_E_DEVICE;
+}
+
+extern "C" int cask_copy(cask_ctx* c, void* dst, const void* src, uint64_t bytes) {
+  if (!c || (bytes && (!dst || !src))) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (bytes && (hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->stream) != hipSuccess ||
+                hipStreamSynchronize(c->stream) != hipSuccess))
+    return CASK_E_DEVICE;
+  return CASK_OK;
+}
+
+extern "C" int cask_shard_keydir(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
+                                 const uint64_t* file_row_offset, const void** block, uint64_t* bytes) {
+  if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
+  if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz)) return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
+  if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+  std::vector<FileDesc> fd(nfiles + 1);
+  std::vector<uint32_t> ids(nfiles + 1, 0);
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
+    ids[i] = files[i].file_id;
+  }
+  void* out = nullptr;
+  uint64_t nb = 0;
+  const int rc = kd_build(c->kd, fd.data(), ids.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz,
+                          rows->ksz, rows->count, c->stream, &out, &nb);
+  if (rc) {
+    snprintf(c->last_error, sizeof(c->last_error), "cask_shard_keydir: %s", rc == CASK_E_NOMEM ? "out of memory" : "device");
+    return rc;
+  }
+  *block = out;
+  *bytes = nb;
+  return CASK_OK;
 }
 
 extern "C" int cask_encode_synthetic_device(cask_ctx* c, uint64_t nrec, const uint64_t* off, const uint64_t* seq,

@@ -1,15 +1,17 @@
-"""Multi-GPU layout of the scan: one process per GPU, data files sharded in contiguous file-id
-ranges (so the per-key fold order is rank order, then file id, then position — SURVEY §8e), no
-collective on the scan itself. The keydir rows meet on rank 0 through point-to-point transfers
-(RCCL over xGMI on the GPU; gloo in the CPU tests), and the replay's max sequence
-(cask.rs:350-352) is an all-reduce(max).
+"""Multi-GPU layout of the replay: one process per GPU, data files sharded in
+contiguous file-id ranges, so that rank order, then file id, then position is the reference's
+replay order (cask.rs:348). The scan needs no collective. Each rank reduces its rows to a keydir
+block on its GPU (cask_amd.keydir.shard_keydir: the records that can decide the keydir, the
+tombstones whose stale count depends on the ranks before, per-file put counts, key bytes); the
+blocks meet on rank 0 through point-to-point transfers — RCCL over xGMI on the GPUs (torch's
+"nccl" backend), gloo in the CPU tests — and rank 0 folds them in rank order
+(cask_amd.keydir.KeydirFold). The replay's max sequence (cask.rs:350-352) travels in the blocks;
+allreduce_max_seq gives it to every rank.
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
-
-ROW_FIELDS = ("pos", "seq", "vsz", "ksz", "status")
 
 
 def shard_files(file_ids, world: int, rank: int):
@@ -27,40 +29,31 @@ def allreduce_max_seq(local_max: int, device) -> int:
     return int(t.item())
 
 
-def gather_rows(rows: dict, count: int, dst: int = 0, file_id=None):
-    """Gather every rank's first `count` rows (SoA tensors) to `dst`, in rank order.
-
-    Returns the list of per-rank row dicts on `dst` (None elsewhere). Row blocks are
-    variable-sized: counts travel first (all_gather), then one send/recv per field per rank.
-    `file_id` (optional int32 tensor, same length) travels along."""
+def gather_blocks(block: torch.Tensor, dst: int = 0):
+    """Gather every rank's keydir block (a uint8 tensor of any length, on the rank's device for
+    RCCL, on the CPU for gloo) to `dst`, one message per rank. Returns the blocks in rank order on
+    `dst`, None elsewhere."""
     rank, world = dist.get_rank(), dist.get_world_size()
-    dev = rows["pos"].device
-    cnt = torch.tensor([int(count)], dtype=torch.int64, device=dev)
-    counts = [torch.zeros_like(cnt) for _ in range(world)]
-    dist.all_gather(counts, cnt)
-    counts = [int(c.item()) for c in counts]
-    fields = list(ROW_FIELDS) + (["file_id"] if file_id is not None else [])
-    src = dict(rows)
-    if file_id is not None:
-        src["file_id"] = file_id
+    dev = block.device
+    n = torch.tensor([block.numel()], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
     if rank == dst:
-        out = []
-        ops = []
+        out, ops = [], []
         for r in range(world):
             if r == dst:
-                out.append({f: src[f][:counts[r]] for f in fields})
+                out.append(block)
                 continue
-            d = {f: torch.empty(counts[r], dtype=src[f].dtype, device=dev) for f in fields}
-            out.append(d)
-            for f in fields:
-                if counts[r]:
-                    ops.append(dist.P2POp(dist.irecv, d[f], r))
+            t = torch.empty(sizes[r], dtype=torch.uint8, device=dev)
+            out.append(t)
+            if sizes[r]:
+                ops.append(dist.P2POp(dist.irecv, t, r))
         if ops:
             for w in dist.batch_isend_irecv(ops):
                 w.wait()
         return out
-    ops = [dist.P2POp(dist.isend, src[f][:count].contiguous(), dst) for f in fields if count]
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
+    if block.numel():
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, block.contiguous(), dst)]):
             w.wait()
     return None

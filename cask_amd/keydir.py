@@ -1,0 +1,88 @@
+"""Multi-GPU replay: a shard's keydir block from its device rows, and rank 0's fold
+of the blocks in rank order. The block format and what it carries are described in
+include/cask_scan.h and cask_amd/csrc/keydir_format.h; all work is in libcask_scan.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+from .cask import Cask, CaskOptions
+from .errors import raise_status
+
+
+def shard_keydir(ctx, files, rows: dict, count: int, file_row_offset):
+    """The keydir block of the files one rank scanned: `files` [(file_id, uint8 CUDA tensor)] as
+    passed to ctx.scan_device, its rows dict and ScanResult.count / file_row_offset (every row Ok).
+    Returns a uint8 CUDA tensor (a copy: the context's buffer is reused by its next call)."""
+    import torch
+    n = len(files)
+    views = (L.FileView * max(n, 1))()
+    for i, (fid, t) in enumerate(files):
+        views[i].file_id = int(fid)
+        views[i].flags = L.VIEW_DEVICE
+        views[i].data = t.data_ptr() if t.numel() else None
+        views[i].len = t.numel()
+    r = L.Rows()
+    r.capacity = rows["pos"].numel()
+    r.count = int(count)
+    r.pos, r.seq = rows["pos"].data_ptr(), rows["seq"].data_ptr()
+    r.vsz, r.ksz, r.status = rows["vsz"].data_ptr(), rows["ksz"].data_ptr(), rows["status"].data_ptr()
+    off = (C.c_uint64 * (n + 1))(*[int(x) for x in file_row_offset])
+    blk, nb = C.c_void_p(), C.c_uint64()
+    ctx._inputs_ready()
+    rc = ctx.lib.cask_shard_keydir(ctx._h, views, n, C.byref(r), off, C.byref(blk), C.byref(nb))
+    raise_status(rc, what=f"cask_shard_keydir: {ctx.last_error()}")
+    dev = torch.device("cuda", ctx.device)
+    out = torch.empty(int(nb.value), dtype=torch.uint8, device=dev)
+    ctx._inputs_ready()  # the allocation is ordered on torch's stream
+    raise_status(ctx.lib.cask_copy(ctx._h, C.c_void_p(out.data_ptr()), blk, nb.value), what="cask_copy")
+    return out
+
+
+class KeydirFold:
+    """Rank 0's fold (cask_keydir_new / _merge / _finish): merge the blocks in rank order, then
+    finish() returns a Cask handle with the keydir, stats and sequence of the whole replay."""
+
+    def __init__(self):
+        self.lib = L.lib()
+        self._h = self.lib.cask_keydir_new()
+        if not self._h:
+            raise MemoryError("cask_keydir_new")
+
+    def merge(self, block):
+        """block: bytes, a numpy uint8 array or a CPU uint8 tensor."""
+        if hasattr(block, "numpy"):
+            block = block.numpy()
+        a = np.ascontiguousarray(np.frombuffer(block, np.uint8) if isinstance(block, (bytes, bytearray)) else block,
+                                 dtype=np.uint8)
+        raise_status(self.lib.cask_keydir_merge(self._h, a.ctypes.data, a.size), what="cask_keydir_merge")
+
+    def finish(self) -> Cask:
+        raise_status(self.lib.cask_keydir_finish(self._h), what="cask_keydir_finish")
+        h, self._h = self._h, None
+        return Cask(h, "")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self.lib.cask_db_close(self._h)
+
+
+def open_multi(path: str, devices, options: CaskOptions | None = None) -> Cask:
+    """cask_db_open_multi: Cask::open with the data files split over `devices` (GPU ordinals of
+    this process, repeats allowed)."""
+    o = options or CaskOptions()
+    lib = L.lib()
+    opts = L.Options()
+    lib.cask_options_default(C.byref(opts))
+    opts.create = 1 if o._create else 0
+    opts.write_hints = 0
+    opts.max_file_size = o._max_file_size
+    devs = (C.c_int * len(devices))(*[int(d) for d in devices])
+    err = L.OpenError()
+    h = lib.cask_db_open_multi(path.encode(), C.byref(opts), devs, len(devices), C.byref(err))
+    if not h:
+        raise_status(err.status, err.file_id, err.pos, err.expected, err.found, what=path)
+    return Cask(h, path, o)

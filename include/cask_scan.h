@@ -286,6 +286,39 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files, uint64_t nfiles, c
 int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts, cask_compact_result* res,
                         cask_open_error* err);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Multi-GPU replay. Data files shard in contiguous file-id ranges; each shard's   */
+/* rows become a keydir block on its GPU; rank 0 folds the blocks in rank order. The block format */
+/* is cask_amd/csrc/keydir_format.h: per key only the records that can decide the final keydir    */
+/* (the suffix-strict maxima of the key's sequences within the shard), each tombstone whose stale */
+/* count depends on the shards before it (with its threshold), per-file put counts, key bytes.    */
+/* Keydir and Stats come out exactly as the single-process Cask::open (cask.rs:346-382, 60-90).   */
+/* ------------------------------------------------------------------------------------------ */
+/* A shard's keydir block from its device rows (cask_scan_device on `files`, every row Ok;
+ * file_row_offset as that call returned it). *block points to device memory owned by the context,
+ * valid until its next call; *bytes is its size. */
+int cask_shard_keydir(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
+                      const uint64_t* file_row_offset, const void** block, uint64_t* bytes);
+
+/* Rank 0's fold: a keydir handle with no files, the blocks merged in rank order (host memory),
+ * then finished (Stats). The result is a cask_db: cask_db_export / _stats / _current_sequence /
+ * _len / _files / _get_entry read it; cask_db_close frees it. */
+/* Copy `bytes` between any two memories (device or host) on the context's stream, synchronously:
+ * e.g. a keydir block out of the context's buffer. */
+int cask_copy(cask_ctx* ctx, void* dst, const void* src, uint64_t bytes);
+
+cask_db* cask_keydir_new(void);
+int cask_keydir_merge(cask_db* db, const uint8_t* block, uint64_t bytes);
+int cask_keydir_finish(cask_db* db);
+
+/* Cask::open over several GPUs of this process (replaces cask.rs:346-382 like cask_db_open): the
+ * data files are split into contiguous ranges, one per entry of `devices` (a device may appear more
+ * than once: its shards run one after another); each range is read, scanned and reduced to its
+ * keydir block on its device, the blocks come back to the host and are folded in order. Every data
+ * file is scanned: hint files are neither read nor written on this path (configs[4]). */
+cask_db* cask_db_open_multi(const char* path, const cask_options* opts, const int* devices, int ndevices,
+                            cask_open_error* err);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,10 +1,11 @@
-"""Multi-rank path on CPU (gloo, world_size 2): file sharding, the max-sequence all-reduce and the
-rank-ordered row gather that feeds the keydir fold. Rows come from the CPU oracle
-here (no GPU in this container); on the GPU box the same functions run over RCCL with rows from
-the HIP scan (bench.py --gpus N).
+"""Multi-rank path on CPU (gloo, world_size 2): file sharding, the max-sequence all-reduce, the
+gather of the ranks' keydir blocks and rank 0's native fold of them. Blocks come from
+the oracle's restatement here (no GPU in this container; tests/test_scan_gpu.py checks that the
+device builds the same bytes); on the GPU box the same functions run over RCCL (bench.py --gpus N).
 
-The gathered, rank-ordered fold must equal a single-process replay of the same directory
-(cask.rs:346-382), including stale tombstones whose stats depend on the global fold order.
+Rank 0 folds only what it received — no data file is read there — and the result must equal a
+single-process replay of the same directory (cask.rs:346-382), including stale tombstones whose
+stats depend on the global fold order.
 """
 import json
 import os
@@ -47,52 +48,41 @@ def _make_db(path):
 
 
 def _worker(rank, world, port, path, out):
+    """Each rank scans its own files (oracle rows: no GPU here), builds its keydir block, and the
+    blocks meet on rank 0, which folds them with the native fold — it reads no data file."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import numpy as np
     import torch.distributed as dist
+    import cask_shard as S
     import oracle_ffi as O
-    from cask_amd.distributed import allreduce_max_seq, gather_rows, shard_files as shard
+    from cask_amd.distributed import allreduce_max_seq, gather_blocks, shard_files as shard
+    from cask_amd.keydir import KeydirFold
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         mine = shard(R.find_data_files(path), world, rank)
-        cols = {f: [] for f in ("pos", "seq", "vsz", "ksz", "status")}
-        fids = []
-        local_max = 0
+        rows, local_max = [], 0
         for fid in mine:
             with open(R.data_file_path(path, fid), "rb") as f:
                 buf = f.read()
-            rows = O.scan(buf)
-            cols["pos"] += [int(x) for x in rows["pos"]]
-            cols["seq"] += [int(x) for x in rows["seq"]]
-            cols["vsz"] += [int(x) for x in rows["vsz_raw"]]
-            cols["ksz"] += [int(x) for x in rows["ksz"]]
-            cols["status"] += [int(x) for x in rows["status"]]
-            fids += [fid] * len(rows)
-            local_max = max([local_max] + [int(x) for x in rows["seq"]])
-        t = {"pos": torch.tensor(cols["pos"], dtype=torch.int64),
-             "seq": torch.tensor(cols["seq"], dtype=torch.int64),
-             "vsz": torch.tensor(cols["vsz"], dtype=torch.int64).to(torch.int32),
-             "ksz": torch.tensor(cols["ksz"], dtype=torch.int32).to(torch.int16),
-             "status": torch.tensor(cols["status"], dtype=torch.uint8)}
+            for r in O.scan(buf):
+                assert int(r["status"]) == 0
+                p, k = int(r["pos"]), int(r["ksz"])
+                rows.append((fid, R.Row(pos=p, seq=int(r["seq"]), ksz=k, vsz_raw=int(r["vsz_raw"]),
+                                        key=buf[p + 18:p + 18 + k])))
+                local_max = max(local_max, int(r["seq"]))
+        block = torch.from_numpy(np.frombuffer(S.shard_block(mine, rows), np.uint8).copy())
         gmax = allreduce_max_seq(local_max, torch.device("cpu"))
-        got = gather_rows(t, len(fids), dst=0, file_id=torch.tensor(fids, dtype=torch.int32))
+        got = gather_blocks(block, dst=0)
         if rank == 0:
-            index = R.Index()
-            bufs = {}
-            for blk in got:
-                for i in range(blk["pos"].numel()):
-                    fid = int(blk["file_id"][i])
-                    if fid not in bufs:
-                        with open(R.data_file_path(path, fid), "rb") as f:
-                            bufs[fid] = f.read()
-                    p, k = int(blk["pos"][i]), int(blk["ksz"][i]) & 0xFFFF
-                    row = R.Row(pos=p, seq=int(blk["seq"][i]), ksz=k, vsz_raw=int(blk["vsz"][i]) & 0xFFFFFFFF,
-                                status=int(blk["status"][i]), key=bufs[fid][p + 18:p + 18 + k])
-                    assert row.status == R.ROW_OK
-                    index.update(row, fid)
-            res = {"max_seq": gmax, "counts": [int(b["pos"].numel()) for b in got],
+            fold = KeydirFold()
+            for b in got:
+                fold.merge(b)
+            db = fold.finish()
+            res = {"max_seq": gmax, "current_sequence": db.current_sequence, "sizes": [int(b.numel()) for b in got],
                    "keydir": sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence]
-                                    for k, e in index.map.items()),
-                   "stats": sorted([f, *s] for f, s in index.stats.map.items())}
+                                    for k, e in db.index().items()),
+                   "stats": sorted([f, *s] for f, s in db.stats().items())}
+            db.close()
             with open(out, "w") as f:
                 json.dump(res, f)
     finally:
@@ -120,9 +110,8 @@ def test_gloo_world2_gather_fold_matches_single_process(tmp_path):
     with open(out) as f:
         got = json.load(f)
     assert got["max_seq"] == want.sequence
-    assert sum(got["counts"]) == sum(len(R.scan_entries(open(R.data_file_path(path, fid), "rb").read()))
-                                     for fid in want.files)
-    assert got["counts"][1] > 0 and got["counts"][0] > 0
+    assert got["current_sequence"] == want.current_sequence
+    assert got["sizes"][1] > 64 and got["sizes"][0] > 64
     assert got["keydir"] == sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence]
                                    for k, e in want.index.map.items())
     assert got["stats"] == sorted([f, *s] for f, s in want.index.stats.map.items())

@@ -1,0 +1,153 @@
+"""The sharded replay on the GPU: the device's keydir blocks against the restatement
+(byte for byte), two shards scanned and reduced in one process on cuda:0 and folded in rank order
+against the single-process Cask::open replay (cask.rs:346-382), and cask_db_open_multi. Needs an MI355X.
+"""
+import os
+import random
+import shutil
+
+import numpy as np
+import pytest
+
+import cask_ref as R
+import cask_shard as S
+
+pytestmark = pytest.mark.gpu
+
+
+def _make_db(path, seed, nfiles=6, nrec=3000, nkeys=400, tomb_p=0.12, back_p=0.1, max_vsz=300):
+    """Data files of overwrites, deletes and out-of-order sequences (stale records)."""
+    rng = random.Random(seed)
+    keys = [rng.randbytes(rng.randrange(0, 24)) for _ in range(nkeys)]
+    seq = 1
+    os.makedirs(path, exist_ok=True)
+    for fid in range(1, nfiles + 1):
+        recs = []
+        for _ in range(nrec):
+            k = rng.choice(keys)
+            s = seq if rng.random() > back_p else max(0, seq - rng.randrange(1, 5000))
+            seq += 1
+            if rng.random() < tomb_p:
+                recs.append(R.entry_deleted(s, k).write_bytes())
+            else:
+                recs.append(R.entry_new(s, k, rng.randbytes(rng.randrange(0, max_vsz))).write_bytes())
+        with open(R.data_file_path(path, fid), "wb") as f:
+            f.write(b"".join(recs))
+
+
+def _files(path):
+    out = []
+    for fid in R.find_data_files(path):
+        with open(R.data_file_path(path, fid), "rb") as f:
+            out.append((fid, f.read()))
+    return out
+
+
+def _device_block(ctx, part):
+    import torch
+    from cask_amd.keydir import shard_keydir
+    tens = [(fid, torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()) for fid, b in part]
+    res = ctx.scan_device(tens)
+    assert res.error is None
+    return shard_keydir(ctx, tens, {"pos": res.pos, "seq": res.seq, "vsz": res.vsz, "ksz": res.ksz,
+                                    "status": res.status}, res.count, res.file_row_offset).cpu().numpy().tobytes()
+
+
+def _oracle_block(part):
+    rows = []
+    for fid, b in part:
+        for r in R.scan_entries(b):
+            assert r.status == R.ROW_OK
+            rows.append((fid, r))
+    return S.shard_block([fid for fid, _ in part], rows)
+
+
+def _want(path):
+    ref = str(path) + "_ref"
+    shutil.copytree(path, ref)
+    rep = R.replay(ref, write_hints=False)
+    assert rep.error is None
+    kd = sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence] for k, e in rep.index.map.items())
+    return kd, sorted([f, *s] for f, s in rep.index.stats.map.items()), rep.current_sequence
+
+
+def _got(db):
+    return (sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence] for k, e in db.index().items()),
+            sorted([f, *s] for f, s in db.stats().items()), db.current_sequence)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_device_block_equals_restatement(gpu_ctx, tmp_path, seed):
+    path = str(tmp_path / "db")
+    _make_db(path, seed, nfiles=4, nrec=2500, nkeys=300 if seed == 1 else 5000)
+    files = _files(path)
+    for part in (files, files[:1], files[1:3]):
+        assert _device_block(gpu_ctx, part) == _oracle_block(part)
+
+
+def test_two_shards_in_process_fold(gpu_ctx, tmp_path):
+    """Two shards' HIP scan + keydir blocks on cuda:0, folded in rank order, against the replay."""
+    from cask_amd.keydir import KeydirFold
+    path = str(tmp_path / "db")
+    _make_db(path, 7)
+    files = _files(path)
+    want = _want(path)
+    for cut in (1, 3, 5):
+        fold = KeydirFold()
+        for part in (files[:cut], files[cut:]):
+            fold.merge(_device_block(gpu_ctx, part))
+        with fold.finish() as db:
+            assert _got(db) == want
+
+
+def test_open_multi_matches_replay(native, tmp_path):
+    from cask_amd.keydir import open_multi
+    path = str(tmp_path / "db")
+    _make_db(path, 11, nfiles=7)
+    want = _want(path)
+    for devices in ([0], [0, 0], [0, 0, 0, 0], [0] * 9):
+        with open_multi(path, devices) as db:
+            assert _got(db) == want, devices
+            assert db.files() == R.find_data_files(path)
+
+
+def test_open_multi_reports_first_failure(native, tmp_path):
+    from cask_amd import errors
+    from cask_amd.keydir import open_multi
+    path = str(tmp_path / "db")
+    _make_db(path, 12, nfiles=4, nrec=500)
+    for fid, at in ((4, 0.5), (2, 0.3)):  # the failure of the earlier file wins
+        p = R.data_file_path(path, fid)
+        b = bytearray(open(p, "rb").read())
+        b[int(len(b) * at)] ^= 0x40
+        open(p, "wb").write(bytes(b))
+    want = R.replay(str(path), write_hints=False).error
+    with pytest.raises((errors.InvalidChecksum, errors.UnexpectedEof)) as ei:
+        open_multi(path, [0, 0])
+    assert (ei.value.file_id, ei.value.pos) == (want.file_id, want.pos)
+
+
+def test_sharded_keydir_unique_keys_large(gpu_ctx):
+    """configs[4]'s record shape (unique keys, 290-B records) at 8 files x 200,000 records in 4
+    shards: every row is kept, the fold has every key with its last position, stats are puts only."""
+    import torch
+    from cask_amd.keydir import KeydirFold, shard_keydir
+    from cask_amd.workloads import fixed_file
+    nrec, fold = 200_000, KeydirFold()
+    files = [fixed_file(gpu_ctx, fid, nrec, 16, 256, 1 + (fid - 1) * nrec, (fid - 1) * nrec, 77 + fid) for fid in range(1, 9)]
+    for s in range(4):
+        part = [(f.file_id, f.data) for f in files[2 * s:2 * s + 2]]
+        res = gpu_ctx.scan_device(part)
+        assert res.error is None and res.count == 2 * nrec
+        blk = shard_keydir(gpu_ctx, part, {"pos": res.pos, "seq": res.seq, "vsz": res.vsz, "ksz": res.ksz,
+                                           "status": res.status}, res.count, res.file_row_offset)
+        assert blk.numel() == 64 + 2 * nrec * (32 + 16) + 2 * 40
+        fold.merge(blk.cpu())
+    with fold.finish() as db:
+        assert len(db) == 8 * nrec and db.current_sequence == 8 * nrec + 1
+        assert db.stats() == {f: (nrec, 0, 0) for f in range(1, 9)}
+        host = files[5].data[:290 * 3].cpu().numpy().tobytes()
+        e = db.get_entry(host[290 * 2 + 18:290 * 2 + 34])
+        assert (e.file_id, e.entry_pos, e.entry_size, e.sequence) == (6, 580, 290, 1 + 5 * nrec + 2)
+    del files
+    torch.cuda.empty_cache()

@@ -7,7 +7,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout
   > gpurun_out/pytest_gpu.log 2>&1 || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -2 gpurun_out/pytest_gpu.log
 for k in 1 2; do
-for mode in fused 2 0; do
+for mode in fused 0; do
   if [ $mode = fused ]; then E=""; else E="CASK_DENSE=$mode"; fi
   timeout -k 10 300 env $E python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --no-segmented > gpurun_out/ab_$mode.log 2>&1 || { tail -5 gpurun_out/ab_$mode.log; exit 1; }
   python -c "
