@@ -134,6 +134,8 @@ SIGNATURES = [
     ("cask_shard_keydir", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                     C.POINTER(C.c_void_p), c_u64p]),
     ("cask_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_hints_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
+                                    C.c_void_p, C.c_uint64, c_u64p]),
     ("cask_keydir_new", C.c_void_p, []),
     ("cask_keydir_merge", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     ("cask_keydir_finish", C.c_int, [C.c_void_p]),

@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <new>
 #include <regex>
 #include <thread>
@@ -379,6 +380,191 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 }  // namespace
 
+// A hint file: body + XXH32 trailer (HintWriter::drop, log.rs:389-395), created/truncated
+// (util.rs:45-49), two write(2)s and no copy of the body.
+bool write_file_raw2(const std::string& p, const uint8_t* b, size_t n, uint32_t trailer) {
+  int fd = open(p.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return false;
+  uint8_t t[4];
+  wr32(t, trailer);
+  bool ok = true;
+  for (int part = 0; part < 2 && ok; ++part) {
+    const uint8_t* q = part ? t : b;
+    size_t m = part ? 4 : n, off = 0;
+    while (off < m) {
+      ssize_t w = write(fd, q + off, m - off);
+      if (w < 0) {
+        if (errno == EINTR) continue;
+        ok = false;
+        break;
+      }
+      off += (size_t)w;
+    }
+  }
+  close(fd);
+  return ok;
+}
+
+// The scan side of Cask::open on one GPU, kept per device for the life of the process (a context,
+// its buffers and a ring of pinned staging buffers are created once, not per open): data files
+// read by host threads into pinned buffers and copied to the device as they arrive, the device
+// scan, and the hint bodies built on the device (cask_hints_device) and copied back.
+struct EngineDev {
+  int device = 0;
+  std::mutex mu;  // one open() at a time per device
+  cask_ctx* ctx = nullptr;
+  struct Buf {
+    uint8_t* p = nullptr;
+    size_t cap = 0;
+    bool ensure(size_t b) {
+      if (b <= cap) return true;
+      if (p) (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+      if (hipMalloc(&p, b + b / 8 + 4096) != hipSuccess) {
+        p = nullptr;
+        return false;
+      }
+      cap = b + b / 8 + 4096;
+      return true;
+    }
+  } data, rows, hint;
+  static constexpr int kReaders = 4, kSlots = 2;
+  static constexpr size_t kSlotBytes = 64ull << 20;
+  void* pin[kReaders][kSlots] = {};
+  hipStream_t rs[kReaders] = {};
+  hipEvent_t ev[kReaders][kSlots] = {};
+  cask_rows r{};
+
+  int prepare() {
+    if (hipSetDevice(device) != hipSuccess) return CASK_E_DEVICE;
+    if (!ctx) {
+      int st = CASK_OK;
+      ctx = cask_ctx_create(device, &st);
+      if (!ctx) return st;
+    }
+    for (int t = 0; t < kReaders; ++t) {
+      if (!rs[t] && hipStreamCreateWithFlags(&rs[t], hipStreamNonBlocking) != hipSuccess) return CASK_E_DEVICE;
+      for (int k = 0; k < kSlots; ++k) {
+        if (!pin[t][k] && hipHostMalloc(&pin[t][k], kSlotBytes, hipHostMallocDefault) != hipSuccess) {
+          pin[t][k] = nullptr;
+          return CASK_E_NOMEM;
+        }
+        if (!ev[t][k] && hipEventCreateWithFlags(&ev[t][k], hipEventDisableTiming) != hipSuccess) return CASK_E_DEVICE;
+      }
+    }
+    return CASK_OK;
+  }
+
+  // Reader thread t takes every kReaders-th 64-MiB piece of the files, alternating between its two
+  // pinned slots: pread into one while the other's copy to the device is in flight.
+  int read_to_device(const std::vector<std::string>& paths, const std::vector<cask_file_view>& v, std::vector<char>& ok) {
+    struct Piece {
+      uint32_t f;
+      uint64_t off, n;
+    };
+    std::vector<Piece> pieces;
+    for (uint32_t f = 0; f < v.size(); ++f)
+      for (uint64_t o = 0; o < v[f].len; o += kSlotBytes) pieces.push_back(Piece{f, o, std::min<uint64_t>(kSlotBytes, v[f].len - o)});
+    const unsigned nt = std::max(1u, std::min<unsigned>((unsigned)kReaders, std::min<unsigned>(host_threads(), (unsigned)pieces.size())));
+    std::vector<int> status(nt, CASK_OK);
+    parallel_for(nt, [&](unsigned t) {
+      if (hipSetDevice(device) != hipSuccess) {
+        status[t] = CASK_E_DEVICE;
+        return;
+      }
+      std::vector<int> fds(v.size(), -1);
+      unsigned k = 0;
+      for (size_t j = t; j < pieces.size(); j += nt, k ^= 1) {
+        const Piece& pc = pieces[j];
+        if (!ok[pc.f]) continue;
+        if (fds[pc.f] < 0 && (fds[pc.f] = open(paths[pc.f].c_str(), O_RDONLY)) < 0) {
+          ok[pc.f] = 0;
+          continue;
+        }
+        if (hipEventSynchronize(ev[t][k]) != hipSuccess) {
+          status[t] = CASK_E_DEVICE;
+          break;
+        }
+        uint64_t got = 0;
+        while (got < pc.n) {
+          const ssize_t m = pread(fds[pc.f], (uint8_t*)pin[t][k] + got, pc.n - got, (off_t)(pc.off + got));
+          if (m < 0 && errno == EINTR) continue;
+          if (m <= 0) break;
+          got += (uint64_t)m;
+        }
+        if (got != pc.n) {  // the file shrank or could not be read
+          ok[pc.f] = 0;
+          continue;
+        }
+        if (hipMemcpyAsync((uint8_t*)v[pc.f].data + pc.off, pin[t][k], pc.n, hipMemcpyHostToDevice, rs[t]) != hipSuccess ||
+            hipEventRecord(ev[t][k], rs[t]) != hipSuccess) {
+          status[t] = CASK_E_DEVICE;
+          break;
+        }
+      }
+      for (int fd : fds)
+        if (fd >= 0) close(fd);
+      if (hipStreamSynchronize(rs[t]) != hipSuccess) status[t] = CASK_E_DEVICE;
+    });
+    for (int s : status)
+      if (s != CASK_OK) return s;
+    return CASK_OK;
+  }
+
+  // Device rows sized from a guess (average record >= 48 B), once more at the exact count if short.
+  int scan(const std::vector<cask_file_view>& v, std::vector<uint64_t>& row_off, cask_scan_error& se) {
+    uint64_t total = 0;
+    for (const auto& f : v) total += f.len;
+    const uint64_t bound = cask_rows_bound(v.data(), (uint32_t)v.size());
+    uint64_t cap = std::min<uint64_t>(bound, total / 48 + v.size() + 1024);
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const uint64_t a8 = (cap * 8 + 255) & ~255ull, a4 = (cap * 4 + 255) & ~255ull, a2 = (cap * 2 + 255) & ~255ull;
+      if (!rows.ensure(2 * a8 + a4 + a2 + cap + 256)) return CASK_E_NOMEM;
+      r = cask_rows{};
+      r.capacity = cap;
+      r.pos = (uint64_t*)rows.p;
+      r.seq = (uint64_t*)(rows.p + a8);
+      r.vsz = (uint32_t*)(rows.p + 2 * a8);
+      r.ksz = (uint16_t*)(rows.p + 2 * a8 + a4);
+      r.status = rows.p + 2 * a8 + a4 + a2;
+      const int st = cask_scan_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), &se);
+      if (st != CASK_E_CAPACITY) return st;
+      cap = r.count;
+    }
+    return CASK_E_DEVICE;
+  }
+
+  int hints(const std::vector<cask_file_view>& v, const std::vector<uint64_t>& row_off, std::vector<uint8_t>& hbuf,
+            std::vector<uint64_t>& hs0, std::vector<uint64_t>& hs1, const std::vector<uint32_t>& view_file) {
+    std::vector<uint64_t> fo(v.size() + 1, 0);
+    int st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), nullptr, 0, fo.data());
+    if (st != CASK_E_CAPACITY && st != CASK_OK) return st;
+    if (!hint.ensure(fo[v.size()] + 256)) return CASK_E_NOMEM;
+    st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), hint.p, hint.cap, fo.data());
+    if (st != CASK_OK) return st;
+    hbuf.resize(fo[v.size()]);
+    if (!hbuf.empty() && cask_copy(ctx, hbuf.data(), hint.p, hbuf.size()) != CASK_OK) return CASK_E_DEVICE;
+    for (size_t k = 0; k < v.size(); ++k) {
+      hs0[view_file[k]] = fo[k];
+      hs1[view_file[k]] = fo[k + 1];
+    }
+    return CASK_OK;
+  }
+};
+
+EngineDev* engine_dev(int device) {
+  static std::mutex mu;
+  static EngineDev* devs[64] = {};
+  if (device < 0 || device >= 64) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!devs[device]) {
+    devs[device] = new (std::nothrow) EngineDev();
+    if (devs[device]) devs[device]->device = device;
+  }
+  return devs[device];
+}
+
 // One record of the replay fold (a hint, or an Ok row of a scanned file), in replay order.
 struct FoldRec {
   const uint8_t* key;
@@ -555,11 +741,12 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   const cask_options opts = db->opts;
   const std::string path = db->path;
 
-  // Which files have a valid hint file (log.rs:121-135, 512-539)?
+  // Which files have a valid hint file (log.rs:121-135, 512-539)? The others are scanned.
   const size_t nf = db->files.size();
-  std::vector<std::vector<uint8_t>> hints(nf), data(nf);
+  std::vector<std::vector<uint8_t>> hints(nf);
   std::vector<char> use_hint(nf, 0), data_ok(nf, 1);
   std::vector<uint32_t> scan_idx;
+  std::vector<uint64_t> flen(nf, 0);
   for (size_t i = 0; i < nf; ++i) {
     const std::string hp = hint_path(path, db->files[i]);
     if (is_file_follow(hp) && read_file(hp, hints[i]) && hints[i].size() >= 4) {
@@ -570,159 +757,154 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
       }
     }
     hints[i].clear();
-    if (!read_file(data_path(path, db->files[i]), data[i])) data_ok[i] = 0;
+    struct stat stt;
+    if (stat(data_path(path, db->files[i]).c_str(), &stt) != 0) data_ok[i] = 0;
+    else flen[i] = (uint64_t)stt.st_size;
     scan_idx.push_back((uint32_t)i);
   }
-  db->timings[0] = ms_since(t0);
 
-  // Device scan of every data file that needs its hints recreated, in one batch.
-  std::vector<uint64_t> pos, seq;
-  std::vector<uint32_t> vsz;
-  std::vector<uint16_t> ksz;
-  std::vector<uint8_t> status;
-  std::vector<uint64_t> row_off;
-  std::vector<int> scan_slot(nf, -1);
-  auto t1 = std::chrono::steady_clock::now();
-  if (!scan_idx.empty()) {
-    std::vector<cask_file_view> views;
-    for (uint32_t i : scan_idx) {
-      if (!data_ok[i]) continue;
-      scan_slot[i] = (int)views.size();
-      cask_file_view v{};
-      v.file_id = db->files[i];
-      v.flags = 0;
-      v.data = data[i].data();
-      v.len = data[i].size();
-      views.push_back(v);
+  // The scanned files: read from disk straight to the device through pinned buffers (file reads on
+  // host threads overlapped with the copies), scanned there, and their hint bodies built there
+  // (cask_hints_device) and brought back: the host never holds the data bytes, only the hint
+  // records it writes and folds.
+  std::vector<uint8_t> hbuf;                 // hint bodies of the scanned files, file after file
+  std::vector<uint64_t> hs0(nf, 0), hs1(nf, 0);  // body of scanned file i: hbuf[hs0[i], hs1[i])
+  cask_scan_error se{};
+  uint32_t err_file = UINT32_MAX;            // index into files of the scan's first failure
+  std::vector<cask_file_view> views;
+  std::vector<uint32_t> view_file;
+  for (uint32_t i : scan_idx)
+    if (data_ok[i]) {
+      views.push_back(cask_file_view{db->files[i], CASK_VIEW_DEVICE, nullptr, flen[i]});
+      view_file.push_back(i);
     }
-    if (!views.empty()) {
-      int st = CASK_OK;
-      cask_ctx* ctx = cask_ctx_create(opts.device, &st);
-      if (!ctx) {
-        delete db;
-        set_err(err, CASK_E_DEVICE);
-        return nullptr;
-      }
-      uint64_t bound = cask_rows_bound(views.data(), (uint32_t)views.size());
-      pos.resize(bound);
-      seq.resize(bound);
-      vsz.resize(bound);
-      ksz.resize(bound);
-      status.resize(bound);
-      row_off.resize(views.size() + 1);
-      cask_rows rows{};
-      rows.capacity = bound;
-      rows.pos = pos.data();
-      rows.seq = seq.data();
-      rows.vsz = vsz.data();
-      rows.ksz = ksz.data();
-      rows.status = status.data();
-      cask_scan_error se{};
-      st = cask_scan_host(ctx, views.data(), (uint32_t)views.size(), &rows, row_off.data(), &se);
-      cask_ctx_destroy(ctx);
-      if (st != CASK_OK) {
-        delete db;
-        set_err(err, st);
-        return nullptr;
-      }
+  double t_read = 0;
+  auto t1 = std::chrono::steady_clock::now();
+  if (!views.empty()) {
+    EngineDev* ed = engine_dev(opts.device);
+    if (!ed) {
+      delete db;
+      set_err(err, CASK_E_DEVICE);
+      return nullptr;
+    }
+    std::lock_guard<std::mutex> g(ed->mu);
+    int st = ed->prepare();
+    std::vector<uint64_t> doff(views.size() + 1, 0);
+    for (size_t v = 0; v < views.size(); ++v) doff[v + 1] = doff[v] + ((views[v].len + 255) & ~255ull);
+    if (st == CASK_OK && !ed->data.ensure(doff.back() + 256)) st = CASK_E_NOMEM;
+    if (st == CASK_OK) {
+      for (size_t v = 0; v < views.size(); ++v) views[v].data = ed->data.p + doff[v];
+      std::vector<std::string> paths;
+      for (uint32_t i : view_file) paths.push_back(data_path(path, db->files[i]));
+      std::vector<char> ok(views.size(), 1);
+      st = ed->read_to_device(paths, views, ok);
+      for (size_t v = 0; v < views.size(); ++v)
+        if (!ok[v]) {  // the file could not be read whole: Log::entries' Io error when its turn comes
+          data_ok[view_file[v]] = 0;
+          views[v].len = 0;
+        }
+    }
+    t_read = ms_since(t1);
+    std::vector<uint64_t> row_off(views.size() + 1);
+    if (st == CASK_OK) st = ed->scan(views, row_off, se);
+    if (st == CASK_OK) st = ed->hints(views, row_off, hbuf, hs0, hs1, view_file);
+    if (st != CASK_OK) {
+      delete db;
+      set_err(err, st);
+      return nullptr;
+    }
+    if (se.kind) {
+      for (size_t v = 0; v < views.size(); ++v)
+        if (views[v].file_id == se.file_id) err_file = view_file[v];
     }
   }
-  db->timings[1] = ms_since(t1);
+  db->timings[0] = ms_since(t0) - ms_since(t1) + t_read;
+  db->timings[1] = ms_since(t1) - t_read;
 
-  // Replay in ascending file order (cask.rs:348-369); the first Err aborts open().
-  double t_hint = 0, t_fold = 0;
+  // Replay in ascending file order (cask.rs:348-369); the first Err aborts open(). Hint files of the
+  // scanned files up to that point are written on threads: each is its body + XXH32 trailer
+  // (RecreateHints keeps draining after an error, so a failing file's hint file has every Ok row).
+  double t_fold = 0;
   std::vector<FoldRec> recs;  // the replay's fold, in order (parallel_fold)
-  for (size_t i = 0; i < nf; ++i) {
+  std::vector<uint32_t> to_write;
+  int fail = CASK_OK;
+  uint32_t fail_fid = 0;
+  uint64_t fail_pos = 0;
+  uint32_t fail_e = 0, fail_f = 0;
+  auto tf = std::chrono::steady_clock::now();
+  for (size_t i = 0; i < nf && fail == CASK_OK; ++i) {
     const uint32_t fid = db->files[i];
+    const uint8_t* hb;
+    uint64_t body;
     if (use_hint[i]) {
-      auto tf = std::chrono::steady_clock::now();
-      const std::vector<uint8_t>& hb = hints[i];
-      const uint64_t body = hb.size() - 4;  // Take(size - 4) (log.rs:129)
-      uint64_t p = 0;
-      while (p < body) {  // Hints::next / Hint::from_read (log.rs:437-447; data.rs:258-276)
-        if (body - p < 22) {
-          t_fold += ms_since(tf);
-          delete db;
-          set_err(err, CASK_E_EOF, fid, p);
-          return nullptr;
-        }
-        const uint8_t* h = hb.data() + p;
-        const uint64_t s = rd64(h);
-        const uint16_t k = rd16(h + 8);
-        const uint32_t v = rd32(h + 10);
-        const uint64_t epos = rd64(h + 14);
-        if (body - p - 22 < k) {
-          delete db;
-          set_err(err, CASK_E_EOF, fid, p);
-          return nullptr;
-        }
-        if (s > db->sequence) db->sequence = s;
-        recs.push_back(FoldRec{h + 22, epos, s, 0, fid, v, k});
-        p += 22ull + k;
-      }
-      t_fold += ms_since(tf);
-      continue;
-    }
-    if (!data_ok[i]) {
+      hb = hints[i].data();
+      body = hints[i].size() - 4;  // Take(size - 4) (log.rs:129)
+    } else if (!data_ok[i]) {
       // HintWriter::new truncated the hint file before Log::entries failed; its Drop then wrote
       // the trailer of an empty body (log.rs:141-142, 389-395).
       if (opts.write_hints) write_file(hint_path(path, fid), {}, cask_xxh::xxh32(nullptr, 0, 0));
-      delete db;
-      set_err(err, CASK_E_IO, fid);
-      return nullptr;
-    }
-    const int slot = scan_slot[i];
-    const uint64_t r0 = row_off[slot], r1 = row_off[slot + 1];
-    const uint8_t* buf = data[i].data();
-    // Hint file: every Ok row (RecreateHints::drop keeps draining after an error), + trailer.
-    auto th = std::chrono::steady_clock::now();
-    if (opts.write_hints) {
-      std::vector<uint8_t> hb;
-      hb.reserve((r1 - r0) * 38);
-      for (uint64_t r = r0; r < r1; ++r) {
-        if (status[r] != CASK_ROW_OK) continue;
-        uint8_t h[22];
-        wr64(h, seq[r]);
-        wr16(h + 8, ksz[r]);
-        wr32(h + 10, vsz[r]);
-        wr64(h + 14, pos[r]);
-        hb.insert(hb.end(), h, h + 22);
-        hb.insert(hb.end(), buf + pos[r] + 18, buf + pos[r] + 18 + ksz[r]);
-      }
-      if (!write_file(hint_path(path, fid), hb, cask_xxh::xxh32(hb.data(), hb.size(), 0))) {
-        delete db;
-        set_err(err, CASK_E_IO, fid);
-        return nullptr;
+      fail = CASK_E_IO;
+      fail_fid = fid;
+      break;
+    } else {
+      hb = hbuf.data() + hs0[i];
+      body = hs1[i] - hs0[i];
+      if (opts.write_hints) to_write.push_back((uint32_t)i);
+      if (err_file == i) {  // the scan's first failing record is in this file
+        fail = se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF;
+        fail_fid = fid;
+        fail_pos = se.pos;
+        fail_e = se.expected;
+        fail_f = se.found;
+        break;
       }
     }
-    t_hint += ms_since(th);
-    auto tf = std::chrono::steady_clock::now();
-    for (uint64_t r = r0; r < r1; ++r) {
-      if (status[r] != CASK_ROW_OK) {
-        const uint64_t p = pos[r];
-        uint32_t e = 0, f = 0;
-        if (p + 18 <= data[i].size()) {
-          e = rd32(buf + p);
-          if (status[r] == CASK_ROW_CHECKSUM) {
-            const uint64_t rl = 18ull + ksz[r] + (vsz[r] == CASK_ENTRY_TOMBSTONE ? 0ull : (uint64_t)vsz[r]);
-            f = cask_xxh::xxh32(buf + p + 4, rl - 4, 0);
-          }
-        }
-        delete db;
-        set_err(err, status[r] == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF, fid, p, e, f);
-        return nullptr;
+    uint64_t p = 0;
+    while (p < body) {  // Hints::next / Hint::from_read (log.rs:437-447; data.rs:258-276)
+      if (body - p < 22 || body - p - 22 < rd16(hb + p + 8)) {
+        fail = CASK_E_EOF;
+        fail_fid = fid;
+        fail_pos = p;
+        break;
       }
-      if (seq[r] > db->sequence) db->sequence = seq[r];
-      recs.push_back(FoldRec{buf + pos[r] + 18, pos[r], seq[r], 0, fid, vsz[r], ksz[r]});
+      const uint8_t* h = hb + p;
+      const uint64_t s = rd64(h);
+      const uint16_t k = rd16(h + 8);
+      if (s > db->sequence) db->sequence = s;
+      recs.push_back(FoldRec{h + 22, rd64(h + 14), s, 0, fid, rd32(h + 10), k});
+      p += 22ull + k;
     }
-    t_fold += ms_since(tf);
   }
-  {  // Index::update + Stats over every record (the keys stay in data[] / hints[] until here)
-    auto tf = std::chrono::steady_clock::now();
+  t_fold += ms_since(tf);
+  auto th = std::chrono::steady_clock::now();
+  {
+    std::vector<char> wok(to_write.size(), 1);
+    const unsigned nt = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)to_write.size()));
+    parallel_for(nt, [&](unsigned t) {
+      for (size_t j = t; j < to_write.size(); j += nt) {
+        const uint32_t i = to_write[j];
+        const uint8_t* b = hbuf.data() + hs0[i];
+        const uint64_t n = hs1[i] - hs0[i];
+        wok[j] = write_file_raw2(hint_path(path, db->files[i]), b, n, cask_xxh::xxh32(b, n, 0));
+      }
+    });
+    for (size_t j = 0; j < to_write.size() && fail == CASK_OK; ++j)
+      if (!wok[j]) {
+        fail = CASK_E_IO;
+        fail_fid = db->files[to_write[j]];
+      }
+  }
+  db->timings[2] = ms_since(th);
+  if (fail != CASK_OK) {
+    delete db;
+    set_err(err, fail, fail_fid, fail_pos, fail_e, fail_f);
+    return nullptr;
+  }
+  {  // Index::update + Stats over every record (the keys stay in hints[] / hbuf until here)
+    auto tf2 = std::chrono::steady_clock::now();
     parallel_fold(recs, db->index);
-    t_fold += ms_since(tf);
+    t_fold += ms_since(tf2);
   }
-  db->timings[2] = t_hint;
   db->timings[3] = t_fold;
   db->timings[4] = ms_since(t0);
   return db;

@@ -267,6 +267,8 @@ __global__ void k_kd_header(KdArgs a, uint64_t rows_in, uint64_t fstat_at, uint6
     hd.bytes = bytes;
     *(ShardHeader*)a.out = hd;
   }
+  const uint64_t end = a.key_at + (a.n ? a.tot[2] : 0);  // zero the padding to the 8-B boundary
+  if (threadIdx.x < bytes - end) a.out[end + threadIdx.x] = 0;
   for (uint32_t f = threadIdx.x; f < a.nfiles; f += blockDim.x) {
     ShardFileStat st{};
     st.file_id = a.file_ids[f];
@@ -416,6 +418,114 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   *out = S_.out;
   *bytes = total;
   return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Hint-file bodies on the device (RecreateHints::next + HintWriter::write, log.rs:382-386,
+// 454-465; Hint::write_bytes, data.rs:242-256): for every Ok row, in order,
+// [sequence u64][key_size u16][value_size u32 (0xFFFFFFFF: tombstone)][entry_pos u64][key],
+// little-endian, one body per file laid out file after file. The host appends the XXH32 trailer
+// (HintWriter::drop, log.rs:389-395) and writes the files.
+// ------------------------------------------------------------------------------------------
+struct HpArgs {
+  const FileDesc* files;
+  const uint64_t* row_off;
+  uint32_t nfiles;
+  const uint64_t* pos;
+  const uint64_t* seq;
+  const uint32_t* vsz;
+  const uint16_t* ksz;
+  const uint8_t* status;
+  uint64_t n;
+  uint64_t* sz;
+  uint64_t* off;
+  uint64_t* fstart;  // nfiles + 1
+  uint8_t* out;
+};
+
+__global__ __launch_bounds__(256) void k_hint_sizes(HpArgs a) {
+  for (uint64_t d = blockIdx.x * 256ull + threadIdx.x; d < a.n; d += (uint64_t)gridDim.x * 256ull)
+    a.sz[d] = a.status[d] == kRowOk ? 22ull + a.ksz[d] : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_hint_write(HpArgs a) {
+  for (uint64_t d = blockIdx.x * 256ull + threadIdx.x; d < a.n; d += (uint64_t)gridDim.x * 256ull) {
+    if (a.status[d] != kRowOk) continue;
+    uint32_t lo = 0, hi = a.nfiles;  // the row's file: last f with row_off[f] <= d
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (a.row_off[mid] <= d) lo = mid; else hi = mid;
+    }
+    uint8_t* o = a.out + a.off[d];
+    const uint64_t s = a.seq[d], p = a.pos[d];
+    const uint32_t k = a.ksz[d], v = a.vsz[d];
+    for (int i = 0; i < 8; ++i) o[i] = (uint8_t)(s >> (8 * i));
+    o[8] = (uint8_t)k;
+    o[9] = (uint8_t)(k >> 8);
+    for (int i = 0; i < 4; ++i) o[10 + i] = (uint8_t)(v >> (8 * i));
+    for (int i = 0; i < 8; ++i) o[14 + i] = (uint8_t)(p >> (8 * i));
+    const uint8_t* key = a.files[lo].data + p + 18;
+    for (uint32_t i = 0; i < k; ++i) o[22 + i] = key[i];
+  }
+}
+
+__global__ void k_hint_starts(HpArgs a) {
+  for (uint32_t f = threadIdx.x; f <= a.nfiles; f += blockDim.x) {
+    const uint64_t r = a.row_off[f];
+    a.fstart[f] = r < a.n ? a.off[r] : (a.n ? a.off[a.n - 1] + a.sz[a.n - 1] : 0ull);
+  }
+}
+
+// Returns 0 or a negative cask_status. file_start (host, nfiles + 1): each file's body in `out`.
+int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const uint64_t* row_off_host,
+              const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz, const uint16_t* ksz, const uint8_t* status,
+              uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream) {
+  KdScratch& S_ = *(KdScratch*)scratch;
+  hipStream_t st = S(stream);
+  size_t t_scan = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                       (int)std::max<uint64_t>(n, 1), st) != hipSuccess)
+    return -11;
+  uint64_t o = 0;
+  auto take = [&](uint64_t b) { const uint64_t r = o; o = al(o + b); return r; };
+  const uint64_t n1 = n ? n : 1;
+  const uint64_t o_fd = take(sizeof(FileDesc) * (nfiles + 1)), o_ro = take(8ull * (nfiles + 1)), o_sz = take(8 * n1),
+                 o_off = take(8 * n1), o_fs = take(8ull * (nfiles + 1)), o_tmp = take(t_scan);
+  if (!S_.ensure(o)) return -13;
+  uint8_t* b = (uint8_t*)S_.p;
+  HpArgs a{};
+  a.files = (const FileDesc*)(b + o_fd);
+  a.row_off = (const uint64_t*)(b + o_ro);
+  a.nfiles = nfiles;
+  a.pos = pos;
+  a.seq = seq;
+  a.vsz = vsz;
+  a.ksz = ksz;
+  a.status = status;
+  a.n = n;
+  a.sz = (uint64_t*)(b + o_sz);
+  a.off = (uint64_t*)(b + o_off);
+  a.fstart = (uint64_t*)(b + o_fs);
+  a.out = out;
+  bool ok = true;
+  auto H = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+  H(hipMemcpyAsync((void*)a.files, files_host, sizeof(FileDesc) * nfiles, hipMemcpyHostToDevice, st));
+  H(hipMemcpyAsync((void*)a.row_off, row_off_host, 8ull * (nfiles + 1), hipMemcpyHostToDevice, st));
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256 + 1, (uint64_t)device_cus() * 16);
+  if (n) {
+    hipLaunchKernelGGL(k_hint_sizes, dim3(grid), dim3(256), 0, st, a);
+    size_t tb = t_scan;
+    H(hipcub::DeviceScan::ExclusiveSum(b + o_tmp, tb, a.sz, a.off, (int)n, st));
+  }
+  hipLaunchKernelGGL(k_hint_starts, dim3(1), dim3(256), 0, st, a);
+  H(hipMemcpyAsync(file_start, a.fstart, 8ull * (nfiles + 1), hipMemcpyDeviceToHost, st));
+  H(hipStreamSynchronize(st));
+  if (!ok) return -11;
+  if (file_start[nfiles] > cap) return -12;  // CASK_E_CAPACITY: file_start[nfiles] bytes are needed
+  if (n) hipLaunchKernelGGL(k_hint_write, dim3(grid), dim3(256), 0, st, a);
+  H(hipStreamSynchronize(st));
+  H(hipGetLastError());
+  return ok ? 0 : -11;
 }
 
 }  // namespace cask_dev

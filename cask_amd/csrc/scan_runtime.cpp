@@ -725,6 +725,22 @@ extern "C" int cask_copy(cask_ctx* c, void* dst, const void* src, uint64_t bytes
   return CASK_OK;
 }
 
+extern "C" int cask_hints_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
+                                 const uint64_t* file_row_offset, uint8_t* out, uint64_t cap, uint64_t* file_hint_offset) {
+  if (!c || !rows || !file_hint_offset || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
+  if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status)) return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
+  if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+  std::vector<FileDesc> fd(nfiles + 1);
+  for (uint32_t i = 0; i < nfiles; ++i) fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
+  return hint_pack(c->kd, fd.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz, rows->status,
+                   rows->count, out, out ? cap : 0, file_hint_offset, c->stream);
+}
+
 extern "C" int cask_shard_keydir(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
                                  const uint64_t* file_row_offset, const void** block, uint64_t* bytes) {
   if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;

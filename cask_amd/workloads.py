@@ -82,3 +82,32 @@ def zipf_sizes(n: int, s: float = 1.1, kmax: int = 4096, seed: int = 0x5A1F, dev
     u = torch.rand(n, generator=g, dtype=torch.float64, device=device)
     kk = torch.searchsorted(cdf, u).clamp_(max=kmax - 1) + 1
     return (kk * 16).to(torch.int32)
+
+
+def zipf_files(ctx: ScanContext, total_gib: float = 32.0, max_file: int = 2 ** 31, seed: int = 0x5A1F):
+    """BASELINE configs[2]: ~total_gib GiB of records with 16 B keys and Zipf(1.1) value sizes
+    (16 B .. 64 KiB), sequences 1.., in files rolled over as LogWriter does (a new file when
+    pos + size > max_file_size, log.rs:282-306). Returns ([(DataFile, record indices)], vsz, n,
+    record lengths) — the generator's own view, for checking rows."""
+    torch = _torch()
+    dev = torch.device("cuda", ctx.device)
+    target = int(total_gib * 2 ** 30)
+    n = int(target / (34 + 5085) * 1.05) + 1024
+    vsz = zipf_sizes(n, seed=seed, device=dev)
+    rl = 34 + vsz.to(torch.int64)
+    cum = torch.cumsum(rl, 0)
+    n = int(torch.searchsorted(cum, torch.tensor([target], device=dev, dtype=torch.int64)).item())
+    files, base, r0 = [], 0, 0
+    while r0 < n:  # greedy rollover: a new file when pos + size > max_file_size
+        r1 = int(torch.searchsorted(cum, torch.tensor([base + max_file], device=dev, dtype=torch.int64),
+                                    right=True).item())
+        r1 = min(max(r1, r0 + 1), n)
+        idx = torch.arange(r0, r1, dtype=torch.int64, device=dev)
+        ks = torch.full((r1 - r0,), 16, dtype=torch.int16, device=dev)
+        f = variable_file(ctx, len(files) + 1, ks, vsz[r0:r1].clone(), idx + 1, idx, seed + len(files))
+        files.append((f, idx))
+        base = int(cum[r1 - 1].item())
+        r0 = r1
+    del cum
+    torch.cuda.synchronize(dev)
+    return files, vsz, n, rl

@@ -286,6 +286,17 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files, uint64_t nfiles, c
 int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts, cask_compact_result* res,
                         cask_open_error* err);
 
+/* Hint-file bodies on the device (RecreateHints::next + HintWriter::write, log.rs:382-386,
+ * 454-465; Hint::write_bytes, data.rs:242-256): for every Ok row of a cask_scan_device call (same
+ * files, rows and file_row_offset), in order, [sequence u64][key_size u16][value_size u32,
+ * 0xFFFFFFFF for a tombstone][entry_pos u64][key], file after file into `out` (device memory,
+ * `cap` bytes). file_hint_offset (host, nfiles + 1) receives where each file's body starts; the
+ * caller appends the XXH32 trailer of each body (HintWriter::drop, log.rs:389-395). Returns
+ * CASK_E_CAPACITY, with file_hint_offset filled in, when cap < file_hint_offset[nfiles]
+ * (out may be NULL to ask for the size). */
+int cask_hints_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
+                      const uint64_t* file_row_offset, uint8_t* out, uint64_t cap, uint64_t* file_hint_offset);
+
 /* ------------------------------------------------------------------------------------------ */
 /* Multi-GPU replay. Data files shard in contiguous file-id ranges; each shard's   */
 /* rows become a keydir block on its GPU; rank 0 folds the blocks in rank order. The block format */

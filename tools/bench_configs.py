@@ -23,35 +23,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def zipf_files(ctx, torch, total_gib, max_file):
-    """configs[2] files on the device: [(DataFile, record indices)], the value sizes, n, rec lens."""
-    from cask_amd.workloads import variable_file, zipf_sizes
-    dev = torch.device("cuda", ctx.device)
-    target = int(total_gib * 2 ** 30)
-    n = int(target / (34 + 5085) * 1.05) + 1024
-    vsz = zipf_sizes(n, device=dev)
-    rl = 34 + vsz.to(torch.int64)
-    cum = torch.cumsum(rl, 0)
-    n = int(torch.searchsorted(cum, torch.tensor([target], device=dev, dtype=torch.int64)).item())
-    files, base, r0 = [], 0, 0
-    while r0 < n:  # greedy rollover: a new file when pos + size > max_file_size
-        r1 = int(torch.searchsorted(cum, torch.tensor([base + max_file], device=dev, dtype=torch.int64),
-                                    right=True).item())
-        r1 = min(max(r1, r0 + 1), n)
-        idx = torch.arange(r0, r1, dtype=torch.int64, device=dev)
-        ks = torch.full((r1 - r0,), 16, dtype=torch.int16, device=dev)
-        f = variable_file(ctx, len(files) + 1, ks, vsz[r0:r1].clone(), idx + 1, idx, 0x5A1F + len(files))
-        files.append((f, idx))
-        base = int(cum[r1 - 1].item())
-        r0 = r1
-    del cum
-    torch.cuda.synchronize(dev)
-    return files, vsz, n, rl
-
-
 def cfg3(ctx, torch, steps, total_gib, max_file):
     dev = torch.device("cuda", ctx.device)
-    files, vsz, n, rl = zipf_files(ctx, torch, total_gib, max_file)
+    from cask_amd.workloads import zipf_files
+    files, vsz, n, rl = zipf_files(ctx, total_gib, max_file)
     views = [(f.file_id, f.data) for f, _ in files]
     nbytes = sum(f.data.numel() for f, _ in files)
     rows = ctx.alloc_rows(n + 16)

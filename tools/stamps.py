@@ -31,9 +31,8 @@ def main():
     L.cask_debug_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     ctx = cask_amd.ScanContext(0)
     if args.zipf_gib > 0:
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from bench_configs import zipf_files
-        files = [f for f, _ in zipf_files(ctx, torch, args.zipf_gib, 2 ** 31)[0]]
+        from cask_amd.workloads import zipf_files
+        files = [f for f, _ in zipf_files(ctx, args.zipf_gib, 2 ** 31)[0]]
     else:
         files = cfg2_files(ctx, nfiles=args.files)
     views = [(f.file_id, f.data) for f in files]
