@@ -113,6 +113,8 @@ SIGNATURES = [
     ("cask_encode_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("cask_xxh32", C.c_uint32, [C.c_void_p, C.c_uint64]),
+    ("cask_read_entries_device", C.c_int, [C.c_void_p, C.c_void_p, c_u64p, C.c_uint32, c_u32p, c_u64p, C.c_uint64,
+                                           c_u64p, c_u8p, c_u32p, c_u32p]),
     ("cask_options_default", None, [C.POINTER(Options)]),
     ("cask_db_open", C.c_void_p, [C.c_char_p, C.POINTER(Options), C.POINTER(OpenError)]),
     ("cask_db_close", None, [C.c_void_p]),

@@ -1006,231 +1006,196 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
   }
   R.ms[0] = ms_since(t0);
 
-  // 2. the live records: read_entry at each hint position, verified by the device scan
-  auto t1 = std::chrono::steady_clock::now();
+  // 2-5. The live records, source file batch by batch (at most ~kBatch bytes of sources on the
+  // device at once): the sources read straight to the device, each live record read and verified
+  // where its hint says it is (Log::read_entry -> Entry::from_read, log.rs:150-166; the device
+  // hashes only the live bytes), placed by the LogWriter rollover (log.rs:282-306), its bytes
+  // gathered on the device in write order and appended to the new data files; then the tombstone
+  // tail. On an error, the files this call created are removed and the reference's error returned.
   const size_t ns = srcs.size();
-  std::vector<std::vector<uint8_t>> data(ns);
-  std::vector<uint8_t*> dsrc(ns, nullptr);
-  cask_ctx* ctx = nullptr;
-  auto cleanup = [&]() {
-    for (uint8_t* p : dsrc)
-      if (p) (void)hipFree(p);
-    if (ctx) cask_ctx_destroy(ctx);
-  };
-  struct Rec {
-    uint32_t src, ksz, vsz;
-    uint64_t pos, seq, len;
-  };
-  std::vector<Rec> recs(ins.size());
-  if (!ins.empty()) {
-    int st = CASK_OK;
-    ctx = cask_ctx_create(db->opts.device, &st);
-    if (!ctx) return CASK_E_DEVICE;
-    std::vector<cask_file_view> views(ns);
-    for (size_t i = 0; i < ns; ++i) {
-      if (!read_file(data_path(path, srcs[i]), data[i])) {
-        cleanup();
-        set_err(err, CASK_E_IO, srcs[i]);
-        return CASK_E_IO;
-      }
-      R.bytes_in += data[i].size();
-      if (hipMalloc(&dsrc[i], data[i].size() + 16) != hipSuccess ||
-          hipMemcpy(dsrc[i], data[i].data(), data[i].size(), hipMemcpyHostToDevice) != hipSuccess) {
-        cleanup();
-        return CASK_E_DEVICE;
-      }
-      views[i] = cask_file_view{srcs[i], CASK_VIEW_DEVICE, dsrc[i], data[i].size()};
-    }
-    const uint64_t bound = cask_rows_bound(views.data(), (uint32_t)ns);
-    void* drow = nullptr;
-    if (hipMalloc(&drow, bound * 23 + 64) != hipSuccess) {
-      cleanup();
-      return CASK_E_DEVICE;
-    }
-    cask_rows rows{};
-    rows.capacity = bound;
-    rows.pos = (uint64_t*)drow;
-    rows.seq = rows.pos + bound;
-    rows.vsz = (uint32_t*)(rows.seq + bound);
-    rows.ksz = (uint16_t*)(rows.vsz + bound);
-    rows.status = (uint8_t*)(rows.ksz + bound);
-    std::vector<uint64_t> row_off(ns + 1);
-    cask_scan_error se{};
-    st = cask_scan_device(ctx, views.data(), (uint32_t)ns, &rows, row_off.data(), &se);
-    std::vector<uint64_t> pos(rows.count), seq(rows.count);
-    std::vector<uint32_t> vsz(rows.count);
-    std::vector<uint16_t> ksz(rows.count);
-    std::vector<uint8_t> stat(rows.count);
-    if (st == CASK_OK && rows.count &&
-        (hipMemcpy(pos.data(), rows.pos, 8 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(seq.data(), rows.seq, 8 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(vsz.data(), rows.vsz, 4 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(ksz.data(), rows.ksz, 2 * rows.count, hipMemcpyDeviceToHost) != hipSuccess ||
-         hipMemcpy(stat.data(), rows.status, rows.count, hipMemcpyDeviceToHost) != hipSuccess))
-      st = CASK_E_DEVICE;
-    (void)hipFree(drow);
-    if (st != CASK_OK) {
-      cleanup();
-      return st;
-    }
-    for (size_t k = 0; k < ins.size(); ++k) {  // in write order: the first failure is the reference's
-      const Ins& in = ins[k];
-      const std::vector<uint8_t>& buf = data[in.src];
-      const uint64_t n = buf.size(), p = in.pos;
-      Rec& rc = recs[k];
-      rc.src = in.src;
-      rc.pos = p;
-      const uint64_t* b = pos.data() + row_off[in.src];
-      const uint64_t* e = pos.data() + row_off[in.src + 1];
-      const uint64_t* f = std::lower_bound(b, e, p);
-      bool ok;
-      if (f != e && *f == p) {  // the record lies on the file's chain: the scan verified it
-        const uint64_t r = (uint64_t)(f - pos.data());
-        ok = stat[r] == CASK_ROW_OK;
-        rc.ksz = ksz[r];
-        rc.vsz = vsz[r];
-        rc.seq = seq[r];
-      } else {  // off the chain (a stale hint): Entry::from_read at p on the host
-        ok = p + 18 <= n;
-        if (ok) {
-          rc.seq = rd64(buf.data() + p + 4);
-          rc.ksz = rd16(buf.data() + p + 12);
-          rc.vsz = rd32(buf.data() + p + 14);
-        }
-      }
-      const uint64_t rl = ok || p + 18 <= n ? 18ull + rc.ksz + (rc.vsz == CASK_ENTRY_TOMBSTONE ? 0ull : (uint64_t)rc.vsz) : 0;
-      if (p + 18 > n || p + rl > n) {  // data.rs:163,172,181
-        cleanup();
-        set_err(err, CASK_E_EOF, srcs[in.src], p);
-        return CASK_E_EOF;
-      }
-      const uint32_t stored = rd32(buf.data() + p);
-      const uint32_t found = ok ? stored : cask_xxh::xxh32(buf.data() + p + 4, rl - 4, 0);
-      if (found != stored) {  // data.rs:193-198
-        cleanup();
-        set_err(err, CASK_E_CHECKSUM, srcs[in.src], p, stored, found);
-        return CASK_E_CHECKSUM;
-      }
-      rc.len = rl;
-    }
-  }
-  R.ms[1] = ms_since(t1);
-
-  // 3. LogWriter rollover (log.rs:282-306): live records in order, then the tombstone tail
-  struct Out {
-    uint32_t file_id;
-    uint64_t pos;
-  };
   const size_t nt = del_keys.size();
-  std::vector<Out> place(ins.size() + nt);
-  std::vector<uint32_t> new_files, tomb_files, out_files;
-  std::vector<uint64_t> out_len;
-  {
-    uint64_t cur = 0;
-    bool have = false;
-    for (size_t k = 0; k < place.size(); ++k) {
-      const uint64_t size = k < ins.size() ? recs[k].len : 18ull + del_keys[k - ins.size()].size();
-      if (!have || cur + size > db->opts.max_file_size) {
-        const uint32_t fid = ++db->file_seq;  // Sequence::increment (util.rs:62-64)
-        (k < ins.size() ? new_files : tomb_files).push_back(fid);  // cask.rs:510-512, 518-520
-        out_files.push_back(fid);
-        out_len.push_back(0);
-        cur = 0;
-        have = true;
-      }
-      place[k] = Out{out_files.back(), cur};
-      cur += size;
-      out_len.back() = cur;
+  struct OutFile {
+    uint32_t fid;
+    uint64_t len = 0;
+    int fd = -1;
+    std::vector<uint8_t> hints;
+  };
+  std::vector<OutFile> outs;
+  std::vector<uint32_t> new_files, tomb_files;
+  uint64_t cur = 0;
+  auto place = [&](uint64_t size, bool live) -> size_t {  // LogWriter::write's rollover
+    if (outs.empty() || cur + size > db->opts.max_file_size) {
+      const uint32_t fid = ++db->file_seq;  // Sequence::increment (util.rs:62-64)
+      (live ? new_files : tomb_files).push_back(fid);  // cask.rs:510-512, 518-520
+      outs.push_back(OutFile{fid});
+      cur = 0;
     }
+    cur += size;
+    return outs.size() - 1;
+  };
+  auto abort_with = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
+    for (OutFile& o : outs) {
+      if (o.fd >= 0) close(o.fd);
+      (void)unlink(data_path(path, o.fid).c_str());
+    }
+    db->file_seq -= (uint32_t)outs.size();
+    set_err(err, st, fid, pos, e, f);
+    return st;
+  };
+  // one record's bytes into its file, and its hint (Hint::new(entry, entry_pos), data.rs:218-226)
+  auto append = [&](size_t oi, const uint8_t* rec, uint64_t n) -> bool {
+    OutFile& o = outs[oi];
+    if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) return false;
+    const uint16_t k = rd16(rec + 12);
+    uint8_t h[22];
+    wr64(h, rd64(rec + 4));
+    wr16(h + 8, k);
+    wr32(h + 10, rd32(rec + 14));
+    wr64(h + 14, o.len);
+    o.hints.insert(o.hints.end(), h, h + 22);
+    o.hints.insert(o.hints.end(), rec + 18, rec + 18 + k);
+    o.len += n;
+    return true;
+  };
+  auto write_all = [&](int fd, const uint8_t* b, uint64_t n) -> bool {
+    while (n) {
+      const ssize_t w = write(fd, b, n);
+      if (w < 0 && errno == EINTR) continue;
+      if (w <= 0) return false;
+      b += w;
+      n -= (uint64_t)w;
+    }
+    return true;
+  };
+  double t_verify = 0, t_gather = 0, t_write = 0;
+  std::vector<uint64_t> slen(ns, 0);
+  for (size_t i = 0; i < ns; ++i) {
+    struct stat stt;
+    slen[i] = stat(data_path(path, srcs[i]).c_str(), &stt) == 0 ? (uint64_t)stt.st_size : 0;
   }
-
-  // 4. live bytes gathered on the device into one buffer laid out file after file
-  auto t2 = std::chrono::steady_clock::now();
-  std::vector<uint64_t> file_base(out_files.size() + 1, 0);
-  for (size_t i = 0; i < out_files.size(); ++i) file_base[i + 1] = file_base[i] + out_len[i];
-  std::vector<uint8_t> out(file_base.back());
   if (!ins.empty()) {
-    std::vector<uint32_t> g_src(ins.size()), g_len(ins.size());
-    std::vector<uint64_t> g_pos(ins.size()), g_dst(ins.size());
-    uint64_t live_bytes = 0;
-    size_t fi = 0;
-    for (size_t k = 0; k < ins.size(); ++k) {
-      while (out_files[fi] != place[k].file_id) ++fi;
-      g_src[k] = recs[k].src;
-      g_pos[k] = recs[k].pos;
-      g_len[k] = (uint32_t)recs[k].len;
-      g_dst[k] = file_base[fi] + place[k].pos;
-      live_bytes = g_dst[k] + recs[k].len;
-    }
-    uint8_t* dout = nullptr;
-    int st = CASK_OK;
-    if (hipMalloc(&dout, live_bytes + 16) != hipSuccess) st = CASK_E_DEVICE;
-    if (st == CASK_OK)
-      st = cask_gather_device(ctx, (const uint8_t* const*)dsrc.data(), (uint32_t)ns, g_src.data(), g_pos.data(),
-                              g_dst.data(), g_len.data(), ins.size(), dout);
-    if (st == CASK_OK && hipMemcpy(out.data(), dout, live_bytes, hipMemcpyDeviceToHost) != hipSuccess)
-      st = CASK_E_DEVICE;
-    if (dout) (void)hipFree(dout);
-    if (st != CASK_OK) {
-      cleanup();
-      return st;
-    }
-  }
-  R.ms[2] = ms_since(t2);
-
-  // 5. data and hint files (EntryWriter::write, HintWriter, log.rs:343-395)
-  auto t3 = std::chrono::steady_clock::now();
-  std::vector<std::vector<uint8_t>> hints(out_files.size());
-  {
-    size_t fi = 0;
-    for (size_t k = 0; k < place.size(); ++k) {
-      while (out_files[fi] != place[k].file_id) ++fi;
-      uint8_t* o = out.data() + file_base[fi] + place[k].pos;
-      uint8_t h[22];
-      const uint8_t* key;
-      uint32_t klen;
-      if (k < ins.size()) {
-        const Rec& rc = recs[k];
-        key = data[rc.src].data() + rc.pos + 18;
-        klen = rc.ksz;
-        wr64(h, rc.seq);
-        wr32(h + 10, rc.vsz == CASK_ENTRY_TOMBSTONE ? CASK_ENTRY_TOMBSTONE : rc.vsz);
-      } else {  // Entry::deleted(sequence, key).write_bytes (data.rs:90-121)
-        const std::string& kk = del_keys[k - ins.size()];
-        key = (const uint8_t*)kk.data();
-        klen = (uint32_t)kk.size();
-        wr64(o + 4, del_seq[k - ins.size()]);
-        wr16(o + 12, (uint16_t)klen);
-        wr32(o + 14, CASK_ENTRY_TOMBSTONE);
-        memcpy(o + 18, key, klen);
-        wr32(o, cask_xxh::xxh32(o + 4, 14ull + klen, 0));
-        wr64(h, del_seq[k - ins.size()]);
-        wr32(h + 10, CASK_ENTRY_TOMBSTONE);
+    EngineDev* ed = engine_dev(db->opts.device);
+    if (!ed) return abort_with(CASK_E_DEVICE);
+    std::lock_guard<std::mutex> g(ed->mu);
+    int st = ed->prepare();
+    if (st != CASK_OK) return abort_with(st);
+    constexpr uint64_t kBatch = 16ull << 30;
+    size_t k0 = 0;
+    for (size_t b0 = 0; b0 < ns;) {
+      auto tv = std::chrono::steady_clock::now();
+      size_t b1 = b0 + 1;
+      uint64_t bytes = (slen[b0] + 255) & ~255ull;
+      while (b1 < ns && bytes + ((slen[b1] + 255) & ~255ull) <= kBatch) bytes += (slen[b1++] + 255) & ~255ull;
+      if (!ed->data.ensure(bytes + 256)) return abort_with(CASK_E_NOMEM);
+      std::vector<std::string> paths;
+      std::vector<cask_file_view> views;
+      std::vector<const uint8_t*> dsrc;
+      uint64_t off = 0;
+      for (size_t i = b0; i < b1; ++i) {
+        paths.push_back(data_path(path, srcs[i]));
+        views.push_back(cask_file_view{srcs[i], CASK_VIEW_DEVICE, ed->data.p + off, slen[i]});
+        dsrc.push_back(ed->data.p + off);
+        off += (slen[i] + 255) & ~255ull;
       }
-      wr16(h + 8, (uint16_t)klen);
-      wr64(h + 14, place[k].pos);  // Hint::new(entry, entry_pos) (data.rs:218-226)
-      hints[fi].insert(hints[fi].end(), h, h + 22);
-      hints[fi].insert(hints[fi].end(), key, key + klen);
+      std::vector<char> okr(views.size(), 1);
+      if ((st = ed->read_to_device(paths, views, okr)) != CASK_OK) return abort_with(st);
+      for (size_t i = 0; i < okr.size(); ++i)  // File::open / read failed: Io (log.rs:150-166)
+        if (!okr[i]) return abort_with(CASK_E_IO, srcs[b0 + i]);
+      R.bytes_in += off;
+      size_t k1 = k0;
+      while (k1 < ins.size() && ins[k1].src < b1) ++k1;
+      const uint64_t n = k1 - k0;
+      std::vector<uint32_t> src(n);
+      std::vector<uint64_t> pos(n), len(n);
+      std::vector<uint8_t> stv(n);
+      std::vector<uint32_t> ex(n), fd(n);
+      for (uint64_t k = 0; k < n; ++k) {
+        src[k] = ins[k0 + k].src - (uint32_t)b0;
+        pos[k] = ins[k0 + k].pos;
+      }
+      std::vector<uint64_t> blen(slen.begin() + b0, slen.begin() + b1);
+      st = cask_read_entries_device(ed->ctx, dsrc.data(), blen.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), n,
+                                    len.data(), stv.data(), ex.data(), fd.data());
+      if (st != CASK_OK) return abort_with(st);
+      for (uint64_t k = 0; k < n; ++k)  // in write order: the first failure is the reference's
+        if (stv[k] != CASK_ROW_OK)
+          return stv[k] == CASK_ROW_EOF ? abort_with(CASK_E_EOF, srcs[ins[k0 + k].src], pos[k])
+                                        : abort_with(CASK_E_CHECKSUM, srcs[ins[k0 + k].src], pos[k], ex[k], fd[k]);
+      t_verify += ms_since(tv);
+      // placement and the batch's bytes, gathered on the device in write order
+      auto tg = std::chrono::steady_clock::now();
+      std::vector<uint64_t> dst(n);
+      std::vector<uint32_t> len32(n);
+      std::vector<size_t> oi(n);
+      uint64_t total = 0;
+      for (uint64_t k = 0; k < n; ++k) {
+        oi[k] = place(len[k], true);
+        dst[k] = total;
+        len32[k] = (uint32_t)len[k];
+        total += len[k];
+      }
+      std::vector<uint8_t> host(total);
+      if (total) {
+        if (!ed->hint.ensure(total + 256)) return abort_with(CASK_E_NOMEM);
+        st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), dst.data(),
+                                len32.data(), n, ed->hint.p);
+        if (st == CASK_OK) st = cask_copy(ed->ctx, host.data(), ed->hint.p, total);
+        if (st != CASK_OK) return abort_with(st);
+      }
+      t_gather += ms_since(tg);
+      auto tw = std::chrono::steady_clock::now();
+      for (uint64_t k = 0; k < n;) {  // runs of records bound for one file: one write each
+        uint64_t e = k;
+        while (e < n && oi[e] == oi[k]) {
+          if (!append(oi[e], host.data() + dst[e], len[e])) return abort_with(CASK_E_IO, outs[oi[e]].fid);
+          ++e;
+        }
+        if (!write_all(outs[oi[k]].fd, host.data() + dst[k], dst[e - 1] + len[e - 1] - dst[k]))
+          return abort_with(CASK_E_IO, outs[oi[k]].fid);
+        k = e;
+      }
+      t_write += ms_since(tw);
+      k0 = k1;
+      b0 = b1;
     }
   }
-  for (size_t i = 0; i < out_files.size(); ++i) {
-    const uint32_t fid = out_files[i];
-    if (!write_raw(data_path(path, fid), out.data() + file_base[i], out_len[i]) ||
-        !write_file(hint_path(path, fid), hints[i], cask_xxh::xxh32(hints[i].data(), hints[i].size(), 0))) {
-      cleanup();
-      set_err(err, CASK_E_IO, fid);
-      return CASK_E_IO;
-    }
+  R.ms[1] = t_verify;
+  R.ms[2] = t_gather;
+  // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen order
+  auto tw = std::chrono::steady_clock::now();
+  for (size_t j = 0; j < nt; ++j) {
+    const std::string& kk = del_keys[j];
+    std::vector<uint8_t> rec(18 + kk.size());
+    wr64(rec.data() + 4, del_seq[j]);
+    wr16(rec.data() + 12, (uint16_t)kk.size());
+    wr32(rec.data() + 14, CASK_ENTRY_TOMBSTONE);
+    memcpy(rec.data() + 18, kk.data(), kk.size());
+    wr32(rec.data(), cask_xxh::xxh32(rec.data() + 4, 14 + kk.size(), 0));
+    const size_t o = place(rec.size(), false);
+    if (!append(o, rec.data(), rec.size()) || !write_all(outs[o].fd, rec.data(), rec.size()))
+      return abort_with(CASK_E_IO, outs[o].fid);
   }
-  R.ms[3] = ms_since(t3);
-  cleanup();
+  // hint files (HintWriter: body + XXH32 trailer), closed data files
+  for (OutFile& o : outs) {
+    if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
+      return abort_with(CASK_E_IO, o.fid);
+    close(o.fd);
+    o.fd = -1;
+    if (!write_file_raw2(hint_path(path, o.fid), o.hints.data(), o.hints.size(),
+                         cask_xxh::xxh32(o.hints.data(), o.hints.size(), 0)))
+      return abort_with(CASK_E_IO, o.fid);
+  }
+  t_write += ms_since(tw);
+  R.ms[3] = t_write;
+  uint64_t bytes_out = 0;
+  for (const OutFile& o : outs) bytes_out += o.len;
 
   // 6. compact_files (cask.rs:528-550): index the new files from their hints, drop the compacted
   // files' stats, swap the file sets
   auto t4 = std::chrono::steady_clock::now();
   for (uint32_t fid : new_files) {
-    const size_t i = (size_t)(std::find(out_files.begin(), out_files.end(), fid) - out_files.begin());
-    const std::vector<uint8_t>& hb = hints[i];
+    const OutFile& o = *std::find_if(outs.begin(), outs.end(), [&](const OutFile& x) { return x.fid == fid; });
+    const std::vector<uint8_t>& hb = o.hints;
     for (uint64_t p = 0; p < hb.size();) {
       const uint8_t* h = hb.data() + p;
       const uint16_t k = rd16(h + 8);
@@ -1256,7 +1221,7 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
   R.n_tomb_only = (uint32_t)tomb_files.size();
   R.live_records = ins.size();
   R.tombstones = nt;
-  R.bytes_out = out.size();
+  R.bytes_out = bytes_out;
   R.ms_total = ms_since(t0);
   if (res) *res = R;
   return CASK_OK;

@@ -756,6 +756,50 @@ __global__ __launch_bounds__(256) void k_gather(const GatherRec* __restrict__ re
   }
 }
 
+// K_read_entries (compaction, cask.rs:505-508 -> Log::read_entry, log.rs:150-166 ->
+// Entry::from_read, data.rs:161-206): the live records only, verified where the hints say they
+// are — not a re-scan of their files. One quad of lanes per record (quad_gbl_xxh32).
+__global__ __launch_bounds__(256) void k_read_entries(const uint64_t* __restrict__ pos, const uint32_t* __restrict__ src,
+                                                      uint64_t n, const uint8_t* const* __restrict__ srcs,
+                                                      const uint64_t* __restrict__ slen, uint64_t* len_out, uint8_t* st_out,
+                                                      uint32_t* exp_out, uint32_t* found_out) {
+  const uint32_t q = threadIdx.x & 3;
+  const uint64_t nq = (uint64_t)gridDim.x * (blockDim.x >> 2);
+  for (uint64_t r = blockIdx.x * (uint64_t)(blockDim.x >> 2) + (threadIdx.x >> 2); r < n; r += nq) {
+    const uint64_t p = pos[r];
+    const uint32_t s = src[r];
+    const uint64_t L = slen[s];
+    const uint8_t* d = srcs[s];
+    uint64_t rl = 0;
+    uint8_t st = kRowEof;
+    uint32_t stored = 0, got = 0;
+    if (p + 18 <= L) {  // read_exact(header) (data.rs:163)
+      stored = gld4(d + p);
+      rl = g_reclen(d + p);
+      if (p + rl <= L) {  // read_exact(key), read_exact(value) (data.rs:172,181)
+        got = quad_gbl_xxh32(d + p + 4, rl - 4, q);
+        st = got == stored ? kRowOk : kRowChecksum;  // data.rs:193-198
+      } else {
+        rl = 0;
+      }
+    }
+    if (q == 0) {
+      len_out[r] = rl;
+      st_out[r] = st;
+      exp_out[r] = stored;
+      found_out[r] = got;
+    }
+  }
+}
+
+void launch_read_entries(const uint64_t* pos, const uint32_t* src, uint64_t n, const uint8_t* const* srcs,
+                         const uint64_t* slen, uint64_t* len, uint8_t* st, uint32_t* expct, uint32_t* found, void* stream) {
+  if (!n) return;
+  uint64_t g = (n + 63) / 64;
+  if (g > 16384) g = 16384;
+  hipLaunchKernelGGL(k_read_entries, dim3((uint32_t)g), dim3(256), 0, S(stream), pos, src, n, srcs, slen, len, st, expct, found);
+}
+
 void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src, uint8_t* dst, void* stream) {
   if (!n) return;
   uint64_t g = (n + 3) / 4;

@@ -180,6 +180,15 @@ int cask_gather_device(cask_ctx* ctx, const uint8_t* const* srcs, uint32_t nsrc,
                        const uint64_t* pos, const uint64_t* dst_off, const uint32_t* len, uint64_t nrec,
                        uint8_t* dst);
 
+/* Log::read_entry + Entry::from_read at caller positions (log.rs:150-166, data.rs:161-206), on the
+ * device — what compaction does for each live record (cask.rs:505-508), without re-scanning whole
+ * files. Record r is read at byte pos[r] of source src[r] (srcs[src[r]]: device pointer to src_len
+ * bytes). Host arrays out: len[r] = 18 + ksz + vsz_eff (0 when the record runs past its source:
+ * UnexpectedEof), status[r] (CASK_ROW_*), expected[r] (stored checksum), found[r] (computed XXH32). */
+int cask_read_entries_device(cask_ctx* ctx, const uint8_t* const* srcs, const uint64_t* src_len, uint32_t nsrc,
+                             const uint32_t* src, const uint64_t* pos, uint64_t n, uint64_t* len, uint8_t* status,
+                             uint32_t* expected, uint32_t* found);
+
 /* XXH32 seed 0 on the host (util.rs:37-41) — convenience for bindings. */
 uint32_t cask_xxh32(const uint8_t* data, uint64_t len);
 
