@@ -96,6 +96,8 @@ def compact(ctx, torch, nfiles, workdir):
         with open(os.path.join(path, f"{i + 1:010}.cask.data"), "wb") as fh:
             fh.write(host.tobytes())
         del f, host
+        if (i + 1) % 8 == 0:
+            print(f"wrote {i + 1}/{nfiles} files", file=sys.stderr, flush=True)
     write_s = time.perf_counter() - t0
     del kid, last, present, tomb_key, vsz
     torch.cuda.empty_cache()
@@ -103,7 +105,9 @@ def compact(ctx, torch, nfiles, workdir):
                      f"deleted, 10 % of keys end in a tombstone), on disk, 1 GPU",
            "files": nfiles, "records": n, "bytes": nbytes, "write_files_s": write_s}
     t0 = time.perf_counter()
+    print(f"files written in {write_s:.1f} s; opening", file=sys.stderr, flush=True)
     with CaskOptions().max_file_size(1 << 30).open(path) as db:
+        print("opened; compacting", file=sys.stderr, flush=True)
         out["open_s"] = time.perf_counter() - t0
         out["open_timings_ms"] = db.open_timings()
         out["open_gibps_e2e"] = nbytes / out["open_s"] / 2 ** 30
@@ -135,6 +139,7 @@ def main():
     ap.add_argument("--max-file", type=int, default=2 ** 31)
     ap.add_argument("--files", type=int, default=4)
     ap.add_argument("--out", default="")
+    ap.add_argument("--dir", default=None, help="parent directory of the compaction database")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -145,7 +150,7 @@ def main():
         if w == "cfg3":
             r = cfg3(ctx, torch, args.steps, args.gib, args.max_file)
         else:
-            wd = tempfile.mkdtemp(prefix="cask_compact_")
+            wd = tempfile.mkdtemp(prefix="cask_compact_", dir=args.dir)
             try:
                 r = compact(ctx, torch, args.files, wd)
             finally:
