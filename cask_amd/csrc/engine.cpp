@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <regex>
@@ -60,8 +61,23 @@ inline uint64_t hash_key(const uint8_t* k, uint32_t n) {
 struct StatsEntry {  // stats.rs:7-11
   uint64_t entries = 0, dead_entries = 0, dead_bytes = 0;
 };
+using StatsMap = std::unordered_map<uint32_t, StatsEntry>;
 
-// HashMap<Vec<u8>, IndexEntry> + Stats (cask.rs:28-31). Open addressing; keys live in an
+// Stats::add_entry / remove_entry (stats.rs:23-48) into `st`. A fold on threads keeps per-table
+// deltas: then `base` is the map entering the fold, and a remove of a file absent from the delta
+// still counts when that file has a row there (remove_entry only skips files with no row at all).
+inline void stats_add(StatsMap& st, uint32_t file_id) { st[file_id].entries += 1; }
+inline void stats_remove(StatsMap& st, const StatsMap* base, uint32_t file_id, uint64_t size) {
+  auto it = st.find(file_id);
+  if (it == st.end()) {
+    if (!base || !base->count(file_id)) return;  // "Tried to reclaim non-existant entry": warn only
+    it = st.emplace(file_id, StatsEntry{}).first;
+  }
+  it->second.dead_entries += 1;
+  it->second.dead_bytes += size;
+}
+
+// One table of HashMap<Vec<u8>, IndexEntry> (cask.rs:28-31). Open addressing; keys live in an
 // append-only arena (the reference copies every key: hint.key.to_vec(), cask.rs:68).
 class KeyDir {
  public:
@@ -75,11 +91,11 @@ class KeyDir {
   std::vector<Slot> slots;
   std::vector<uint8_t> arena;
   uint64_t live = 0, used = 0;
-  std::unordered_map<uint32_t, StatsEntry> stats;
 
-  KeyDir() { slots.assign(1024, Slot{}); }
+  KeyDir() { slots.assign(256, Slot{}); }
 
   const uint8_t* key_of(const Slot& s) const { return arena.data() + s.key_off; }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[h & (slots.size() - 1)]); }
 
   int64_t find(const uint8_t* k, uint32_t n, uint64_t h) const {
     const uint64_t m = slots.size() - 1;
@@ -90,12 +106,16 @@ class KeyDir {
     }
   }
 
-  void grow() {
+  // Room for n live keys without growing; a rebuild drops the slots of deleted keys.
+  void reserve(uint64_t n) {
+    uint64_t cap = slots.size();
+    while (cap * 3 < (std::max(n, live) + 1) * 4) cap *= 2;
+    if (cap == slots.size() && (used + 1) * 4 <= cap * 3) return;
     std::vector<Slot> old;
     old.swap(slots);
-    slots.assign(old.size() * 2, Slot{});
+    slots.assign(cap, Slot{});
     used = 0;
-    const uint64_t m = slots.size() - 1;
+    const uint64_t m = cap - 1;
     for (const Slot& s : old) {
       if (s.state != 1) continue;
       uint64_t i = s.hash & m;
@@ -105,52 +125,12 @@ class KeyDir {
     }
   }
 
-  const cask_index_entry* get(const uint8_t* k, uint32_t n) const {  // Index::get (cask.rs:41-43)
-    const int64_t f = find(k, n, hash_key(k, n));
-    return f >= 0 ? &slots[(uint64_t)f].e : nullptr;
-  }
-
-  // Stats::add_entry / remove_entry (stats.rs:23-48)
-  void stats_add(uint32_t file_id) { stats[file_id].entries += 1; }
-  void stats_remove(uint32_t file_id, uint64_t size) {
-    auto it = stats.find(file_id);
-    if (it == stats.end()) return;  // "Tried to reclaim non-existant entry": warn only
-    it->second.dead_entries += 1;
-    it->second.dead_bytes += size;
-  }
-
-  // Room for n keys without growing.
-  void reserve(uint64_t n) {
-    uint64_t cap = 1024;
-    while (cap * 3 < (n + 1) * 4) cap *= 2;
-    if (cap > slots.size()) {
-      std::vector<Slot> old;
-      old.swap(slots);
-      slots.assign(cap, Slot{});
-      used = 0;
-      for (const Slot& s : old)
-        if (s.state == 1) insert_new(s);
-    }
-  }
-  // A key known to be absent (a live slot of another table).
-  void insert_new(const Slot& s0, const uint8_t* key = nullptr) {
-    const uint64_t m = slots.size() - 1;
-    uint64_t i = s0.hash & m;
-    while (slots[i].state) i = (i + 1) & m;
-    slots[i] = s0;
-    if (key) {
-      slots[i].key_off = arena.size();
-      arena.insert(arena.end(), key, key + s0.ksz);
-    }
-    ++used;
-  }
-
   // Index::update's effect on the keydir alone (cask.rs:60-90 without the Stats calls): the fold of
   // the sharded replay, whose stats come from per-file counts (cask_keydir_finish).
-  void update_kd(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+  void update_kd(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq,
+                 uint64_t h) {
     const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
-    const uint64_t h = hash_key(key, ksz);
-    if ((used + 1) * 4 > slots.size() * 3) grow();
+    if ((used + 1) * 4 > slots.size() * 3) reserve(live + live / 2 + 1);
     const int64_t f = find(key, ksz, h);
     if (f >= 0) {
       Slot& s = slots[f];
@@ -165,59 +145,92 @@ class KeyDir {
       return;
     }
     if (deleted) return;
-    Slot& s = slots[(uint64_t)(-f - 1)];
-    s.hash = h;
-    s.key_off = arena.size();
-    s.ksz = ksz;
-    s.state = 1;
-    s.e = cask_index_entry{file_id, 0, pos, 18ull + ksz + vsz_raw, seq};
-    arena.insert(arena.end(), key, key + ksz);
-    ++live;
-    ++used;
+    insert_at((uint64_t)(-f - 1), key, ksz, h, cask_index_entry{file_id, 0, pos, 18ull + ksz + vsz_raw, seq});
   }
 
   // Index::update (cask.rs:60-90). vsz_raw is the hint's value_size field.
-  void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
-    update_h(key, ksz, file_id, pos, vsz_raw, seq, hash_key(key, ksz));
-  }
-  void update_h(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq,
-                uint64_t h) {
+  void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq,
+              uint64_t h, StatsMap& st, const StatsMap* base) {
     const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
     cask_index_entry ie{};
     ie.file_id = file_id;
     ie.entry_pos = pos;
     ie.entry_size = 18ull + ksz + (deleted ? 0ull : (uint64_t)vsz_raw);  // data.rs:238-240
     ie.sequence = seq;
-    if ((used + 1) * 4 > slots.size() * 3) grow();
+    if ((used + 1) * 4 > slots.size() * 3) reserve(live + live / 2 + 1);
     int64_t f = find(key, ksz, h);
     if (f >= 0) {  // Occupied
       Slot& s = slots[f];
       if (s.e.sequence <= seq) {
-        stats_remove(s.e.file_id, s.e.entry_size);
+        stats_remove(st, base, s.e.file_id, s.e.entry_size);
         if (deleted) {
           s.state = 2;
           --live;
         } else {
-          stats_add(file_id);
+          stats_add(st, file_id);
           s.e = ie;
         }
       } else {
-        stats_add(file_id);
-        stats_remove(file_id, ie.entry_size);
+        stats_add(st, file_id);
+        stats_remove(st, base, file_id, ie.entry_size);
       }
       return;
     }
     if (deleted) return;  // Vacant + tombstone: nothing
-    stats_add(file_id);
-    Slot& s = slots[(uint64_t)(-f - 1)];
+    stats_add(st, file_id);
+    insert_at((uint64_t)(-f - 1), key, ksz, h, ie);
+  }
+
+ private:
+  void insert_at(uint64_t i, const uint8_t* key, uint32_t ksz, uint64_t h, const cask_index_entry& e) {
+    Slot& s = slots[i];
     s.hash = h;
     s.key_off = arena.size();
     s.ksz = ksz;
     s.state = 1;
-    s.e = ie;
+    s.e = e;
     arena.insert(arena.end(), key, key + ksz);
     ++live;
     ++used;
+  }
+};
+
+// The keydir (Index, cask.rs:28-95): kSub tables split by key hash, so a fold on threads writes each
+// table from one thread with no merge pass afterwards; one Stats map.
+class Index {
+ public:
+  static constexpr unsigned kSub = 64;
+  KeyDir sub[kSub];
+  StatsMap stats;
+
+  static unsigned sub_of(uint64_t h) { return (unsigned)(h >> 58); }
+  uint64_t live() const {
+    uint64_t n = 0;
+    for (const KeyDir& k : sub) n += k.live;
+    return n;
+  }
+  const cask_index_entry* get(const uint8_t* k, uint32_t n) const {  // Index::get (cask.rs:41-43)
+    return get_h(k, n, hash_key(k, n));
+  }
+  const cask_index_entry* get_h(const uint8_t* k, uint32_t n, uint64_t h) const {
+    const KeyDir& t = sub[sub_of(h)];
+    const int64_t f = t.find(k, n, h);
+    return f >= 0 ? &t.slots[(uint64_t)f].e : nullptr;
+  }
+  void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+    const uint64_t h = hash_key(key, ksz);
+    sub[sub_of(h)].update(key, ksz, file_id, pos, vsz_raw, seq, h, stats, nullptr);
+  }
+  void update_kd(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
+    const uint64_t h = hash_key(key, ksz);
+    sub[sub_of(h)].update_kd(key, ksz, file_id, pos, vsz_raw, seq, h);
+  }
+  void prefetch(uint64_t h) const { sub[sub_of(h)].prefetch(h); }
+  template <class F>
+  void for_each_live(F fn) const {
+    for (const KeyDir& t : sub)
+      for (const KeyDir::Slot& s : t.slots)
+        if (s.state == 1) fn(t, s);
   }
 };
 
@@ -573,65 +586,70 @@ struct FoldRec {
   uint32_t ksz;
 };
 
-// The replay fold of Cask::open (cask.rs:346-382) over every file's records at once, sharded by
-// key hash over threads. Index::update's outcome for a key depends only on that key's records in
-// order, and every shard sees its keys' records in replay order; Stats rows are per-file counters
-// (order-free sums), and during open every remove_entry follows an add_entry of the same key and
-// file, so no shard drops a remove the single fold would count. The shards' live keys and stats
-// rows then merge into `out`. Small replays fold on the calling thread.
-void parallel_fold(std::vector<FoldRec>& recs, KeyDir& out) {
+// Index::update over records in replay order (the open replay, cask.rs:346-382; compact_files'
+// re-index, cask.rs:528-536), on threads by key-hash table. Index::update's outcome for a key depends
+// only on that key's records in order, and each table sees its keys' records in replay order. Stats
+// rows are per-file counters (order-free sums): each table keeps deltas, summed at the end; a remove
+// counts when its file has a row in the delta or in the map entering the fold. The two differ from
+// one serial fold only if a key's entry pointed at a file with no stats row, which cannot happen:
+// every entry's file got its row when the entry was written, and compaction drops a file's row only
+// after re-indexing all of its live entries elsewhere. Small replays fold on the calling thread.
+void parallel_fold(FoldRec* recs, uint64_t n, Index& out) {
   const char* mv = getenv("CASK_PAR_FOLD_MIN");  // tuning/test knob: smallest replay folded in parallel
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
-  const unsigned nt = host_threads();
-  if (recs.size() < min_par || nt == 1 || out.live || !out.stats.empty()) {
-    for (const FoldRec& r : recs) out.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq);
+  const unsigned nt = std::min(host_threads(), Index::kSub);
+  if (n < min_par || nt == 1) {
+    for (uint64_t i = 0; i < n; ++i) {
+      const FoldRec& r = recs[i];
+      out.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq);
+    }
     return;
   }
-  const uint64_t n = recs.size();
-  // 1. hashes, and per (range, shard) lists of record indices, ranges in replay order
-  std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(nt));
+  constexpr unsigned S = Index::kSub;
+  // 1. hashes, and per (range, table) lists of record indices, ranges in replay order
+  std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(S));
   parallel_for(nt, [&](unsigned t) {
     const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    for (auto& l : lists[t]) l.reserve((hi - lo) / nt + 16);
+    for (auto& l : lists[t]) l.reserve((hi - lo) / S + 16);
     for (uint64_t i = lo; i < hi; ++i) {
       FoldRec& r = recs[i];
       r.hash = hash_key(r.key, r.ksz);
-      lists[t][(r.hash >> 40) % nt].push_back((uint32_t)(i - lo));
+      lists[t][Index::sub_of(r.hash)].push_back((uint32_t)(i - lo));
     }
   });
-  // 2. each shard folds its keys in replay order
-  std::vector<KeyDir> shard(nt);
+  // 2. each table folds its keys in replay order, stats into its own delta map
+  std::vector<StatsMap> delta(S);
   parallel_for(nt, [&](unsigned t) {
-    uint64_t cnt = 0;
-    for (unsigned g = 0; g < nt; ++g) cnt += lists[g][t].size();
-    shard[t].reserve(cnt / 2);
-    for (unsigned g = 0; g < nt; ++g) {
-      const uint64_t lo = n * g / nt;
-      for (uint32_t j : lists[g][t]) {
-        const FoldRec& r = recs[lo + j];
-        shard[t].update_h(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash);
+    for (unsigned q = t; q < S; q += nt) {
+      KeyDir& kd = out.sub[q];
+      uint64_t cnt = 0;
+      for (unsigned g = 0; g < nt; ++g) cnt += lists[g][q].size();
+      kd.reserve(kd.live + cnt / 2);
+      for (unsigned g = 0; g < nt; ++g) {
+        const uint64_t lo = n * g / nt;
+        const std::vector<uint32_t>& L = lists[g][q];
+        const size_t m = L.size();
+        for (size_t j = 0; j < m; ++j) {  // the record 16 ahead, and the slot and key of the one 8 ahead
+          if (j + 16 < m) __builtin_prefetch(&recs[lo + L[j + 16]]);
+          if (j + 8 < m) {
+            const FoldRec& a = recs[lo + L[j + 8]];
+            kd.prefetch(a.hash);
+            __builtin_prefetch(a.key);
+          }
+          const FoldRec& r = recs[lo + L[j]];
+          kd.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, delta[q], &out.stats);
+        }
       }
     }
   });
-  // 3. merge: disjoint key sets
-  uint64_t live = 0, keyb = 0;
-  for (const KeyDir& k : shard) {
-    live += k.live;
-    keyb += k.arena.size();
-  }
-  out.reserve(out.live + live);
-  out.arena.reserve(out.arena.size() + keyb);
-  for (const KeyDir& k : shard) {
-    for (const auto& sl : k.slots)
-      if (sl.state == 1) out.insert_new(sl, k.key_of(sl));
-    out.live += k.live;
-    for (const auto& kv : k.stats) {
+  // 3. stats deltas
+  for (const StatsMap& d : delta)
+    for (const auto& kv : d) {
       StatsEntry& e = out.stats[kv.first];
       e.entries += kv.second.entries;
       e.dead_entries += kv.second.dead_entries;
       e.dead_bytes += kv.second.dead_bytes;
     }
-  }
 }
 
 struct cask_db {
@@ -639,7 +657,7 @@ struct cask_db {
   cask_options opts{};
   int lock_fd = -1;
   std::vector<uint32_t> files;
-  KeyDir index;
+  Index index;
   uint64_t sequence = 0;
   uint32_t file_seq = 0;  // Log::file_id_seq: the last data file id at open (log.rs:63-69)
   double timings[5] = {0, 0, 0, 0, 0};
@@ -747,16 +765,24 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   std::vector<char> use_hint(nf, 0), data_ok(nf, 1);
   std::vector<uint32_t> scan_idx;
   std::vector<uint64_t> flen(nf, 0);
-  for (size_t i = 0; i < nf; ++i) {
-    const std::string hp = hint_path(path, db->files[i]);
-    if (is_file_follow(hp) && read_file(hp, hints[i]) && hints[i].size() >= 4) {
-      const size_t n = hints[i].size();
-      if (cask_xxh::xxh32(hints[i].data(), n - 4, 0) == rd32(hints[i].data() + n - 4)) {
-        use_hint[i] = 1;
-        continue;
+  {  // hint files read and checked on threads
+    const unsigned nt = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)nf));
+    parallel_for(nt, [&](unsigned t) {
+      for (size_t i = t; i < nf; i += nt) {
+        const std::string hp = hint_path(path, db->files[i]);
+        if (is_file_follow(hp) && read_file(hp, hints[i]) && hints[i].size() >= 4) {
+          const size_t n = hints[i].size();
+          if (cask_xxh::xxh32(hints[i].data(), n - 4, 0) == rd32(hints[i].data() + n - 4)) {
+            use_hint[i] = 1;
+            continue;
+          }
+        }
+        std::vector<uint8_t>().swap(hints[i]);
       }
-    }
-    hints[i].clear();
+    });
+  }
+  for (size_t i = 0; i < nf; ++i) {
+    if (use_hint[i]) continue;
     struct stat stt;
     if (stat(data_path(path, db->files[i]).c_str(), &stt) != 0) data_ok[i] = 0;
     else flen[i] = (uint64_t)stt.st_size;
@@ -825,30 +851,59 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   // scanned files up to that point are written on threads: each is its body + XXH32 trailer
   // (RecreateHints keeps draining after an error, so a failing file's hint file has every Ok row).
   double t_fold = 0;
-  std::vector<FoldRec> recs;  // the replay's fold, in order (parallel_fold)
+  std::unique_ptr<FoldRec[]> recs;  // the replay's fold, in order (parallel_fold); not zero-filled
   std::vector<uint32_t> to_write;
   int fail = CASK_OK;
   uint32_t fail_fid = 0;
   uint64_t fail_pos = 0;
   uint32_t fail_e = 0, fail_f = 0;
   auto tf = std::chrono::steady_clock::now();
+  // each file's hint body (a hint file's, or the one built for a scanned file), walked on threads:
+  // its record count, highest sequence and first short read (Hints::next / Hint::from_read,
+  // log.rs:437-447; data.rs:258-276)
+  struct Body {
+    const uint8_t* b = nullptr;
+    uint64_t n = 0, cnt = 0, max_seq = 0, bad = UINT64_MAX, base = 0;
+  };
+  std::vector<Body> bodies(nf);
+  for (size_t i = 0; i < nf; ++i) {
+    if (use_hint[i]) {
+      bodies[i].b = hints[i].data();
+      bodies[i].n = hints[i].size() - 4;  // Take(size - 4) (log.rs:129)
+    } else if (data_ok[i]) {
+      bodies[i].b = hbuf.data() + hs0[i];
+      bodies[i].n = hs1[i] - hs0[i];
+    }
+  }
+  const unsigned ntb = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)std::max<size_t>(nf, 1)));
+  parallel_for(ntb, [&](unsigned t) {
+    for (size_t i = t; i < nf; i += ntb) {
+      Body& B = bodies[i];
+      for (uint64_t p = 0; p < B.n;) {
+        if (B.n - p < 22 || B.n - p - 22 < rd16(B.b + p + 8)) {
+          B.bad = p;
+          break;
+        }
+        B.max_seq = std::max(B.max_seq, rd64(B.b + p));
+        ++B.cnt;
+        p += 22ull + rd16(B.b + p + 8);
+      }
+    }
+  });
+  // replay in ascending file order (cask.rs:348-369): the first Err aborts
+  size_t nrep = 0;
+  uint64_t total = 0;
   for (size_t i = 0; i < nf && fail == CASK_OK; ++i) {
     const uint32_t fid = db->files[i];
-    const uint8_t* hb;
-    uint64_t body;
-    if (use_hint[i]) {
-      hb = hints[i].data();
-      body = hints[i].size() - 4;  // Take(size - 4) (log.rs:129)
-    } else if (!data_ok[i]) {
-      // HintWriter::new truncated the hint file before Log::entries failed; its Drop then wrote
-      // the trailer of an empty body (log.rs:141-142, 389-395).
-      if (opts.write_hints) write_file(hint_path(path, fid), {}, cask_xxh::xxh32(nullptr, 0, 0));
-      fail = CASK_E_IO;
-      fail_fid = fid;
-      break;
-    } else {
-      hb = hbuf.data() + hs0[i];
-      body = hs1[i] - hs0[i];
+    if (!use_hint[i]) {
+      if (!data_ok[i]) {
+        // HintWriter::new truncated the hint file before Log::entries failed; its Drop then wrote
+        // the trailer of an empty body (log.rs:141-142, 389-395).
+        if (opts.write_hints) write_file(hint_path(path, fid), {}, cask_xxh::xxh32(nullptr, 0, 0));
+        fail = CASK_E_IO;
+        fail_fid = fid;
+        break;
+      }
       if (opts.write_hints) to_write.push_back((uint32_t)i);
       if (err_file == i) {  // the scan's first failing record is in this file
         fail = se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF;
@@ -859,21 +914,34 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
         break;
       }
     }
-    uint64_t p = 0;
-    while (p < body) {  // Hints::next / Hint::from_read (log.rs:437-447; data.rs:258-276)
-      if (body - p < 22 || body - p - 22 < rd16(hb + p + 8)) {
-        fail = CASK_E_EOF;
-        fail_fid = fid;
-        fail_pos = p;
-        break;
-      }
-      const uint8_t* h = hb + p;
-      const uint64_t s = rd64(h);
-      const uint16_t k = rd16(h + 8);
-      if (s > db->sequence) db->sequence = s;
-      recs.push_back(FoldRec{h + 22, rd64(h + 14), s, 0, fid, rd32(h + 10), k});
-      p += 22ull + k;
+    if (bodies[i].bad != UINT64_MAX) {
+      fail = CASK_E_EOF;
+      fail_fid = fid;
+      fail_pos = bodies[i].bad;
+      break;
     }
+    if (bodies[i].cnt && bodies[i].max_seq > db->sequence) db->sequence = bodies[i].max_seq;
+    bodies[i].base = total;
+    total += bodies[i].cnt;
+    nrep = i + 1;
+  }
+  if (fail == CASK_OK) {  // the fold's records, file by file on threads
+    recs.reset(new (std::nothrow) FoldRec[std::max<uint64_t>(total, 1)]);
+    if (!recs) fail = CASK_E_NOMEM;
+  }
+  if (fail == CASK_OK) {
+    parallel_for(ntb, [&](unsigned t) {
+      for (size_t i = t; i < nrep; i += ntb) {
+        const Body& B = bodies[i];
+        FoldRec* out = recs.get() + B.base;
+        for (uint64_t p = 0, j = 0; j < B.cnt; ++j) {
+          const uint8_t* h = B.b + p;
+          const uint16_t k = rd16(h + 8);
+          out[j] = FoldRec{h + 22, rd64(h + 14), rd64(h), 0, db->files[i], rd32(h + 10), k};
+          p += 22ull + k;
+        }
+      }
+    });
   }
   t_fold += ms_since(tf);
   auto th = std::chrono::steady_clock::now();
@@ -902,7 +970,7 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   }
   {  // Index::update + Stats over every record (the keys stay in hints[] / hbuf until here)
     auto tf2 = std::chrono::steady_clock::now();
-    parallel_fold(recs, db->index);
+    parallel_fold(recs.get(), total, db->index);
     t_fold += ms_since(tf2);
   }
   db->timings[3] = t_fold;
@@ -939,70 +1007,184 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
                              [&](uint32_t f) { return !std::binary_search(db->files.begin(), db->files.end(), f); }),
               files.end());
 
-  // 1. hints of each file with a valid hint file (files without one are skipped: cask.rs:456-468)
+  // 1. hints of each file with a valid hint file (files without one are skipped: cask.rs:456-468).
+  // Hints::next (log.rs:437-447) per file on threads: the record offsets (`hint?` aborts,
+  // cask.rs:483, the first bad file in order wins), then the keydir lookups (read-only), the live
+  // list and the tombstone tail in hint order.
   struct Ins {
     uint32_t src;  // index into `srcs`
     uint64_t pos;
   };
-  std::vector<uint32_t> compacted, srcs;      // srcs: compacted files with live records
-  std::vector<Ins> ins;
-  std::vector<std::string> del_keys;           // the tombstone tail, in first-seen order
-  std::vector<uint64_t> del_seq;
-  std::unordered_map<std::string, size_t> del_at;
-  for (uint32_t fid : files) {
+  struct HintFile {
     std::vector<uint8_t> hb;
-    const std::string hp = hint_path(path, fid);
-    if (!is_file_follow(hp) || !read_file(hp, hb) || hb.size() < 4 ||
-        cask_xxh::xxh32(hb.data(), hb.size() - 4, 0) != rd32(hb.data() + hb.size() - 4))
-      continue;
-    const uint64_t body = hb.size() - 4;
-    const uint32_t si = (uint32_t)srcs.size();
-    bool any = false;
-    // Hints::next (log.rs:437-447): record offsets first (`hint?` aborts, cask.rs:483), then the
-    // keydir lookups on threads (read-only), then the tail and the live list in hint order.
+    bool ok = false;
+    uint64_t bad = UINT64_MAX, base = 0, nlive = 0, ntomb = 0, ins0 = 0, tomb0 = 0;
     std::vector<uint64_t> offs;
-    for (uint64_t p = 0; p < body;) {
-      if (body - p < 22 || body - p - 22 < rd16(hb.data() + p + 8)) {
-        set_err(err, CASK_E_EOF, fid, p);
+    std::vector<uint8_t> kind;  // 1: live (cask.rs:500-502); 2: tombstone of an absent key (:487-499)
+  };
+  std::vector<uint32_t> compacted, srcs;  // srcs: compacted files with live records
+  std::vector<Ins> ins;
+  std::vector<uint8_t> del_key_bytes;     // the tombstone tail, in first-seen order
+  std::vector<uint64_t> del_key_off, del_seq;
+  {
+    const size_t nh = files.size();
+    std::vector<HintFile> hf(nh);
+    const unsigned ntf = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)std::max<size_t>(nh, 1)));
+    parallel_for(ntf, [&](unsigned t) {
+      for (size_t i = t; i < nh; i += ntf) {
+        HintFile& H = hf[i];
+        const std::string hp = hint_path(path, files[i]);
+        if (!is_file_follow(hp) || !read_file(hp, H.hb) || H.hb.size() < 4 ||
+            cask_xxh::xxh32(H.hb.data(), H.hb.size() - 4, 0) != rd32(H.hb.data() + H.hb.size() - 4)) {
+          std::vector<uint8_t>().swap(H.hb);
+          continue;
+        }
+        H.ok = true;
+        const uint64_t body = H.hb.size() - 4;
+        for (uint64_t p = 0; p < body;) {
+          if (body - p < 22 || body - p - 22 < rd16(H.hb.data() + p + 8)) {
+            H.bad = p;
+            break;
+          }
+          H.offs.push_back(p);
+          p += 22ull + rd16(H.hb.data() + p + 8);
+        }
+      }
+    });
+    uint64_t nrec = 0;
+    std::vector<size_t> used;  // indices into hf of the compacted files, in order
+    for (size_t i = 0; i < nh; ++i) {
+      if (!hf[i].ok) continue;
+      if (hf[i].bad != UINT64_MAX) {
+        set_err(err, CASK_E_EOF, files[i], hf[i].bad);
         return CASK_E_EOF;
       }
-      offs.push_back(p);
-      p += 22ull + rd16(hb.data() + p + 8);
+      hf[i].base = nrec;
+      nrec += hf[i].offs.size();
+      hf[i].kind.resize(hf[i].offs.size());
+      used.push_back(i);
     }
-    std::vector<uint8_t> kind(offs.size());  // 1: live (cask.rs:500-502); 2: tombstone of an absent key (:487-499)
-    auto classify = [&](uint64_t lo, uint64_t hi) {
-      for (uint64_t i = lo; i < hi; ++i) {
-        const uint8_t* h = hb.data() + offs[i];
-        const cask_index_entry* ie = db->index.get(h + 22, rd16(h + 8));
-        kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
-      }
-    };
     unsigned nt = host_threads();
     const char* mv = getenv("CASK_PAR_FOLD_MIN");  // the same knob as parallel_fold
-    if (offs.size() < (mv ? strtoull(mv, nullptr, 10) : (1ull << 16))) nt = 1;
-    parallel_for(nt, [&](unsigned t) { classify(offs.size() * t / nt, offs.size() * (t + 1) / nt); });
-    for (uint64_t i = 0; i < offs.size(); ++i) {
-      if (!kind[i]) continue;
-      const uint8_t* h = hb.data() + offs[i];
-      const uint64_t seq = rd64(h);
-      const uint16_t k = rd16(h + 8);
-      if (kind[i] == 2) {
-        std::string key((const char*)h + 22, k);
-        auto it = del_at.find(key);
-        if (it == del_at.end()) {
-          del_at.emplace(key, del_keys.size());
-          del_keys.push_back(std::move(key));
-          del_seq.push_back(seq);
-        } else if (del_seq[it->second] < seq) {
-          del_seq[it->second] = seq;
+    if (nrec < (mv ? strtoull(mv, nullptr, 10) : (1ull << 16))) nt = 1;
+    // keydir lookups over all the records, split evenly over threads
+    parallel_for(nt, [&](unsigned t) {
+      const uint64_t lo = nrec * t / nt, hi = nrec * (t + 1) / nt;
+      size_t u = 0;
+      while (u + 1 < used.size() && hf[used[u + 1]].base <= lo) ++u;
+      for (uint64_t g = lo; g < hi;) {
+        HintFile& H = hf[used[u]];
+        const uint64_t e = std::min<uint64_t>(hi, H.base + H.offs.size());
+        constexpr uint64_t D = 8;  // lookups in flight: hashes computed D records ahead, slots prefetched
+        uint64_t hr[D];
+        auto hash_at = [&](uint64_t i) {
+          const uint8_t* h = H.hb.data() + H.offs[i];
+          return hash_key(h + 22, rd16(h + 8));
+        };
+        const uint64_t i0 = g - H.base, i1 = e - H.base;
+        for (uint64_t i = i0; i < std::min(i1, i0 + D); ++i) {
+          hr[i % D] = hash_at(i);
+          db->index.prefetch(hr[i % D]);
         }
-      } else {
-        ins.push_back(Ins{si, rd64(h + 14)});
-        any = true;
+        for (uint64_t i = i0; i < i1; ++i) {
+          const uint8_t* h = H.hb.data() + H.offs[i];
+          const cask_index_entry* ie = db->index.get_h(h + 22, rd16(h + 8), hr[i % D]);
+          H.kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
+          if (i + D < i1) {
+            hr[i % D] = hash_at(i + D);
+            db->index.prefetch(hr[i % D]);
+          }
+        }
+        g = e;
+        ++u;
       }
+    });
+    const unsigned ntu = std::max(1u, std::min<unsigned>(nt, (unsigned)std::max<size_t>(used.size(), 1)));
+    parallel_for(ntu, [&](unsigned t) {
+      for (size_t j = t; j < used.size(); j += ntu) {
+        HintFile& H = hf[used[j]];
+        for (uint8_t k : H.kind) {
+          H.nlive += k == 1;
+          H.ntomb += k == 2;
+        }
+      }
+    });
+    uint64_t nins = 0, ntomb = 0;
+    for (size_t u : used) {
+      HintFile& H = hf[u];
+      compacted.push_back(files[u]);
+      H.ins0 = nins;
+      H.tomb0 = ntomb;
+      if (H.nlive) srcs.push_back(files[u]);
+      nins += H.nlive;
+      ntomb += H.ntomb;
     }
-    compacted.push_back(fid);
-    if (any) srcs.push_back(fid);
+    // the live list (hint order) and the tombstones of absent keys (hint order), file by file
+    struct Tomb {
+      const uint8_t* key;
+      uint64_t seq;
+      uint64_t hash;
+      uint32_t ksz;
+      uint32_t first;  // 1: the key's first tombstone (its place in the tail)
+    };
+    ins.resize(nins);
+    std::vector<Tomb> tombs(ntomb);
+    parallel_for(ntu, [&](unsigned t) {
+      for (size_t j = t; j < used.size(); j += ntu) {
+        const HintFile& H = hf[used[j]];
+        const uint32_t si = (uint32_t)(std::lower_bound(srcs.begin(), srcs.end(), files[used[j]]) - srcs.begin());
+        uint64_t a = H.ins0, d = H.tomb0;
+        for (uint64_t i = 0; i < H.kind.size(); ++i) {
+          if (!H.kind[i]) continue;
+          const uint8_t* h = H.hb.data() + H.offs[i];
+          if (H.kind[i] == 1) {
+            ins[a++] = Ins{si, rd64(h + 14)};
+          } else {
+            const uint16_t k = rd16(h + 8);
+            tombs[d++] = Tomb{h + 22, rd64(h), hash_key(h + 22, k), k, 0};
+          }
+        }
+      }
+    });
+    // the tail: each absent key once, at its first tombstone, with its highest sequence; keys
+    // deduplicated by hash-split tables on threads
+    constexpr unsigned S = Index::kSub;
+    std::vector<std::vector<uint64_t>> tl(S);
+    for (uint64_t i = 0; i < ntomb; ++i) tl[Index::sub_of(tombs[i].hash)].push_back(i);
+    const unsigned ntt = ntomb < 4096 ? 1u : std::min(nt, S);
+    parallel_for(ntt, [&](unsigned t) {
+      for (unsigned q = t; q < S; q += ntt) {
+        std::unordered_map<uint64_t, uint64_t> seen;  // hash -> the key's first tombstone
+        std::vector<uint64_t> more;                     // first tombstones of keys whose hash was taken
+        seen.reserve(tl[q].size());
+        auto same = [&](const Tomb& A, const Tomb& B) {
+          return A.hash == B.hash && A.ksz == B.ksz && (A.ksz == 0 || memcmp(A.key, B.key, A.ksz) == 0);
+        };
+        for (uint64_t i : tl[q]) {
+          Tomb& T = tombs[i];
+          auto ins_at = seen.emplace(T.hash, i);
+          uint64_t f = UINT64_MAX;
+          if (!ins_at.second) {
+            if (same(tombs[ins_at.first->second], T)) f = ins_at.first->second;
+            for (size_t m = 0; f == UINT64_MAX && m < more.size(); ++m)
+              if (same(tombs[more[m]], T)) f = more[m];
+            if (f == UINT64_MAX) more.push_back(i);
+          }
+          if (f == UINT64_MAX) {
+            T.first = 1;
+          } else if (tombs[f].seq < T.seq) {
+            tombs[f].seq = T.seq;
+          }
+        }
+      }
+    });
+    for (const Tomb& T : tombs) {
+      if (!T.first) continue;
+      del_key_off.push_back(del_key_bytes.size());
+      del_key_bytes.insert(del_key_bytes.end(), T.key, T.key + T.ksz);
+      del_seq.push_back(T.seq);
+    }
+    del_key_off.push_back(del_key_bytes.size());
   }
   R.ms[0] = ms_since(t0);
 
@@ -1013,7 +1195,7 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
   // gathered on the device in write order and appended to the new data files; then the tombstone
   // tail. On an error, the files this call created are removed and the reference's error returned.
   const size_t ns = srcs.size();
-  const size_t nt = del_keys.size();
+  const size_t nt = del_seq.size();
   struct OutFile {
     uint32_t fid;
     uint64_t len = 0;
@@ -1134,26 +1316,37 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
         len32[k] = (uint32_t)len[k];
         total += len[k];
       }
-      std::vector<uint8_t> host(total);
+      std::unique_ptr<uint8_t[]> host(new (std::nothrow) uint8_t[std::max<uint64_t>(total, 1)]);
+      if (!host) return abort_with(CASK_E_NOMEM);
       if (total) {
         if (!ed->hint.ensure(total + 256)) return abort_with(CASK_E_NOMEM);
         st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), dst.data(),
                                 len32.data(), n, ed->hint.p);
-        if (st == CASK_OK) st = cask_copy(ed->ctx, host.data(), ed->hint.p, total);
+        if (st == CASK_OK) st = cask_copy(ed->ctx, host.get(), ed->hint.p, total);
         if (st != CASK_OK) return abort_with(st);
       }
       t_gather += ms_since(tg);
       auto tw = std::chrono::steady_clock::now();
-      for (uint64_t k = 0; k < n;) {  // runs of records bound for one file: one write each
+      // runs of records bound for one file (placement only moves forward): each run's hints and its
+      // one write, runs on threads (distinct files)
+      std::vector<std::pair<uint64_t, uint64_t>> runs;
+      for (uint64_t k = 0; k < n;) {
         uint64_t e = k;
-        while (e < n && oi[e] == oi[k]) {
-          if (!append(oi[e], host.data() + dst[e], len[e])) return abort_with(CASK_E_IO, outs[oi[e]].fid);
-          ++e;
-        }
-        if (!write_all(outs[oi[k]].fd, host.data() + dst[k], dst[e - 1] + len[e - 1] - dst[k]))
-          return abort_with(CASK_E_IO, outs[oi[k]].fid);
+        while (e < n && oi[e] == oi[k]) ++e;
+        runs.emplace_back(k, e);
         k = e;
       }
+      std::vector<char> wok(runs.size(), 1);
+      const unsigned ntw = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)runs.size()));
+      parallel_for(ntw, [&](unsigned t) {
+        for (size_t r = t; r < runs.size(); r += ntw) {
+          const uint64_t k = runs[r].first, e = runs[r].second;
+          for (uint64_t j = k; j < e && wok[r]; ++j) wok[r] = append(oi[j], host.get() + dst[j], len[j]);
+          if (wok[r]) wok[r] = write_all(outs[oi[k]].fd, host.get() + dst[k], dst[e - 1] + len[e - 1] - dst[k]);
+        }
+      });
+      for (size_t r = 0; r < runs.size(); ++r)
+        if (!wok[r]) return abort_with(CASK_E_IO, outs[oi[runs[r].first]].fid);
       t_write += ms_since(tw);
       k0 = k1;
       b0 = b1;
@@ -1161,19 +1354,36 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
   }
   R.ms[1] = t_verify;
   R.ms[2] = t_gather;
-  // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen order
+  // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen
+  // order; one write per run of records bound for one file
   auto tw = std::chrono::steady_clock::now();
-  for (size_t j = 0; j < nt; ++j) {
-    const std::string& kk = del_keys[j];
-    std::vector<uint8_t> rec(18 + kk.size());
-    wr64(rec.data() + 4, del_seq[j]);
-    wr16(rec.data() + 12, (uint16_t)kk.size());
-    wr32(rec.data() + 14, CASK_ENTRY_TOMBSTONE);
-    memcpy(rec.data() + 18, kk.data(), kk.size());
-    wr32(rec.data(), cask_xxh::xxh32(rec.data() + 4, 14 + kk.size(), 0));
-    const size_t o = place(rec.size(), false);
-    if (!append(o, rec.data(), rec.size()) || !write_all(outs[o].fd, rec.data(), rec.size()))
-      return abort_with(CASK_E_IO, outs[o].fid);
+  {
+    std::vector<uint8_t> run;
+    size_t run_file = SIZE_MAX;
+    auto flush = [&]() -> bool {
+      if (run.empty()) return true;
+      const bool ok = write_all(outs[run_file].fd, run.data(), run.size());
+      run.clear();
+      return ok;
+    };
+    for (size_t j = 0; j < nt; ++j) {
+      const uint64_t ko = del_key_off[j], kn = del_key_off[j + 1] - ko;
+      uint8_t rec_h[18];
+      wr64(rec_h + 4, del_seq[j]);
+      wr16(rec_h + 12, (uint16_t)kn);
+      wr32(rec_h + 14, CASK_ENTRY_TOMBSTONE);
+      const size_t o = place(18 + kn, false);
+      if (o != run_file) {
+        if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
+        run_file = o;
+      }
+      const size_t at = run.size();
+      run.insert(run.end(), rec_h, rec_h + 18);
+      run.insert(run.end(), del_key_bytes.data() + ko, del_key_bytes.data() + ko + kn);
+      wr32(run.data() + at, cask_xxh::xxh32(run.data() + at + 4, 14 + kn, 0));
+      if (!append(o, run.data() + at, 18 + kn)) return abort_with(CASK_E_IO, outs[o].fid);
+    }
+    if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
   }
   // hint files (HintWriter: body + XXH32 trailer), closed data files
   for (OutFile& o : outs) {
@@ -1193,24 +1403,39 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
   // 6. compact_files (cask.rs:528-550): index the new files from their hints, drop the compacted
   // files' stats, swap the file sets
   auto t4 = std::chrono::steady_clock::now();
-  for (uint32_t fid : new_files) {
-    const OutFile& o = *std::find_if(outs.begin(), outs.end(), [&](const OutFile& x) { return x.fid == fid; });
-    const std::vector<uint8_t>& hb = o.hints;
-    for (uint64_t p = 0; p < hb.size();) {
-      const uint8_t* h = hb.data() + p;
-      const uint16_t k = rd16(h + 8);
-      db->index.update(h + 22, k, fid, rd64(h + 14), rd32(h + 10), rd64(h));
-      p += 22ull + k;
+  {
+    std::vector<FoldRec> recs;
+    recs.reserve(ins.size());
+    for (uint32_t fid : new_files) {
+      const OutFile& o = *std::find_if(outs.begin(), outs.end(), [&](const OutFile& x) { return x.fid == fid; });
+      const std::vector<uint8_t>& hb = o.hints;
+      for (uint64_t p = 0; p < hb.size();) {
+        const uint8_t* h = hb.data() + p;
+        const uint16_t k = rd16(h + 8);
+        recs.push_back(FoldRec{h + 22, rd64(h + 14), rd64(h), 0, fid, rd32(h + 10), k});
+        p += 22ull + k;
+      }
     }
+    parallel_fold(recs.data(), recs.size(), db->index);
   }
   for (uint32_t fid : compacted) db->index.stats.erase(fid);  // Stats::remove_files (stats.rs:50-54)
-  for (uint32_t fid : compacted) {  // Log::swap_files (log.rs:198-217)
-    db->files.erase(std::lower_bound(db->files.begin(), db->files.end(), fid));
-    if (unlink(data_path(path, fid).c_str()) != 0) {
-      set_err(err, CASK_E_IO, fid);
-      return CASK_E_IO;
+  {  // Log::swap_files (log.rs:198-217): the compacted files removed (on threads; the first failure
+     // in file order is the error, as the reference's loop would return it)
+    std::vector<char> gone(compacted.size(), 1);
+    const unsigned ntu = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)compacted.size()));
+    parallel_for(ntu, [&](unsigned t) {
+      for (size_t j = t; j < compacted.size(); j += ntu) {
+        gone[j] = unlink(data_path(path, compacted[j]).c_str()) == 0;
+        if (gone[j]) (void)unlink(hint_path(path, compacted[j]).c_str());
+      }
+    });
+    for (size_t j = 0; j < compacted.size(); ++j) {
+      db->files.erase(std::lower_bound(db->files.begin(), db->files.end(), compacted[j]));
+      if (!gone[j]) {
+        set_err(err, CASK_E_IO, compacted[j]);
+        return CASK_E_IO;
+      }
     }
-    (void)unlink(hint_path(path, fid).c_str());
   }
   db->files.insert(db->files.end(), new_files.begin(), new_files.end());
   std::sort(db->files.begin(), db->files.end());
@@ -1340,12 +1565,11 @@ int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
 int cask_keydir_finish(cask_db* db) {
   if (!db || !db->merging) return CASK_E_INVALID_ARG;
   std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> live;  // file -> (entries, bytes)
-  for (const auto& sl : db->index.slots)
-    if (sl.state == 1) {
-      auto& l = live[sl.e.file_id];
-      l.first += 1;
-      l.second += sl.e.entry_size;
-    }
+  db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& sl) {
+    auto& l = live[sl.e.file_id];
+    l.first += 1;
+    l.second += sl.e.entry_size;
+  });
   db->index.stats.clear();
   for (const auto& kv : db->terms) {
     const cask_db::ShardTerms& t = kv.second;
@@ -1507,43 +1731,45 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
 
 void cask_db_close(cask_db* db) { delete db; }
 
-uint64_t cask_db_len(const cask_db* db) { return db ? db->index.live : 0; }
+uint64_t cask_db_len(const cask_db* db) { return db ? db->index.live() : 0; }
 
 int cask_db_get_entry(const cask_db* db, const uint8_t* key, uint64_t ksz, cask_index_entry* out) {
   if (!db || (ksz && !key) || ksz > 0xFFFF) return 0;
-  int64_t f = db->index.find(key, (uint32_t)ksz, hash_key(key, (uint32_t)ksz));
-  if (f < 0) return 0;
-  if (out) *out = db->index.slots[f].e;
+  const cask_index_entry* e = db->index.get(key, (uint32_t)ksz);
+  if (!e) return 0;
+  if (out) *out = *e;
   return 1;
 }
 
 int64_t cask_db_export(const cask_db* db, uint8_t* key_bytes, uint64_t key_cap, uint64_t* key_off,
                        uint64_t* key_len, cask_index_entry* entries, uint64_t nkeys) {
   if (!db) return CASK_E_INVALID_ARG;
-  const KeyDir& ix = db->index;
-  std::vector<uint64_t> idx;
-  idx.reserve(ix.live);
-  for (uint64_t i = 0; i < ix.slots.size(); ++i)
-    if (ix.slots[i].state == 1) idx.push_back(i);
-  std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) {
-    const auto& A = ix.slots[a];
-    const auto& B = ix.slots[b];
+  struct Ref {
+    const uint8_t* key;
+    uint32_t ksz;
+    const cask_index_entry* e;
+  };
+  std::vector<Ref> idx;
+  idx.reserve(db->index.live());
+  db->index.for_each_live(
+      [&](const KeyDir& t, const KeyDir::Slot& s) { idx.push_back(Ref{t.key_of(s), s.ksz, &s.e}); });
+  std::sort(idx.begin(), idx.end(), [](const Ref& A, const Ref& B) {
     const uint32_t n = std::min(A.ksz, B.ksz);
-    int c = n ? memcmp(ix.key_of(A), ix.key_of(B), n) : 0;
+    int c = n ? memcmp(A.key, B.key, n) : 0;
     if (c) return c < 0;
     return A.ksz < B.ksz;
   });
   uint64_t total = 0;
-  for (uint64_t j = 0; j < idx.size(); ++j) total += ix.slots[idx[j]].ksz;
+  for (const Ref& r : idx) total += r.ksz;
   if (nkeys < idx.size() || (key_bytes && key_cap < total)) return CASK_E_CAPACITY;
   uint64_t off = 0;
   for (uint64_t j = 0; j < idx.size(); ++j) {
-    const auto& s = ix.slots[idx[j]];
-    if (key_bytes && s.ksz) memcpy(key_bytes + off, ix.key_of(s), s.ksz);
+    const Ref& r = idx[j];
+    if (key_bytes && r.ksz) memcpy(key_bytes + off, r.key, r.ksz);
     if (key_off) key_off[j] = off;
-    if (key_len) key_len[j] = s.ksz;
-    if (entries) entries[j] = s.e;
-    off += s.ksz;
+    if (key_len) key_len[j] = r.ksz;
+    if (entries) entries[j] = *r.e;
+    off += r.ksz;
   }
   return (int64_t)total;
 }

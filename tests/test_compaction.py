@@ -127,6 +127,51 @@ def test_oracle_compact_select_defaults(tmp_path):
     assert not trig and files == [1]  # small file, no trigger
 
 
+# ----------------------------------------------------------------------------- engine, hint path (CPU)
+@pytest.mark.parametrize("threads", [1, 3, 16])
+@pytest.mark.parametrize("seed", [31, 32])
+def test_engine_open_from_hints_matches_oracle(native, tmp_path, seed, threads, monkeypatch):
+    """Every data file has a valid hint file, so Cask::open folds hints only (log.rs:121-135) and
+    no device is needed: the keydir fold (Index::update + Stats, cask.rs:60-90) on 1, 3 and 16 host
+    threads, split by key hash, against the restatement's replay."""
+    from cask_amd import CaskOptions
+    monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0")
+    monkeypatch.setenv("CASK_HOST_THREADS", str(threads))
+    rng = random.Random(seed)
+    path, ref = _both(tmp_path, _workload(rng, 20000, 1500, del_p=0.2), 32 << 10)
+    rdb = R.replay(ref)
+    with CaskOptions().max_file_size(32 << 10).open(path) as db:
+        assert db.files() == rdb.files
+        assert db.stats() == {f: tuple(s) for f, s in rdb.index.stats.map.items()}
+        got = db.index()
+        assert len(got) == len(rdb.index.map) == len(db)
+        for k, v in rdb.index.map.items():
+            e = got[k]
+            assert (e.file_id, e.entry_pos, e.entry_size, e.sequence) == (v.file_id, v.entry_pos, v.entry_size,
+                                                                           v.sequence)
+
+
+def test_engine_open_bad_hint_body(native, tmp_path):
+    """A hint file whose trailer checks but whose body ends inside a record: open() fails with the
+    reference's UnexpectedEof (Hint::from_read's read_exact, data.rs:258-276), as the restatement's
+    replay does."""
+    from cask_amd import CaskOptions
+    from cask_amd.errors import UnexpectedEof
+    rng = random.Random(5)
+    path = str(tmp_path / "db")
+    files = R.write_log(path, _workload(rng, 500, 50), max_file_size=8 << 10)
+    hp = R.hint_file_path(path, files[1])
+    body = open(hp, "rb").read()[:-4][:-3]  # cut the last hint short
+    with open(hp, "wb") as f:
+        f.write(body + R.xxhash32(body).to_bytes(4, "little"))
+    ref = str(tmp_path / "ref")
+    shutil.copytree(path, ref)
+    rerr = R.replay(ref).error
+    with pytest.raises(UnexpectedEof) as ei:
+        CaskOptions().open(path)
+    assert rerr.kind == "eof" and ei.value.file_id == rerr.file_id == files[1]
+
+
 # ----------------------------------------------------------------------------- engine (GPU)
 def _both(tmp_path, ents, max_file_size, drop_hints=()):
     path = str(tmp_path / "db")
