@@ -110,6 +110,9 @@ SIGNATURES = [
     ("cask_last_dense", C.c_int, [C.c_void_p]),
     ("cask_encode_synthetic_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),
+    ("cask_log_write", C.c_int64, [C.c_char_p, C.c_uint32, C.c_uint64, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_uint64]),
     ("cask_encode_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("cask_xxh32", C.c_uint32, [C.c_void_p, C.c_uint64]),

@@ -1729,6 +1729,117 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
   return db;
 }
 
+// LogWriter::write (log.rs:282-306) for a batch of entries written through one writer that is then
+// dropped — a bulk load. EntryWriter's bytes (Entry::write_bytes, data.rs:90-121) are encoded and
+// checksummed on the device (cask_encode_device); HintWriter's records (Hint::write_bytes,
+// data.rs:242-256) and its trailer on Drop (log.rs:367-395) are built per file on host threads.
+// Rollover: a new file when there is no writer or pos + size > max_file_size (a record larger than
+// the limit gets a file of its own). File ids are first_file_id, first_file_id + 1, ...
+int64_t cask_log_write(const char* dir_c, uint32_t first_file_id, uint64_t max_file_size, int write_hints, int device,
+                       uint64_t n, const uint64_t* seq, const uint16_t* ksz, const uint32_t* vsz_raw,
+                       const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
+                       uint32_t* file_ids, uint64_t cap) {
+  if (!dir_c || (n && (!seq || !ksz || !vsz_raw || !key_off || !val_off))) return CASK_E_INVALID_ARG;
+  const std::string dir = dir_c;
+  if (!n) return 0;  // the writer is created by the first write (log.rs:282-290)
+  // 1. placement: file of each record and its position there; key/value extents to upload
+  std::vector<uint64_t> goff(n), fpos(n);
+  std::vector<uint64_t> fstart;  // first record of each file
+  uint64_t total = 0, pos = 0, kend = 0, vend = 0;
+  for (uint64_t r = 0; r < n; ++r) {
+    const uint64_t ve = vsz_raw[r] == CASK_ENTRY_TOMBSTONE ? 0 : vsz_raw[r];
+    const uint64_t size = 18ull + ksz[r] + ve;  // Entry::size (data.rs:63-65)
+    if (fstart.empty() || pos + size > max_file_size) {
+      fstart.push_back(r);
+      pos = 0;
+    }
+    goff[r] = total;
+    fpos[r] = pos;
+    pos += size;
+    total += size;
+    kend = std::max(kend, key_off[r] + ksz[r]);
+    vend = std::max(vend, ve ? val_off[r] + ve : 0);
+  }
+  if ((kend && !keys) || (vend && !vals)) return CASK_E_INVALID_ARG;
+  const uint64_t nf = fstart.size();
+  if ((uint64_t)first_file_id + nf - 1 > UINT32_MAX) return CASK_E_INVALID_ARG;
+  fstart.push_back(n);
+  // 2. the bytes, encoded on the device
+  std::unique_ptr<uint8_t[]> host(new (std::nothrow) uint8_t[total]);
+  if (!host) return CASK_E_NOMEM;
+  {
+    EngineDev* ed = engine_dev(device);
+    if (!ed) return CASK_E_DEVICE;
+    std::lock_guard<std::mutex> g(ed->mu);
+    int st = ed->prepare();
+    if (st != CASK_OK) return st;
+    auto al = [](uint64_t b) { return (b + 255) & ~255ull; };
+    const uint64_t a8 = al(8 * n), a4 = al(4 * n), a2 = al(2 * n);
+    if (!ed->rows.ensure(4 * a8 + a4 + a2) || !ed->hint.ensure(al(kend) + al(vend) + 256) ||
+        !ed->data.ensure(total + 256))
+      return CASK_E_NOMEM;
+    uint8_t* R = ed->rows.p;
+    uint64_t* d_off = (uint64_t*)R;
+    uint64_t* d_seq = (uint64_t*)(R + a8);
+    uint64_t* d_koff = (uint64_t*)(R + 2 * a8);
+    uint64_t* d_voff = (uint64_t*)(R + 3 * a8);
+    uint32_t* d_vsz = (uint32_t*)(R + 4 * a8);
+    uint16_t* d_ksz = (uint16_t*)(R + 4 * a8 + a4);
+    uint8_t* d_keys = ed->hint.p;
+    uint8_t* d_vals = ed->hint.p + al(kend);
+    bool ok = hipSetDevice(device) == hipSuccess &&
+              hipMemcpy(d_off, goff.data(), 8 * n, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_seq, seq, 8 * n, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_koff, key_off, 8 * n, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_voff, val_off, 8 * n, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_vsz, vsz_raw, 4 * n, hipMemcpyHostToDevice) == hipSuccess &&
+              hipMemcpy(d_ksz, ksz, 2 * n, hipMemcpyHostToDevice) == hipSuccess &&
+              (!kend || hipMemcpy(d_keys, keys, kend, hipMemcpyHostToDevice) == hipSuccess) &&
+              (!vend || hipMemcpy(d_vals, vals, vend, hipMemcpyHostToDevice) == hipSuccess);
+    if (!ok) return CASK_E_DEVICE;
+    st = cask_encode_device(ed->ctx, n, d_off, d_seq, d_ksz, d_vsz, d_keys, d_koff, d_vals, d_voff, ed->data.p);
+    if (st == CASK_OK) st = cask_copy(ed->ctx, host.get(), ed->data.p, total);
+    if (st != CASK_OK) return st;
+  }
+  // 3. each file's data bytes and hint file, files on threads
+  std::vector<char> fok(nf, 1);
+  const unsigned nt = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)nf));
+  parallel_for(nt, [&](unsigned t) {
+    for (uint64_t f = t; f < nf; f += nt) {
+      const uint32_t fid = first_file_id + (uint32_t)f;
+      const uint64_t r0 = fstart[f], r1 = fstart[f + 1];
+      const uint64_t b0 = goff[r0], b1 = r1 < n ? goff[r1] : total;
+      int fd = open(data_path(dir, fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+      bool ok = fd >= 0;
+      for (uint64_t b = b0; ok && b < b1;) {
+        const ssize_t w = write(fd, host.get() + b, b1 - b);
+        if (w < 0 && errno == EINTR) continue;
+        ok = w > 0;
+        if (ok) b += (uint64_t)w;
+      }
+      if (fd >= 0) close(fd);
+      if (ok && write_hints) {
+        std::vector<uint8_t> hb;
+        for (uint64_t r = r0; r < r1; ++r) {
+          uint8_t h[22];
+          wr64(h, seq[r]);
+          wr16(h + 8, ksz[r]);
+          wr32(h + 10, vsz_raw[r]);  // the hint's value_size: 0xFFFFFFFF for a tombstone (data.rs:246-250)
+          wr64(h + 14, fpos[r]);
+          hb.insert(hb.end(), h, h + 22);
+          hb.insert(hb.end(), host.get() + goff[r] + 18, host.get() + goff[r] + 18 + ksz[r]);
+        }
+        ok = write_file_raw2(hint_path(dir, fid), hb.data(), hb.size(), cask_xxh::xxh32(hb.data(), hb.size(), 0));
+      }
+      fok[f] = ok;
+    }
+  });
+  for (uint64_t f = 0; f < nf; ++f)
+    if (!fok[f]) return CASK_E_IO;
+  for (uint64_t f = 0; f < nf && f < cap && file_ids; ++f) file_ids[f] = first_file_id + (uint32_t)f;
+  return (int64_t)nf;
+}
+
 void cask_db_close(cask_db* db) { delete db; }
 
 uint64_t cask_db_len(const cask_db* db) { return db ? db->index.live() : 0; }

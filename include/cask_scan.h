@@ -172,6 +172,19 @@ int cask_encode_device(cask_ctx* ctx, uint64_t nrec, const uint64_t* off, const 
                        const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
                        uint8_t* out);
 
+/* Bulk load through one LogWriter that is then dropped (LogWriter::write rollover, log.rs:282-306;
+ * EntryWriter / HintWriter, log.rs:317-395): entries r = 0..n-1 in write order (host memory; key r =
+ * keys[key_off[r] .. +ksz[r]], value r = vals[val_off[r] .. +vsz_raw[r]], vsz_raw = CASK_ENTRY_TOMBSTONE
+ * for a deletion) are encoded and checksummed on `device` (Entry::write_bytes, data.rs:90-121) and
+ * written to data files first_file_id, first_file_id + 1, ... in `dir`, each with its hint file
+ * (hints + XXH32 trailer) when write_hints. Replaces the per-entry Log::append_entry /
+ * LogWriter::write loop (log.rs:168-183, 282-306) for a batch. Returns the number of files
+ * written (their ids in file_ids[0..min(count, cap))) or a negative status. */
+int64_t cask_log_write(const char* dir, uint32_t first_file_id, uint64_t max_file_size, int write_hints, int device,
+                       uint64_t n, const uint64_t* seq, const uint16_t* ksz, const uint32_t* vsz_raw,
+                       const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
+                       uint32_t* file_ids, uint64_t cap);
+
 /* Compaction rewrite (Cask::compact_files_aux, cask.rs:505-513; LogWriter::write, log.rs:282-306):
  * nrec records copied byte for byte into dst (device memory). Record r is len[r] bytes of source
  * file src[r] (device pointer srcs[src[r]]) from byte pos[r], written at dst[dst_off[r]]. The

@@ -482,8 +482,8 @@ int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint3
   orc_xxh32_state hint_hasher;
   orc_xxh32_reset(&hint_hasher, 0);
   uint64_t pos = 0;
-  int stop = 0;
-  while (limit > 0 && !stop) {
+  int draining = 0;  /* after the first InvalidChecksum: RecreateHints::drop's drain */
+  while (limit > 0) {
     uint64_t before = limit;
     /* Entry::from_read (data.rs:161-206): three Vec allocations per record */
     uint8_t* header = (uint8_t*)calloc(18, 1);
@@ -523,8 +523,8 @@ int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint3
     uint64_t read_bytes = before - limit;
     res->bytes += read_bytes;
     if (hash != stored) {
-      /* InvalidChecksum aborts open() at the `?` (cask.rs:365); the drain that follows in
-       * RecreateHints::drop is not part of the timed replay. */
+      /* InvalidChecksum aborts open() at the `?` (cask.rs:365): no more folding. RecreateHints::drop
+       * (log.rs:466-470) then drains the iterator: later Ok records still get their hints. */
       if (!res->err_kind) {
         res->err_kind = ORC_ROW_CHECKSUM;
         res->err_file_id = file_id;
@@ -532,7 +532,7 @@ int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint3
         res->err_expected = stored;
         res->err_found = hash;
       }
-      stop = 1;
+      draining = 1;
     } else {
       uint64_t seq = rd64(header + 4);
       /* HintWriter::write: Hint::write_bytes into the file (5 write(2)) and the hasher. */
@@ -553,10 +553,12 @@ int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint3
         write_all_fd(hfd, key, ksz);
         orc_xxh32_update(&hint_hasher, key, ksz);
       }
-      /* Cask::open closure (cask.rs:349-355) */
-      if (seq > res->max_seq) res->max_seq = seq;
-      orc_index_update(ix, key, ksz, file_id, pos, deleted ? ORC_ENTRY_TOMBSTONE : vsz_raw, seq);
-      res->records++;
+      /* Cask::open closure (cask.rs:349-355), until the first error */
+      if (!draining) {
+        if (seq > res->max_seq) res->max_seq = seq;
+        orc_index_update(ix, key, ksz, file_id, pos, deleted ? ORC_ENTRY_TOMBSTONE : vsz_raw, seq);
+        res->records++;
+      }
     }
     pos += read_bytes;
     free(header); free(key); free(value);

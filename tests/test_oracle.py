@@ -171,12 +171,12 @@ def test_c_oracle_faithful_replay(oracle_lib, case, tmp_path):
         hp = str(tmp_path / f"{fe['file_id']}.hint")
         r = O.replay_faithful(R.data_file_path(os.path.join(GOLDEN, case), fe["file_id"]), hp, fe["file_id"], ix)
         seq = max(seq, int(r.max_seq))
+        with open(hp, "rb") as f:  # on a failing file too: RecreateHints::drop drains (log.rs:466-470)
+            assert f.read().hex() == fe["recreated_hint_hex"]
         if r.err_kind:
             err = {"kind": {1: "checksum", 2: "eof"}[r.err_kind], "file_id": int(r.err_file_id),
                    "pos": int(r.err_pos), "expected": int(r.err_expected), "found": int(r.err_found)}
             break
-        with open(hp, "rb") as f:
-            assert f.read().hex() == fe["recreated_hint_hex"]
     assert seq == rep["sequence"]
     if rep["error"] is None:
         assert err is None
