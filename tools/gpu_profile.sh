@@ -22,4 +22,11 @@ rm -rf "$R/gpurun_out/prof_$TAG"
 TAILN=1 step prof_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG/kt" -o kt --output-format csv -- python3 $B
 step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_$TAG/fetch" -o fetch --output-format csv -- python3 $B
 step prof_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/prof_$TAG/write" -o write --output-format csv -- python3 $B
-find "$R/gpurun_out/prof_$TAG" -name "*.csv" | head -20
+if [ -n "$CFG2" ]; then  # configs[2] (32 GiB Zipf): the same three passes over tools/bench_configs.py cfg3
+  C="$R/tools/bench_configs.py cfg3 --steps 2"
+  rm -rf "$R/gpurun_out/prof_${TAG}_cfg2"
+  TAILN=1 step cfg2_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${TAG}_cfg2/kt" -o kt --output-format csv -- python3 $C
+  step cfg2_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_${TAG}_cfg2/fetch" -o fetch --output-format csv -- python3 $C
+  step cfg2_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/prof_${TAG}_cfg2/write" -o write --output-format csv -- python3 $C
+fi
+find "$R/gpurun_out/prof_$TAG"* -name "*.csv" | head -20

@@ -47,6 +47,9 @@ def main():
         lines.append(f"{k},{nf.get(k, 0)},{avg:.0f},{f2:.0f},{w:.0f},{f2 + w:.0f}")
     with open(os.path.join(out, f"{tag}_pmc_traffic.csv"), "w") as f:
         f.write("\n".join(lines) + "\n")
+    if len(sys.argv) > 2 and sys.argv[2] == "--no-json":  # another workload (e.g. configs[2]): tables only
+        print("\n".join(lines))
+        return
     scan = next(k for k in table if k.startswith("k_scan_chunks"))
     with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
         json.dump({"kernel": scan, "hbm_bytes_per_launch": table[scan]["hbm_bytes"],
