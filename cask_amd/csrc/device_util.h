@@ -224,6 +224,13 @@ __device__ __forceinline__ uint32_t quad_xxh32(const uint32_t* w, uint32_t xs, u
   return lds_tail_fin(w, xs + (nstr << 4), len & 15, h + len);
 }
 
+// A value every lane holds equally (read from the same LDS word), moved to scalar registers so
+// that the loops and branches it controls compile to scalar control flow.
+__device__ __forceinline__ uint64_t uni64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((uint64_t)hi << 32) | lo;
+}
+
 // Unaligned global loads: gfx950 runs in unaligned-access mode, so these memcpys become
 // global_load_dwordx4 / global_load_dword at any byte address.
 __device__ __forceinline__ u32x4 gld16(const uint8_t* p) {
@@ -310,6 +317,8 @@ __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
 // contiguous bytes per instruction, 4 blocks ahead), quad_transpose hands every lane its word of
 // the block's four stripes. The four lanes must be active together and call with the same p/len;
 // all four return the hash.
+// D: blocks in flight per quad (64 B each; k_long_hash: 4 / 8 / 16 = 7.0 / 6.26 / 6.2 ms on configs[2]).
+template <uint32_t D = 8>
 __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t len, uint32_t q) {
   const uint64_t nstr = len >> 4;
   uint32_t h;
@@ -317,7 +326,6 @@ __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t le
     uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
     const uint64_t nblk = nstr >> 2;
     if (nblk) {
-      constexpr uint32_t D = 8;  // blocks in flight per quad (64 B each; 4 / 8 / 16: 7.0 / 6.26 / 6.2 ms on configs[2])
       const uint8_t* lp = p + 16 * q;
       u32x4 A[D];
 #pragma unroll

@@ -442,8 +442,8 @@ struct EngineDev {
       return true;
     }
   } data, rows, hint;
-  static constexpr int kReaders = 4, kSlots = 2;
-  static constexpr size_t kSlotBytes = 64ull << 20;
+  static constexpr int kReaders = 8, kSlots = 2;
+  static constexpr size_t kSlotBytes = 32ull << 20;
   void* pin[kReaders][kSlots] = {};
   hipStream_t rs[kReaders] = {};
   hipEvent_t ev[kReaders][kSlots] = {};
@@ -469,7 +469,7 @@ struct EngineDev {
     return CASK_OK;
   }
 
-  // Reader thread t takes every kReaders-th 64-MiB piece of the files, alternating between its two
+  // Reader thread t takes every kReaders-th 32-MiB piece of the files, alternating between its two
   // pinned slots: pread into one while the other's copy to the device is in flight.
   int read_to_device(const std::vector<std::string>& paths, const std::vector<cask_file_view>& v, std::vector<char>& ok) {
     struct Piece {

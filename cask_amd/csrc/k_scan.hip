@@ -202,13 +202,6 @@ __device__ __forceinline__ bool quad_row(const uint32_t* W, const ChunkPos& c, u
   return fail;
 }
 
-// A value every lane holds equally (read from the same LDS word), moved to scalar registers so
-// that the loops and branches it controls compile to scalar control flow.
-__device__ __forceinline__ uint64_t uni64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-  return ((uint64_t)hi << 32) | lo;
-}
-
 // ceil(a / b) for 0 < b < a <= 2^16 (wave-uniform): a float quotient, corrected to the exact one.
 __device__ __forceinline__ uint32_t ceil_div_small(uint32_t a, uint32_t b) {
   uint32_t c = (uint32_t)__builtin_ceilf((float)a / (float)b);

@@ -1,0 +1,406 @@
+// k_walk_runs — the speculative pass for logs of long records (walk mode), gfx950.
+//
+// k_scan_chunks stages every byte of a chunk to find and verify the records that start in it; on a
+// log whose bytes are mostly in records longer than ScanArgs::big (configs[2]: Zipf value sizes up
+// to 64 KiB, 96 % of the bytes in records > 2 KiB) those bytes are then read a second time by
+// k_long_hash. Here a wave walks a run of chunks by chasing record headers (Entries::next,
+// log.rs:403-429: each record starts where the previous one ends; a KiB staged in LDS per round
+// trip) and hashes every record itself from HBM (Entry::from_read's check, data.rs:185-198), a quad
+// of lanes per record, 16 records of one length class at a time — so every byte is read once and
+// the latency of the chase is hidden behind other waves' hashing. Records over kWalkHashMax are
+// left to k_long_hash.
+//
+// The output is the chunk table and slot rows of k_scan_chunks (spec, exit, count, long_r, cerr,
+// long_done, slot rows; never a regular chunk), so k_finish, the validation/repair passes and
+// k_long_hash run unchanged: a run's first start is speculative and k_finish checks it
+// (spec[c] == T[c]) like any other.
+//
+// First start of a run (its first chunk's c0 != 0): the lowest offset >= c0 holding a record of at
+// most kSearchShort bytes whose XXH32 matches (pass A, windows staged in LDS); then, going back, the
+// lowest offset >= c0 whose header gives a record longer than kSearchShort that ends exactly at the
+// start found (repeated: a chain of long records before the first verified one).
+#include "device_util.h"
+
+#include <stdlib.h>
+
+namespace cask_dev {
+
+constexpr uint32_t kWalkWin = 4096;                   // LDS window (16-B aligned)
+constexpr uint32_t kWalkUse = kWalkWin - 16;          // bytes usable from any start in the window
+constexpr uint32_t kSearchShort = 2048;               // pass A verifies records up to this long
+constexpr uint32_t kStepA = kWalkUse - 18;            // candidate offsets per pass-A window
+constexpr uint32_t kStepB = kWalkUse - 18;            // candidate offsets per hop-back window
+constexpr uint32_t kSearchPast = 1u << 20;            // pass A looks this far past the run's end
+constexpr uint32_t kLongList = 256;                   // pass A's long candidates kept for the hop back
+constexpr uint32_t kBatch = 16;                       // records hashed together (one per quad)
+// The records k_scan_chunks would hash out of LDS (lds_hashed: at most `big` bytes) are hashed here,
+// a quad per record, 16 records per batch; longer ones go to k_long_hash, which keeps far more bytes
+// in flight per CU than a walking wave can (hashing them here measured 12.8 ms against 4.5 + 6.6 ms
+// on configs[2]). A wave's batch outlives its runs (a row's verdict goes to LDS while its run is the
+// wave's current one, else straight to the chunk table), so every flush is full.
+constexpr uint32_t kClasses = 1;
+
+struct WalkEnt {
+  const uint8_t* rec;  // the record's first byte
+  uint32_t rl, st;     // length, stored checksum
+  uint32_t t, r;       // chunk, row
+  u32x4 row;
+};
+
+#ifdef CASK_STAMPS  // diagnostic build: per-wave s_memtime sums -> a.stamps[0..7] (tools/walk_stamps.py)
+#define WST(v) const uint64_t v = __builtin_amdgcn_s_memtime();
+#define WADD(i, v) wst[i] += __builtin_amdgcn_s_memtime() - (v);
+#define WCNT(i) wst[i] += 1;
+#else
+#define WST(v)
+#define WADD(i, v)
+#define WCNT(i)
+#endif
+
+struct WalkLds {
+  uint32_t win[kWalkWin / 4 + 16];
+  uint64_t spec[kMaxRun], exitv[kMaxRun];
+  uint32_t cnt[kMaxRun], lr[kMaxRun], cerr[kMaxRun];
+  WalkEnt ent[kClasses][kBatch];
+  uint32_t cand[64];             // pass A: plausible short candidates of a block, in offset order
+  uint64_t lx[kLongList], le[kLongList];  // pass A: long candidates x and their ends x + rl
+};
+
+// Stage the window whose first usable byte is file byte wb: NL 16-B loads per lane (NL KiB), the
+// file bytes [wb, min(wb + NL KiB - 16, len)) readable. Returns the LDS byte index of wb.
+template <uint32_t NL>
+__device__ __forceinline__ uint32_t walk_stage(uint32_t* W, const uint8_t* data, uint64_t len, uint64_t wb) {
+  constexpr uint32_t use = NL * 1024 - 16;
+  const uintptr_t g = (uintptr_t)(data + wb), a0 = g & ~(uintptr_t)15;
+  const uint64_t we = (wb + use < len) ? wb + use : len;
+  const uintptr_t aend = ((uintptr_t)(data + we) + 15) & ~(uintptr_t)15;
+  const uint32_t n16 = (uint32_t)((aend - a0) >> 4);  // >= 1: wb < len
+  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+  const gu32x4* src = (const gu32x4*)a0;
+  u32x4 v[NL];
+#pragma unroll
+  for (uint32_t k = 0; k < NL; ++k) {
+    const uint32_t i = threadIdx.x + 64 * k;
+    v[k] = src[i < n16 ? i : n16 - 1];
+  }
+  __syncthreads();  // every lane is done with the previous window
+#pragma unroll
+  for (uint32_t k = 0; k < NL; ++k) {
+    const uint32_t i = threadIdx.x + 64 * k;
+    ((u32x4*)W)[i < n16 ? i : n16 - 1] = v[k];
+  }
+  __syncthreads();
+  return (uint32_t)(g - a0);
+}
+constexpr uint32_t kSearchNL = kWalkWin / 1024;  // the search's windows: 4 KiB
+constexpr uint32_t kChaseNL = 1;                 // the chase's windows: 1 KiB
+constexpr uint32_t kChaseUse = kChaseNL * 1024 - 16;
+
+// The first record start >= b0 of the chain, speculatively (see the file comment); kNone if pass A
+// finds no verified short record before min(len, b1 + kSearchPast).
+// Pass A, per 64 offsets: every lane decodes the header at its offset; the offsets whose record is
+// at most kSearchShort long and fits the file are hashed 16 at a time by quads (from LDS when the
+// record is staged, else from HBM), in offset order, until one matches its stored checksum. Offsets
+// whose record is longer and ends within the search horizon are listed (x, x + rl) for the hop back,
+// so it needs no second pass over the bytes (random bytes give an end that close ~1e-5 of the time).
+__device__ uint64_t walk_search(WalkLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
+  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
+  const uint64_t lim = (b1 + kSearchPast < len) ? b1 + kSearchPast : len;
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes < this one
+  uint64_t kA = kNone;
+  uint32_t nl = 0;  // long candidates listed
+  bool over = false;  // the list overflowed: the hop back rescans instead
+  for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kStepA) {
+    const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
+    const uint64_t wend = (wb + kWalkUse < len) ? wb + kWalkUse : len;  // staged bytes end here
+    for (uint32_t k0 = 0; k0 < kStepA; k0 += 64) {
+      const uint64_t x = wb + k0 + lane;
+      bool shortc = false, longc = false;
+      uint64_t rl = 0;
+      if (k0 + lane < kStepA && x < lim && x + 18 <= len) {
+        rl = lds_reclen(L.win, x0 + k0 + lane);
+        shortc = rl <= kSearchShort && x + rl <= len;
+        longc = rl > kSearchShort && x + rl <= lim;
+      }
+      const unsigned long long ml = __ballot(longc);
+      if (ml) {  // append in offset order
+        const uint32_t at = nl + (uint32_t)__builtin_popcountll(ml & below);
+        if (longc && at < kLongList) {
+          L.lx[at] = x;
+          L.le[at] = x + rl;
+        }
+        nl += (uint32_t)__builtin_popcountll(ml);
+        if (nl > kLongList) over = true;
+      }
+      unsigned long long ms = __ballot(shortc);
+      while (ms && kA == kNone) {  // the next 16 short candidates, one per quad
+        if (shortc) {
+          const uint32_t rk = (uint32_t)__builtin_popcountll(ms & below);
+          if (rk < 16) L.cand[rk] = k0 + lane;
+        }
+        __syncthreads();
+        const uint32_t nc = (uint32_t)__builtin_popcountll(ms) < 16 ? (uint32_t)__builtin_popcountll(ms) : 16u;
+        bool ok = false;
+        if (q < nc) {
+          const uint32_t ko = L.cand[q];
+          const uint64_t xc = wb + ko;
+          const uint64_t rlc = lds_reclen(L.win, x0 + ko);
+          const uint32_t st = lds_u32(L.win, x0 + ko);
+          const uint32_t h = (xc + rlc <= wend) ? quad_xxh32(L.win, x0 + ko + 4, (uint32_t)rlc - 4, qa)
+                                                 : quad_gbl_xxh32<2>(data + xc + 4, rlc - 4, qa);
+          ok = qa == 0 && h == st;
+        }
+        const unsigned long long mo = __ballot(ok);
+        if (mo) kA = wb + L.cand[__builtin_ctzll(mo) >> 2];  // quads are in offset order
+        __syncthreads();
+        // drop the 16 candidates just tried
+        for (uint32_t d = 0; d < nc; ++d) ms &= ms - 1;
+        if (shortc && !((ms >> lane) & 1ull)) shortc = false;
+      }
+      if (kA != kNone) break;
+    }
+  }
+  if (kA == kNone) return kNone;
+  // hop back over long records ending exactly at the current target: from the list (it holds every
+  // long candidate before kA whose end is in the horizon), or by rescanning if it overflowed
+  uint64_t target = kA;
+  for (int it = 0; it < 64; ++it) {
+    uint64_t found = kNone;
+    if (!over) {
+      const uint32_t n = nl < kLongList ? nl : kLongList;
+      for (uint32_t i0 = 0; i0 < n && found == kNone; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const bool hit = i < n && L.lx[i] < target && L.le[i] == target;
+        const unsigned long long m = __ballot(hit);
+        if (m) found = L.lx[i0 + __builtin_ctzll(m)];
+      }
+    } else {
+      for (uint64_t wb = b0; wb < target && found == kNone; wb += kStepB) {
+        const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
+        for (uint32_t k0 = 0; k0 < kStepB; k0 += 64) {
+          const uint64_t x = wb + k0 + lane;
+          bool hit = false;
+          if (k0 + lane < kStepB && x < target && x + 18 <= len) {
+            const uint64_t rl = lds_reclen(L.win, x0 + k0 + lane);
+            hit = rl > kSearchShort && x + rl == target;
+          }
+          const unsigned long long m = __ballot(hit);
+          if (m) {
+            found = wb + k0 + (uint64_t)__builtin_ctzll(m);
+            break;
+          }
+        }
+      }
+    }
+    if (found == kNone) break;
+    target = found;
+  }
+  return target;
+}
+
+// Hash class k's batch: quad q takes entry q; its row goes out with the verdict (data.rs:193-198).
+// A failing row of chunk t lowers the chunk's first failing row: in LDS while t is in the wave's
+// current segment [t0, t1) (written out with the segment), else in the chunk table.
+__device__ void walk_flush(WalkLds& L, const ScanArgs& a, uint32_t k, uint32_t n, uint64_t t0, uint64_t t1,
+                           uint64_t* wst) {
+  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
+  WST(tf0)
+  __syncthreads();
+  if (q < n) {  // whole quads
+    const WalkEnt e = L.ent[k][q];
+    const uint32_t h = quad_gbl_xxh32<2>(e.rec + 4, e.rl - 4, qa);
+    if (qa == 0) {
+      u32x4 row = e.row;
+      if (h != e.st) {
+        row.w |= kSlotBad;
+        if (e.t >= t0 && e.t < t1) atomicMin(&L.cerr[e.t - t0], e.r);
+        else atomicMin(&a.cerr[e.t], e.r);
+      }
+      *(u32x4*)(a.slots + ((uint64_t)e.t * a.slot_cap + e.r) * 4) = row;
+    }
+  }
+  __syncthreads();
+  WADD(2, tf0)
+}
+
+// One stretch of a run inside one file: chunks [t0, t1) of file fd.
+__device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, uint64_t t0, uint64_t t1,
+                             uint32_t* nbk, uint64_t* wst) {
+  const uint32_t lane = threadIdx.x;
+  const uint32_t nch = (uint32_t)(t1 - t0);
+  const uint64_t CH = a.chunk, len = fd.len;
+  const uint8_t* data = fd.data;
+  const uint64_t b0 = (t0 - fd.first_chunk) * CH;
+  const uint64_t b1 = ((t1 - fd.first_chunk) * CH < len) ? (t1 - fd.first_chunk) * CH : len;
+  if (lane < nch) {
+    L.spec[lane] = kNone;
+    L.exitv[lane] = 0;
+    L.cnt[lane] = 0;
+    L.lr[lane] = 0xFFFFFFFFu;
+    L.cerr[lane] = 0xFFFFFFFFu;
+  }
+  __syncthreads();
+  WST(ts0)
+  uint64_t p = uni64(b0 == 0 ? 0 : walk_search(L, data, len, b0, b1));
+  WADD(0, ts0)
+  if (b0) { WCNT(6) }
+  // the chase: uniform state of the chunk the chain is in
+  uint32_t cj = 0xFFFFFFFFu, cn = 0;  // current chunk (segment index) and its rows so far
+  uint64_t wb = 0, wv = 0;  // the chase's window: file bytes [wb, wv) at LDS byte x0
+  uint32_t x0 = 0;
+  while (p != kNone && p < b1) {
+    const uint32_t j = (uint32_t)((p - b0) / CH);
+    if (j != cj) {  // the chain enters chunk j: the previous chunk's rows and exit are final
+      if (cj != 0xFFFFFFFFu && lane == 0) {
+        L.cnt[cj] = cn;
+        L.exitv[cj] = p;
+      }
+      cj = j;
+      cn = 0;
+      if (lane == 0) L.spec[j] = p;
+    }
+    WCNT(5)
+    const uint32_t off = (uint32_t)(p - b0 - (uint64_t)j * CH);
+    const uint32_t r = cn++;
+    u32x4 row = u32x4{0u, 0u, 0u, off << 16};
+    bool fail = false, eof = false;
+    uint64_t rl = 0;
+    uint32_t stored = 0;
+    if (p + 18 > len) {
+      fail = eof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163)
+    } else {
+      if (p < wb || p + 18 > wv) {  // the header is not staged: one round trip brings the next KiB
+        WST(tw0)
+        x0 = walk_stage<kChaseNL>(L.win, data, len, p);
+        WADD(1, tw0)
+        WCNT(4)
+        wb = p;
+        wv = (p + kChaseUse < len) ? p + kChaseUse : len;
+      }
+      Hdr h = lds_hdr(L.win, x0 + (uint32_t)(p - wb));  // wave-uniform: into scalar registers
+      h.stored = __builtin_amdgcn_readfirstlane(h.stored);
+      h.seq = uni64(h.seq);
+      h.ksz = __builtin_amdgcn_readfirstlane(h.ksz);
+      h.vsz = __builtin_amdgcn_readfirstlane(h.vsz);
+      stored = h.stored;
+      row = u32x4{(uint32_t)h.seq, (uint32_t)(h.seq >> 32), h.vsz, h.ksz | (off << 16)};
+      rl = 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
+      if (p + rl > len) fail = eof = true;  // key/value cut short (data.rs:172,181)
+    }
+    const uint64_t c0j = b0 + (uint64_t)j * CH;
+    const uint64_t wend = (c0j + a.win < len) ? c0j + a.win : len;
+    const uint32_t k = (!eof && lds_hashed(p, rl, wend, a.big)) ? 0u : kClasses;
+    if (k == kClasses) {  // the row goes out now: an EOF row, or a record left to k_long_hash
+      if (lane == 0) {
+        *(u32x4*)(a.slots + ((t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
+        if (fail) atomicMin(&L.cerr[j], r);
+        else atomicMin(&L.lr[j], r);
+      }
+    } else {  // hashed with its class's batch
+      if (lane == 0) L.ent[k][nbk[k]] = WalkEnt{data + p, (uint32_t)rl, stored, (uint32_t)(t0 + j), r, row};
+      if (++nbk[k] == kBatch) {
+        walk_flush(L, a, k, kBatch, t0, t1, wst);
+        nbk[k] = 0;
+      }
+    }
+    if (eof) {
+      if (lane == 0) {
+        L.cnt[j] = cn;
+        L.exitv[j] = kTerm;
+      }
+      cj = 0xFFFFFFFFu;
+      break;
+    }
+    p += rl;
+  }
+  if (cj != 0xFFFFFFFFu && lane == 0) {
+    L.cnt[cj] = cn;
+    L.exitv[cj] = p;  // >= b1, the end of the segment's last chunk
+  }
+  __syncthreads();
+  if (lane < nch) {
+    const uint64_t t = t0 + lane;
+    const uint64_t sp = L.spec[lane];
+    a.spec[t] = sp;
+    a.exit[t] = sp == kNone ? 0ull : L.exitv[lane];
+    a.count[t] = L.cnt[lane];
+    a.long_r[t] = L.lr[lane];
+    a.cerr[t] = L.cerr[lane];
+    a.long_done[t] = 0;
+  }
+  // the table entries are stored before any later batch flush lowers a.cerr[t] with an atomic
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __syncthreads();
+}
+
+// Persistent grid of single-wave workgroups; runs of a.run chunks claimed from ctr->run_next.
+__global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __restrict__ files) {
+  __shared__ WalkLds L;
+  uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  uint32_t nbk[kClasses];  // entries waiting in each class's batch (wave-uniform)
+  for (uint32_t k = 0; k < kClasses; ++k) nbk[k] = 0;
+  WST(tk0)
+  const uint64_t R = a.run;
+  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  for (;;) {
+    uint32_t r = 0;
+    if (threadIdx.x == 0) r = atomicAdd(&a.ctr->run_next, 1u);
+    r = __shfl(r, 0, 64);
+    if (r >= nruns) break;
+    uint64_t t = (uint64_t)r * R;
+    const uint64_t tend = (t + R < a.total_chunks) ? t + R : a.total_chunks;
+    while (t < tend) {
+      const uint32_t fi = find_file(files, a.nfiles, t);
+      const FileDesc fd = files[fi];
+      const uint64_t fend = fd.first_chunk + fd.nchunks;
+      const uint64_t se = fend < tend ? fend : tend;
+      walk_segment(L, a, fd, t, se, nbk, wst);
+      t = se;
+    }
+  }
+  for (uint32_t k = 0; k < kClasses; ++k)  // the partial batches: verdicts to the chunk table
+    if (nbk[k]) walk_flush(L, a, k, nbk[k], 0, 0, wst);
+#ifdef CASK_STAMPS
+  WADD(3, tk0)
+  if (a.stamps && threadIdx.x == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[i], (unsigned long long)wst[i]);
+#endif
+}
+
+// Mean record length at the head of each file (at most 64 files, 32 records each, exact from
+// offset 0): out[0] bytes, out[1] records. The host picks the walk mode from it.
+__global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out) {
+  const uint32_t f = threadIdx.x;
+  uint64_t bytes = 0, recs = 0;
+  if (f < nfiles && f < 64) {
+    const FileDesc fd = files[(uint64_t)f * nfiles / (nfiles < 64 ? nfiles : 64)];
+    uint64_t p = 0;
+    for (int k = 0; k < 32 && p + 18 <= fd.len; ++k) {
+      const uint64_t rl = g_reclen(fd.data + p);
+      if (p + rl > fd.len) break;
+      bytes += rl;
+      ++recs;
+      p += rl;
+    }
+  }
+  if (recs) {
+    atomicAdd(&out[0], (unsigned long long)bytes);
+    atomicAdd(&out[1], (unsigned long long)recs);
+  }
+}
+
+void launch_walk_runs(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  // CASK_WALK_WAVES (tuning knob): waves per CU of the persistent grid
+  static const uint32_t per_cu = getenv("CASK_WALK_WAVES") ? (uint32_t)atoi(getenv("CASK_WALK_WAVES")) : 16u;
+  uint64_t grid = (uint64_t)device_cus() * per_cu;
+  if (grid > nruns) grid = nruns;
+  hipLaunchKernelGGL(k_walk_runs, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
+}
+
+void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {
+  hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, files, nfiles, out);
+}
+
+}  // namespace cask_dev

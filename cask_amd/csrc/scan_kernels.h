@@ -147,6 +147,9 @@ __host__ __device__ __forceinline__ bool lds_hashed(uint64_t p, uint64_t rl, uin
 }
 
 constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
+// Walk mode (k_walk.hip): chunks per run, and the mean record length (bytes, sampled at the heads
+// of the files by k_probe) from which a call takes it.
+constexpr uint32_t kWalkRun = 64, kWalkMean = 1024;
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
 struct SummaryHead {
@@ -190,6 +193,8 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
               const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz, const uint16_t* ksz, const uint8_t* status,
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
+void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: the walk-mode speculative pass
+void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,
                          const uint16_t* ksz, const uint32_t* vsz_raw, const uint64_t* key_id,

@@ -113,6 +113,9 @@ struct cask_ctx {
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
   int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
+  int last_walk = 0;   // the last call's speculative pass was k_walk_runs
+  uint64_t probe_sig = 0;  // files of the last k_probe, and its answer
+  bool probe_walk = false;
   std::mutex mu;
   char last_error[256] = {0};
   ~cask_ctx() {
@@ -204,6 +207,8 @@ int cask_last_timings(const cask_ctx* c, float* ms6) {
 }
 
 int cask_last_dense(const cask_ctx* c) { return c ? c->last_dense : 0; }
+
+int cask_last_walk(const cask_ctx* c) { return c ? c->last_walk : 0; }
 
 int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
   if (!c || !c5) return CASK_E_INVALID_ARG;
@@ -394,9 +399,52 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   c->last_error[0] = 0;
   (void)hipGetLastError();  // drop any stale error another library left on this thread
   H(hipMemcpyAsync(d_files, fd, fd_bytes + call_bytes, hipMemcpyHostToDevice, st), "file table H2D");
+  // Walk mode (k_walk_runs: header chase, long bodies read once, by k_long) when the records at the
+  // heads of the files average kWalkMean bytes or more: k_probe, once per set of files (the answer
+  // is cached on the context; it decides speed only). CASK_SCAN_MODE=walk|chunk (test and tuning
+  // knob) forces a mode.
+  bool walk = false;
+  {
+    const char* mode = getenv("CASK_SCAN_MODE");
+    if (mode && !strcmp(mode, "walk")) {
+      walk = true;
+    } else if (mode && !strcmp(mode, "chunk")) {
+      walk = false;
+    } else if (total_chunks) {
+      uint64_t sig = 0x9E3779B97F4A7C15ull ^ nfiles;
+      for (uint32_t i = 0; i < nfiles; ++i) {
+        sig = (sig ^ (uint64_t)(uintptr_t)files[i].data) * 0xBF58476D1CE4E5B9ull;
+        sig = (sig ^ files[i].len) * 0x94D049BB133111EBull;
+        sig ^= sig >> 31;
+      }
+      if (sig != c->probe_sig) {
+        unsigned long long* d = c->err2.as<unsigned long long>();
+        unsigned long long hp[2] = {0, 0};
+        H(hipMemsetAsync(d, 0, 16, st), "probe memset");
+        launch_probe(d_files, nfiles, d, st);
+        L("k_probe");
+        H(hipMemcpyAsync(hp, d, 16, hipMemcpyDeviceToHost, st), "probe D2H");
+        H(hipStreamSynchronize(st), "probe sync");
+        if (!ok) return CASK_E_DEVICE;
+        c->probe_sig = sig;
+        c->probe_walk = hp[1] && hp[0] >= kWalkMean * hp[1];
+      }
+      walk = c->probe_walk;
+    }
+  }
+  if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
+    const char* wr = getenv("CASK_WALK_RUN");
+    a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : kWalkRun;
+  }
+  c->last_walk = walk ? 1 : 0;
   H(hipEventRecord(c->ev[1], st));
-  launch_scan_chunks(a, c->geo, st);
-  L("k_scan_chunks");
+  if (walk) {
+    launch_walk_runs(a, st);
+    L("k_walk_runs");
+  } else {
+    launch_scan_chunks(a, c->geo, st);
+    L("k_scan_chunks");
+  }
   H(hipEventRecord(c->ev[2], st));
   if (dense) {
     launch_finish(a, st);

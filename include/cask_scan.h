@@ -152,6 +152,9 @@ int cask_last_counters(const cask_ctx* ctx, uint64_t* c5);
 /* 1 if the last cask_scan_device / cask_scan_host call took the two-kernel dense path (k_scan_chunks
  * + k_finish: every speculated chunk start held), 0 if it went through the repair path. */
 int cask_last_dense(const cask_ctx* ctx);
+/* 1 if the last call's speculative pass was the walk mode (k_walk_runs: record headers chased from
+ * HBM, chosen when the records at the heads of the files average >= 1 KiB), 0 for k_scan_chunks. */
+int cask_last_walk(const cask_ctx* ctx);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Batched record encoder (Entry::write_bytes, data.rs:90-121) — the bulk write path and the   */

@@ -69,15 +69,20 @@ def cfg2(gpu_ctx):
 
 
 @pytest.mark.timeout(600)
-def test_cfg2_full_size_against_generator(gpu_ctx, cfg2):
+@pytest.mark.parametrize("mode", ["chunk", "walk"])
+def test_cfg2_full_size_against_generator(gpu_ctx, cfg2, mode, monkeypatch):
+    """Both speculative passes: k_scan_chunks (forced) and k_walk_runs (what the library picks for
+    these records), every row against the generator."""
     import torch
+    monkeypatch.setenv("CASK_SCAN_MODE", mode)
     files, vsz, n, rl = cfg2
     dev = vsz.device
     rows = gpu_ctx.alloc_rows(n + 16)
     res = gpu_ctx.scan_device([(f.file_id, f.data) for f, _ in files], rows)
     assert res.error is None and res.count == n
     cnt = gpu_ctx.last_counters()
-    assert cnt["walked"] == 0 and cnt["long_records"] > 1_000_000, cnt
+    assert cnt["walked"] == 0 and cnt["walk_mode"] == (mode == "walk"), cnt
+    assert cnt["long_records"] > 1_000_000 if mode == "chunk" else cnt["dense_path"] == 1, cnt
     assert sum(f.data.numel() for f, _ in files) > 31 * 2 ** 30 and len(files) >= 16
     assert int((rows["status"][:n] != 0).sum().item()) == 0
     assert bool((rows["seq"][:n].to(torch.int64) == torch.arange(1, n + 1, device=dev)).all())
@@ -117,18 +122,25 @@ def test_cfg2_full_size_corrupted_against_oracle(gpu_ctx, cfg2):
     off = torch.cumsum(rlf, 0) - rlf
     r = int(torch.nonzero(rlf > 4096).flatten()[100])
     f.data[int(off[r]) + 14] ^= 0x01  # value_size low byte: the chain after this record changes
-    res = gpu_ctx.scan_device([(fd.file_id, fd.data) for fd, _ in files])
     hosts = [fd.data.cpu().numpy() for fd, _ in files]
     with cf.ThreadPoolExecutor(max_workers=min(16, os.cpu_count() or 4)) as ex:
         want = list(ex.map(O.scan, hosts))  # ctypes releases the GIL: files scan in parallel
     first = None
     for i, ((fd, _), w) in enumerate(zip(files, want)):
-        _assert_rows_equal(_dev_rows(res, res.file_rows(i)), w, f"file {fd.file_id}")
         bad = np.nonzero(w["status"] != 0)[0]
         if first is None and bad.size:
             b = w[bad[0]]
             first = (int(b["status"]), fd.file_id, int(b["pos"]), int(b["expected"]),
                      int(b["found"]) if int(b["status"]) == 1 else 0)
     assert len(flipped) >= 12
-    e = res.error
-    assert (e.kind, e.file_id, e.pos, e.expected, e.found) == first
+    for mode in ("chunk", "walk"):  # both speculative passes
+        os.environ["CASK_SCAN_MODE"] = mode
+        try:
+            res = gpu_ctx.scan_device([(fd.file_id, fd.data) for fd, _ in files])
+            assert gpu_ctx.last_counters()["walk_mode"] == (mode == "walk")
+        finally:
+            del os.environ["CASK_SCAN_MODE"]
+        for i, ((fd, _), w) in enumerate(zip(files, want)):
+            _assert_rows_equal(_dev_rows(res, res.file_rows(i)), w, f"{mode}: file {fd.file_id}")
+        e = res.error
+        assert (e.kind, e.file_id, e.pos, e.expected, e.found) == first, mode

@@ -20,6 +20,17 @@ import oracle_ffi as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True, params=["auto", "walk"])
+def scan_mode(request, monkeypatch):
+    """Every test here runs twice: the mode the library picks (k_scan_chunks for these mostly short
+    records, the walk for the long-record cases) and the walk mode forced (k_walk_runs)."""
+    if request.param == "walk":
+        monkeypatch.setenv("CASK_SCAN_MODE", "walk")
+    else:
+        monkeypatch.delenv("CASK_SCAN_MODE", raising=False)
+    return request.param
+
+
 def _expected(case):
     with open(os.path.join(GOLDEN, case, "expected.json")) as f:
         return json.load(f)
@@ -203,7 +214,8 @@ def test_variable_sizes_with_long_records(gpu_ctx):
         return r.randrange(4096, 70000)
     buf = make_records(rng, 3000, lambda r: r.randrange(0, 40), vsz, tomb_p=0.1)
     check_against_oracle(gpu_ctx, [buf])
-    assert gpu_ctx.last_counters()["long_records"] > 0
+    cnt = gpu_ctx.last_counters()
+    assert cnt["long_records"] > 0 or cnt["walk_mode"] == 1, cnt  # k_long_hash, or the walk hashed them
 
 
 def _zipf_vsz(rng, s=1.1, kmax=4096):
@@ -230,7 +242,7 @@ def test_zipf_sizes_long_records(gpu_ctx, seed):
     buf = make_records(rng, 4000, lambda r: 16, _zipf_vsz(rng), tomb_p=0.02)
     check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 3]], device=True)
     cnt = gpu_ctx.last_counters()
-    assert cnt["long_records"] > 0
+    assert cnt["long_records"] > 0 or cnt["walk_mode"] == 1, cnt
     assert cnt["walked"] == 0, cnt
 
 
@@ -256,8 +268,22 @@ def test_long_record_hash_every_length_residue(gpu_ctx):
         seq += 1
     buf = b"".join(recs)
     res = check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 2]], device=True)
-    assert gpu_ctx.last_counters()["long_records"] > 0
+    cnt = gpu_ctx.last_counters()
+    assert cnt["long_records"] > 0 or cnt["walk_mode"] == 1, cnt
     assert res.error is not None
+
+
+def test_records_past_walk_hash_limit(gpu_ctx):
+    """Records over 2 MiB (the walk leaves them to k_long_hash) between short ones, one corrupted."""
+    rng = random.Random(48)
+    recs = []
+    for i, vsz in enumerate([40, 2_500_000, 17, 2_200_000, 3000, 2_097_200, 9]):
+        rec = bytearray(R.entry_new(i + 1, rng.randbytes(16), rng.randbytes(vsz)).write_bytes())
+        if i == 3:
+            rec[18 + 16 + 777_777] ^= 0x10
+        recs.append(bytes(rec))
+    check_against_oracle(gpu_ctx, [b"".join(recs)], device=True)
+    assert gpu_ctx.last_counters()["long_records"] >= 3
 
 
 def test_many_files_empty_and_tiny(gpu_ctx):
@@ -287,7 +313,8 @@ def test_adversarial_embedded_records_repair(gpu_ctx):
         out.append(R.entry_new(i + 1, b"outer%d" % i, v).write_bytes())
     check_against_oracle(gpu_ctx, [b"".join(out)])
     cnt = gpu_ctx.last_counters()
-    assert cnt["repaired_chunks"] > 0 and cnt["dense_path"] == 0, cnt
+    if not cnt["walk_mode"]:  # the walk's search may pick the true starts here
+        assert cnt["repaired_chunks"] > 0 and cnt["dense_path"] == 0, cnt
 
 
 def test_adversarial_repair_by_walk_only(gpu_ctx):
@@ -300,7 +327,8 @@ def test_adversarial_repair_by_walk_only(gpu_ctx):
     os.environ["CASK_LOCAL_REPAIRS"] = "0"
     try:
         check_against_oracle(gpu_ctx, [b"".join(out)])
-        assert gpu_ctx.last_counters()["walked"] == 1
+        cnt = gpu_ctx.last_counters()
+        assert cnt["walked"] == 1 or (cnt["walk_mode"] and cnt["dense_path"]), cnt
     finally:
         del os.environ["CASK_LOCAL_REPAIRS"]
 
