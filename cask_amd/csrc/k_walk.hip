@@ -98,7 +98,7 @@ constexpr uint32_t kChaseUse = kChaseNL * 1024 - 16;
 
 // The first record start >= b0 of the chain, speculatively (see the file comment); kNone if pass A
 // finds no verified short record before min(len, b1 + kSearchPast).
-// Pass A, per 64 offsets: every lane decodes the header at its offset; the offsets whose record is
+// Pass A, 256 offsets a step (4 per lane): the length fields of every offset are decoded; offsets whose record is
 // at most kSearchShort long and fits the file are hashed 16 at a time by quads (from LDS when the
 // record is staged, else from HBM), in offset order, until one matches its stored checksum. Offsets
 // whose record is longer and ends within the search horizon are listed (x, x + rl) for the hop back,
@@ -113,33 +113,64 @@ __device__ uint64_t walk_search(WalkLds& L, const uint8_t* data, uint64_t len, u
   for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kStepA) {
     const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
     const uint64_t wend = (wb + kWalkUse < len) ? wb + kWalkUse : len;  // staged bytes end here
-    for (uint32_t k0 = 0; k0 < kStepA; k0 += 64) {
-      const uint64_t x = wb + k0 + lane;
-      bool shortc = false, longc = false;
-      uint64_t rl = 0;
-      if (k0 + lane < kStepA && x < lim && x + 18 <= len) {
-        rl = lds_reclen(L.win, x0 + k0 + lane);
-        shortc = rl <= kSearchShort && x + rl <= len;
-        longc = rl > kSearchShort && x + rl <= lim;
+    // 256 offsets per step: lane l decodes the length fields of offsets k0 + 4l .. k0 + 4l + 3
+    // from the four aligned dwords that cover them
+    for (uint32_t k0 = 0; k0 < kStepA && kA == kNone; k0 += 256) {
+      const uint32_t o = k0 + 4 * lane;
+      const uint32_t B = x0 + o + 12, i0 = B >> 2, sh = B & 3;
+      const uint32_t d0 = L.win[i0], d1 = L.win[i0 + 1], d2 = L.win[i0 + 2], d3 = L.win[i0 + 3];
+      uint32_t sm = 0, lm = 0;  // bit s: offset o + s is a short / long candidate
+      uint64_t rls[4];
+#pragma unroll
+      for (uint32_t e = 0; e < 4; ++e) {
+        const uint32_t t = sh + e;
+        const uint32_t w3 = t < 4 ? fun(d0, d1, t) : fun(d1, d2, t - 4);
+        const uint32_t w4 = t < 4 ? fun(d1, d2, t) : fun(d2, d3, t - 4);
+        const uint32_t ksz = w3 & 0xFFFFu, vsz = (w3 >> 16) | (w4 << 16);
+        const uint64_t rl = 18ull + ksz + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+        const uint64_t x = wb + o + e;
+        const bool valid = o + e < kStepA && x < lim && x + 18 <= len;
+        rls[e] = rl;
+        sm |= (uint32_t)(valid && rl <= kSearchShort && x + rl <= len) << e;
+        lm |= (uint32_t)(valid && rl > kSearchShort && x + rl <= lim) << e;
       }
-      const unsigned long long ml = __ballot(longc);
-      if (ml) {  // append in offset order
-        const uint32_t at = nl + (uint32_t)__builtin_popcountll(ml & below);
-        if (longc && at < kLongList) {
-          L.lx[at] = x;
-          L.le[at] = x + rl;
-        }
-        nl += (uint32_t)__builtin_popcountll(ml);
+      // ranks in offset order (lane-major, then e)
+      unsigned long long mS[4], mL[4];
+      uint32_t nS = 0, nL = 0, rS = 0, rL = 0;  // totals; this lane's first ranks
+#pragma unroll
+      for (uint32_t e = 0; e < 4; ++e) {
+        mS[e] = __ballot((sm >> e) & 1u);
+        mL[e] = __ballot((lm >> e) & 1u);
+        nS += (uint32_t)__builtin_popcountll(mS[e]);
+        nL += (uint32_t)__builtin_popcountll(mL[e]);
+        rS += (uint32_t)__builtin_popcountll(mS[e] & below);
+        rL += (uint32_t)__builtin_popcountll(mL[e] & below);
+      }
+      if (nL) {  // long candidates, appended in offset order
+        uint32_t r = nl + rL;
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e)
+          if ((lm >> e) & 1u) {
+            if (r < kLongList) {
+              L.lx[r] = wb + o + e;
+              L.le[r] = wb + o + e + rls[e];
+            }
+            ++r;
+          }
+        nl += nL;
         if (nl > kLongList) over = true;
       }
-      unsigned long long ms = __ballot(shortc);
-      while (ms && kA == kNone) {  // the next 16 short candidates, one per quad
-        if (shortc) {
-          const uint32_t rk = (uint32_t)__builtin_popcountll(ms & below);
-          if (rk < 16) L.cand[rk] = k0 + lane;
-        }
+      // short candidates: 16 at a time (ranks [r0, r0 + 16)), one per quad, in offset order
+      for (uint32_t r0 = 0; r0 < nS && kA == kNone; r0 += 16) {
+        uint32_t r = rS;
+#pragma unroll
+        for (uint32_t e = 0; e < 4; ++e)
+          if ((sm >> e) & 1u) {
+            if (r >= r0 && r < r0 + 16) L.cand[r - r0] = o + e;
+            ++r;
+          }
         __syncthreads();
-        const uint32_t nc = (uint32_t)__builtin_popcountll(ms) < 16 ? (uint32_t)__builtin_popcountll(ms) : 16u;
+        const uint32_t nc = nS - r0 < 16 ? nS - r0 : 16u;
         bool ok = false;
         if (q < nc) {
           const uint32_t ko = L.cand[q];
@@ -153,11 +184,7 @@ __device__ uint64_t walk_search(WalkLds& L, const uint8_t* data, uint64_t len, u
         const unsigned long long mo = __ballot(ok);
         if (mo) kA = wb + L.cand[__builtin_ctzll(mo) >> 2];  // quads are in offset order
         __syncthreads();
-        // drop the 16 candidates just tried
-        for (uint32_t d = 0; d < nc; ++d) ms &= ms - 1;
-        if (shortc && !((ms >> lane) & 1ull)) shortc = false;
       }
-      if (kA != kNone) break;
     }
   }
   if (kA == kNone) return kNone;
@@ -229,6 +256,7 @@ __device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, 
   const uint32_t lane = threadIdx.x;
   const uint32_t nch = (uint32_t)(t1 - t0);
   const uint64_t CH = a.chunk, len = fd.len;
+  const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   const uint8_t* data = fd.data;
   const uint64_t b0 = (t0 - fd.first_chunk) * CH;
   const uint64_t b1 = ((t1 - fd.first_chunk) * CH < len) ? (t1 - fd.first_chunk) * CH : len;
@@ -249,7 +277,7 @@ __device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, 
   uint64_t wb = 0, wv = 0;  // the chase's window: file bytes [wb, wv) at LDS byte x0
   uint32_t x0 = 0;
   while (p != kNone && p < b1) {
-    const uint32_t j = (uint32_t)((p - b0) / CH);
+    const uint32_t j = (uint32_t)((p - b0) >> csh);  // chunk sizes are powers of two
     if (j != cj) {  // the chain enters chunk j: the previous chunk's rows and exit are final
       if (cj != 0xFFFFFFFFu && lane == 0) {
         L.cnt[cj] = cn;

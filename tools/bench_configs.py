@@ -60,8 +60,9 @@ def cfg3(ctx, torch, steps, total_gib, max_file):
     return {"config": "configs[2]: 32 GiB, Zipf(1.1) value sizes 16 B-64 KiB, 1 GPU, device-resident",
             "files": len(files), "records": n, "bytes": nbytes, "mean_record_bytes": nbytes / n,
             "gibps": nbytes * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps,
-            "k_scan_chunks_ms": kavg, "k_scan_chunks_gbps": nbytes / (kavg * 1e-3) / 1e9,
-            "k_scan_chunks_frac_of_8TBps": nbytes / (kavg * 1e-3) / 8e12, "breakdown_ms": brk,
+            "log_bytes_over_step_frac_of_8TBps": nbytes * steps / el / 8e12,
+            "first_pass_kernel": "k_walk_runs" if counters.get("walk_mode") else "k_scan_chunks",
+            "first_pass_ms": kavg, "breakdown_ms": brk,
             "counters": counters, "parity": "rows == generator (count, pos, seq, ksz, vsz, status)"}
 
 
