@@ -317,7 +317,8 @@ __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
 // contiguous bytes per instruction, 4 blocks ahead), quad_transpose hands every lane its word of
 // the block's four stripes. The four lanes must be active together and call with the same p/len;
 // all four return the hash.
-// D: blocks in flight per quad (64 B each; k_long_hash: 4 / 8 / 16 = 7.0 / 6.26 / 6.2 ms on configs[2]).
+// D: blocks in flight per quad (64 B each; k_long_hash: 4 / 8 / 16 = 7.0 / 6.26 / 6.2 ms on configs[2];
+// a ring of D = 8 / 12 / 16 registers, refilled as each block is mixed, ran 6.8 ms at every D).
 template <uint32_t D = 8>
 __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t len, uint32_t q) {
   const uint64_t nstr = len >> 4;

@@ -16,17 +16,23 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(path, steps, files):
+def child(path, steps, files, zipf_gib):
     sys.path.insert(0, ROOT)
     import torch
     import cask_amd
     if path != "product":
         cask_amd._lib.use_library(path)
-    from cask_amd.workloads import cfg2_files
     ctx = cask_amd.ScanContext(0)
-    fs = cfg2_files(ctx, nfiles=files)
+    if zipf_gib > 0:  # configs[2]-shaped
+        from cask_amd.workloads import zipf_files
+        fs, _, n, _ = zipf_files(ctx, zipf_gib, 2 ** 31)
+        fs = [f for f, _ in fs]
+    else:
+        from cask_amd.workloads import cfg2_files
+        fs = cfg2_files(ctx, nfiles=files)
+        n = sum(f.nrec for f in fs)
     views = [(f.file_id, f.data) for f in fs]
-    rows = ctx.alloc_rows(sum(f.nrec for f in fs))
+    rows = ctx.alloc_rows(n + 16)
     nbytes = sum(f.data.numel() for f in fs)
     for _ in range(3):
         ctx.scan_device(views, rows)
@@ -48,15 +54,17 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--files", type=int, default=8)
     ap.add_argument("--child", default="")
+    ap.add_argument("--zipf-gib", type=float, default=0.0, help="configs[2]-shaped files of this size")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     if a.child:
-        return child(a.child, a.steps, a.files)
+        return child(a.child, a.steps, a.files, a.zipf_gib)
     for r in range(a.rounds):
         for spec in a.libs:
             name, path = spec.split("=", 1)
             out = subprocess.run([sys.executable, __file__, "--child", path, "--steps", str(a.steps),
-                                  "--files", str(a.files)], capture_output=True, text=True, timeout=300)
+                                  "--files", str(a.files), "--zipf-gib", str(a.zipf_gib)],
+                                 capture_output=True, text=True, timeout=300)
             if out.returncode != 0:
                 print(name, "FAILED", out.stderr[-2000:])
                 sys.exit(1)
