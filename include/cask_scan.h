@@ -336,13 +336,13 @@ int cask_hints_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfile
 int cask_shard_keydir(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
                       const uint64_t* file_row_offset, const void** block, uint64_t* bytes);
 
-/* Rank 0's fold: a keydir handle with no files, the blocks merged in rank order (host memory),
- * then finished (Stats). The result is a cask_db: cask_db_export / _stats / _current_sequence /
- * _len / _files / _get_entry read it; cask_db_close frees it. */
 /* Copy `bytes` between any two memories (device or host) on the context's stream, synchronously:
  * e.g. a keydir block out of the context's buffer. */
 int cask_copy(cask_ctx* ctx, void* dst, const void* src, uint64_t bytes);
 
+/* Rank 0's fold: a keydir handle with no files, the blocks merged in rank order (host memory),
+ * then finished (Stats). The result is a cask_db: cask_db_export / _stats / _current_sequence /
+ * _len / _files / _get_entry read it; cask_db_close frees it. */
 cask_db* cask_keydir_new(void);
 int cask_keydir_merge(cask_db* db, const uint8_t* block, uint64_t bytes);
 int cask_keydir_finish(cask_db* db);
