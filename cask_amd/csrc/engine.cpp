@@ -1517,35 +1517,69 @@ int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     return CASK_E_INVALID_ARG;
   const ShardRec* rec = (const ShardRec*)(blk + rec_at);
   const uint8_t* keys = blk + key_at;
-  auto stale = [&](uint32_t fid, uint32_t ksz) {  // Stats add + remove of a stale tombstone
-    cask_db::ShardTerms& t = db->terms[fid];
-    t.stale += 1;
-    t.stale_bytes += 18ull + ksz;
-  };
-  // 1. thresholds, against the keydir entering the shard
-  uint64_t ko = 0;
-  for (uint64_t i = 0; i < hd.nrec; ++i) {
-    const ShardRec& r = rec[i];
-    if (ko + r.ksz > hd.key_bytes) return CASK_E_INVALID_ARG;
-    if (r.kind == kCond) {
-      const cask_index_entry* e = db->index.get(keys + ko, r.ksz);
-      if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+  const uint64_t n = hd.nrec;
+  // 0. every record's key offset, checked before anything changes
+  std::vector<uint64_t> ko(n);
+  {
+    uint64_t o = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      ko[i] = o;
+      o += rec[i].ksz;
+      if (o > hd.key_bytes) return CASK_E_INVALID_ARG;
     }
-    ko += r.ksz;
   }
-  // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
-  ko = 0;
-  for (uint64_t i = 0; i < hd.nrec; ++i) {
-    const ShardRec& r = rec[i];
-    const uint8_t* k = keys + ko;
-    ko += r.ksz;
-    if (r.kind == kCond) continue;
-    if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
-      const cask_index_entry* e = db->index.get(k, r.ksz);
-      if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+  // The fold of a block depends on each key's records alone, in order: on threads by keydir table
+  // (parallel_fold's split), each table taking its records in block order — first the thresholds
+  // against the keydir entering the shard, then the updates. Stale terms are per-file sums.
+  const char* mv = getenv("CASK_PAR_FOLD_MIN");
+  const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
+  const unsigned nt = n < min_par ? 1u : std::min(host_threads(), Index::kSub);
+  constexpr unsigned S = Index::kSub;
+  std::vector<uint64_t> hs(n);
+  std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(S));
+  parallel_for(nt, [&](unsigned t) {
+    const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
+    for (uint64_t i = lo; i < hi; ++i) {
+      hs[i] = hash_key(keys + ko[i], rec[i].ksz);
+      lists[t][Index::sub_of(hs[i])].push_back((uint32_t)(i - lo));
     }
-    db->index.update_kd(k, r.ksz, r.file_id, r.pos, r.vsz, r.seq);
-  }
+  });
+  std::vector<std::unordered_map<uint32_t, cask_db::ShardTerms>> sterms(nt);
+  parallel_for(nt, [&](unsigned t) {
+    auto stale = [&](uint32_t fid, uint32_t ksz) {  // Stats add + remove of a stale tombstone
+      cask_db::ShardTerms& x = sterms[t][fid];
+      x.stale += 1;
+      x.stale_bytes += 18ull + ksz;
+    };
+    for (unsigned q = t; q < S; q += nt) {
+      KeyDir& kd = db->index.sub[q];
+      for (int phase = 0; phase < 2; ++phase)
+        for (unsigned g = 0; g < nt; ++g) {
+          const uint64_t lo = n * g / nt;
+          for (uint32_t j : lists[g][q]) {
+            const uint64_t i = lo + j;
+            const ShardRec& r = rec[i];
+            const uint8_t* k = keys + ko[i];
+            const int64_t f = kd.find(k, r.ksz, hs[i]);
+            const cask_index_entry* e = f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
+            if (phase == 0) {  // 1. thresholds, against the keydir entering the shard
+              if (r.kind == kCond && (e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+              continue;
+            }
+            // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
+            if (r.kind == kCond) continue;
+            if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE && e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+            kd.update_kd(k, r.ksz, r.file_id, r.pos, r.vsz, r.seq, hs[i]);
+          }
+        }
+    }
+  });
+  for (const auto& m : sterms)
+    for (const auto& kv : m) {
+      cask_db::ShardTerms& x = db->terms[kv.first];
+      x.stale += kv.second.stale;
+      x.stale_bytes += kv.second.stale_bytes;
+    }
   const ShardFileStat* fs = (const ShardFileStat*)(blk + fst_at);
   for (uint32_t f = 0; f < hd.nfiles; ++f) {
     cask_db::ShardTerms& t = db->terms[fs[f].file_id];

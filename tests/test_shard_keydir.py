@@ -88,8 +88,12 @@ def _native_fold(native, blocks):
     return out
 
 
+@pytest.mark.parametrize("threads", [1, 5])
 @pytest.mark.parametrize("seed", range(12))
-def test_native_fold_matches(native, seed):
+def test_native_fold_matches(native, seed, threads, monkeypatch):
+    """threads=5: the merge on threads by keydir table (CASK_PAR_FOLD_MIN=0 forces it)."""
+    monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if threads > 1 else str(1 << 62))
+    monkeypatch.setenv("CASK_HOST_THREADS", str(threads))
     rng = random.Random(100 + seed)
     files = _random_files(rng, 7, 60, rng.choice([2, 10, 50]), 0.25, 0.25)
     want = _full_fold(files)
