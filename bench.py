@@ -229,6 +229,16 @@ def main():
             extra["keydir_block_bytes_per_rank"] = int(blk.numel())
             if rank == 0:
                 extra["keydir_gathered_bytes"] = int(sum(b.numel() for b in got))
+                # rank 0's fold of the blocks in rank order (host keydir, exact stats)
+                from cask_amd.keydir import KeydirFold
+                tf = time.perf_counter()
+                fold = KeydirFold()
+                for b in got:
+                    fold.merge(b.cpu())
+                db = fold.finish()
+                extra["keydir_fold_ms"] = (time.perf_counter() - tf) * 1e3
+                extra["keydir_live_keys"] = len(db)
+                db.close()
             del blk, got
         except Exception as e:  # noqa: BLE001 - reported in the line
             extra["keydir_gather_error"] = f"{type(e).__name__}: {e}"[:300]

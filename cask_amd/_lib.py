@@ -99,6 +99,8 @@ SIGNATURES = [
     ("cask_ctx_last_error", C.c_char_p, [C.c_void_p]),
     ("cask_scan_chunk_bytes", C.c_uint32, []),
     ("cask_rows_bound", C.c_uint64, [C.POINTER(FileView), C.c_uint32]),
+    ("cask_parse_hints_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
+                                   C.POINTER(ScanError)]),
     ("cask_scan_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                    C.POINTER(ScanError)]),
     ("cask_scan_device_segmented", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Segments),

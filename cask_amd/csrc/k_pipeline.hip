@@ -519,13 +519,14 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
         const u32x4 w = *(const u32x4*)(a.slots + ((tile * TC + j) * (uint64_t)a.slot_cap + r) * 4);
         const uint32_t ksz = w.w & 0xFFFFu;
         const uint64_t p = cc0 + ((w.w >> 16) & 0x7FFFu);
-        const uint64_t end = p + 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+        const uint64_t hb = a.hint ? 22ull : 18ull;  // header bytes (a hint: data.rs:242-256)
+        const uint64_t end = p + hb + ksz + ((a.hint || w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
         const uint64_t fl = s_len[j];
         P4[q] = p;
         S4[q] = ((uint64_t)w.y << 32) | w.x;
         V4[q] = w.z;
         K4[q] = ksz;
-        T4[q] = (p + 18 > fl || end > fl) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
+        T4[q] = (p + hb > fl || end > fl) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
       }
     }
     if (a.vec_ok && inr[0] && inr[3] && d0 + 3 < cap) {
@@ -607,8 +608,9 @@ __global__ __launch_bounds__(256) void k_compact(ScanArgs a, const uint64_t* sum
       const u32x4 w = src[r];
       const uint64_t p = c0 + ((w.w >> 16) & 0x7FFFu);
       const uint32_t ksz = w.w & 0xFFFFu;
-      const uint64_t end = p + 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
-      const uint8_t st = (p + 18 > fd.len || end > fd.len) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
+      const uint64_t hb = a.hint ? 22ull : 18ull;
+      const uint64_t end = p + hb + ksz + ((a.hint || w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+      const uint8_t st = (p + hb > fd.len || end > fd.len) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
       const uint64_t d = dst0 + r;
       if (d < a.row_cap) {
         a.pos[d] = p;

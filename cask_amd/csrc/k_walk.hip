@@ -225,6 +225,50 @@ __device__ uint64_t walk_search(WalkLds& L, const uint8_t* data, uint64_t len, u
   return target;
 }
 
+// Hint-file bodies (cask_parse_hints_device): records `seq u64 | ksz u16 | vsz u32 | entry_pos u64 |
+// key` (Hint::write_bytes, data.rs:242-256), 22 + ksz bytes, no checksum of their own. A run's first
+// start is the lowest offset >= b0 whose record, and the two after it, have entry positions that
+// follow on from each other (each data record starts where the previous one ended: RecreateHints
+// writes one hint per Ok record in order, log.rs:454-465) — or whose record ends the body exactly.
+// The chain is then checked by k_finish like any speculated start.
+__device__ __forceinline__ uint64_t hint_field64(const uint32_t* W, uint32_t x) {
+  return (uint64_t)lds_u32(W, x) | ((uint64_t)lds_u32(W, x + 4) << 32);
+}
+__device__ uint64_t hint_search(WalkLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t wb = b0; wb < b1; wb += kStepB) {
+    const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
+    const uint64_t wend = (wb + kWalkUse < len) ? wb + kWalkUse : len;
+    for (uint32_t k0 = 0; k0 < kStepB; k0 += 64) {
+      const uint64_t x = wb + k0 + lane;
+      bool hit = false;
+      if (k0 + lane < kStepB && x < b1 && x + 22 <= wend) {
+        uint64_t y = x, pos = 0;
+        hit = true;
+        for (int h = 0; h < 3; ++h) {  // x and the two records after it
+          const uint32_t xi = x0 + (uint32_t)(y - wb);
+          const uint32_t ksz = lds_u32(L.win, xi + 8) & 0xFFFFu, vsz = lds_u32(L.win, xi + 10);
+          const uint64_t ep = hint_field64(L.win, xi + 14);
+          if (h && ep != pos) {  // not where the previous record's entry ended
+            hit = false;
+            break;
+          }
+          pos = ep + 18 + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+          y += 22ull + ksz;
+          if (y == len || h == 2) break;  // ends the body exactly, or three records chained
+          if (y + 22 > wend) {            // past the body, or the next header is not staged
+            hit = false;
+            break;
+          }
+        }
+      }
+      const unsigned long long m = __ballot(hit);
+      if (m) return wb + k0 + (uint64_t)__builtin_ctzll(m);
+    }
+  }
+  return kNone;
+}
+
 // Hash class k's batch: quad q takes entry q; its row goes out with the verdict (data.rs:193-198).
 // A failing row of chunk t lowers the chunk's first failing row: in LDS while t is in the wave's
 // current segment [t0, t1) (written out with the segment), else in the chunk table.
@@ -251,8 +295,11 @@ __device__ void walk_flush(WalkLds& L, const ScanArgs& a, uint32_t k, uint32_t n
 }
 
 // One stretch of a run inside one file: chunks [t0, t1) of file fd.
-__device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, uint64_t t0, uint64_t t1,
-                             uint32_t* nbk, uint64_t* wst) {
+// s_in: the exact start of the segment's first chunk (repair passes: spec[t0]), or kSearch for a
+// speculative one. Returns the chain position after the segment (kTerm after an EOF row).
+constexpr uint64_t kSearch = ~0ull - 1;
+__device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, uint64_t t0, uint64_t t1,
+                                 uint64_t s_in, uint32_t* nbk, uint64_t* wst) {
   const uint32_t lane = threadIdx.x;
   const uint32_t nch = (uint32_t)(t1 - t0);
   const uint64_t CH = a.chunk, len = fd.len;
@@ -269,9 +316,12 @@ __device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, 
   }
   __syncthreads();
   WST(ts0)
-  uint64_t p = uni64(b0 == 0 ? 0 : walk_search(L, data, len, b0, b1));
+  const bool hint = a.hint != 0;
+  const uint32_t hdr = hint ? 22u : 18u;
+  uint64_t p = uni64(b0 == 0 ? 0 : s_in != kSearch ? s_in
+                     : hint ? hint_search(L, data, len, b0, b1) : walk_search(L, data, len, b0, b1));
   WADD(0, ts0)
-  if (b0) { WCNT(6) }
+  if (b0 && s_in == kSearch) { WCNT(6) }
   // the chase: uniform state of the chunk the chain is in
   uint32_t cj = 0xFFFFFFFFu, cn = 0;  // current chunk (segment index) and its rows so far
   uint64_t wb = 0, wv = 0;  // the chase's window: file bytes [wb, wv) at LDS byte x0
@@ -294,10 +344,10 @@ __device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, 
     bool fail = false, eof = false;
     uint64_t rl = 0;
     uint32_t stored = 0;
-    if (p + 18 > len) {
-      fail = eof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163)
+    if (p + hdr > len) {
+      fail = eof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163; a hint: data.rs:258-265)
     } else {
-      if (p < wb || p + 18 > wv) {  // the header is not staged: one round trip brings the next KiB
+      if (p < wb || p + hdr > wv) {  // the header is not staged: one round trip brings the next KiB
         WST(tw0)
         x0 = walk_stage<kChaseNL>(L.win, data, len, p);
         WADD(1, tw0)
@@ -305,24 +355,34 @@ __device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, 
         wb = p;
         wv = (p + kChaseUse < len) ? p + kChaseUse : len;
       }
-      Hdr h = lds_hdr(L.win, x0 + (uint32_t)(p - wb));  // wave-uniform: into scalar registers
+      Hdr h;
+      if (hint) {  // seq u64 | ksz u16 | vsz u32 | entry_pos u64
+        const uint32_t xi = x0 + (uint32_t)(p - wb);
+        h.stored = 0;
+        h.seq = hint_field64(L.win, xi);
+        h.ksz = lds_u32(L.win, xi + 8) & 0xFFFFu;
+        h.vsz = lds_u32(L.win, xi + 10);
+      } else {
+        h = lds_hdr(L.win, x0 + (uint32_t)(p - wb));
+      }
+      // wave-uniform: into scalar registers
       h.stored = __builtin_amdgcn_readfirstlane(h.stored);
       h.seq = uni64(h.seq);
       h.ksz = __builtin_amdgcn_readfirstlane(h.ksz);
       h.vsz = __builtin_amdgcn_readfirstlane(h.vsz);
       stored = h.stored;
       row = u32x4{(uint32_t)h.seq, (uint32_t)(h.seq >> 32), h.vsz, h.ksz | (off << 16)};
-      rl = 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
-      if (p + rl > len) fail = eof = true;  // key/value cut short (data.rs:172,181)
+      rl = hint ? 22ull + h.ksz : 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
+      if (p + rl > len) fail = eof = true;  // key/value cut short (data.rs:172,181; a hint's key: :266-270)
     }
     const uint64_t c0j = b0 + (uint64_t)j * CH;
     const uint64_t wend = (c0j + a.win < len) ? c0j + a.win : len;
-    const uint32_t k = (!eof && lds_hashed(p, rl, wend, a.big)) ? 0u : kClasses;
+    const uint32_t k = (!eof && !hint && lds_hashed(p, rl, wend, a.big)) ? 0u : kClasses;  // hints: no checksum
     if (k == kClasses) {  // the row goes out now: an EOF row, or a record left to k_long_hash
       if (lane == 0) {
         *(u32x4*)(a.slots + ((t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
         if (fail) atomicMin(&L.cerr[j], r);
-        else atomicMin(&L.lr[j], r);
+        else if (!hint) atomicMin(&L.lr[j], r);
       }
     } else {  // hashed with its class's batch
       if (lane == 0) L.ent[k][nbk[k]] = WalkEnt{data + p, (uint32_t)rl, stored, (uint32_t)(t0 + j), r, row};
@@ -359,6 +419,7 @@ __device__ void walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, 
   // the table entries are stored before any later batch flush lowers a.cerr[t] with an atomic
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
+  return cj == 0xFFFFFFFFu && p != kNone && p < b1 ? kTerm : p;
 }
 
 // Persistent grid of single-wave workgroups; runs of a.run chunks claimed from ctr->run_next.
@@ -369,20 +430,26 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
   for (uint32_t k = 0; k < kClasses; ++k) nbk[k] = 0;
   WST(tk0)
   const uint64_t R = a.run;
-  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  // a repair pass walks the stretches in a.runs from their exact starts (spec[first]); otherwise
+  // runs of R chunks, each from a speculative start
+  const uint64_t nruns = a.runs ? a.nruns_list : (a.total_chunks + R - 1) / R;
   for (;;) {
     uint32_t r = 0;
     if (threadIdx.x == 0) r = atomicAdd(&a.ctr->run_next, 1u);
     r = __shfl(r, 0, 64);
     if (r >= nruns) break;
-    uint64_t t = (uint64_t)r * R;
-    const uint64_t tend = (t + R < a.total_chunks) ? t + R : a.total_chunks;
+    uint64_t t = a.runs ? a.runs[2ull * r] : (uint64_t)r * R;
+    const uint64_t tend = a.runs ? a.runs[2ull * r + 1] : ((t + R < a.total_chunks) ? t + R : a.total_chunks);
+    uint64_t s = a.runs ? uni64(a.spec[t]) : kSearch;
     while (t < tend) {
       const uint32_t fi = find_file(files, a.nfiles, t);
       const FileDesc fd = files[fi];
       const uint64_t fend = fd.first_chunk + fd.nchunks;
-      const uint64_t se = fend < tend ? fend : tend;
-      walk_segment(L, a, fd, t, se, nbk, wst);
+      uint64_t se = fend < tend ? fend : tend;
+      if (se - t > kMaxRun) se = t + kMaxRun;  // the chunk state of a segment lives in LDS
+      const uint64_t ex = walk_segment(L, a, fd, t, se, s, nbk, wst);
+      // the next piece of a stretch continues the chain; a new file starts at 0 (walk_segment)
+      s = a.runs ? ex : kSearch;
       t = se;
     }
   }

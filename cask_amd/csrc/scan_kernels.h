@@ -131,7 +131,7 @@ struct ScanArgs {
   uint64_t* row_off;           // call block: per file first dense row
   unsigned long long* err_inv; // call block: per file ~first failing dense row (0: none)
   uint32_t vec_ok;             // dense arrays aligned for the 4-row vector stores of k_finish
-  uint32_t pad_;
+  uint32_t hint;               // 1: the files are hint-file bodies (cask_parse_hints_device), not data files
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -150,6 +150,7 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // Walk mode (k_walk.hip): chunks per run, and the mean record length (bytes, sampled at the heads
 // of the files by k_probe) from which a call takes it.
 constexpr uint32_t kWalkRun = 64, kWalkMean = 1024;
+constexpr uint32_t kHintRun = 2;  // hint bodies: 22 + ksz-byte records, ~1,700 per 64 KiB run
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
 struct SummaryHead {

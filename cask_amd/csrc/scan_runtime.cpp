@@ -227,7 +227,8 @@ int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
 // no long records. If some start was wrong the repair path takes over (validate, exact re-scans,
 // k_compact), as does the segmented output.
 static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
-                            cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err) {
+                            cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err,
+                            bool hint = false) {
   if (nfiles && !files) return CASK_E_INVALID_ARG;
   if (rows && rows->capacity && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status))
     return CASK_E_INVALID_ARG;
@@ -339,6 +340,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
                 (uintptr_t)rows->ksz % 8 == 0 && (uintptr_t)rows->status % 4 == 0) ? 1u : 0u;
   }
   a.stamps = nullptr;
+  a.hint = hint ? 1u : 0u;
   {  // CASK_RUN_CHUNKS (tuning knob): chunks per workgroup run; one boundary search per run.
     // Default: about 16 runs per resident workgroup (the counter's balance), at least kDefaultRun and
     // at most kMaxRun chunks — longer runs search less often, which is what variable-length logs
@@ -404,7 +406,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // is cached on the context; it decides speed only). CASK_SCAN_MODE=walk|chunk (test and tuning
   // knob) forces a mode.
   bool walk = false;
-  {
+  if (hint) {
+    walk = true;  // hint bodies are always walked (k_walk_runs' hint mode)
+  } else {
     const char* mode = getenv("CASK_SCAN_MODE");
     if (mode && !strcmp(mode, "walk")) {
       walk = true;
@@ -434,7 +438,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
   if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
     const char* wr = getenv("CASK_WALK_RUN");
-    a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : kWalkRun;
+    a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : hint ? kHintRun : kWalkRun;
   }
   c->last_walk = walk ? 1 : 0;
   H(hipEventRecord(c->ev[1], st));
@@ -503,7 +507,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
         err->file_id = files[f].file_id;
         err->pos = (uint64_t)e5[3] | ((uint64_t)e5[4] << 32);
         err->row = d;
-        err->expected = e5[0];
+        err->expected = hint ? 0 : e5[0];  // a hint has no checksum of its own
         err->found = e5[2] == CASK_ROW_CHECKSUM ? e5[1] : 0;
         break;
       }
@@ -535,8 +539,13 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   };
   auto pass = [&]() {
     reset();
-    launch_scan_chunks(a, c->geo, st);
-    L("k_scan_chunks");
+    if (hint) {  // hint bodies: the walker from the exact starts (a.runs) or from each file's start
+      launch_walk_runs(a, st);
+      L("k_walk_runs");
+    } else {
+      launch_scan_chunks(a, c->geo, st);
+      L("k_scan_chunks");
+    }
     post(false);
   };
   // the first scan has run (its counters are in the call block): keep its run counter's effects,
@@ -612,7 +621,21 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       if (!ok) return CASK_E_DEVICE;
       ++local_passes;
     }
-    if (head->any_invalid) {
+    if (head->any_invalid && hint) {  // every file walked whole from its first record
+      walked = 1;
+      invalid_chunks += total_chunks;
+      runs.clear();
+      for (uint32_t f = 0; f < nfiles; ++f)
+        if (fd[f].nchunks) {
+          runs.push_back(fd[f].first_chunk);
+          runs.push_back(fd[f].first_chunk + fd[f].nchunks);
+        }
+      H(hipMemcpyAsync(d_runs, runs.data(), runs.size() * 8, hipMemcpyHostToDevice, st), "runs H2D");
+      a.runs = d_runs;
+      a.nruns_list = runs.size() / 2;
+      pass();
+      if (!ok) return CASK_E_DEVICE;
+    } else if (head->any_invalid) {
       walked = 1;
       invalid_chunks += total_chunks;
       a.runs = nullptr;  // the walk rewrites every start from each file's first bad chunk: re-scan all
@@ -685,12 +708,21 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       err->file_id = files[f].file_id;
       err->pos = (uint64_t)e5[3] | ((uint64_t)e5[4] << 32);
       err->row = ferr_row[f];
-      err->expected = e5[0];
+      err->expected = hint ? 0 : e5[0];
       err->found = e5[2] == CASK_ROW_CHECKSUM ? e5[1] : 0;
       break;
     }
   }
   return CASK_OK;
+}
+
+extern "C" int cask_parse_hints_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                                       uint64_t* file_row_offset, cask_scan_error* err) {
+  if (!c || !rows) return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  return scan_device_impl(c, files, nfiles, rows, nullptr, file_row_offset, err, true);
 }
 
 extern "C" int cask_scan_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,

@@ -109,6 +109,16 @@ class ScanContext:
 
     def scan_device(self, files, rows: dict | None = None, raise_on_capacity: bool = True) -> ScanResult:
         """files: list of (file_id, uint8 CUDA tensor). rows: dict from alloc_rows (reused if given)."""
+        return self._scan_device(self.lib.cask_scan_device, "cask_scan_device", files, rows, raise_on_capacity)
+
+    def parse_hints_device(self, bodies, rows: dict | None = None, raise_on_capacity: bool = True) -> ScanResult:
+        """Hint-file bodies (trailer excluded) on the device, parsed there (cask_parse_hints_device:
+        Hints::next / Hint::from_read, log.rs:437-447, data.rs:258-276). Row pos = the hint's offset in
+        its body; seq, ksz, vsz as in the hint; status Ok or EOF (a body cut short)."""
+        return self._scan_device(self.lib.cask_parse_hints_device, "cask_parse_hints_device", bodies, rows,
+                                 raise_on_capacity)
+
+    def _scan_device(self, fn, name, files, rows, raise_on_capacity):
         n = len(files)
         views = (L.FileView * max(n, 1))()
         for i, (fid, t) in enumerate(files):
@@ -126,12 +136,12 @@ class ScanContext:
         off = (C.c_uint64 * (n + 1))()
         e = L.ScanError()
         self._inputs_ready()
-        rc = self.lib.cask_scan_device(self._h, views, n, C.byref(r), off, C.byref(e))
+        rc = fn(self._h, views, n, C.byref(r), off, C.byref(e))
         if rc == L.E_CAPACITY:
             if raise_on_capacity:
                 raise CapacityError(int(r.count))
         else:
-            raise_status(rc, what=f"cask_scan_device: {self.last_error()}")
+            raise_status(rc, what=f"{name}: {self.last_error()}")
         return ScanResult(int(r.count), rows["pos"], rows["seq"], rows["vsz"], rows["ksz"], rows["status"],
                           list(off), _err(e))
 

@@ -311,6 +311,16 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files, uint64_t nfiles, c
 int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts, cask_compact_result* res,
                         cask_open_error* err);
 
+/* The hint-file fast path's parse on the device (Log::hints -> Hints::next -> Hint::from_read,
+ * log.rs:121-135, 437-447; data.rs:258-276): `files` are hint-file bodies in device memory, each
+ * without its 4-byte XXH32 trailer (the caller checks it: is_valid_hint_file, log.rs:512-539).
+ * Rows as cask_scan_device's, per hint record in order: pos = the record's offset in its body,
+ * seq, ksz, vsz (raw: 0xFFFFFFFF for a tombstone), status Ok, or EOF for a record the body cuts
+ * short (the first failure goes to *err: Io(UnexpectedEof), expected = found = 0). The entry
+ * position and key are at pos + 14 and pos + 22 of the body. */
+int cask_parse_hints_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                            uint64_t* file_row_offset, cask_scan_error* err);
+
 /* Hint-file bodies on the device (RecreateHints::next + HintWriter::write, log.rs:382-386,
  * 454-465; Hint::write_bytes, data.rs:242-256): for every Ok row of a cask_scan_device call (same
  * files, rows and file_row_offset), in order, [sequence u64][key_size u16][value_size u32,

@@ -183,6 +183,24 @@ def parse_hints(body: bytes):
         yield Row(pos=epos, seq=seq, ksz=ksz, vsz_raw=vsz, key=key)
 
 
+def hint_offsets(body: bytes):
+    """Hints::next over a body (log.rs:437-447; Hint::from_read, data.rs:258-276) in the device
+    parser's row form: (offset of the hint in the body, seq, ksz, value_size raw, status) per record,
+    the last one ROW_EOF if the body cuts it short (then iteration stops, as `hint?` does)."""
+    out, pos, n = [], 0, len(body)
+    while pos < n:
+        if n - pos < 22:
+            out.append((pos, 0, 0, 0, ROW_EOF))
+            break
+        seq, ksz, vsz, _ = struct.unpack_from("<QHIQ", body, pos)
+        if n - pos - 22 < ksz:
+            out.append((pos, seq, ksz, vsz, ROW_EOF))
+            break
+        out.append((pos, seq, ksz, vsz, ROW_OK))
+        pos += 22 + ksz
+    return out
+
+
 def is_valid_hint_bytes(buf: bytes) -> bool:
     """is_valid_hint_file (log.rs:512-539)."""
     return len(buf) >= 4 and xxhash32(buf[:-4]) == struct.unpack("<I", buf[-4:])[0]
