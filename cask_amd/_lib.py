@@ -139,6 +139,8 @@ SIGNATURES = [
                                         C.POINTER(OpenError)]),
     ("cask_db_compact", C.c_int64, [C.c_void_p, C.POINTER(CompactOptions), C.POINTER(CompactResult),
                                     C.POINTER(OpenError)]),
+    ("cask_shard_keydir_hints", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
+                                    C.POINTER(C.c_void_p), c_u64p]),
     ("cask_shard_keydir", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                     C.POINTER(C.c_void_p), c_u64p]),
     ("cask_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),

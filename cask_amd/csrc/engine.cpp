@@ -1623,8 +1623,12 @@ int cask_keydir_finish(cask_db* db) {
 }
 
 // Cask::open over several GPUs of this process: contiguous file-id ranges, one per devices[] entry;
-// each range is read, scanned and reduced to its keydir block on its device (one host thread per
-// distinct device, its ranges one after another), and the blocks are folded here in range order.
+// each range is reduced to keydir blocks on its device (one host thread per distinct device, its
+// ranges one after another), and the blocks are folded here in range order. Within a range, files
+// with a valid hint file take the fast path (log.rs:121-135): their bodies are parsed on the device
+// (cask_parse_hints_device) and reduced (cask_shard_keydir_hints); the others are scanned
+// (cask_scan_device, cask_shard_keydir) and, with write_hints, get their hint files from the device
+// (cask_hints_device). Each maximal stretch of files of one kind gives one block.
 cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, const int* devices, int ndev,
                             cask_open_error* err) {
   set_err(err, CASK_OK);
@@ -1637,9 +1641,25 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
   if (!db) return nullptr;
   const std::string path = db->path;
   const size_t nf = db->files.size();
+  // which files have a valid hint file (is_valid_hint_file, log.rs:512-539), on threads
+  std::vector<std::vector<uint8_t>> hints(nf);
+  std::vector<char> use_hint(nf, 0);
+  {
+    const unsigned nt = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)std::max<size_t>(nf, 1)));
+    parallel_for(nt, [&](unsigned t) {
+      for (size_t i = t; i < nf; i += nt) {
+        const std::string hp = hint_path(path, db->files[i]);
+        if (is_file_follow(hp) && read_file(hp, hints[i]) && hints[i].size() >= 4 &&
+            cask_xxh::xxh32(hints[i].data(), hints[i].size() - 4, 0) == rd32(hints[i].data() + hints[i].size() - 4))
+          use_hint[i] = 1;
+        else
+          std::vector<uint8_t>().swap(hints[i]);
+      }
+    });
+  }
   struct Shard {
     size_t lo = 0, hi = 0;
-    std::vector<uint8_t> block;
+    std::vector<std::vector<uint8_t>> blocks;
     cask_open_error e{};
     double ms_read = 0, ms_scan = 0;
   };
@@ -1648,52 +1668,54 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
     sh[r].lo = nf * (size_t)r / (size_t)ndev;
     sh[r].hi = nf * (size_t)(r + 1) / (size_t)ndev;
   }
-  auto run_shard = [&](int r) {
-    Shard& s = sh[r];
-    if (s.lo == s.hi) return;
+  const bool write_hints = db->opts.write_hints != 0;
+  // one stretch [lo, hi) of files of one kind on device `dev`; false on failure (s.e set)
+  auto run_stretch = [&](Shard& s, int dev, cask_ctx* ctx, size_t lo, size_t hi, bool hint) -> bool {
     auto fail = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
       s.e = cask_open_error{st, fid, pos, e, f};
+      return false;
     };
     auto tr = std::chrono::steady_clock::now();
-    const size_t n = s.hi - s.lo;
+    const size_t n = hi - lo;
     std::vector<std::vector<uint8_t>> data(n);
+    std::vector<uint64_t> blen(n);
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) {
-      if (!read_file(data_path(path, db->files[s.lo + i]), data[i])) return fail(CASK_E_IO, db->files[s.lo + i]);
-      total += (data[i].size() + 255) & ~255ull;
+      if (hint) {
+        blen[i] = hints[lo + i].size() - 4;  // the body: Take(size - 4) (log.rs:129)
+      } else {
+        if (!read_file(data_path(path, db->files[lo + i]), data[i])) return fail(CASK_E_IO, db->files[lo + i]);
+        blen[i] = data[i].size();
+      }
+      total += (blen[i] + 255) & ~255ull;
     }
-    s.ms_read = ms_since(tr);
+    s.ms_read += ms_since(tr);
     auto ts = std::chrono::steady_clock::now();
-    int st = CASK_OK;
-    cask_ctx* ctx = cask_ctx_create(devices[r], &st);
-    if (!ctx) return fail(st);
     uint8_t* dbuf = nullptr;
     void* drows = nullptr;
-    auto done = [&]() {
-      if (dbuf) (void)hipFree(dbuf);
-      if (drows) (void)hipFree(drows);
-      cask_ctx_destroy(ctx);
-    };
-    if (hipSetDevice(devices[r]) != hipSuccess || hipMalloc(&dbuf, total + 256) != hipSuccess) {
-      done();
-      return fail(CASK_E_DEVICE);
-    }
+    uint8_t* dhint = nullptr;
+    struct Free {
+      uint8_t*& a;
+      void*& b;
+      uint8_t*& c;
+      ~Free() {
+        if (a) (void)hipFree(a);
+        if (b) (void)hipFree(b);
+        if (c) (void)hipFree(c);
+      }
+    } release{dbuf, drows, dhint};
+    if (hipSetDevice(dev) != hipSuccess || hipMalloc(&dbuf, total + 256) != hipSuccess) return fail(CASK_E_DEVICE);
     std::vector<cask_file_view> views(n);
     uint64_t off = 0;
     for (size_t i = 0; i < n; ++i) {
-      if (!data[i].empty() && hipMemcpy(dbuf + off, data[i].data(), data[i].size(), hipMemcpyHostToDevice) != hipSuccess) {
-        done();
-        return fail(CASK_E_DEVICE);
-      }
-      views[i] = cask_file_view{db->files[s.lo + i], CASK_VIEW_DEVICE, dbuf + off, data[i].size()};
-      off += (data[i].size() + 255) & ~255ull;
+      const uint8_t* src = hint ? hints[lo + i].data() : data[i].data();
+      if (blen[i] && hipMemcpy(dbuf + off, src, blen[i], hipMemcpyHostToDevice) != hipSuccess) return fail(CASK_E_DEVICE);
+      views[i] = cask_file_view{db->files[lo + i], CASK_VIEW_DEVICE, dbuf + off, blen[i]};
+      off += (blen[i] + 255) & ~255ull;
     }
     const uint64_t bound = cask_rows_bound(views.data(), (uint32_t)n);
     const uint64_t a8 = (bound * 8 + 255) & ~255ull, a4 = (bound * 4 + 255) & ~255ull, a2 = (bound * 2 + 255) & ~255ull;
-    if (hipMalloc(&drows, 2 * a8 + a4 + a2 + bound + 256) != hipSuccess) {
-      done();
-      return fail(CASK_E_DEVICE);
-    }
+    if (hipMalloc(&drows, 2 * a8 + a4 + a2 + bound + 256) != hipSuccess) return fail(CASK_E_DEVICE);
     uint8_t* rb = (uint8_t*)drows;
     cask_rows rows{};
     rows.capacity = bound;
@@ -1704,25 +1726,57 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
     rows.status = rb + 2 * a8 + a4 + a2;
     std::vector<uint64_t> roff(n + 1);
     cask_scan_error se{};
-    st = cask_scan_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
-    if (st != CASK_OK) {
-      done();
-      return fail(st);
+    int st = hint ? cask_parse_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se)
+                  : cask_scan_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
+    if (st != CASK_OK) return fail(st);
+    if (!hint && write_hints) {  // RecreateHints (log.rs:137-148): every Ok row of each file, trailer
+      std::vector<uint64_t> fo(n + 1, 0);
+      st = cask_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), nullptr, 0, fo.data());
+      if (st == CASK_E_CAPACITY || st == CASK_OK) {
+        st = hipMalloc(&dhint, fo[n] + 256) == hipSuccess ? CASK_OK : CASK_E_DEVICE;
+        if (st == CASK_OK) st = cask_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), dhint, fo[n] + 256, fo.data());
+      }
+      std::vector<uint8_t> hb(fo[n]);
+      if (st == CASK_OK && !hb.empty()) st = cask_copy(ctx, hb.data(), dhint, hb.size());
+      if (st != CASK_OK) return fail(st);
+      // files up to the first failing one (that one included: the drain on drop, log.rs:466-470)
+      for (size_t i = 0; i < n; ++i) {
+        if (!write_file_raw2(hint_path(path, db->files[lo + i]), hb.data() + fo[i], fo[i + 1] - fo[i],
+                             cask_xxh::xxh32(hb.data() + fo[i], fo[i + 1] - fo[i], 0)))
+          return fail(CASK_E_IO, db->files[lo + i]);
+        if (se.kind && se.file_id == db->files[lo + i]) break;
+      }
     }
-    if (se.kind) {  // the shard's first failing record: Cask::open's `?` (cask.rs:360,365)
-      done();
+    if (se.kind)  // the stretch's first failing record: Cask::open's `?` (cask.rs:360,365)
       return fail(se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF, se.file_id, se.pos, se.expected, se.found);
-    }
     const void* blk = nullptr;
     uint64_t nb = 0;
-    st = cask_shard_keydir(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb);
+    st = hint ? cask_shard_keydir_hints(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb)
+              : cask_shard_keydir(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb);
     if (st == CASK_OK) {
-      s.block.resize(nb);
-      if (hipMemcpy(s.block.data(), blk, nb, hipMemcpyDeviceToHost) != hipSuccess) st = CASK_E_DEVICE;
+      s.blocks.emplace_back(nb);
+      if (hipMemcpy(s.blocks.back().data(), blk, nb, hipMemcpyDeviceToHost) != hipSuccess) st = CASK_E_DEVICE;
     }
-    done();
     if (st != CASK_OK) return fail(st);
-    s.ms_scan = ms_since(ts);
+    s.ms_scan += ms_since(ts);
+    return true;
+  };
+  auto run_shard = [&](int r) {
+    Shard& s = sh[r];
+    if (s.lo == s.hi) return;
+    int st = CASK_OK;
+    cask_ctx* ctx = cask_ctx_create(devices[r], &st);
+    if (!ctx) {
+      s.e = cask_open_error{st, 0, 0, 0, 0};
+      return;
+    }
+    for (size_t i = s.lo; i < s.hi;) {  // maximal stretches of one kind, in order
+      size_t j = i + 1;
+      while (j < s.hi && use_hint[j] == use_hint[i]) ++j;
+      if (!run_stretch(s, devices[r], ctx, i, j, use_hint[i] != 0)) break;
+      i = j;
+    }
+    cask_ctx_destroy(ctx);
   };
   // one thread per distinct device; a device's shards run in order on its thread
   std::vector<int> devs;
@@ -1743,17 +1797,18 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
     rd = std::max(rd, s.ms_read);
     sc = std::max(sc, s.ms_scan);
   }
+  std::vector<std::vector<uint8_t>>().swap(hints);
   auto tf = std::chrono::steady_clock::now();
   db->merging = true;
-  for (int r = 0; r < ndev; ++r) {
-    if (sh[r].block.empty()) continue;
-    const int st = cask_keydir_merge(db, sh[r].block.data(), sh[r].block.size());
-    if (st != CASK_OK) {
-      set_err(err, st);
-      delete db;
-      return nullptr;
+  for (int r = 0; r < ndev; ++r)
+    for (const auto& b : sh[r].blocks) {
+      const int st = cask_keydir_merge(db, b.data(), b.size());
+      if (st != CASK_OK) {
+        set_err(err, st);
+        delete db;
+        return nullptr;
+      }
     }
-  }
   cask_keydir_finish(db);
   db->timings[0] = rd;
   db->timings[1] = sc;

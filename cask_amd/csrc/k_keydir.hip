@@ -55,6 +55,7 @@ struct KdArgs {
   unsigned long long* tot;  // [0] max seq + 1, [1] records, [2] key bytes
   uint8_t* out;       // the block
   uint64_t rec_at, key_at;
+  const uint64_t* key_at_row;  // per row: offset of its key in its file's bytes (null: pos + 18)
 };
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
@@ -86,8 +87,9 @@ __device__ __forceinline__ uint32_t row_file(const KdArgs& a, uint64_t d) {
   return lo;
 }
 
+// A row's key: at pos + 18 of a data file, or at key_at[d] of its file's bytes (a hint body).
 __device__ __forceinline__ const uint8_t* row_key(const KdArgs& a, uint64_t d, uint32_t f) {
-  return a.files[f].data + a.pos[d] + 18;
+  return a.files[f].data + (a.key_at_row ? a.key_at_row[d] : a.pos[d] + 18);
 }
 
 // Hash every row's key; per-file put counts and bytes, max sequence.
@@ -322,7 +324,7 @@ void kd_scratch_destroy(void* s) { delete (KdScratch*)s; }
 // scratch, valid until the next call).
 int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids_host, uint32_t nfiles,
              const uint64_t* row_off_host, const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz,
-             const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes) {
+             const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes, const uint64_t* key_at) {
   KdScratch& S_ = *(KdScratch*)scratch;
   hipStream_t st = S(stream);
   if (n >= (1ull << 32)) return -10;  // row indices are 32-bit per shard
@@ -357,6 +359,7 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   a.vsz = vsz;
   a.ksz = ksz;
   a.n = n;
+  a.key_at_row = key_at;
   a.h = (uint64_t*)(b + o_h);
   a.idx = (uint32_t*)(b + o_idx);
   a.fidx = (uint32_t*)(b + o_fidx);
@@ -474,6 +477,44 @@ __global__ void k_hint_starts(HpArgs a) {
     const uint64_t r = a.row_off[f];
     a.fstart[f] = r < a.n ? a.off[r] : (a.n ? a.off[a.n - 1] + a.sz[a.n - 1] : 0ull);
   }
+}
+
+// Rows of hint bodies (cask_parse_hints_device) into keydir rows: pos becomes the entry position
+// the hint records (bytes 14..21 of the hint, Hint::write_bytes, data.rs:242-256) and key_at the
+// key's offset in the body (22 bytes in).
+__global__ __launch_bounds__(256) void k_hint_entries(const FileDesc* files, const uint64_t* row_off, uint32_t nfiles,
+                                                      uint64_t n, uint64_t* pos, uint64_t* key_at) {
+  for (uint64_t d = blockIdx.x * 256ull + threadIdx.x; d < n; d += (uint64_t)gridDim.x * 256ull) {
+    uint32_t lo = 0, hi = nfiles;  // the row's file: last f with row_off[f] <= d
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (row_off[mid] <= d) lo = mid; else hi = mid;
+    }
+    const uint64_t off = pos[d];
+    const uint8_t* h = files[lo].data + off;
+    uint64_t ep = 0;
+    for (int i = 0; i < 8; ++i) ep |= (uint64_t)h[14 + i] << (8 * i);
+    pos[d] = ep;
+    key_at[d] = off + 22;
+  }
+}
+
+int hint_entries(void* scratch, const FileDesc* files_host, uint32_t nfiles, const uint64_t* row_off_host,
+                 uint64_t n, uint64_t* pos, uint64_t* key_at, void* stream) {
+  KdScratch& S_ = *(KdScratch*)scratch;
+  hipStream_t st = S(stream);
+  const uint64_t o_rowoff = al(sizeof(FileDesc) * (nfiles + 1));
+  if (!S_.ensure(o_rowoff + 8ull * (nfiles + 1))) return -13;
+  FileDesc* d_fd = (FileDesc*)S_.p;
+  uint64_t* d_ro = (uint64_t*)((uint8_t*)S_.p + o_rowoff);
+  bool ok = hipMemcpyAsync(d_fd, files_host, sizeof(FileDesc) * nfiles, hipMemcpyHostToDevice, st) == hipSuccess &&
+            hipMemcpyAsync(d_ro, row_off_host, 8ull * (nfiles + 1), hipMemcpyHostToDevice, st) == hipSuccess;
+  if (!ok) return -11;
+  if (n) {
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 255) / 256, (uint64_t)device_cus() * 16);
+    hipLaunchKernelGGL(k_hint_entries, dim3(grid), dim3(256), 0, st, d_fd, d_ro, nfiles, n, pos, key_at);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -11;
 }
 
 // Returns 0 or a negative cask_status. file_start (host, nfiles + 1): each file's body in `out`.

@@ -189,7 +189,10 @@ void* kd_scratch_create();
 void kd_scratch_destroy(void* s);
 int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids_host, uint32_t nfiles,
              const uint64_t* row_off_host, const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz,
-             const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes);
+             const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes,
+             const uint64_t* key_at = nullptr);
+int hint_entries(void* scratch, const FileDesc* files_host, uint32_t nfiles, const uint64_t* row_off_host,
+                 uint64_t n, uint64_t* pos, uint64_t* key_at, void* stream);
 int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const uint64_t* row_off_host,
               const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz, const uint16_t* ksz, const uint8_t* status,
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream);

@@ -94,6 +94,7 @@ struct cask_ctx {
   DevBuf repair;     // runs (u64 x 2 per chunk) | cerr (u32) | redo (u8) | long_done (u8)
   DevBuf lq;         // long-record queue (slot indices by length class)
   DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
+  DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
   uint32_t epoch = 0;
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
@@ -819,6 +820,41 @@ extern "C" int cask_hints_device(cask_ctx* c, const cask_file_view* files, uint3
   for (uint32_t i = 0; i < nfiles; ++i) fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
   return hint_pack(c->kd, fd.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz, rows->status,
                    rows->count, out, out ? cap : 0, file_hint_offset, c->stream);
+}
+
+// The shard block of hint-file bodies (the hint fast path on the multi-GPU replay): rows as
+// cask_parse_hints_device left them; their pos is rewritten to the entry positions.
+extern "C" int cask_shard_keydir_hints(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                                       const uint64_t* file_row_offset, const void** block, uint64_t* bytes) {
+  if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
+  if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz)) return CASK_E_INVALID_ARG;
+  for (uint32_t i = 0; i < nfiles; ++i)
+    if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
+  if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+  if (!c->keyat.ensure(8 * (rows->count + 1))) return CASK_E_NOMEM;
+  std::vector<FileDesc> fd(nfiles + 1);
+  std::vector<uint32_t> ids(nfiles + 1, 0);
+  for (uint32_t i = 0; i < nfiles; ++i) {
+    fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
+    ids[i] = files[i].file_id;
+  }
+  uint64_t* key_at = c->keyat.as<uint64_t>();
+  int rc = hint_entries(c->kd, fd.data(), nfiles, file_row_offset, rows->count, rows->pos, key_at, c->stream);
+  void* out = nullptr;
+  uint64_t nb = 0;
+  if (!rc)
+    rc = kd_build(c->kd, fd.data(), ids.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz,
+                  rows->count, c->stream, &out, &nb, key_at);
+  if (rc) {
+    snprintf(c->last_error, sizeof(c->last_error), "cask_shard_keydir_hints: %s", rc == CASK_E_NOMEM ? "out of memory" : "device");
+    return rc;
+  }
+  *block = out;
+  *bytes = nb;
+  return CASK_OK;
 }
 
 extern "C" int cask_shard_keydir(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,

@@ -17,6 +17,18 @@ def shard_keydir(ctx, files, rows: dict, count: int, file_row_offset):
     """The keydir block of the files one rank scanned: `files` [(file_id, uint8 CUDA tensor)] as
     passed to ctx.scan_device, its rows dict and ScanResult.count / file_row_offset (every row Ok).
     Returns a uint8 CUDA tensor (a copy: the context's buffer is reused by its next call)."""
+    return _shard(ctx, ctx.lib.cask_shard_keydir, "cask_shard_keydir", files, rows, count, file_row_offset)
+
+
+def shard_keydir_hints(ctx, bodies, rows: dict, count: int, file_row_offset):
+    """The same block from hint-file bodies (the hint fast path, log.rs:121-135): `bodies`
+    [(file_id, uint8 CUDA tensor without the trailer)] and the rows of ctx.parse_hints_device
+    (every row Ok; their pos is rewritten to entry positions)."""
+    return _shard(ctx, ctx.lib.cask_shard_keydir_hints, "cask_shard_keydir_hints", bodies, rows, count,
+                  file_row_offset)
+
+
+def _shard(ctx, fn, name, files, rows, count, file_row_offset):
     import torch
     n = len(files)
     views = (L.FileView * max(n, 1))()
@@ -33,8 +45,8 @@ def shard_keydir(ctx, files, rows: dict, count: int, file_row_offset):
     off = (C.c_uint64 * (n + 1))(*[int(x) for x in file_row_offset])
     blk, nb = C.c_void_p(), C.c_uint64()
     ctx._inputs_ready()
-    rc = ctx.lib.cask_shard_keydir(ctx._h, views, n, C.byref(r), off, C.byref(blk), C.byref(nb))
-    raise_status(rc, what=f"cask_shard_keydir: {ctx.last_error()}")
+    rc = fn(ctx._h, views, n, C.byref(r), off, C.byref(blk), C.byref(nb))
+    raise_status(rc, what=f"{name}: {ctx.last_error()}")
     dev = torch.device("cuda", ctx.device)
     out = torch.empty(int(nb.value), dtype=torch.uint8, device=dev)
     ctx._inputs_ready()  # the allocation is ordered on torch's stream
@@ -72,13 +84,14 @@ class KeydirFold:
 
 def open_multi(path: str, devices, options: CaskOptions | None = None) -> Cask:
     """cask_db_open_multi: Cask::open with the data files split over `devices` (GPU ordinals of
-    this process, repeats allowed)."""
+    this process, repeats allowed). Files with a valid hint file are replayed from it (parsed on the
+    device); the others are scanned and, unless options.write_hints(False), get their hint files."""
     o = options or CaskOptions()
     lib = L.lib()
     opts = L.Options()
     lib.cask_options_default(C.byref(opts))
     opts.create = 1 if o._create else 0
-    opts.write_hints = 0
+    opts.write_hints = 1 if o._write_hints else 0
     opts.max_file_size = o._max_file_size
     devs = (C.c_int * len(devices))(*[int(d) for d in devices])
     err = L.OpenError()

@@ -346,6 +346,12 @@ int cask_hints_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfile
 int cask_shard_keydir(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
                       const uint64_t* file_row_offset, const void** block, uint64_t* bytes);
 
+/* The same block from hint-file bodies (the hint fast path of the replay, log.rs:121-135): `files`
+ * and `rows` as cask_parse_hints_device took and returned them, every row Ok; the rows' pos is
+ * rewritten to the entry positions the hints hold. */
+int cask_shard_keydir_hints(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
+                            const uint64_t* file_row_offset, const void** block, uint64_t* bytes);
+
 /* Copy `bytes` between any two memories (device or host) on the context's stream, synchronously:
  * e.g. a keydir block out of the context's buffer. */
 int cask_copy(cask_ctx* ctx, void* dst, const void* src, uint64_t bytes);
@@ -359,9 +365,11 @@ int cask_keydir_finish(cask_db* db);
 
 /* Cask::open over several GPUs of this process (replaces cask.rs:346-382 like cask_db_open): the
  * data files are split into contiguous ranges, one per entry of `devices` (a device may appear more
- * than once: its shards run one after another); each range is read, scanned and reduced to its
- * keydir block on its device, the blocks come back to the host and are folded in order. Every data
- * file is scanned: hint files are neither read nor written on this path (configs[4]). */
+ * than once: its shards run one after another); within a range, files with a valid hint file are
+ * replayed from it (the body parsed on the device, cask_parse_hints_device), the others scanned
+ * (and given their hint files when opts->write_hints); each stretch of files of one kind becomes a
+ * keydir block on its device, and the blocks are folded on the host in order. On a failure, hint
+ * files of ranges after the failing file may have been written too (the ranges run in parallel). */
 cask_db* cask_db_open_multi(const char* path, const cask_options* opts, const int* devices, int ndevices,
                             cask_open_error* err);
 

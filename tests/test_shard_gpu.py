@@ -101,14 +101,77 @@ def test_two_shards_in_process_fold(gpu_ctx, tmp_path):
 
 
 def test_open_multi_matches_replay(native, tmp_path):
+    from cask_amd import CaskOptions
     from cask_amd.keydir import open_multi
     path = str(tmp_path / "db")
     _make_db(path, 11, nfiles=7)
     want = _want(path)
     for devices in ([0], [0, 0], [0, 0, 0, 0], [0] * 9):
-        with open_multi(path, devices) as db:
+        with open_multi(path, devices, CaskOptions().write_hints(False)) as db:
             assert _got(db) == want, devices
             assert db.files() == R.find_data_files(path)
+    assert not any(f.endswith(".hint") for f in os.listdir(path))
+
+
+def test_open_multi_hint_files(native, tmp_path):
+    """The hint fast path on the multi-GPU replay: the scanned files get their hint files (byte for
+    byte the restatement's RecreateHints output); a second open takes the hints — parsed on the
+    device — even for data files corrupted since (the reference trusts a valid hint file,
+    log.rs:121-135); a mix of hinted and scanned files in one shard; a truncated hint body."""
+    from cask_amd import errors
+    from cask_amd.keydir import open_multi
+    path = str(tmp_path / "db")
+    _make_db(path, 13, nfiles=6)
+    want = _want(path)
+    ref = str(tmp_path) + "/ref_hints"
+    shutil.copytree(path, ref)
+    R.replay(ref)  # writes the hint files
+    with open_multi(path, [0, 0, 0]) as db:
+        assert _got(db) == want
+    for f in R.find_data_files(path):
+        assert open(R.hint_file_path(path, f), "rb").read() == open(R.hint_file_path(ref, f), "rb").read()
+    # corrupt every data file: the hints are trusted
+    for f in R.find_data_files(path):
+        p = R.data_file_path(path, f)
+        b = bytearray(open(p, "rb").read())
+        b[len(b) // 2] ^= 0x20
+        open(p, "wb").write(bytes(b))
+    for devices in ([0], [0, 0], [0] * 4):
+        with open_multi(path, devices) as db:
+            assert _got(db) == want, devices
+    # mixed: files 2 and 5 lose their hint files (restore their data first)
+    for f in (2, 5):
+        shutil.copy(R.data_file_path(ref, f), R.data_file_path(path, f))
+        os.remove(R.hint_file_path(path, f))
+    with open_multi(path, [0, 0]) as db:
+        assert _got(db) == want
+    assert os.path.exists(R.hint_file_path(path, 2))
+    # a hint body cut short inside a record (valid trailer): Io(UnexpectedEof), as Hints::next
+    hp = R.hint_file_path(path, 4)
+    body = open(hp, "rb").read()[:-4][:-7]
+    open(hp, "wb").write(body + R.xxhash32(body).to_bytes(4, "little"))
+    with pytest.raises(errors.UnexpectedEof) as ei:
+        open_multi(path, [0, 0])
+    assert ei.value.file_id == 4
+
+
+def test_hint_block_equals_data_block(gpu_ctx, tmp_path):
+    """A shard's block from its hint bodies (parsed on the device) is byte for byte the block from
+    its data files."""
+    import torch
+    from cask_amd.keydir import shard_keydir_hints
+    path = str(tmp_path / "db")
+    _make_db(path, 14, nfiles=4, nrec=4000)
+    R.replay(path)
+    files = _files(path)
+    for part in (files, files[1:3]):
+        bodies = [(fid, torch.from_numpy(np.frombuffer(open(R.hint_file_path(path, fid), "rb").read()[:-4],
+                                                       np.uint8).copy()).cuda()) for fid, _ in part]
+        res = gpu_ctx.parse_hints_device(bodies)
+        assert res.error is None
+        blk = shard_keydir_hints(gpu_ctx, bodies, {"pos": res.pos, "seq": res.seq, "vsz": res.vsz, "ksz": res.ksz,
+                                                   "status": res.status}, res.count, res.file_row_offset)
+        assert blk.cpu().numpy().tobytes() == _device_block(gpu_ctx, part)
 
 
 def test_open_multi_reports_first_failure(native, tmp_path):
