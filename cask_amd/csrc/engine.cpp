@@ -1553,6 +1553,9 @@ int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     };
     for (unsigned q = t; q < S; q += nt) {
       KeyDir& kd = db->index.sub[q];
+      uint64_t cnt = 0;  // room for every record's key: a block holds about one record per key
+      for (unsigned g = 0; g < nt; ++g) cnt += lists[g][q].size();
+      kd.reserve(kd.live + cnt);
       for (int phase = 0; phase < 2; ++phase)
         for (unsigned g = 0; g < nt; ++g) {
           const uint64_t lo = n * g / nt;
