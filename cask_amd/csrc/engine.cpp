@@ -96,6 +96,11 @@ class KeyDir {
 
   const uint8_t* key_of(const Slot& s) const { return arena.data() + s.key_off; }
   void prefetch(uint64_t h) const { __builtin_prefetch(&slots[h & (slots.size() - 1)]); }
+  // the key bytes of the slot h lands on, once that slot is in cache (prefetch() a few records before)
+  void prefetch_key(uint64_t h) const {
+    const Slot& s = slots[h & (slots.size() - 1)];
+    if (s.state == 1 && s.hash == h) __builtin_prefetch(arena.data() + s.key_off);
+  }
 
   int64_t find(const uint8_t* k, uint32_t n, uint64_t h) const {
     const uint64_t m = slots.size() - 1;
@@ -226,6 +231,7 @@ class Index {
     sub[sub_of(h)].update_kd(key, ksz, file_id, pos, vsz_raw, seq, h);
   }
   void prefetch(uint64_t h) const { sub[sub_of(h)].prefetch(h); }
+  void prefetch_key(uint64_t h) const { sub[sub_of(h)].prefetch_key(h); }
   template <class F>
   void for_each_live(F fn) const {
     for (const KeyDir& t : sub)
@@ -418,6 +424,22 @@ bool write_file_raw2(const std::string& p, const uint8_t* b, size_t n, uint32_t 
   return ok;
 }
 
+// A host byte buffer that is not zero-filled (a std::vector<uint8_t> of the hint bodies would write
+// every byte once more before the copy from the device overwrites it).
+struct RawBytes {
+  std::unique_ptr<uint8_t[]> p;
+  uint64_t n = 0;
+  bool resize(uint64_t b) {
+    p.reset(b ? new (std::nothrow) uint8_t[b] : nullptr);
+    n = p || !b ? b : 0;
+    return p || !b;
+  }
+  uint8_t* data() { return p.get(); }
+  const uint8_t* data() const { return p.get(); }
+  uint64_t size() const { return n; }
+  bool empty() const { return n == 0; }
+};
+
 // The scan side of Cask::open on one GPU, kept per device for the life of the process (a context,
 // its buffers and a ring of pinned staging buffers are created once, not per open): data files
 // read by host threads into pinned buffers and copied to the device as they arrive, the device
@@ -548,7 +570,7 @@ struct EngineDev {
     return CASK_E_DEVICE;
   }
 
-  int hints(const std::vector<cask_file_view>& v, const std::vector<uint64_t>& row_off, std::vector<uint8_t>& hbuf,
+  int hints(const std::vector<cask_file_view>& v, const std::vector<uint64_t>& row_off, RawBytes& hbuf,
             std::vector<uint64_t>& hs0, std::vector<uint64_t>& hs1, const std::vector<uint32_t>& view_file) {
     std::vector<uint64_t> fo(v.size() + 1, 0);
     int st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), nullptr, 0, fo.data());
@@ -556,7 +578,7 @@ struct EngineDev {
     if (!hint.ensure(fo[v.size()] + 256)) return CASK_E_NOMEM;
     st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), hint.p, hint.cap, fo.data());
     if (st != CASK_OK) return st;
-    hbuf.resize(fo[v.size()]);
+    if (!hbuf.resize(fo[v.size()])) return CASK_E_NOMEM;
     if (!hbuf.empty() && cask_copy(ctx, hbuf.data(), hint.p, hbuf.size()) != CASK_OK) return CASK_E_DEVICE;
     for (size_t k = 0; k < v.size(); ++k) {
       hs0[view_file[k]] = fo[k];
@@ -629,13 +651,15 @@ void parallel_fold(FoldRec* recs, uint64_t n, Index& out) {
         const uint64_t lo = n * g / nt;
         const std::vector<uint32_t>& L = lists[g][q];
         const size_t m = L.size();
-        for (size_t j = 0; j < m; ++j) {  // the record 16 ahead, and the slot and key of the one 8 ahead
+        for (size_t j = 0; j < m; ++j) {  // the record 16 ahead, the slot and key of the one 8 ahead,
+                                          // the keydir's copy of the key of the one 4 ahead
           if (j + 16 < m) __builtin_prefetch(&recs[lo + L[j + 16]]);
           if (j + 8 < m) {
             const FoldRec& a = recs[lo + L[j + 8]];
             kd.prefetch(a.hash);
             __builtin_prefetch(a.key);
           }
+          if (j + 4 < m) kd.prefetch_key(recs[lo + L[j + 4]].hash);
           const FoldRec& r = recs[lo + L[j]];
           kd.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, delta[q], &out.stats);
         }
@@ -793,7 +817,7 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   // host threads overlapped with the copies), scanned there, and their hint bodies built there
   // (cask_hints_device) and brought back: the host never holds the data bytes, only the hint
   // records it writes and folds.
-  std::vector<uint8_t> hbuf;                 // hint bodies of the scanned files, file after file
+  RawBytes hbuf;                             // hint bodies of the scanned files, file after file
   std::vector<uint64_t> hs0(nf, 0), hs1(nf, 0);  // body of scanned file i: hbuf[hs0[i], hs1[i])
   cask_scan_error se{};
   uint32_t err_file = UINT32_MAX;            // index into files of the scan's first failure
@@ -1075,7 +1099,7 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
       for (uint64_t g = lo; g < hi;) {
         HintFile& H = hf[used[u]];
         const uint64_t e = std::min<uint64_t>(hi, H.base + H.offs.size());
-        constexpr uint64_t D = 8;  // lookups in flight: hashes computed D records ahead, slots prefetched
+        constexpr uint64_t D = 16;  // lookups in flight: slots prefetched D records ahead, keys D/2
         uint64_t hr[D];
         auto hash_at = [&](uint64_t i) {
           const uint8_t* h = H.hb.data() + H.offs[i];
@@ -1087,6 +1111,7 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
           db->index.prefetch(hr[i % D]);
         }
         for (uint64_t i = i0; i < i1; ++i) {
+          if (i + D / 2 < i1) db->index.prefetch_key(hr[(i + D / 2) % D]);
           const uint8_t* h = H.hb.data() + H.offs[i];
           const cask_index_entry* ie = db->index.get_h(h + 22, rd16(h + 8), hr[i % D]);
           H.kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
@@ -1559,8 +1584,11 @@ int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
       for (int phase = 0; phase < 2; ++phase)
         for (unsigned g = 0; g < nt; ++g) {
           const uint64_t lo = n * g / nt;
-          for (uint32_t j : lists[g][q]) {
-            const uint64_t i = lo + j;
+          const std::vector<uint32_t>& Lq = lists[g][q];
+          for (size_t jj = 0; jj < Lq.size(); ++jj) {
+            if (jj + 8 < Lq.size()) kd.prefetch(hs[lo + Lq[jj + 8]]);
+            if (jj + 4 < Lq.size()) kd.prefetch_key(hs[lo + Lq[jj + 4]]);
+            const uint64_t i = lo + Lq[jj];
             const ShardRec& r = rec[i];
             const uint8_t* k = keys + ko[i];
             const int64_t f = kd.find(k, r.ksz, hs[i]);
