@@ -111,6 +111,40 @@ class ScanContext:
         """files: list of (file_id, uint8 CUDA tensor). rows: dict from alloc_rows (reused if given)."""
         return self._scan_device(self.lib.cask_scan_device, "cask_scan_device", files, rows, raise_on_capacity)
 
+    def prepare_scan(self, files, rows: dict):
+        """A repeatable cask_scan_device call on the same device-resident files and rows, its ctypes
+        arguments built once (what a compiled caller of the C ABI pays per call: the call itself).
+        Returns (run, timings): run() issues the scan and returns the row count (raising on any
+        error); timings(out) copies the call's six phase times (ms) into a float array."""
+        n = len(files)
+        views = (L.FileView * max(n, 1))()
+        for i, (fid, t) in enumerate(files):
+            assert t.is_cuda and t.dtype.itemsize == 1 and t.is_contiguous()
+            views[i].file_id = int(fid)
+            views[i].flags = L.VIEW_DEVICE
+            views[i].data = t.data_ptr() if t.numel() else None
+            views[i].len = t.numel()
+        r = L.Rows()
+        r.capacity = rows["pos"].numel()
+        r.pos, r.seq = rows["pos"].data_ptr(), rows["seq"].data_ptr()
+        r.vsz, r.ksz, r.status = rows["vsz"].data_ptr(), rows["ksz"].data_ptr(), rows["status"].data_ptr()
+        off = (C.c_uint64 * (n + 1))()
+        e = L.ScanError()
+        self._inputs_ready()
+        fn, h, rr, ee, lib = self.lib.cask_scan_device, self._h, C.byref(r), C.byref(e), self.lib
+
+        def run():
+            rc = fn(h, views, n, rr, off, ee)
+            if rc or e.kind:
+                raise_status(rc, what=f"cask_scan_device: {self.last_error()}")
+                raise RuntimeError(f"scan failure {_err(e)}")
+            return r.count
+
+        def timings(out):
+            lib.cask_last_timings(h, out)
+
+        return run, timings
+
     def parse_hints_device(self, bodies, rows: dict | None = None, raise_on_capacity: bool = True) -> ScanResult:
         """Hint-file bodies (trailer excluded) on the device, parsed there (cask_parse_hints_device:
         Hints::next / Hint::from_read, log.rs:437-447, data.rs:258-276). Row pos = the hint's offset in
