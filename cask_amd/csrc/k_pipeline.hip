@@ -388,8 +388,12 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   __shared__ u32x4 s_desc[TC];            // regular chunk: first row; else slot row of the chunk
   __shared__ uint64_t s_c0[TC], s_len[TC];
   __shared__ uint32_t s_reg[TC];          // regular flag
+  __shared__ uint32_t s_long;             // the tile has a record for k_long_hash
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(&a.ctr->tile_next, 1u);
+  if (tid == 0) {
+    s_tile = atomicAdd(&a.ctr->tile_next, 1u);
+    s_long = 0u;
+  }
   __syncthreads();
   const uint64_t tile = s_tile;
   const uint64_t c = tile * TC + tid;
@@ -468,7 +472,9 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
     if (cerr != 0xFFFFFFFFu) atomicMax(&a.err_inv[fi], ~(unsigned long long)(base + cerr));
     if (c + 1 == a.total_chunks) a.ctr->total_rows = base + n;
   }
-  if (__ballot(act && lr != 0xFFFFFFFFu) && lane == 0) atomicOr(&a.ctr->long_pending, 1u);
+  // one store per tile that has long records (configs[2]: nearly every tile; an atomic per wave on
+  // one word serialised thousands of updates in L2)
+  if (__ballot(act && lr != 0xFFFFFFFFu) && lane == 0) s_long = 1u;
   // rows of the tile: [tile_lo, tile_lo + tile_rows)
   const uint64_t tile_lo = P.rows, tile_rows = total.rows;
   s_base[tid] = (uint32_t)(base - tile_lo);
@@ -478,6 +484,7 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   s_len[tid] = len;
   if (act && (cw & kCountRegular)) s_desc[tid] = ((const u32x4*)a.desc)[c];
   __syncthreads();
+  if (tid == 0 && s_long) a.ctr->long_pending = 1u;  // every writer stores the same value
   if (!tile_rows) return;
   const uint64_t cap = a.row_cap;
   const uint64_t g0 = tile_lo >> 2, g1 = (tile_lo + tile_rows + 3) >> 2;
@@ -717,11 +724,13 @@ int device_cus() {
   return cached[dev];
 }
 
-void launch_long(const ScanArgs& a, void* stream) {
+void launch_long(const ScanArgs& a, void* stream, bool enqueue) {
   if (!a.total_chunks) return;
-  uint64_t blocks = (a.total_chunks + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(k_long_enqueue, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
+  if (enqueue) {  // (the walk mode's first pass queues its long records itself)
+    uint64_t blocks = (a.total_chunks + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(k_long_enqueue, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
+  }
   const int cus = device_cus();
   hipLaunchKernelGGL(k_long_hash, dim3((uint32_t)cus * 8u), dim3(256), 0, S(stream), a);
 }

@@ -177,7 +177,7 @@ uint32_t geometry_chunk(int geo);
 uint32_t geometry_halo(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
 int device_cus();  // compute units of the current device (cached per device)
-void launch_long(const ScanArgs& a, void* stream);  // k_long_enqueue + k_long_hash
+void launch_long(const ScanArgs& a, void* stream, bool enqueue = true);  // k_long_enqueue + k_long_hash
 void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);

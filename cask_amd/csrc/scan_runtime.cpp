@@ -451,10 +451,23 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     L("k_scan_chunks");
   }
   H(hipEventRecord(c->ev[2], st));
+  // walk mode (logs of long records): the long-record pass follows k_finish on the device with no
+  // host round trip between them (it fixes dense statuses; if some start turns out wrong the repair
+  // path below re-hashes every long record, so nothing it wrote is kept). Queueing the long records
+  // from the walk itself instead of k_long_enqueue measured 1 ms slower (the queue counters'
+  // atomics).
+  const bool long_now = dense && walk && !hint;
   if (dense) {
     launch_finish(a, st);
     L("k_finish");
     H(hipEventRecord(c->ev[3], st));
+    if (long_now) {
+      ScanArgs ad = a;
+      ad.dense = 1;
+      launch_long(ad, st);
+      L("k_long");
+      H(hipEventRecord(c->ev[4], st));
+    }
     read_call();
     if (!ok) return CASK_E_DEVICE;
   }
@@ -464,12 +477,13 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // every speculated start held: the rows are final but for the long records' checksums
     a.dense = 1;
     c->last_dense = 1;
-    if (hc->long_pending) {
+    const bool more = !long_now && hc->long_pending;
+    if (more) {
       launch_long(a, st);
       L("k_long");
     }
-    H(hipEventRecord(c->ev[4], st));
-    if (hc->long_pending) read_call();
+    if (!long_now) H(hipEventRecord(c->ev[4], st));
+    if (more) read_call();
     else H(hipEventSynchronize(c->ev[4]), "event sync");
     if (!ok) return CASK_E_DEVICE;
     float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0;
@@ -549,6 +563,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     }
     post(false);
   };
+  if (long_now)  // the dense attempt's long hashing is void: every long record is queued again
+    H(hipMemsetAsync(a.long_done, 0, total_chunks, st), "memset long_done");
   // the first scan has run (its counters are in the call block): keep its run counter's effects,
   // clear the per-file error state the validation builds
   H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
