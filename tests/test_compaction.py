@@ -299,3 +299,37 @@ def test_engine_compact_trigger(native, tmp_path):
         assert rep is not None and rep["compacted"] == len(sel)
         _check_same(db, path, rdb, ref)
         assert db.compact() is None  # the new file has no dead entries and no trigger fires
+
+
+@pytest.mark.gpu
+def test_device_memory_flat_over_repeated_open_compact(native, tmp_path):
+    """Round-1 advice: contexts and per-open buffers must not leak HBM. The engine keeps one
+    context and its buffers per device for the process (sized to the largest open so far), so
+    after the first open + compaction, repeating them leaves free device memory where it was; a
+    ScanContext created and destroyed in a loop gives back what it took."""
+    import torch
+    from cask_amd import CaskOptions, ScanContext
+    rng = random.Random(31)
+    path = str(tmp_path / "db")
+    R.write_log(path, _workload(rng, 20000, 3000), max_file_size=256 << 10, write_hints=False)
+
+    def cycle():
+        for f in os.listdir(path):  # every open scans (no hint files), every compaction rewrites
+            if f.endswith(".cask.hint"):
+                os.remove(os.path.join(path, f))
+        with CaskOptions().max_file_size(256 << 10).open(path) as db:
+            db.compact_files(db.files())
+        torch.cuda.synchronize()
+
+    cycle()
+    free0 = torch.cuda.mem_get_info()[0]
+    for _ in range(4):
+        cycle()
+    assert abs(torch.cuda.mem_get_info()[0] - free0) < (64 << 20)
+    x = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")  # ScanContext scratch is per context
+    for _ in range(5):
+        ctx = ScanContext(0)
+        ctx.scan_device([(1, x)])
+        ctx.close()
+    torch.cuda.synchronize()
+    assert abs(torch.cuda.mem_get_info()[0] - free0) < (64 << 20)
