@@ -76,11 +76,12 @@ __global__ __launch_bounds__(256) void k_long_enqueue(ScanArgs a) {
   __shared__ uint32_t cnt1[kLqClasses], cnt2[kLqClasses];
   __shared__ uint64_t gb[kLqClasses];
   uint32_t nl = 0;
-  for (uint64_t base = blockIdx.x * 256ull; base < a.total_chunks; base += (uint64_t)gridDim.x * 256ull) {
+  const uint64_t t_hi = a.t_hi ? a.t_hi : a.total_chunks;
+  for (uint64_t base = a.t_lo + blockIdx.x * 256ull; base < t_hi; base += (uint64_t)gridDim.x * 256ull) {
     if (threadIdx.x < kLqClasses) cnt1[threadIdx.x] = cnt2[threadIdx.x] = 0;
     __syncthreads();
     const uint64_t t = base + threadIdx.x;
-    const bool act = t < a.total_chunks && a.long_r[t] != 0xFFFFFFFFu && !a.long_done[t];
+    const bool act = t < t_hi && a.long_r[t] != 0xFFFFFFFFu && !a.long_done[t];
     if (act) long_rows(a, t, [&](uint64_t, uint32_t c) { atomicAdd(&cnt1[c], 1u); });
     __syncthreads();
     if (threadIdx.x < kLqClasses && cnt1[threadIdx.x])
@@ -129,9 +130,12 @@ __global__ __launch_bounds__(256) void k_long_hash(ScanArgs a) {
   if (threadIdx.x < kLqClasses) {
     const uint32_t b = kLqMinLog + threadIdx.x;
     const uint64_t cap = lq_region_cap(a.total_chunks, a.chunk, b);
-    const uint64_t c = a.ctr->lq_cnt[threadIdx.x];
-    cnt[threadIdx.x] = c < cap ? c : cap;
-    base[threadIdx.x] = lq_region_base(a.total_chunks, a.chunk, b);
+    uint64_t hi = a.lq_hi ? a.lq_hi[threadIdx.x] : a.ctr->lq_cnt[threadIdx.x];
+    uint64_t lo = a.lq_lo ? a.lq_lo[threadIdx.x] : 0u;
+    hi = hi < cap ? hi : cap;
+    lo = lo < hi ? lo : hi;
+    cnt[threadIdx.x] = hi - lo;
+    base[threadIdx.x] = lq_region_base(a.total_chunks, a.chunk, b) + lo;
   }
   __syncthreads();
   uint64_t total = 0;
@@ -724,15 +728,28 @@ int device_cus() {
   return cached[dev];
 }
 
-void launch_long(const ScanArgs& a, void* stream, bool enqueue) {
+void launch_long_enqueue(const ScanArgs& a, void* stream) {
+  const uint64_t t_hi = a.t_hi ? a.t_hi : a.total_chunks;
+  if (t_hi <= a.t_lo) return;
+  uint64_t blocks = (t_hi - a.t_lo + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(k_long_enqueue, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
+}
+void launch_long_hash(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
-  if (enqueue) {  // (the walk mode's first pass queues its long records itself)
-    uint64_t blocks = (a.total_chunks + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(k_long_enqueue, dim3((uint32_t)blocks), dim3(256), 0, S(stream), a);
-  }
   const int cus = device_cus();
   hipLaunchKernelGGL(k_long_hash, dim3((uint32_t)cus * 8u), dim3(256), 0, S(stream), a);
+}
+void launch_long(const ScanArgs& a, void* stream, bool enqueue) {
+  if (!a.total_chunks) return;
+  if (enqueue) launch_long_enqueue(a, stream);
+  launch_long_hash(a, stream);
+}
+__global__ void k_lq_snap(const Counters* ctr, uint32_t* out) {
+  if (threadIdx.x < kLqClasses) out[threadIdx.x] = ctr->lq_cnt[threadIdx.x];
+}
+void launch_lq_snap(const ScanArgs& a, uint32_t* out, void* stream) {
+  hipLaunchKernelGGL(k_lq_snap, dim3(1), dim3(64), 0, S(stream), a.ctr, out);
 }
 void launch_validate(const ScanArgs& a, void* stream) {
   if (!a.nfiles) return;

@@ -5,10 +5,8 @@
 // to 64 KiB, 96 % of the bytes in records > 2 KiB) those bytes are then read a second time by
 // k_long_hash. Here a wave walks a run of chunks by chasing record headers (Entries::next,
 // log.rs:403-429: each record starts where the previous one ends; a KiB staged in LDS per round
-// trip) and hashes every record itself from HBM (Entry::from_read's check, data.rs:185-198), a quad
-// of lanes per record, 16 records of one length class at a time — so every byte is read once and
-// the latency of the chase is hidden behind other waves' hashing. Records over kWalkHashMax are
-// left to k_long_hash.
+// trip), writing the rows; k_hash_short then hashes the short records from HBM and k_long_hash the
+// long ones, so every byte is read once.
 //
 // The output is the chunk table and slot rows of k_scan_chunks (spec, exit, count, long_r, cerr,
 // long_done, slot rows; never a regular chunk), so k_finish, the validation/repair passes and
@@ -23,6 +21,8 @@
 
 #include <stdlib.h>
 
+#include <algorithm>
+
 namespace cask_dev {
 
 constexpr uint32_t kWalkWin = 4096;                   // LDS window (16-B aligned)
@@ -32,21 +32,6 @@ constexpr uint32_t kStepA = kWalkUse - 18;            // candidate offsets per p
 constexpr uint32_t kStepB = kWalkUse - 18;            // candidate offsets per hop-back window
 constexpr uint32_t kSearchPast = 1u << 20;            // pass A looks this far past the run's end
 constexpr uint32_t kLongList = 256;                   // pass A's long candidates kept for the hop back
-constexpr uint32_t kBatch = 16;                       // records hashed together (one per quad)
-// The records k_scan_chunks would hash out of LDS (lds_hashed: at most `big` bytes) are hashed here,
-// a quad per record, 16 records per batch; longer ones go to k_long_hash, which keeps far more bytes
-// in flight per CU than a walking wave can (hashing them here measured 12.8 ms against 4.5 + 6.6 ms
-// on configs[2]). A wave's batch outlives its runs (a row's verdict goes to LDS while its run is the
-// wave's current one, else straight to the chunk table), so every flush is full.
-constexpr uint32_t kClasses = 1;
-
-struct WalkEnt {
-  const uint8_t* rec;  // the record's first byte
-  uint32_t rl, st;     // length, stored checksum
-  uint32_t t, r;       // chunk, row
-  u32x4 row;
-};
-
 #ifdef CASK_STAMPS  // diagnostic build: per-wave s_memtime sums -> a.stamps[0..7] (tools/walk_stamps.py)
 #define WST(v) const uint64_t v = __builtin_amdgcn_s_memtime();
 #define WADD(i, v) wst[i] += __builtin_amdgcn_s_memtime() - (v);
@@ -57,14 +42,29 @@ struct WalkEnt {
 #define WCNT(i)
 #endif
 
+// LDS of a chasing wave (k_walk_runs): a 1-KiB window and the chunk state of its segment.
 struct WalkLds {
-  uint32_t win[kWalkWin / 4 + 16];
+  uint32_t win[1024 / 4 + 16];
   uint64_t spec[kMaxRun], exitv[kMaxRun];
   uint32_t cnt[kMaxRun], lr[kMaxRun], cerr[kMaxRun];
-  WalkEnt ent[kClasses][kBatch];
+};
+// LDS of a searching wave (k_walk_search): a 4-KiB window, the short candidates of a step and the
+// long candidates kept for the hop back.
+struct SearchLds {
+  uint32_t win[kWalkWin / 4 + 16];
   uint32_t cand[64];             // pass A: plausible short candidates of a block, in offset order
   uint64_t lx[kLongList], le[kLongList];  // pass A: long candidates x and their ends x + rl
 };
+
+// A single-wave workgroup's claim of the next item of a work counter: every lane takes part in the
+// atomic (adding 1 from lane 0, 0 from the rest) and lane 0's old value is read out. (No lane-0
+// branch: with one, the compiler threads that branch into the claiming loop's back edge, the loop
+// becomes a per-lane one, and the other lanes run on without lane 0 forever — k_walk_search hung
+// that way, barriers or not, as a one-wave workgroup's barrier is only a wave barrier.)
+__device__ __forceinline__ uint32_t wave_claim(unsigned int* ctr) {
+  const uint32_t old = atomicAdd(ctr, threadIdx.x == 0 ? 1u : 0u);
+  return __builtin_amdgcn_readfirstlane(old);
+}
 
 // Stage the window whose first usable byte is file byte wb: NL 16-B loads per lane (NL KiB), the
 // file bytes [wb, min(wb + NL KiB - 16, len)) readable. Returns the LDS byte index of wb.
@@ -103,7 +103,7 @@ constexpr uint32_t kChaseUse = kChaseNL * 1024 - 16;
 // record is staged, else from HBM), in offset order, until one matches its stored checksum. Offsets
 // whose record is longer and ends within the search horizon are listed (x, x + rl) for the hop back,
 // so it needs no second pass over the bytes (random bytes give an end that close ~1e-5 of the time).
-__device__ uint64_t walk_search(WalkLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
+__device__ __forceinline__ uint64_t walk_search(SearchLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
   const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
   const uint64_t lim = (b1 + kSearchPast < len) ? b1 + kSearchPast : len;
   const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes < this one
@@ -234,15 +234,16 @@ __device__ uint64_t walk_search(WalkLds& L, const uint8_t* data, uint64_t len, u
 __device__ __forceinline__ uint64_t hint_field64(const uint32_t* W, uint32_t x) {
   return (uint64_t)lds_u32(W, x) | ((uint64_t)lds_u32(W, x + 4) << 32);
 }
-__device__ uint64_t hint_search(WalkLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
+__device__ __forceinline__ uint64_t hint_search(WalkLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
   const uint32_t lane = threadIdx.x;
-  for (uint64_t wb = b0; wb < b1; wb += kStepB) {
-    const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
-    const uint64_t wend = (wb + kWalkUse < len) ? wb + kWalkUse : len;
-    for (uint32_t k0 = 0; k0 < kStepB; k0 += 64) {
+  constexpr uint32_t step = kChaseUse - 22;  // (1-KiB windows: hint records are small)
+  for (uint64_t wb = b0; wb < b1; wb += step) {
+    const uint32_t x0 = walk_stage<kChaseNL>(L.win, data, len, wb);
+    const uint64_t wend = (wb + kChaseUse < len) ? wb + kChaseUse : len;
+    for (uint32_t k0 = 0; k0 < step; k0 += 64) {
       const uint64_t x = wb + k0 + lane;
       bool hit = false;
-      if (k0 + lane < kStepB && x < b1 && x + 22 <= wend) {
+      if (k0 + lane < step && x < b1 && x + 22 <= wend) {
         uint64_t y = x, pos = 0;
         hit = true;
         for (int h = 0; h < 3; ++h) {  // x and the two records after it
@@ -269,37 +270,12 @@ __device__ uint64_t hint_search(WalkLds& L, const uint8_t* data, uint64_t len, u
   return kNone;
 }
 
-// Hash class k's batch: quad q takes entry q; its row goes out with the verdict (data.rs:193-198).
-// A failing row of chunk t lowers the chunk's first failing row: in LDS while t is in the wave's
-// current segment [t0, t1) (written out with the segment), else in the chunk table.
-__device__ void walk_flush(WalkLds& L, const ScanArgs& a, uint32_t k, uint32_t n, uint64_t t0, uint64_t t1,
-                           uint64_t* wst) {
-  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
-  WST(tf0)
-  __syncthreads();
-  if (q < n) {  // whole quads
-    const WalkEnt e = L.ent[k][q];
-    const uint32_t h = quad_gbl_xxh32<2>(e.rec + 4, e.rl - 4, qa);
-    if (qa == 0) {
-      u32x4 row = e.row;
-      if (h != e.st) {
-        row.w |= kSlotBad;
-        if (e.t >= t0 && e.t < t1) atomicMin(&L.cerr[e.t - t0], e.r);
-        else atomicMin(&a.cerr[e.t], e.r);
-      }
-      *(u32x4*)(a.slots + ((uint64_t)e.t * a.slot_cap + e.r) * 4) = row;
-    }
-  }
-  __syncthreads();
-  WADD(2, tf0)
-}
-
 // One stretch of a run inside one file: chunks [t0, t1) of file fd.
 // s_in: the exact start of the segment's first chunk (repair passes: spec[t0]), or kSearch for a
 // speculative one. Returns the chain position after the segment (kTerm after an EOF row).
 constexpr uint64_t kSearch = ~0ull - 1;
-__device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, uint64_t t0, uint64_t t1,
-                                 uint64_t s_in, uint32_t* nbk, uint64_t* wst) {
+__device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, uint64_t t0, uint64_t t1,
+                                 uint64_t s_in, uint64_t* wst) {
   const uint32_t lane = threadIdx.x;
   const uint32_t nch = (uint32_t)(t1 - t0);
   const uint64_t CH = a.chunk, len = fd.len;
@@ -318,8 +294,8 @@ __device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& 
   WST(ts0)
   const bool hint = a.hint != 0;
   const uint32_t hdr = hint ? 22u : 18u;
-  uint64_t p = uni64(b0 == 0 ? 0 : s_in != kSearch ? s_in
-                     : hint ? hint_search(L, data, len, b0, b1) : walk_search(L, data, len, b0, b1));
+  // (data files get their speculative starts from k_walk_search: here only hint bodies search)
+  uint64_t p = uni64(b0 == 0 ? 0 : s_in != kSearch ? s_in : hint ? hint_search(L, data, len, b0, b1) : kNone);
   WADD(0, ts0)
   if (b0 && s_in == kSearch) { WCNT(6) }
   // the chase: uniform state of the chunk the chain is in
@@ -343,7 +319,6 @@ __device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& 
     u32x4 row = u32x4{0u, 0u, 0u, off << 16};
     bool fail = false, eof = false;
     uint64_t rl = 0;
-    uint32_t stored = 0;
     if (p + hdr > len) {
       fail = eof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163; a hint: data.rs:258-265)
     } else {
@@ -366,30 +341,21 @@ __device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& 
         h = lds_hdr(L.win, x0 + (uint32_t)(p - wb));
       }
       // wave-uniform: into scalar registers
-      h.stored = __builtin_amdgcn_readfirstlane(h.stored);
       h.seq = uni64(h.seq);
       h.ksz = __builtin_amdgcn_readfirstlane(h.ksz);
       h.vsz = __builtin_amdgcn_readfirstlane(h.vsz);
-      stored = h.stored;
       row = u32x4{(uint32_t)h.seq, (uint32_t)(h.seq >> 32), h.vsz, h.ksz | (off << 16)};
       rl = hint ? 22ull + h.ksz : 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
       if (p + rl > len) fail = eof = true;  // key/value cut short (data.rs:172,181; a hint's key: :266-270)
     }
     const uint64_t c0j = b0 + (uint64_t)j * CH;
     const uint64_t wend = (c0j + a.win < len) ? c0j + a.win : len;
-    const uint32_t k = (!eof && !hint && lds_hashed(p, rl, wend, a.big)) ? 0u : kClasses;  // hints: no checksum
-    if (k == kClasses) {  // the row goes out now: an EOF row, or a record left to k_long_hash
-      if (lane == 0) {
-        *(u32x4*)(a.slots + ((t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
-        if (fail) atomicMin(&L.cerr[j], r);
-        else if (!hint) atomicMin(&L.lr[j], r);
-      }
-    } else {  // hashed with its class's batch
-      if (lane == 0) L.ent[k][nbk[k]] = WalkEnt{data + p, (uint32_t)rl, stored, (uint32_t)(t0 + j), r, row};
-      if (++nbk[k] == kBatch) {
-        walk_flush(L, a, k, kBatch, t0, t1, wst);
-        nbk[k] = 0;
-      }
+    // the row goes out now: records k_scan_chunks would hash out of LDS are hashed by
+    // k_hash_short, longer ones by k_long_hash; an EOF row fails here
+    if (lane == 0) {
+      *(u32x4*)(a.slots + ((t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
+      if (fail) atomicMin(&L.cerr[j], r);
+      else if (!hint && !lds_hashed(p, rl, wend, a.big)) atomicMin(&L.lr[j], r);
     }
     if (eof) {
       if (lane == 0) {
@@ -416,8 +382,6 @@ __device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& 
     a.cerr[t] = L.cerr[lane];
     a.long_done[t] = 0;
   }
-  // the table entries are stored before any later batch flush lowers a.cerr[t] with an atomic
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __syncthreads();
   return cj == 0xFFFFFFFFu && p != kNone && p < b1 ? kTerm : p;
 }
@@ -426,40 +390,120 @@ __device__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& 
 __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __restrict__ files) {
   __shared__ WalkLds L;
   uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  uint32_t nbk[kClasses];  // entries waiting in each class's batch (wave-uniform)
-  for (uint32_t k = 0; k < kClasses; ++k) nbk[k] = 0;
   WST(tk0)
   const uint64_t R = a.run;
   // a repair pass walks the stretches in a.runs from their exact starts (spec[first]); otherwise
   // runs of R chunks, each from a speculative start
-  const uint64_t nruns = a.runs ? a.nruns_list : (a.total_chunks + R - 1) / R;
+  const uint64_t nruns = a.runs ? a.nruns_list : a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
   for (;;) {
-    uint32_t r = 0;
-    if (threadIdx.x == 0) r = atomicAdd(&a.ctr->run_next, 1u);
-    r = __shfl(r, 0, 64);
+    const uint64_t r = a.runs ? wave_claim(&a.ctr->run_next) : a.run_lo + wave_claim(&a.ctr->walk_next[a.grp]);
     if (r >= nruns) break;
     uint64_t t = a.runs ? a.runs[2ull * r] : (uint64_t)r * R;
     const uint64_t tend = a.runs ? a.runs[2ull * r + 1] : ((t + R < a.total_chunks) ? t + R : a.total_chunks);
-    uint64_t s = a.runs ? uni64(a.spec[t]) : kSearch;
+    uint64_t s = a.runs ? uni64(a.spec[t]) : a.walk_pre ? uni64(a.tin[t]) : kSearch;
     while (t < tend) {
       const uint32_t fi = find_file(files, a.nfiles, t);
       const FileDesc fd = files[fi];
       const uint64_t fend = fd.first_chunk + fd.nchunks;
       uint64_t se = fend < tend ? fend : tend;
       if (se - t > kMaxRun) se = t + kMaxRun;  // the chunk state of a segment lives in LDS
-      const uint64_t ex = walk_segment(L, a, fd, t, se, s, nbk, wst);
+      const uint64_t ex = walk_segment(L, a, fd, t, se, s, wst);
       // the next piece of a stretch continues the chain; a new file starts at 0 (walk_segment)
       s = a.runs ? ex : kSearch;
       t = se;
     }
   }
-  for (uint32_t k = 0; k < kClasses; ++k)  // the partial batches: verdicts to the chunk table
-    if (nbk[k]) walk_flush(L, a, k, nbk[k], 0, 0, wst);
 #ifdef CASK_STAMPS
   WADD(3, tk0)
   if (a.stamps && threadIdx.x == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[i], (unsigned long long)wst[i]);
 #endif
+}
+
+// Each walk run's speculative first start (walk_search), ahead of the chase: a run whose first chunk
+// starts a file needs none, and only the first segment of a run can. Kept out of k_walk_runs: the
+// search's registers would lower how many chasing waves fit on a CU.
+__global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
+  __shared__ SearchLds L;
+  const uint64_t R = a.run;
+  const uint64_t nruns = a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
+  for (;;) {
+    const uint64_t r = a.run_lo + wave_claim(&a.ctr->search_next[a.grp]);
+    if (r >= nruns) break;
+    const uint64_t t = (uint64_t)r * R;
+    const uint32_t fi = find_file(files, a.nfiles, t);
+    const FileDesc fd = files[fi];
+    const uint64_t fend = fd.first_chunk + fd.nchunks;
+    const uint64_t tend = (t + R < a.total_chunks) ? t + R : a.total_chunks;
+    const uint64_t se = fend < tend ? fend : tend;
+    const uint64_t b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+    const uint64_t b1 = ((se - fd.first_chunk) * (uint64_t)a.chunk < fd.len) ? (se - fd.first_chunk) * (uint64_t)a.chunk : fd.len;
+    const uint64_t s0 = b0 == 0 ? 0 : walk_search(L, fd.data, fd.len, b0, b1);
+    if (threadIdx.x == 0) a.tin[t] = s0;
+  }
+}
+
+// The records the walk left unhashed that k_scan_chunks would have hashed out of LDS (lds_hashed:
+// at most `big` bytes): Entry::from_read's check (data.rs:185-198) from HBM, a lane per record; a
+// failure sets the slot row's bad bit and lowers the chunk's first failing row. A wave takes 64
+// chunks (lane l holds chunk t0 + l: its row count, where its bytes start and its window's end;
+// a prefix sum of the counts over the wave) and hashes their rows as one flat list, 64 a step: a
+// chunk holds few records when they are long, and a wave (or quads) per chunk left most lanes
+// idle, and a quad per row kept too few bytes in flight (1.4 / 1.25 ms on configs[2]). Kept out of
+// k_walk_runs so that the walking waves stay small (more of them in flight: the walk is bound by
+// the latency of its header chase).
+__global__ __launch_bounds__(256) void k_hash_short(ScanArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
+  const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
+  const uint64_t t_hi = a.t_hi ? a.t_hi : a.total_chunks;
+  for (uint64_t t0 = a.t_lo + w0 * 64; t0 < t_hi; t0 += nw * 64) {
+    const uint64_t t = t0 + lane;
+    uint32_t n = 0, wlen = 0;  // rows; bytes from the chunk's start to its window's end
+    uint64_t cb = 0;           // address of the chunk's first byte
+    if (t < t_hi && a.spec[t] != kNone) {
+      n = a.count[t] & kCountMask;
+      const FileDesc fd = a.files[find_file(a.files, a.nfiles, t)];
+      const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+      wlen = (uint32_t)(((c0 + a.win < fd.len) ? c0 + a.win : fd.len) - c0);
+      cb = (uint64_t)(uintptr_t)(fd.data + c0);
+    }
+    uint32_t inc = n;  // inclusive prefix of the row counts over the wave's chunks
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if ((int)lane >= o) inc += u;
+    }
+    const uint32_t total = __shfl(inc, 63, 64);
+    for (uint32_t r0 = 0; r0 < total; r0 += 64) {
+      const uint32_t i = r0 + lane;  // this lane's row of the flat list
+      uint32_t j = 0;                // its chunk: the number of chunks whose prefix is <= i
+#pragma unroll
+      for (uint32_t s = 32; s; s >>= 1) {
+        const uint32_t v = __shfl(inc, (int)(j + s - 1), 64);
+        if (v <= i) j += s;
+      }
+      const uint32_t jc = j < 63 ? j : 63u;
+      const uint32_t incj = __shfl(inc, (int)jc, 64), nj = __shfl(n, (int)jc, 64);
+      const uint32_t wl = __shfl(wlen, (int)jc, 64);
+      const uint64_t base = ((uint64_t)(uint32_t)__shfl((uint32_t)(cb >> 32), (int)jc, 64) << 32) |
+                            (uint32_t)__shfl((uint32_t)cb, (int)jc, 64);
+      if (i >= total) continue;
+      const uint64_t tj = t0 + jc;
+      const uint32_t r = i - (incj - nj);
+      uint32_t* w = a.slots + (tj * a.slot_cap + r) * 4;
+      const uint32_t w3 = w[3], vsz = w[2];
+      const uint32_t x = (w3 >> 16) & 0x7FFFu;  // offset in the chunk
+      const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
+      // lds_hashed with p - c0 = x: fits the window (so the file too) and is at most `big` long
+      if (!(x + rl <= wl && rl <= a.big)) continue;
+      const uint8_t* rec = (const uint8_t*)(uintptr_t)base + x;
+      if (gbl_xxh32(rec + 4, rl - 4) != gld4(rec)) {
+        w[3] = w3 | kSlotBad;
+        atomicMin(&a.cerr[tj], r);
+      }
+    }
+  }
 }
 
 // Mean record length at the head of each file (at most 64 files, 32 records each, exact from
@@ -484,14 +528,37 @@ __global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long lo
   }
 }
 
+// Runs a launch covers: its group's, or the repair pass's list.
+static uint64_t launch_runs(const ScanArgs& a) {
+  if (a.runs) return a.nruns_list;
+  const uint64_t hi = a.run_hi ? a.run_hi : (a.total_chunks + a.run - 1) / a.run;
+  return hi > a.run_lo ? hi - a.run_lo : 0;
+}
+
 void launch_walk_runs(const ScanArgs& a, void* stream) {
-  if (!a.total_chunks) return;
-  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  const uint64_t nruns = launch_runs(a);
+  if (!a.total_chunks || !nruns) return;
   // CASK_WALK_WAVES (tuning knob): waves per CU of the persistent grid
-  static const uint32_t per_cu = getenv("CASK_WALK_WAVES") ? (uint32_t)atoi(getenv("CASK_WALK_WAVES")) : 16u;
+  // (7 waves per SIMD fit: 66 VGPRs, 2.9 KB of LDS)
+  static const uint32_t per_cu = getenv("CASK_WALK_WAVES") ? (uint32_t)atoi(getenv("CASK_WALK_WAVES")) : 28u;
   uint64_t grid = (uint64_t)device_cus() * per_cu;
   if (grid > nruns) grid = nruns;
   hipLaunchKernelGGL(k_walk_runs, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
+}
+
+void launch_walk_search(const ScanArgs& a, void* stream) {
+  const uint64_t nruns = launch_runs(a);
+  if (!a.total_chunks || !nruns) return;
+  uint64_t grid = (uint64_t)device_cus() * 20u;  // 5 waves per SIMD (95 VGPRs)
+  if (grid > nruns) grid = nruns;
+  hipLaunchKernelGGL(k_walk_search, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
+}
+
+void launch_hash_short(const ScanArgs& a, void* stream) {
+  const uint64_t t_hi = a.t_hi ? a.t_hi : a.total_chunks;
+  if (t_hi <= a.t_lo) return;
+  const uint64_t blocks = std::min<uint64_t>((t_hi - a.t_lo + 255) / 256, (uint64_t)device_cus() * 8u);  // 64 chunks a wave
+  hipLaunchKernelGGL(k_hash_short, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, a);
 }
 
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {

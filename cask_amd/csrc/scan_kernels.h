@@ -48,6 +48,8 @@ struct Counters {
   unsigned int any_invalid;      // k_finish: some chunk's speculated start is wrong (repair path)
   unsigned int long_pending;     // k_finish: some chunk has rows for k_long
   unsigned int lq_cnt[22];       // long-record queue: entries per length class 2^10 .. 2^31+
+  unsigned int walk_next[8];     // k_walk_runs: next run of each walk group to hand out (kWalkGroups)
+  unsigned int search_next[8];   // k_walk_search: the same, for the searches
 };
 
 // Layout of the call block: Counters, then row_off[nfiles + 1] (each file's first dense row,
@@ -132,6 +134,15 @@ struct ScanArgs {
   unsigned long long* err_inv; // call block: per file ~first failing dense row (0: none)
   uint32_t vec_ok;             // dense arrays aligned for the 4-row vector stores of k_finish
   uint32_t hint;               // 1: the files are hint-file bodies (cask_parse_hints_device), not data files
+  uint32_t walk_pre;           // 1: k_walk_search left each run's speculative start in tin[first chunk]
+  uint32_t grp;                // walk mode: the group of runs a launch covers (its claim counters)
+  // walk mode, one group of runs per launch (0 = to the end): runs [run_lo, run_hi) for
+  // k_walk_search / k_walk_runs, chunks [t_lo, t_hi) for k_hash_short / k_long_enqueue, and per
+  // length class the queue entries [lq_lo, lq_hi) for k_long_hash (null: from 0 / to lq_cnt)
+  uint64_t run_lo, run_hi;
+  uint64_t t_lo, t_hi;
+  const uint32_t* lq_lo;
+  const uint32_t* lq_hi;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -151,6 +162,10 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // of the files by k_probe) from which a call takes it.
 constexpr uint32_t kWalkRun = 64, kWalkMean = 1024;
 constexpr uint32_t kHintRun = 2;  // hint bodies: 22 + ksz-byte records, ~1,700 per 64 KiB run
+// Walk mode on data files runs in groups of runs: group g's long records are hashed on a second
+// stream while group g + 1 is walked (the walk is bound by latency, the long hash by HBM).
+constexpr uint32_t kWalkGroups = 8, kWalkGroupsDefault = 4;
+static_assert(sizeof(((Counters*)nullptr)->walk_next) == 4 * kWalkGroups, "a claim counter per walk group");
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
 struct SummaryHead {
@@ -178,6 +193,9 @@ uint32_t geometry_halo(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);
 int device_cus();  // compute units of the current device (cached per device)
 void launch_long(const ScanArgs& a, void* stream, bool enqueue = true);  // k_long_enqueue + k_long_hash
+void launch_long_enqueue(const ScanArgs& a, void* stream);
+void launch_long_hash(const ScanArgs& a, void* stream);
+void launch_lq_snap(const ScanArgs& a, uint32_t* out, void* stream);  // out[c] = ctr->lq_cnt[c]
 void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);
@@ -198,6 +216,8 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: the walk-mode speculative pass
+void launch_hash_short(const ScanArgs& a, void* stream);  // k_walk.hip: the walked short records' checksums
+void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each walk run's speculative start
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

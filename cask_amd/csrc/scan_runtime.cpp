@@ -95,6 +95,7 @@ struct cask_ctx {
   DevBuf lq;         // long-record queue (slot indices by length class)
   DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
   DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
+  DevBuf lqsnap;     // walk groups: the long-record queue counts after each group's enqueue
   uint32_t epoch = 0;
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
@@ -110,6 +111,9 @@ struct cask_ctx {
   int geo = 0;       // k_scan_chunks geometry (CASK_SCAN_GEOMETRY overrides the default)
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
+  hipStream_t side = nullptr;   // walk mode: the long-record hashing of each walked group
+  hipStream_t side2 = nullptr;  // walk mode: the short-record hashing of each walked group
+  hipEvent_t gev[kWalkGroups + 2] = {};  // group g walked (stream -> sides); sides done (-> stream)
   void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
@@ -122,8 +126,14 @@ struct cask_ctx {
   ~cask_ctx() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (side) (void)hipStreamSynchronize(side);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : gev)
+      if (e) (void)hipEventDestroy(e);
+    if (side2) (void)hipStreamSynchronize(side2);
+    if (side) (void)hipStreamDestroy(side);
+    if (side2) (void)hipStreamDestroy(side2);
     if (evw) (void)hipEventDestroy(evw);
     if (kd) kd_scratch_destroy(kd);
     if (own) (void)hipStreamDestroy(own);
@@ -389,7 +399,11 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   static const bool sync_each = getenv("CASK_SYNC_EACH") != nullptr;
   auto L = [&](const char* what) {
     H(hipGetLastError(), what);
-    if (sync_each) H(hipStreamSynchronize(st), what);
+    if (sync_each) {  // (names the kernel a hang or fault is in, on stderr)
+      fprintf(stderr, "cask: %s ...", what);
+      H(hipDeviceSynchronize(), what);  // (the walk groups' side streams too)
+      fprintf(stderr, " done\n");
+    }
   };
   const Counters* hc = (const Counters*)c->hcall.p;
   const uint64_t* h_rowoff = (const uint64_t*)((const uint8_t*)c->hcall.p + CallLayout::kHead);
@@ -443,7 +457,65 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
   c->last_walk = walk ? 1 : 0;
   H(hipEventRecord(c->ev[1], st));
-  if (walk) {
+  // walk mode on data files: the runs in G groups; per group the speculative starts (k_walk_search),
+  // the walk, the short records' checksums and the long records' queueing on the call's stream,
+  // then the long records' hashing on the side stream, overlapping the next group's walk (the walk
+  // waits on header loads, the long hash on HBM bandwidth). Long records hashed before k_finish
+  // mark their rows like any failed check (slot bad bit, cerr), so k_finish sees them.
+  bool long_pre = false;
+  if (walk && !hint) {
+    static const uint32_t groups_env = getenv("CASK_WALK_GROUPS") ? (uint32_t)atoi(getenv("CASK_WALK_GROUPS")) : 0u;
+    const uint64_t nruns = (total_chunks + a.run - 1) / a.run;
+    uint64_t G = groups_env ? groups_env : kWalkGroupsDefault;
+    G = std::max<uint64_t>(1, std::min<uint64_t>({G, (uint64_t)kWalkGroups, nruns}));
+    if (!c->side) {
+      if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+          hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess) {
+        snprintf(c->last_error, sizeof(c->last_error), "side stream create failed");
+        return CASK_E_DEVICE;  // (the destructor releases whichever was made)
+      }
+      for (auto& e : c->gev) H(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
+      if (!ok) return CASK_E_DEVICE;
+    }
+    if (!c->lqsnap.ensure(4ull * 32 * kWalkGroups)) return CASK_E_NOMEM;
+    uint32_t* snap = c->lqsnap.as<uint32_t>();
+    // every run's speculative start first, in one launch: a search's latency (a stretch of long
+    // records to cross) does not shrink with the group, so per-group launches each paid the longest
+    launch_walk_search(a, st);
+    L("k_walk_search");
+    a.walk_pre = 1;
+    for (uint64_t g = 0; g < G && ok; ++g) {
+      ScanArgs ag = a;
+      ag.grp = (uint32_t)g;
+      ag.run_lo = nruns * g / G;
+      ag.run_hi = nruns * (g + 1) / G;
+      ag.t_lo = ag.run_lo * a.run;
+      ag.t_hi = std::min<uint64_t>(ag.run_hi * a.run, total_chunks);
+      launch_walk_runs(ag, st);
+      L("k_walk_runs");
+      launch_long_enqueue(ag, st);
+      L("k_long_enqueue");
+      launch_lq_snap(ag, snap + 32 * g, st);
+      L("k_lq_snap");
+      H(hipEventRecord(c->gev[g], st), "event record");
+      H(hipStreamWaitEvent(c->side, c->gev[g], 0), "stream wait");
+      H(hipStreamWaitEvent(c->side2, c->gev[g], 0), "stream wait");
+      ScanArgs al = a;
+      al.lq_lo = g ? snap + 32 * (g - 1) : nullptr;
+      al.lq_hi = snap + 32 * g;
+      launch_long_hash(al, c->side);
+      L("k_long_hash (side)");
+      launch_hash_short(ag, c->side2);
+      L("k_hash_short (side)");
+    }
+    H(hipEventRecord(c->gev[kWalkGroups], c->side), "event record");
+    H(hipEventRecord(c->gev[kWalkGroups + 1], c->side2), "event record");
+    H(hipStreamWaitEvent(st, c->gev[kWalkGroups], 0), "stream wait");
+    H(hipStreamWaitEvent(st, c->gev[kWalkGroups + 1], 0), "stream wait");
+    a.walk_pre = 0;
+    long_pre = true;
+    if (!ok) return CASK_E_DEVICE;
+  } else if (walk) {  // hint bodies: the walk searches its own starts (cheaply: hint records are small)
     launch_walk_runs(a, st);
     L("k_walk_runs");
   } else {
@@ -451,23 +523,14 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     L("k_scan_chunks");
   }
   H(hipEventRecord(c->ev[2], st));
-  // walk mode (logs of long records): the long-record pass follows k_finish on the device with no
-  // host round trip between them (it fixes dense statuses; if some start turns out wrong the repair
-  // path below re-hashes every long record, so nothing it wrote is kept). Queueing the long records
-  // from the walk itself instead of k_long_enqueue measured 1 ms slower (the queue counters'
-  // atomics).
-  const bool long_now = dense && walk && !hint;
+  // (walk mode has hashed its long records already. Queueing them from the walk itself instead of
+  // k_long_enqueue measured 1 ms slower: the queue counters' atomics.)
+  const bool long_now = long_pre;
   if (dense) {
     launch_finish(a, st);
     L("k_finish");
     H(hipEventRecord(c->ev[3], st));
-    if (long_now) {
-      ScanArgs ad = a;
-      ad.dense = 1;
-      launch_long(ad, st);
-      L("k_long");
-      H(hipEventRecord(c->ev[4], st));
-    }
+    if (long_now) H(hipEventRecord(c->ev[4], st));
     read_call();
     if (!ok) return CASK_E_DEVICE;
   }
@@ -563,8 +626,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     }
     post(false);
   };
-  if (long_now)  // the dense attempt's long hashing is void: every long record is queued again
-    H(hipMemsetAsync(a.long_done, 0, total_chunks, st), "memset long_done");
+  // (long records hashed before k_finish keep their marks: a re-scanned chunk is queued again)
   // the first scan has run (its counters are in the call block): keep its run counter's effects,
   // clear the per-file error state the validation builds
   H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
