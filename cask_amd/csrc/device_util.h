@@ -232,13 +232,27 @@ __device__ __forceinline__ uint64_t uni64(uint64_t v) {
 }
 
 // Unaligned global loads: gfx950 runs in unaligned-access mode, so these memcpys become
-// global_load_dwordx4 / global_load_dword at any byte address.
+// global_load_dwordx4 / global_load_dword at any byte address. Through a global-address-space
+// pointer: from a generic one they compile to flat loads, and every wait on a flat load is a
+// wait for all of them (vmcnt(0) lgkmcnt(0)) — a loop that issued the next block's loads before
+// mixing this one's then waited for both, and the double buffering bought nothing.
+typedef __attribute__((address_space(1))) const uint8_t g_u8;
 __device__ __forceinline__ u32x4 gld16(const uint8_t* p) {
+  u32x4 v;
+  __builtin_memcpy(&v, (g_u8*)p, 16);
+  return v;
+}
+__device__ __forceinline__ uint32_t gld4(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, (g_u8*)p, 4);
+  return v;
+}
+__device__ __forceinline__ u32x4 gld16g(const g_u8* p) {
   u32x4 v;
   __builtin_memcpy(&v, p, 16);
   return v;
 }
-__device__ __forceinline__ uint32_t gld4(const uint8_t* p) {
+__device__ __forceinline__ uint32_t gld4g(const g_u8* p) {
   uint32_t v;
   __builtin_memcpy(&v, p, 4);
   return v;
@@ -314,11 +328,15 @@ __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
 
 // XXH32 (seed 0) of global bytes [p, p+len) by a quad of lanes (q = lane & 3), lane q keeping stripe
 // accumulator v_{q+1}. Lane q loads stripe q of each 64-B block (one 16-B load: the quad reads 64
-// contiguous bytes per instruction, 4 blocks ahead), quad_transpose hands every lane its word of
-// the block's four stripes. The four lanes must be active together and call with the same p/len;
-// all four return the hash.
-// D: blocks in flight per quad (64 B each; k_long_hash: 4 / 8 / 16 = 7.0 / 6.26 / 6.2 ms on configs[2];
-// a ring of D = 8 / 12 / 16 registers, refilled as each block is mixed, ran 6.8 ms at every D).
+// contiguous bytes per instruction), quad_transpose hands every lane its word of the block's four
+// stripes. The four lanes must be active together and call with the same p/len; all four return
+// the hash. Rounds of D blocks: the next round's loads are in flight while this one mixes, two
+// register sets in turn (no copies), and the loads of a round share one address register
+// (immediate offsets), the last partial round loaded under a predicate rather than at clamped
+// addresses. k_long_hash is VALU-bound as much as HBM-bound (XXH32's two quarter-rate multiplies
+// per word; 64 % VALU-busy before these address and copy savings), and a dword per lane per stripe
+// instead of the transpose ran it at half speed (4x the load instructions).
+// D: blocks per round (64 B each).
 template <uint32_t D = 8>
 __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t len, uint32_t q) {
   const uint64_t nstr = len >> 4;
@@ -326,31 +344,56 @@ __device__ __forceinline__ uint32_t quad_gbl_xxh32(const uint8_t* p, uint64_t le
   if (nstr) {
     uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
     const uint64_t nblk = nstr >> 2;
-    if (nblk) {
-      const uint8_t* lp = p + 16 * q;
-      u32x4 A[D];
+    const g_u8* lp = (const g_u8*)p + 16 * q;  // stripe q of block b: lp + 64 b
+    auto mix = [&](u32x4 X) {
+      quad_transpose(X, q);
+      v = xround(v, X.x);
+      v = xround(v, X.y);
+      v = xround(v, X.z);
+      v = xround(v, X.w);
+    };
+    uint64_t k = 0;  // blocks mixed
+    if (nblk >= D) {
+      u32x4 A[D], B[D];
 #pragma unroll
-      for (uint32_t d = 0; d < D; ++d) A[d] = gld16(lp + 64 * (d < nblk ? d : nblk - 1));
-      for (uint64_t k = 0; k < nblk; k += D) {
-        u32x4 B[D];
+      for (uint32_t d = 0; d < D; ++d) A[d] = gld16g(lp + 64 * d);
+      for (;;) {  // A holds blocks [k, k + D)
+        if (k + 2 * D > nblk) {
 #pragma unroll
-        for (uint32_t d = 0; d < D; ++d) {
-          const uint64_t kb = k + D + d;
-          B[d] = gld16(lp + 64 * (kb < nblk ? kb : nblk - 1));  // clamped: no branch around a load
+          for (uint32_t d = 0; d < D; ++d) mix(A[d]);
+          k += D;
+          break;
         }
+        const g_u8* bp = lp + 64 * (k + D);
 #pragma unroll
-        for (uint32_t d = 0; d < D; ++d) {
-          if (k + d < nblk) {
-            quad_transpose(A[d], q);
-            v = xround(v, A[d].x);
-            v = xround(v, A[d].y);
-            v = xround(v, A[d].z);
-            v = xround(v, A[d].w);
-          }
+        for (uint32_t d = 0; d < D; ++d) B[d] = gld16g(bp + 64 * d);
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) mix(A[d]);
+        k += D;  // B holds blocks [k, k + D)
+        if (k + 2 * D > nblk) {
+#pragma unroll
+          for (uint32_t d = 0; d < D; ++d) mix(B[d]);
+          k += D;
+          break;
         }
+        const g_u8* ap = lp + 64 * (k + D);
 #pragma unroll
-        for (uint32_t d = 0; d < D; ++d) A[d] = B[d];
+        for (uint32_t d = 0; d < D; ++d) A[d] = gld16g(ap + 64 * d);
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) mix(B[d]);
+        k += D;
       }
+    }
+    {  // the last nblk - k < D blocks, loaded together
+      const uint32_t tb = (uint32_t)(nblk - k);
+      const g_u8* tp = lp + 64 * k;
+      u32x4 T[D];
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d)
+        if (d < tb) T[d] = gld16g(tp + 64 * d);
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d)
+        if (d < tb) mix(T[d]);
     }
     const uint32_t rem = (uint32_t)(nstr & 3);
     if (rem) {  // the last 1-3 stripes: lanes q < rem load one each

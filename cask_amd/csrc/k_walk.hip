@@ -92,6 +92,22 @@ __device__ __forceinline__ uint32_t walk_stage(uint32_t* W, const uint8_t* data,
   __syncthreads();
   return (uint32_t)(g - a0);
 }
+// The chase's window: the first n16 lanes load 16 B each (n16 <= 64: at most 1 KiB), the file bytes
+// [wb, min(wb + 16 n16 - 16, len)) readable. Returns the LDS byte index of wb.
+__device__ __forceinline__ uint32_t chase_stage(uint32_t* W, const uint8_t* data, uint64_t len, uint64_t wb, uint32_t n16) {
+  const uintptr_t g = (uintptr_t)(data + wb), a0 = g & ~(uintptr_t)15;
+  const uint64_t we = (wb + 16 * n16 - 16 < len) ? wb + 16 * n16 - 16 : len;
+  const uintptr_t aend = ((uintptr_t)(data + we) + 15) & ~(uintptr_t)15;
+  const uint32_t n = (uint32_t)((aend - a0) >> 4);  // >= 1: wb < len
+  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
+  const uint32_t i = threadIdx.x;
+  u32x4 v = u32x4{0u, 0u, 0u, 0u};
+  if (i < n) v = ((const gu32x4*)a0)[i];
+  __syncthreads();  // every lane is done with the previous window
+  if (i < n) ((u32x4*)W)[i] = v;
+  __syncthreads();
+  return (uint32_t)(g - a0);
+}
 constexpr uint32_t kSearchNL = kWalkWin / 1024;  // the search's windows: 4 KiB
 constexpr uint32_t kChaseNL = 1;                 // the chase's windows: 1 KiB
 constexpr uint32_t kChaseUse = kChaseNL * 1024 - 16;
@@ -324,11 +340,11 @@ __device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, 
     } else {
       if (p < wb || p + hdr > wv) {  // the header is not staged: one round trip brings the next KiB
         WST(tw0)
-        x0 = walk_stage<kChaseNL>(L.win, data, len, p);
+        x0 = chase_stage(L.win, data, len, p, a.chase16);
         WADD(1, tw0)
         WCNT(4)
         wb = p;
-        wv = (p + kChaseUse < len) ? p + kChaseUse : len;
+        wv = (p + 16 * a.chase16 - 16 < len) ? p + 16 * a.chase16 - 16 : len;
       }
       Hdr h;
       if (hint) {  // seq u64 | ksz u16 | vsz u32 | entry_pos u64

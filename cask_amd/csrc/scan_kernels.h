@@ -143,6 +143,8 @@ struct ScanArgs {
   uint64_t t_lo, t_hi;
   const uint32_t* lq_lo;
   const uint32_t* lq_hi;
+  uint32_t chase16;            // k_walk_runs: 16-B loads per chase window (<= 64: 1 KiB)
+  uint32_t pad3_;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,

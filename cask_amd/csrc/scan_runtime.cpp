@@ -113,7 +113,8 @@ struct cask_ctx {
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
   hipStream_t side = nullptr;   // walk mode: the long-record hashing of each walked group
   hipStream_t side2 = nullptr;  // walk mode: the short-record hashing of each walked group
-  hipEvent_t gev[kWalkGroups + 2] = {};  // group g walked (stream -> sides); sides done (-> stream)
+  // walk groups: group g walked (stream -> sides); sides done (-> stream); searches (both ways)
+  hipEvent_t gev[kWalkGroups + 4] = {};
   void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
   float last_ms[6] = {0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
@@ -451,6 +452,10 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       walk = c->probe_walk;
     }
   }
+  {  // CASK_CHASE_BYTES (tuning knob): the walk's chase window, 256 .. 1024 bytes
+    static const uint32_t cb = getenv("CASK_CHASE_BYTES") ? (uint32_t)atoi(getenv("CASK_CHASE_BYTES")) : 1024u;
+    a.chase16 = std::min<uint32_t>(64u, std::max<uint32_t>(16u, cb / 16));
+  }
   if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
     const char* wr = getenv("CASK_WALK_RUN");
     a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : hint ? kHintRun : kWalkRun;
@@ -479,10 +484,23 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     }
     if (!c->lqsnap.ensure(4ull * 32 * kWalkGroups)) return CASK_E_NOMEM;
     uint32_t* snap = c->lqsnap.as<uint32_t>();
-    // every run's speculative start first, in one launch: a search's latency (a stretch of long
-    // records to cross) does not shrink with the group, so per-group launches each paid the longest
-    launch_walk_search(a, st);
-    L("k_walk_search");
+    // the speculative starts: group 0's first, then (on the short-hash stream, while group 0 is
+    // walked) every other group's in one launch — a search's latency (a stretch of long records to
+    // cross) does not shrink with the group, so a launch per group would pay the longest each time
+    {
+      ScanArgs as = a;
+      as.run_hi = nruns / G;
+      launch_walk_search(as, st);
+      L("k_walk_search");
+      H(hipEventRecord(c->gev[kWalkGroups + 2], st), "event record");
+      H(hipStreamWaitEvent(c->side2, c->gev[kWalkGroups + 2], 0), "stream wait");
+      as.run_lo = nruns / G;
+      as.run_hi = nruns;
+      as.grp = 1;  // (its claim counter: group 1's, unused by the walk groups' searches)
+      launch_walk_search(as, c->side2);
+      L("k_walk_search (side)");
+      H(hipEventRecord(c->gev[kWalkGroups + 3], c->side2), "event record");
+    }
     a.walk_pre = 1;
     for (uint64_t g = 0; g < G && ok; ++g) {
       ScanArgs ag = a;
@@ -491,6 +509,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       ag.run_hi = nruns * (g + 1) / G;
       ag.t_lo = ag.run_lo * a.run;
       ag.t_hi = std::min<uint64_t>(ag.run_hi * a.run, total_chunks);
+      if (g == 1) H(hipStreamWaitEvent(st, c->gev[kWalkGroups + 3], 0), "stream wait");  // the other searches
       launch_walk_runs(ag, st);
       L("k_walk_runs");
       launch_long_enqueue(ag, st);
