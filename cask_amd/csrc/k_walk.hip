@@ -5,8 +5,8 @@
 // to 64 KiB, 96 % of the bytes in records > 2 KiB) those bytes are then read a second time by
 // k_long_hash. Here a wave walks a run of chunks by chasing record headers (Entries::next,
 // log.rs:403-429: each record starts where the previous one ends; a KiB staged in LDS per round
-// trip), writing the rows; k_hash_short then hashes the short records from HBM and k_long_hash the
-// long ones, so every byte is read once.
+// trip), writing the rows and hashing the records that fit that KiB out of LDS; k_long_hash hashes
+// the longer ones, so every byte is read about once.
 //
 // The output is the chunk table and slot rows of k_scan_chunks (spec, exit, count, long_r, cerr,
 // long_done, slot rows; never a regular chunk), so k_finish, the validation/repair passes and
@@ -47,6 +47,9 @@ struct WalkLds {
   uint32_t win[1024 / 4 + 16];
   uint64_t spec[kMaxRun], exitv[kMaxRun];
   uint32_t cnt[kMaxRun], lr[kMaxRun], cerr[kMaxRun];
+  // records of the window waiting for their checksum (walk_flush): LDS byte, length, chunk, row
+  uint32_t hx[16], hrl[16], hj[16], hr[16];
+  u32x4 hrow[16];
 };
 // LDS of a searching wave (k_walk_search): a 4-KiB window, the short candidates of a step and the
 // long candidates kept for the hop back.
@@ -92,25 +95,10 @@ __device__ __forceinline__ uint32_t walk_stage(uint32_t* W, const uint8_t* data,
   __syncthreads();
   return (uint32_t)(g - a0);
 }
-// The chase's window: the first n16 lanes load 16 B each (n16 <= 64: at most 1 KiB), the file bytes
-// [wb, min(wb + 16 n16 - 16, len)) readable. Returns the LDS byte index of wb.
-__device__ __forceinline__ uint32_t chase_stage(uint32_t* W, const uint8_t* data, uint64_t len, uint64_t wb, uint32_t n16) {
-  const uintptr_t g = (uintptr_t)(data + wb), a0 = g & ~(uintptr_t)15;
-  const uint64_t we = (wb + 16 * n16 - 16 < len) ? wb + 16 * n16 - 16 : len;
-  const uintptr_t aend = ((uintptr_t)(data + we) + 15) & ~(uintptr_t)15;
-  const uint32_t n = (uint32_t)((aend - a0) >> 4);  // >= 1: wb < len
-  typedef __attribute__((address_space(1))) const u32x4 gu32x4;
-  const uint32_t i = threadIdx.x;
-  u32x4 v = u32x4{0u, 0u, 0u, 0u};
-  if (i < n) v = ((const gu32x4*)a0)[i];
-  __syncthreads();  // every lane is done with the previous window
-  if (i < n) ((u32x4*)W)[i] = v;
-  __syncthreads();
-  return (uint32_t)(g - a0);
-}
 constexpr uint32_t kSearchNL = kWalkWin / 1024;  // the search's windows: 4 KiB
 constexpr uint32_t kChaseNL = 1;                 // the chase's windows: 1 KiB
 constexpr uint32_t kChaseUse = kChaseNL * 1024 - 16;
+static_assert(kChaseUse == kWalkHashMax, "the walker hashes records that fit its window");
 
 // The first record start >= b0 of the chain, speculatively (see the file comment); kNone if pass A
 // finds no verified short record before min(len, b1 + kSearchPast).
@@ -286,9 +274,36 @@ __device__ __forceinline__ uint64_t hint_search(WalkLds& L, const uint8_t* data,
   return kNone;
 }
 
+// The window's records waiting for their checksum (lane 0 listed them: LDS byte, length, chunk,
+// row): a quad per record hashes it out of the window (Entry::from_read's check, data.rs:193-198),
+// then writes its slot row with the verdict; a failure lowers its chunk's first failing row.
+// Runs before the window is restaged and before the segment's chunk state goes out.
+__device__ __forceinline__ void walk_flush(WalkLds& L, const ScanArgs& a, uint64_t t0, uint32_t n) {
+  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
+  __syncthreads();  // the list is in LDS
+  if (q < n) {      // whole quads
+    const uint32_t x = L.hx[q], rl = L.hrl[q];
+    const uint32_t h = quad_xxh32(L.win, x + 4, rl - 4, qa);
+    if (qa == 0) {
+      u32x4 row = L.hrow[q];
+      const uint32_t j = L.hj[q], r = L.hr[q];
+      if (h != lds_u32(L.win, x)) {
+        row.w |= kSlotBad;
+        atomicMin(&L.cerr[j], r);
+      }
+      *(u32x4*)(a.slots + ((t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
+    }
+  }
+  __syncthreads();  // before the list or the window is reused
+}
+
 // One stretch of a run inside one file: chunks [t0, t1) of file fd.
 // s_in: the exact start of the segment's first chunk (repair passes: spec[t0]), or kSearch for a
 // speculative one. Returns the chain position after the segment (kTerm after an EOF row).
+// Data files: a record of at most ScanArgs::big bytes (kWalkHashMax: the window's usable bytes) is
+// hashed out of the chase's window — when it runs past the window the window is restaged at its
+// header first — 16 at a time or when the window moves on (walk_flush); longer ones are left to
+// k_long_hash (long_r). Hint bodies have no checksums.
 constexpr uint64_t kSearch = ~0ull - 1;
 __device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, const FileDesc& fd, uint64_t t0, uint64_t t1,
                                  uint64_t s_in, uint64_t* wst) {
@@ -318,6 +333,17 @@ __device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, 
   uint32_t cj = 0xFFFFFFFFu, cn = 0;  // current chunk (segment index) and its rows so far
   uint64_t wb = 0, wv = 0;  // the chase's window: file bytes [wb, wv) at LDS byte x0
   uint32_t x0 = 0;
+  uint32_t nh = 0;  // records listed for walk_flush
+  auto stage = [&](uint64_t at) {  // the next KiB from `at`, after the listed records are hashed
+    if (nh) walk_flush(L, a, t0, nh);
+    nh = 0;
+    WST(tw0)
+    x0 = walk_stage<kChaseNL>(L.win, data, len, at);
+    WADD(1, tw0)
+    WCNT(4)
+    wb = at;
+    wv = (at + kChaseUse < len) ? at + kChaseUse : len;
+  };
   while (p != kNone && p < b1) {
     const uint32_t j = (uint32_t)((p - b0) >> csh);  // chunk sizes are powers of two
     if (j != cj) {  // the chain enters chunk j: the previous chunk's rows and exit are final
@@ -338,14 +364,7 @@ __device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, 
     if (p + hdr > len) {
       fail = eof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163; a hint: data.rs:258-265)
     } else {
-      if (p < wb || p + hdr > wv) {  // the header is not staged: one round trip brings the next KiB
-        WST(tw0)
-        x0 = chase_stage(L.win, data, len, p, a.chase16);
-        WADD(1, tw0)
-        WCNT(4)
-        wb = p;
-        wv = (p + 16 * a.chase16 - 16 < len) ? p + 16 * a.chase16 - 16 : len;
-      }
+      if (p < wb || p + hdr > wv) stage(p);  // the header is not staged: one round trip brings the next KiB
       Hdr h;
       if (hint) {  // seq u64 | ksz u16 | vsz u32 | entry_pos u64
         const uint32_t xi = x0 + (uint32_t)(p - wb);
@@ -364,14 +383,26 @@ __device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, 
       rl = hint ? 22ull + h.ksz : 18ull + h.ksz + ((h.vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)h.vsz);
       if (p + rl > len) fail = eof = true;  // key/value cut short (data.rs:172,181; a hint's key: :266-270)
     }
-    const uint64_t c0j = b0 + (uint64_t)j * CH;
-    const uint64_t wend = (c0j + a.win < len) ? c0j + a.win : len;
-    // the row goes out now: records k_scan_chunks would hash out of LDS are hashed by
-    // k_hash_short, longer ones by k_long_hash; an EOF row fails here
-    if (lane == 0) {
+    // a data record of at most `big` bytes is hashed out of the window (restaged at its header if
+    // it runs past the window's end: it then fits, as big <= kChaseUse)
+    const bool inwin = !hint && !fail && rl <= a.big;
+    if (inwin) {
+      if (p + rl > wv) stage(p);
+      if (lane == 0) {
+        L.hx[nh] = x0 + (uint32_t)(p - wb);
+        L.hrl[nh] = (uint32_t)rl;
+        L.hj[nh] = j;
+        L.hr[nh] = r;
+        L.hrow[nh] = row;
+      }
+      if (++nh == 16) {
+        walk_flush(L, a, t0, nh);
+        nh = 0;
+      }
+    } else if (lane == 0) {  // the row goes out now: an EOF row fails here, a longer record is k_long's
       *(u32x4*)(a.slots + ((t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
       if (fail) atomicMin(&L.cerr[j], r);
-      else if (!hint && !lds_hashed(p, rl, wend, a.big)) atomicMin(&L.lr[j], r);
+      else if (!hint) atomicMin(&L.lr[j], r);  // (rl > big: not lds_hashed, data.rs:193-198 in k_long_hash)
     }
     if (eof) {
       if (lane == 0) {
@@ -383,6 +414,7 @@ __device__ __forceinline__ uint64_t walk_segment(WalkLds& L, const ScanArgs& a, 
     }
     p += rl;
   }
+  if (nh) walk_flush(L, a, t0, nh);
   if (cj != 0xFFFFFFFFu && lane == 0) {
     L.cnt[cj] = cn;
     L.exitv[cj] = p;  // >= b1, the end of the segment's last chunk
@@ -459,69 +491,6 @@ __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* 
   }
 }
 
-// The records the walk left unhashed that k_scan_chunks would have hashed out of LDS (lds_hashed:
-// at most `big` bytes): Entry::from_read's check (data.rs:185-198) from HBM, a lane per record; a
-// failure sets the slot row's bad bit and lowers the chunk's first failing row. A wave takes 64
-// chunks (lane l holds chunk t0 + l: its row count, where its bytes start and its window's end;
-// a prefix sum of the counts over the wave) and hashes their rows as one flat list, 64 a step: a
-// chunk holds few records when they are long, and a wave (or quads) per chunk left most lanes
-// idle, and a quad per row kept too few bytes in flight (1.4 / 1.25 ms on configs[2]). Kept out of
-// k_walk_runs so that the walking waves stay small (more of them in flight: the walk is bound by
-// the latency of its header chase).
-__global__ __launch_bounds__(256) void k_hash_short(ScanArgs a) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  const uint64_t w0 = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6);
-  const uint64_t t_hi = a.t_hi ? a.t_hi : a.total_chunks;
-  for (uint64_t t0 = a.t_lo + w0 * 64; t0 < t_hi; t0 += nw * 64) {
-    const uint64_t t = t0 + lane;
-    uint32_t n = 0, wlen = 0;  // rows; bytes from the chunk's start to its window's end
-    uint64_t cb = 0;           // address of the chunk's first byte
-    if (t < t_hi && a.spec[t] != kNone) {
-      n = a.count[t] & kCountMask;
-      const FileDesc fd = a.files[find_file(a.files, a.nfiles, t)];
-      const uint64_t c0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
-      wlen = (uint32_t)(((c0 + a.win < fd.len) ? c0 + a.win : fd.len) - c0);
-      cb = (uint64_t)(uintptr_t)(fd.data + c0);
-    }
-    uint32_t inc = n;  // inclusive prefix of the row counts over the wave's chunks
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if ((int)lane >= o) inc += u;
-    }
-    const uint32_t total = __shfl(inc, 63, 64);
-    for (uint32_t r0 = 0; r0 < total; r0 += 64) {
-      const uint32_t i = r0 + lane;  // this lane's row of the flat list
-      uint32_t j = 0;                // its chunk: the number of chunks whose prefix is <= i
-#pragma unroll
-      for (uint32_t s = 32; s; s >>= 1) {
-        const uint32_t v = __shfl(inc, (int)(j + s - 1), 64);
-        if (v <= i) j += s;
-      }
-      const uint32_t jc = j < 63 ? j : 63u;
-      const uint32_t incj = __shfl(inc, (int)jc, 64), nj = __shfl(n, (int)jc, 64);
-      const uint32_t wl = __shfl(wlen, (int)jc, 64);
-      const uint64_t base = ((uint64_t)(uint32_t)__shfl((uint32_t)(cb >> 32), (int)jc, 64) << 32) |
-                            (uint32_t)__shfl((uint32_t)cb, (int)jc, 64);
-      if (i >= total) continue;
-      const uint64_t tj = t0 + jc;
-      const uint32_t r = i - (incj - nj);
-      uint32_t* w = a.slots + (tj * a.slot_cap + r) * 4;
-      const uint32_t w3 = w[3], vsz = w[2];
-      const uint32_t x = (w3 >> 16) & 0x7FFFu;  // offset in the chunk
-      const uint64_t rl = 18ull + (w3 & 0xFFFFu) + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
-      // lds_hashed with p - c0 = x: fits the window (so the file too) and is at most `big` long
-      if (!(x + rl <= wl && rl <= a.big)) continue;
-      const uint8_t* rec = (const uint8_t*)(uintptr_t)base + x;
-      if (gbl_xxh32(rec + 4, rl - 4) != gld4(rec)) {
-        w[3] = w3 | kSlotBad;
-        atomicMin(&a.cerr[tj], r);
-      }
-    }
-  }
-}
-
 // Mean record length at the head of each file (at most 64 files, 32 records each, exact from
 // offset 0): out[0] bytes, out[1] records. The host picks the walk mode from it.
 __global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out) {
@@ -568,13 +537,6 @@ void launch_walk_search(const ScanArgs& a, void* stream) {
   uint64_t grid = (uint64_t)device_cus() * 20u;  // 5 waves per SIMD (95 VGPRs)
   if (grid > nruns) grid = nruns;
   hipLaunchKernelGGL(k_walk_search, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
-}
-
-void launch_hash_short(const ScanArgs& a, void* stream) {
-  const uint64_t t_hi = a.t_hi ? a.t_hi : a.total_chunks;
-  if (t_hi <= a.t_lo) return;
-  const uint64_t blocks = std::min<uint64_t>((t_hi - a.t_lo + 255) / 256, (uint64_t)device_cus() * 8u);  // 64 chunks a wave
-  hipLaunchKernelGGL(k_hash_short, dim3((uint32_t)blocks), dim3(256), 0, (hipStream_t)stream, a);
 }
 
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {

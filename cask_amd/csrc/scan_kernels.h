@@ -137,14 +137,12 @@ struct ScanArgs {
   uint32_t walk_pre;           // 1: k_walk_search left each run's speculative start in tin[first chunk]
   uint32_t grp;                // walk mode: the group of runs a launch covers (its claim counters)
   // walk mode, one group of runs per launch (0 = to the end): runs [run_lo, run_hi) for
-  // k_walk_search / k_walk_runs, chunks [t_lo, t_hi) for k_hash_short / k_long_enqueue, and per
+  // k_walk_search / k_walk_runs, chunks [t_lo, t_hi) for k_long_enqueue, and per
   // length class the queue entries [lq_lo, lq_hi) for k_long_hash (null: from 0 / to lq_cnt)
   uint64_t run_lo, run_hi;
   uint64_t t_lo, t_hi;
   const uint32_t* lq_lo;
   const uint32_t* lq_hi;
-  uint32_t chase16;            // k_walk_runs: 16-B loads per chase window (<= 64: 1 KiB)
-  uint32_t pad3_;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -167,6 +165,10 @@ constexpr uint32_t kHintRun = 2;  // hint bodies: 22 + ksz-byte records, ~1,700 
 // Walk mode on data files runs in groups of runs: group g's long records are hashed on a second
 // stream while group g + 1 is walked (the walk is bound by latency, the long hash by HBM).
 constexpr uint32_t kWalkGroups = 8, kWalkGroupsDefault = 4;
+// Walk mode on data files: ScanArgs::big. The walker hashes records up to this long out of its
+// 1-KiB LDS window (its usable bytes); longer ones go to k_long_hash. (Length class 10 of the
+// long-record queue holds them: at most (chunk >> 10) + 1 records longer than this start per chunk.)
+constexpr uint32_t kWalkHashMax = 1008;
 static_assert(sizeof(((Counters*)nullptr)->walk_next) == 4 * kWalkGroups, "a claim counter per walk group");
 
 // Per-call summary written by k_summary, copied to the host in one transfer.
@@ -218,7 +220,6 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: the walk-mode speculative pass
-void launch_hash_short(const ScanArgs& a, void* stream);  // k_walk.hip: the walked short records' checksums
 void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each walk run's speculative start
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);

@@ -452,21 +452,18 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       walk = c->probe_walk;
     }
   }
-  {  // CASK_CHASE_BYTES (tuning knob): the walk's chase window, 256 .. 1024 bytes
-    static const uint32_t cb = getenv("CASK_CHASE_BYTES") ? (uint32_t)atoi(getenv("CASK_CHASE_BYTES")) : 1024u;
-    a.chase16 = std::min<uint32_t>(64u, std::max<uint32_t>(16u, cb / 16));
-  }
+  if (walk && !hint) a.big = kWalkHashMax;  // the walker hashes what fits its window, k_long the rest
   if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
     const char* wr = getenv("CASK_WALK_RUN");
     a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : hint ? kHintRun : kWalkRun;
   }
   c->last_walk = walk ? 1 : 0;
   H(hipEventRecord(c->ev[1], st));
-  // walk mode on data files: the runs in G groups; per group the speculative starts (k_walk_search),
-  // the walk, the short records' checksums and the long records' queueing on the call's stream,
-  // then the long records' hashing on the side stream, overlapping the next group's walk (the walk
-  // waits on header loads, the long hash on HBM bandwidth). Long records hashed before k_finish
-  // mark their rows like any failed check (slot bad bit, cerr), so k_finish sees them.
+  // walk mode on data files: the runs in G groups; per group the walk (which hashes the records
+  // that fit its window) and the long records' queueing on the call's stream, then their hashing
+  // on a side stream, overlapping the next group's walk (the walk waits on header loads, the long
+  // hash on HBM bandwidth). Long records hashed before k_finish mark their rows like any failed
+  // check (slot bad bit, cerr), so k_finish sees them.
   bool long_pre = false;
   if (walk && !hint) {
     static const uint32_t groups_env = getenv("CASK_WALK_GROUPS") ? (uint32_t)atoi(getenv("CASK_WALK_GROUPS")) : 0u;
@@ -484,7 +481,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     }
     if (!c->lqsnap.ensure(4ull * 32 * kWalkGroups)) return CASK_E_NOMEM;
     uint32_t* snap = c->lqsnap.as<uint32_t>();
-    // the speculative starts: group 0's first, then (on the short-hash stream, while group 0 is
+    // the speculative starts: group 0's first, then (on the second side stream, while group 0 is
     // walked) every other group's in one launch — a search's latency (a stretch of long records to
     // cross) does not shrink with the group, so a launch per group would pay the longest each time
     {
@@ -518,14 +515,11 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       L("k_lq_snap");
       H(hipEventRecord(c->gev[g], st), "event record");
       H(hipStreamWaitEvent(c->side, c->gev[g], 0), "stream wait");
-      H(hipStreamWaitEvent(c->side2, c->gev[g], 0), "stream wait");
       ScanArgs al = a;
       al.lq_lo = g ? snap + 32 * (g - 1) : nullptr;
       al.lq_hi = snap + 32 * g;
       launch_long_hash(al, c->side);
       L("k_long_hash (side)");
-      launch_hash_short(ag, c->side2);
-      L("k_hash_short (side)");
     }
     H(hipEventRecord(c->gev[kWalkGroups], c->side), "event record");
     H(hipEventRecord(c->gev[kWalkGroups + 1], c->side2), "event record");
