@@ -110,6 +110,7 @@ SIGNATURES = [
     ("cask_last_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     ("cask_last_counters", C.c_int, [C.c_void_p, c_u64p]),
     ("cask_last_walk", C.c_int, [C.c_void_p]),
+    ("cask_last_geometry", C.c_int, [C.c_void_p]),
     ("cask_last_dense", C.c_int, [C.c_void_p]),
     ("cask_encode_synthetic_device", C.c_int, [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p,
                                                C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]),

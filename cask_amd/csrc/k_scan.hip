@@ -24,9 +24,12 @@
 
 namespace cask_dev {
 
-template <uint32_t CH, uint32_t HALO, uint32_t NT, uint32_t PER_CU>
+template <uint32_t CH, uint32_t HALO, uint32_t NT, uint32_t PER_CU, bool NT_LOADS = false>
 struct Geo {
   static constexpr uint32_t kCh = CH, kHaloB = HALO, kNT = NT, kWinB = CH + HALO, kPerCU = PER_CU;
+  // staging loads with the nontemporal policy (the bytes are read once): measured faster only
+  // together with the short halo (GeoS), see DESIGN.md
+  static constexpr bool kNtLoads = NT_LOADS;
   static constexpr uint32_t kWavesPerSimd = PER_CU * NT / 256;  // 4 SIMDs of 64-lane waves per CU
   static constexpr uint32_t kMaxStartsG = CH / 18 + 2;  // every record is >= 18 bytes
   static constexpr uint32_t kRowBuf = kMaxStartsG / 16;   // slot rows per LDS row buffer (2 in starts' space)
@@ -127,14 +130,17 @@ __device__ __forceinline__ void stage_issue(u32x4 (&v)[G::kNL], const ChunkPos& 
   if (c.n16 == G::kNL * G::kLoadT) {  // the whole window is inside the file: no clamping
 #pragma unroll
     for (uint32_t j = 0; j < G::kNL; ++j) {
-      v[j] = src[threadIdx.x + j * G::kLoadT];
+      if constexpr (G::kNtLoads) v[j] = __builtin_nontemporal_load(&src[threadIdx.x + j * G::kLoadT]);
+      else v[j] = src[threadIdx.x + j * G::kLoadT];
     }
     return;
   }
 #pragma unroll
   for (uint32_t j = 0; j < G::kNL; ++j) {
     const uint32_t i = threadIdx.x + j * G::kLoadT;
-    v[j] = src[i < c.n16 ? i : c.n16 - 1];
+    // (the same policy on both paths: the compiler merges them, and a merged load keeps no policy)
+    if constexpr (G::kNtLoads) v[j] = __builtin_nontemporal_load(&src[i < c.n16 ? i : c.n16 - 1]);
+    else v[j] = src[i < c.n16 ? i : c.n16 - 1];
   }
 }
 
@@ -676,17 +682,23 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #endif
 }
 
-#ifndef CASK_HALO_A
-#define CASK_HALO_A 4080
-#endif
-using GeoA = Geo<32768, CASK_HALO_A, 256, 4>;  // window + 16-B slop = 9 loads per thread
+// Geometry 0 (wide halo): a record of up to ~4 KiB that starts in the chunk is still hashed out of
+// LDS. Geometry 3 (short halo, nontemporal staging): 11 instead of 12 loads per loader thread (3 %
+// of halo instead of 12.5 %), picked when the records at the file heads are short (kShortHaloMean);
+// a longer record that crosses the window's end goes to k_long like any other (correct either way).
+using GeoA = Geo<32768, 4080, 256, 4>;
 using GeoB = Geo<16384, 2032, 128, 8>;
 using GeoC = Geo<8192, 1008, 64, 16>;
+using GeoS = Geo<32768, 1008, 256, 4, true>;
 
 static inline hipStream_t S(void* s) { return (hipStream_t)s; }
 
-uint32_t geometry_chunk(int geo) { return geo == 1 ? GeoB::kCh : geo == 2 ? GeoC::kCh : GeoA::kCh; }
-uint32_t geometry_halo(int geo) { return geo == 1 ? GeoB::kHaloB : geo == 2 ? GeoC::kHaloB : GeoA::kHaloB; }
+uint32_t geometry_chunk(int geo) {
+  return geo == 1 ? GeoB::kCh : geo == 2 ? GeoC::kCh : geo == 3 ? GeoS::kCh : GeoA::kCh;
+}
+uint32_t geometry_halo(int geo) {
+  return geo == 1 ? GeoB::kHaloB : geo == 2 ? GeoC::kHaloB : geo == 3 ? GeoS::kHaloB : GeoA::kHaloB;
+}
 
 template <class G>
 static void launch_geo(const ScanArgs& a, void* stream) {
@@ -712,6 +724,8 @@ void launch_scan_chunks(const ScanArgs& a, int geo, void* stream) {
     launch_geo<GeoB>(a, stream);
   else if (geo == 2)
     launch_geo<GeoC>(a, stream);
+  else if (geo == 3)
+    launch_geo<GeoS>(a, stream);
   else
     launch_geo<GeoA>(a, stream);
 }

@@ -491,11 +491,12 @@ __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* 
   }
 }
 
-// Mean record length at the head of each file (at most 64 files, 32 records each, exact from
-// offset 0): out[0] bytes, out[1] records. The host picks the walk mode from it.
+// Record lengths at the head of each file (at most 64 files, 32 records each, exact from offset
+// 0): out[0] bytes, out[1] records, out[2] the longest. The host picks the walk mode and the chunk
+// scan's halo from it.
 __global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out) {
   const uint32_t f = threadIdx.x;
-  uint64_t bytes = 0, recs = 0;
+  uint64_t bytes = 0, recs = 0, mx = 0;
   if (f < nfiles && f < 64) {
     const FileDesc fd = files[(uint64_t)f * nfiles / (nfiles < 64 ? nfiles : 64)];
     uint64_t p = 0;
@@ -504,12 +505,14 @@ __global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long lo
       if (p + rl > fd.len) break;
       bytes += rl;
       ++recs;
+      mx = rl > mx ? rl : mx;
       p += rl;
     }
   }
   if (recs) {
     atomicAdd(&out[0], (unsigned long long)bytes);
     atomicAdd(&out[1], (unsigned long long)recs);
+    atomicMax(&out[2], (unsigned long long)mx);
   }
 }
 

@@ -161,6 +161,11 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // Walk mode (k_walk.hip): chunks per run, and the mean record length (bytes, sampled at the heads
 // of the files by k_probe) from which a call takes it.
 constexpr uint32_t kWalkRun = 64, kWalkMean = 1024;
+// Chunk mode: the short-halo geometry (kGeoShortHalo, a 1,008-B halo) when the records at the file
+// heads average at most kShortHaloMean bytes and none is longer than kShortHaloMax; else the wide
+// halo (kDefaultGeometry, 4,080 B). Speed only: a record that crosses the window goes to k_long.
+constexpr int kGeoShortHalo = 3;
+constexpr uint32_t kShortHaloMean = 512, kShortHaloMax = 1008;
 constexpr uint32_t kHintRun = 2;  // hint bodies: 22 + ksz-byte records, ~1,700 per 64 KiB run
 // Walk mode on data files runs in groups of runs: group g's long records are hashed on a second
 // stream while group g + 1 is walked (the walk is bound by latency, the long hash by HBM).

@@ -108,7 +108,7 @@ struct cask_ctx {
   // host-scan staging
   DevBuf stage_data;
   DevBuf stage_rows;
-  int geo = 0;       // k_scan_chunks geometry (CASK_SCAN_GEOMETRY overrides the default)
+  int geo = -1;      // k_scan_chunks geometry: -1 picks one per call (CASK_SCAN_GEOMETRY forces one)
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
   hipStream_t side = nullptr;   // walk mode: the long-record hashing of each walked group
@@ -120,8 +120,10 @@ struct cask_ctx {
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
   int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
   int last_walk = 0;   // the last call's speculative pass was k_walk_runs
+  int last_geo = -1;   // the last call's k_scan_chunks geometry (-1: walk mode)
   uint64_t probe_sig = 0;  // files of the last k_probe, and its answer
   bool probe_walk = false;
+  bool probe_short = false;  // chunk mode: the short-halo geometry (kGeoShortHalo)
   std::mutex mu;
   char last_error[256] = {0};
   ~cask_ctx() {
@@ -165,7 +167,7 @@ cask_ctx* cask_ctx_create(int device, int* status) {
     return nullptr;
   }
   c->stream = c->own;
-  c->geo = kDefaultGeometry;
+  c->geo = -1;
   if (const char* g = getenv("CASK_SCAN_GEOMETRY")) c->geo = atoi(g);
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   (void)hipEventCreateWithFlags(&c->evw, hipEventDisableTiming);
@@ -222,6 +224,8 @@ int cask_last_dense(const cask_ctx* c) { return c ? c->last_dense : 0; }
 
 int cask_last_walk(const cask_ctx* c) { return c ? c->last_walk : 0; }
 
+int cask_last_geometry(const cask_ctx* c) { return c ? c->last_geo : -1; }
+
 int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
   if (!c || !c5) return CASK_E_INVALID_ARG;
   memcpy(c5, c->last_counters, sizeof(c->last_counters));
@@ -249,8 +253,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   if (set_dev(c)) return CASK_E_DEVICE;
   hipStream_t st = c->stream;
 
-  // file table
-  const uint32_t chunk = geometry_chunk(c->geo);
+  // file table (every geometry picked automatically has the default's chunk size)
+  int geo = c->geo >= 0 ? c->geo : kDefaultGeometry;
+  const uint32_t chunk = geometry_chunk(geo);
   // slot rows per chunk, rounded to 8 rows: every chunk's rows start on a 128-B line, so the
   // scan's 1-KiB row stores cover whole lines and need no fill from HBM
   const uint32_t slot_cap = ((chunk / 18 + 2) + 7) & ~7u;
@@ -373,7 +378,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
   a.big = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
   if (a.big < kMinBigRec) a.big = kMinBigRec;  // the long-record queue's smallest length class
-  a.win = chunk + geometry_halo(c->geo);
+  a.win = chunk + geometry_halo(geo);
   // the dense path: CASK_DENSE=0 (tuning knob) sends every call through the repair path's k_compact
   static const bool dense_on = !(getenv("CASK_DENSE") && atoi(getenv("CASK_DENSE")) == 0);
   const bool dense = rows != nullptr && dense_on && total_chunks > 0;
@@ -421,7 +426,10 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // heads of the files average kWalkMean bytes or more: k_probe, once per set of files (the answer
   // is cached on the context; it decides speed only). CASK_SCAN_MODE=walk|chunk (test and tuning
   // knob) forces a mode.
+  // The chunk scan's halo comes from the same probe: CASK_SCAN_MODE=wide|narrow forces the chunk
+  // mode with the wide (4,080-B) or the short (1,008-B) halo.
   bool walk = false;
+  int halo_pick = 0;  // 1: wide, 2: short (forced); 0: from the probe
   if (hint) {
     walk = true;  // hint bodies are always walked (k_walk_runs' hint mode)
   } else {
@@ -430,7 +438,12 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       walk = true;
     } else if (mode && !strcmp(mode, "chunk")) {
       walk = false;
-    } else if (total_chunks) {
+    } else if (mode && !strcmp(mode, "wide")) {
+      halo_pick = 1;
+    } else if (mode && !strcmp(mode, "narrow")) {
+      halo_pick = 2;
+    }
+    if (!mode && total_chunks) {
       uint64_t sig = 0x9E3779B97F4A7C15ull ^ nfiles;
       for (uint32_t i = 0; i < nfiles; ++i) {
         sig = (sig ^ (uint64_t)(uintptr_t)files[i].data) * 0xBF58476D1CE4E5B9ull;
@@ -439,19 +452,26 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       }
       if (sig != c->probe_sig) {
         unsigned long long* d = c->err2.as<unsigned long long>();
-        unsigned long long hp[2] = {0, 0};
-        H(hipMemsetAsync(d, 0, 16, st), "probe memset");
+        unsigned long long hp[3] = {0, 0, 0};
+        H(hipMemsetAsync(d, 0, 24, st), "probe memset");
         launch_probe(d_files, nfiles, d, st);
         L("k_probe");
-        H(hipMemcpyAsync(hp, d, 16, hipMemcpyDeviceToHost, st), "probe D2H");
+        H(hipMemcpyAsync(hp, d, 24, hipMemcpyDeviceToHost, st), "probe D2H");
         H(hipStreamSynchronize(st), "probe sync");
         if (!ok) return CASK_E_DEVICE;
         c->probe_sig = sig;
         c->probe_walk = hp[1] && hp[0] >= kWalkMean * hp[1];
+        c->probe_short = hp[1] && hp[0] <= kShortHaloMean * hp[1] && hp[2] <= kShortHaloMax;
       }
       walk = c->probe_walk;
+      halo_pick = c->probe_short ? 2 : 1;
     }
   }
+  if (c->geo < 0 && !walk && halo_pick == 2) {
+    geo = kGeoShortHalo;  // same chunk size: only the window (and the kernel) change
+    a.win = chunk + geometry_halo(geo);
+  }
+  c->last_geo = walk ? -1 : geo;
   if (walk && !hint) a.big = kWalkHashMax;  // the walker hashes what fits its window, k_long the rest
   if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
     const char* wr = getenv("CASK_WALK_RUN");
@@ -532,7 +552,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_walk_runs(a, st);
     L("k_walk_runs");
   } else {
-    launch_scan_chunks(a, c->geo, st);
+    launch_scan_chunks(a, geo, st);
     L("k_scan_chunks");
   }
   H(hipEventRecord(c->ev[2], st));
@@ -634,7 +654,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       launch_walk_runs(a, st);
       L("k_walk_runs");
     } else {
-      launch_scan_chunks(a, c->geo, st);
+      launch_scan_chunks(a, geo, st);
       L("k_scan_chunks");
     }
     post(false);

@@ -246,7 +246,8 @@ class ScanContext:
         return {"chunks": int(c[0]), "long_records": int(c[1]), "repaired_chunks": int(c[2]),
                 "local_repair_passes": int(c[3]), "walked": int(c[4]),
                 "dense_path": int(self.lib.cask_last_dense(self._h)),
-                "walk_mode": int(self.lib.cask_last_walk(self._h))}
+                "walk_mode": int(self.lib.cask_last_walk(self._h)),
+                "geometry": int(self.lib.cask_last_geometry(self._h))}
 
     # -- encoder ------------------------------------------------------------------------------
     def encode_synthetic(self, off, seq, ksz, vsz_raw, key_id, value_seed: int, out):

@@ -155,6 +155,9 @@ int cask_last_dense(const cask_ctx* ctx);
 /* 1 if the last call's speculative pass was the walk mode (k_walk_runs: record headers chased from
  * HBM, chosen when the records at the heads of the files average >= 1 KiB), 0 for k_scan_chunks. */
 int cask_last_walk(const cask_ctx* ctx);
+/* The last call's k_scan_chunks geometry: 0 for the wide 4,080-B halo, 3 for the short 1,008-B halo
+ * (picked when the records at the heads of the files are short), -1 when the walk mode ran. */
+int cask_last_geometry(const cask_ctx* ctx);
 
 /* ------------------------------------------------------------------------------------------ */
 /* Batched record encoder (Entry::write_bytes, data.rs:90-121) — the bulk write path and the   */

@@ -69,10 +69,10 @@ def cfg2(gpu_ctx):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("mode", ["chunk", "walk"])
+@pytest.mark.parametrize("mode", ["chunk", "narrow", "walk"])
 def test_cfg2_full_size_against_generator(gpu_ctx, cfg2, mode, monkeypatch):
-    """Both speculative passes: k_scan_chunks (forced) and k_walk_runs (what the library picks for
-    these records), every row against the generator."""
+    """Both speculative passes: k_scan_chunks (forced, with either halo) and k_walk_runs (what the
+    library picks for these records), every row against the generator."""
     import torch
     monkeypatch.setenv("CASK_SCAN_MODE", mode)
     files, vsz, n, rl = cfg2
@@ -82,7 +82,7 @@ def test_cfg2_full_size_against_generator(gpu_ctx, cfg2, mode, monkeypatch):
     assert res.error is None and res.count == n
     cnt = gpu_ctx.last_counters()
     assert cnt["walked"] == 0 and cnt["walk_mode"] == (mode == "walk"), cnt
-    assert cnt["long_records"] > 1_000_000 if mode == "chunk" else cnt["dense_path"] == 1, cnt
+    assert cnt["long_records"] > 1_000_000 if mode != "walk" else cnt["dense_path"] == 1, cnt
     assert sum(f.data.numel() for f, _ in files) > 31 * 2 ** 30 and len(files) >= 16
     assert int((rows["status"][:n] != 0).sum().item()) == 0
     assert bool((rows["seq"][:n].to(torch.int64) == torch.arange(1, n + 1, device=dev)).all())
@@ -133,7 +133,7 @@ def test_cfg2_full_size_corrupted_against_oracle(gpu_ctx, cfg2):
             first = (int(b["status"]), fd.file_id, int(b["pos"]), int(b["expected"]),
                      int(b["found"]) if int(b["status"]) == 1 else 0)
     assert len(flipped) >= 12
-    for mode in ("chunk", "walk"):  # both speculative passes
+    for mode in ("chunk", "narrow", "walk"):  # both speculative passes, both halos
         os.environ["CASK_SCAN_MODE"] = mode
         try:
             res = gpu_ctx.scan_device([(fd.file_id, fd.data) for fd, _ in files])

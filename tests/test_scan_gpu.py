@@ -20,14 +20,16 @@ import oracle_ffi as O
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=["auto", "walk"])
+@pytest.fixture(autouse=True, params=["auto", "walk", "wide"])
 def scan_mode(request, monkeypatch):
-    """Every test here runs twice: the mode the library picks (k_scan_chunks for these mostly short
-    records, the walk for the long-record cases) and the walk mode forced (k_walk_runs)."""
-    if request.param == "walk":
-        monkeypatch.setenv("CASK_SCAN_MODE", "walk")
-    else:
+    """Every test here runs three times: the mode the library picks (k_scan_chunks for these mostly
+    short records — with the short 1,008-B halo when the file heads hold short records — and the
+    walk for the long-record cases), the walk mode forced (k_walk_runs), and the chunk scan forced
+    with the wide 4,080-B halo."""
+    if request.param == "auto":
         monkeypatch.delenv("CASK_SCAN_MODE", raising=False)
+    else:
+        monkeypatch.setenv("CASK_SCAN_MODE", request.param)
     return request.param
 
 
@@ -195,6 +197,21 @@ def test_uniform_290(gpu_ctx):
     res = check_against_oracle(gpu_ctx, [buf])
     cnt = gpu_ctx.last_counters()
     assert cnt["repaired_chunks"] == 0 and cnt["dense_path"] == 1, cnt
+
+
+def test_short_halo_records_crossing_the_window(gpu_ctx):
+    """Short records at the file heads pick the 1,008-B halo; records of 1-4 KiB later in the file
+    then cross the window's end and go to k_long_hash (some corrupted), row for row."""
+    rng = random.Random(11)
+    head = make_records(rng, 300, lambda r: 16, lambda r: 100)
+    tail = bytearray(make_records(rng, 2000, lambda r: r.randrange(0, 30),
+                                  lambda r: r.randrange(0, 4000), tomb_p=0.05, seq0=301))
+    for _ in range(6):
+        tail[rng.randrange(len(tail))] ^= 1 << rng.randrange(8)
+    check_against_oracle(gpu_ctx, [head + bytes(tail)], device=True)
+    cnt = gpu_ctx.last_counters()
+    if os.environ.get("CASK_SCAN_MODE") is None:
+        assert cnt["geometry"] == 3 and cnt["long_records"] > 0, cnt
 
 
 def test_uniform_82_device(gpu_ctx):
@@ -449,6 +466,7 @@ def test_cfg2_full_size_properties(gpu_ctx):
     assert int((res.vsz[:res.count] != 256).sum().item()) == 0
     cnt = gpu_ctx.last_counters()
     assert cnt["repaired_chunks"] == 0 and cnt["dense_path"] == 1, cnt
+    assert cnt["geometry"] == {"auto": 3, "wide": 0, "walk": -1}[os.environ.get("CASK_SCAN_MODE", "auto")], cnt
     # a 64 MiB slice of file 1 against the oracle, all five row fields
     sl_bytes = (64 << 20) // 290 * 290
     host = files[0].data[:sl_bytes].cpu().numpy()

@@ -1,6 +1,6 @@
 """A/B timing of library builds on one box (tools only; bench.py always times the product build).
 
-  python tools/ab.py [--rounds 3] [--steps 20] NAME=PATH [NAME=PATH ...]
+  python tools/ab.py [--rounds 3] [--steps 20] NAME=PATH[@VAR=VALUE,...] [NAME=PATH ...]
 
 Each build runs in its own process (the library is picked with cask_amd._lib.use_library, never by
 an environment variable the package reads); the builds alternate `--rounds` times so box drift
@@ -45,7 +45,8 @@ def child(path, steps, files, zipf_gib):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     print(json.dumps({"gibps": nbytes * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps,
-                      "k_scan_ms": sum(k) / len(k), "timings": ctx.last_timings()}))
+                      "k_scan_ms": sum(k) / len(k), "timings": ctx.last_timings(),
+                      "geometry": ctx.last_counters()["geometry"]}))
 
 
 def main():
@@ -62,15 +63,19 @@ def main():
     for r in range(a.rounds):
         for spec in a.libs:
             name, path = spec.split("=", 1)
+            env = dict(os.environ)
+            if "@" in path:  # NAME=PATH@VAR=VALUE[,VAR=VALUE]: environment of that run only
+                path, kv = path.split("@", 1)
+                env.update(x.split("=", 1) for x in kv.split(","))
             out = subprocess.run([sys.executable, __file__, "--child", path, "--steps", str(a.steps),
                                   "--files", str(a.files), "--zipf-gib", str(a.zipf_gib)],
-                                 capture_output=True, text=True, timeout=300)
+                                 capture_output=True, text=True, timeout=300, env=env)
             if out.returncode != 0:
                 print(name, "FAILED", out.stderr[-2000:])
                 sys.exit(1)
             d = json.loads(out.stdout.strip().splitlines()[-1])
             print(f"round {r} {name}: {d['gibps']:.1f} GiB/s  {d['ms_per_step']:.4f} ms/step  "
-                  f"k_scan {d['k_scan_ms']:.4f} ms  {json.dumps(d['timings'])}", flush=True)
+                  f"k_scan {d['k_scan_ms']:.4f} ms  {json.dumps(d['timings'])} geo {d.get('geometry')}", flush=True)
 
 
 if __name__ == "__main__":
