@@ -545,15 +545,6 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
       const uint64_t kw = (uint64_t)(K4[0] & 0xFFFFu) | ((uint64_t)(K4[1] & 0xFFFFu) << 16) |
                           ((uint64_t)(K4[2] & 0xFFFFu) << 32) | ((uint64_t)(K4[3] & 0xFFFFu) << 48);
       const uint32_t tw = T4[0] | (T4[1] << 8) | (T4[2] << 16) | (T4[3] << 24);
-#ifdef CASK_FIN_NT
-      __builtin_nontemporal_store(u64x2{P4[0], P4[1]}, (u64x2*)(a.pos + d0));
-      __builtin_nontemporal_store(u64x2{P4[2], P4[3]}, (u64x2*)(a.pos + d0 + 2));
-      __builtin_nontemporal_store(u64x2{S4[0], S4[1]}, (u64x2*)(a.seq + d0));
-      __builtin_nontemporal_store(u64x2{S4[2], S4[3]}, (u64x2*)(a.seq + d0 + 2));
-      __builtin_nontemporal_store(u32x4{V4[0], V4[1], V4[2], V4[3]}, (u32x4*)(a.vsz + d0));
-      __builtin_nontemporal_store(kw, (uint64_t*)(a.ksz + d0));
-      __builtin_nontemporal_store(tw, (uint32_t*)(a.status + d0));
-#else
       *(u64x2*)(a.pos + d0) = u64x2{P4[0], P4[1]};
       *(u64x2*)(a.pos + d0 + 2) = u64x2{P4[2], P4[3]};
       *(u64x2*)(a.seq + d0) = u64x2{S4[0], S4[1]};
@@ -561,7 +552,6 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
       *(u32x4*)(a.vsz + d0) = u32x4{V4[0], V4[1], V4[2], V4[3]};
       *(uint64_t*)(a.ksz + d0) = kw;
       *(uint32_t*)(a.status + d0) = tw;
-#endif
     } else {
 #pragma unroll
       for (uint32_t q = 0; q < 4; ++q) {
