@@ -532,15 +532,22 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   // run ahead), so workgroups that run slower take fewer runs and all finish together; each run is
   // walked in order with a carry.
   // A repair pass re-scans only the stretches listed in a.runs (each one walked like a run).
-  const uint64_t R = a.run;
-  const uint64_t nruns = a.runs ? a.nruns_list : (a.total_chunks + R - 1) / R;
+  // The last stretch of chunks (from a.run_tail) goes out in shorter runs of a.run_small, so that
+  // the workgroups run out of work closer together (a run of 16 chunks is ~90 us of one workgroup).
+  const uint64_t R = a.run, Rs = a.run_small;
+  const uint64_t nbig = a.run_tail / R;  // a.run_tail: a multiple of R (>= total_chunks: no tail)
+  const uint64_t nruns = a.runs ? a.nruns_list
+                         : a.run_tail < a.total_chunks ? nbig + (a.total_chunks - a.run_tail + Rs - 1) / Rs
+                                                       : (a.total_chunks + R - 1) / R;
   auto run_at = [&](uint64_t r, uint64_t& first, uint64_t& end) {
     if (a.runs) {
       first = a.runs[2 * r];
       end = a.runs[2 * r + 1];
     } else {
-      first = r * R;
-      end = first + R < a.total_chunks ? first + R : a.total_chunks;
+      const bool big = r < nbig;
+      first = big ? r * R : a.run_tail + (r - nbig) * Rs;
+      end = first + (big ? R : Rs);
+      end = end < a.total_chunks ? end : a.total_chunks;
     }
   };
   uint32_t my_claim = 0;  // thread kMetaT: the run claimed for after the current one

@@ -113,6 +113,9 @@ struct ScanArgs {
   uint64_t row_cap;
   unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums
   uint32_t run;                // k_scan_chunks: consecutive chunks a workgroup walks with a carry
+  uint32_t run_small;          // k_scan_chunks: chunks per run from run_tail on
+  uint64_t run_tail;           // k_scan_chunks: first chunk of the short runs (a multiple of run;
+                               // >= total_chunks: none)
   uint32_t regular_ok;         // 1: a regular chunk may keep only its first slot row (kCountRegular)
   uint32_t respec;             // 1: validation rewrites an invalid chunk's start from T[c] (local repair)
   uint32_t big;                // records longer than this are hashed by k_long from HBM, not in LDS

@@ -370,6 +370,18 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       const uint64_t per_wg = total_chunks / ((uint64_t)cus * 4u * 16u);
       a.run = (uint32_t)std::min<uint64_t>(kMaxRun, std::max<uint64_t>(kDefaultRun, per_wg));
     }
+    // The last grid's worth of runs in runs of a quarter of the length (CASK_RUN_TAIL=0: tuning
+    // knob, no short runs): the workgroups then run dry within a short run of each other.
+    static const bool tail_on = !(getenv("CASK_RUN_TAIL") && atoi(getenv("CASK_RUN_TAIL")) == 0);
+    const uint64_t grid_runs = (uint64_t)device_cus() * 4u;  // resident k_scan_chunks workgroups
+    // CASK_RUN_SMALL / CASK_RUN_TAIL_X (tuning knobs): the short runs' length; the tail's length in
+    // resident workgroups x run, in quarters
+    static const uint32_t rs_env = getenv("CASK_RUN_SMALL") ? (uint32_t)atoi(getenv("CASK_RUN_SMALL")) : 0u;
+    static const uint64_t tx = getenv("CASK_RUN_TAIL_X") ? (uint64_t)atoi(getenv("CASK_RUN_TAIL_X")) : 4u;
+    a.run_small = rs_env ? std::min(rs_env, a.run) : std::max<uint32_t>(2u, a.run / 4);
+    a.run_tail = ~0ull;
+    const uint64_t tail = grid_runs * a.run * tx / 4;
+    if (tail_on && total_chunks >= 4 * tail) a.run_tail = (total_chunks - tail) / a.run * a.run;
   }
   // regular chunks keep only their first slot row when the rows go to the dense output (k_finish
   // and k_compact expand them); the segmented output hands the slots to the caller
@@ -476,6 +488,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
     const char* wr = getenv("CASK_WALK_RUN");
     a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : hint ? kHintRun : kWalkRun;
+    a.run_tail = ~0ull;  // (the chunk scan's short tail runs were sized for its own run length)
   }
   c->last_walk = walk ? 1 : 0;
   H(hipEventRecord(c->ev[1], st));
