@@ -439,9 +439,9 @@ __device__ __forceinline__ uint64_t g_reclen(const uint8_t* hdr) {
 }
 
 // ------------------------------------------------------------------------------------------
-// Decoupled look-back (single-pass prefix scan over elements handed out in order): the dense row
-// numbering and the chunk-start validation of k_finish (tiles) and of the dense k_scan_chunks
-// (runs) are a prefix over every earlier chunk of (row count, max chain exit within the file).
+// Single-pass prefix over elements handed out in order (k_finish's tiles): the dense row numbering
+// and the chunk-start validation are a prefix over every earlier chunk of (row count, max chain
+// exit within the file).
 // ------------------------------------------------------------------------------------------
 struct SegAgg {  // prefix aggregate: rows, and the max exit within the last file seen
   uint64_t rows, mx;
@@ -503,55 +503,56 @@ __device__ __forceinline__ bool agg_get(const uint64_t* p, uint32_t epoch, SegAg
   return ok != 0;
 }
 
-// Exclusive prefix of element `idx` (> 0: a tile of k_finish, a run of k_scan_chunks) by one whole
-// wave: lane l reads element idx - 1 - l (its inclusive prefix if published, else its aggregate);
-// the nearest inclusive prefix ends the walk. An element with neither has not finished yet
-// (elements are handed out in order, so it is being worked on and will publish): with `block` the
-// wave polls it, without it returns false and the caller tries again later. A blocking walk gives up
-// (returns false) after about a quarter of a second of polling, so that a protocol fault ends in the
-// repair path rather than in a hung kernel; the caller then flags the call invalid.
-__device__ bool lookback(const uint64_t* state, uint32_t epoch, uint64_t idx, bool block, SegAgg& out) {
-  const uint32_t lane = threadIdx.x & 63;
-  SegAgg acc{0, 0, 0xFFFFFFFFu, 0};  // combined (older) ... (newer) of the elements walked so far
-  int64_t top = (int64_t)idx - 1;   // newest element of the current window (lane 0)
+__device__ __forceinline__ SegAgg seg_shfl_down(const SegAgg& v, uint32_t o) {
+  SegAgg u;
+  u.rows = __shfl_down(v.rows, o, 64);
+  u.mx = __shfl_down(v.mx, o, 64);
+  u.fl = __shfl_down(v.fl, o, 64);
+  u.hs = __shfl_down(v.hs, o, 64);
+  return u;
+}
+
+// Ordered combination of the aggregates of elements [lo, hi) (state: 8 granules per element,
+// aggregate at 0..2) by a whole 256-thread workgroup, 256 elements per round trip; every thread
+// calls it and gets the result. An element that has not published yet is polled (elements are
+// handed out in order, so it is being worked on); gives up (returns false) after about a quarter of
+// a second of polling, so that a protocol fault ends in the repair path, not in a hung kernel.
+__device__ bool block_prefix(const uint64_t* state, uint32_t epoch, uint64_t lo, uint64_t hi, SegAgg& out) {
+  __shared__ uint32_t s_miss;
+  __shared__ SegAgg s_w[4];
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const SegAgg id{0, 0, 0xFFFFFFFFu, 0};
+  SegAgg acc = id;
   uint32_t polls = 0;
-  for (;;) {
-    const int64_t j = top - (int64_t)lane;
-    SegAgg x{0, 0, 0xFFFFFFFFu, 0};
-    uint32_t st = 2;  // 2: inclusive, 1: aggregate, 0: nothing yet
-    if (j >= 0) {
-      const uint64_t* g = state + 8ull * (uint64_t)j;
-      if (agg_get(g + 3, epoch, x)) st = 2;
-      else if (agg_get(g, epoch, x)) st = 1;
-      else st = 0;
-    }
-    const unsigned long long m_inc = __ballot(st == 2), m_none = __ballot(st == 0);
-    const uint32_t f_inc = m_inc ? (uint32_t)__builtin_ctzll(m_inc) : 64u;
-    const uint32_t f_none = m_none ? (uint32_t)__builtin_ctzll(m_none) : 64u;
-    if (f_none < f_inc) {  // an element before the nearest inclusive one has not published yet
-      if (!block || ++polls > (1u << 20)) return false;
+  for (uint64_t r = lo; r < hi;) {
+    const uint64_t j = r + tid;
+    SegAgg v = id;
+    bool have = true;
+    if (j < hi) have = agg_get(state + 8ull * j, epoch, v);
+    if (tid == 0) s_miss = 0;
+    __syncthreads();
+    if (!have) s_miss = 1;
+    __syncthreads();
+    const bool miss = s_miss != 0;
+    __syncthreads();  // (s_miss is reset by the next round)
+    if (miss) {
+      if (++polls > (1u << 20)) return false;
       __builtin_amdgcn_s_sleep(2);
       continue;
     }
-    const uint32_t last = f_inc < 64u ? f_inc : 63u;  // lanes last .. 0, oldest first
-    SegAgg w{0, 0, 0xFFFFFFFFu, 0};
-    for (int l = (int)last; l >= 0; --l) {
-      SegAgg y;
-      y.rows = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x.rows >> 32), l) << 32) |
-               __builtin_amdgcn_readlane((uint32_t)x.rows, l);
-      y.mx = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(x.mx >> 32), l) << 32) |
-             __builtin_amdgcn_readlane((uint32_t)x.mx, l);
-      y.fl = __builtin_amdgcn_readlane(x.fl, l);
-      y.hs = __builtin_amdgcn_readlane(x.hs, l);
-      w = seg_combine(w, y);
+    // lane l + o holds newer elements than lane l
+    for (uint32_t o = 1; o < 64; o <<= 1) {
+      const SegAgg u = seg_shfl_down(v, o);
+      if (lane + o < 64) v = seg_combine(v, u);
     }
-    acc = seg_combine(w, acc);
-    if (f_inc < 64u) {
-      out = acc;
-      return true;
-    }
-    top -= 64;
+    if (lane == 0) s_w[wave] = v;
+    __syncthreads();
+    acc = seg_combine(acc, seg_combine(seg_combine(seg_combine(s_w[0], s_w[1]), s_w[2]), s_w[3]));
+    __syncthreads();
+    r += 256;
   }
+  out = acc;
+  return true;
 }
 
 // Last file with first_chunk <= t (empty files share first_chunk with their successor). Call it

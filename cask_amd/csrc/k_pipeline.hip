@@ -387,7 +387,6 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   constexpr uint32_t TC = kFinTile;
   __shared__ uint32_t s_tile;
   __shared__ SegAgg s_wave[4];
-  __shared__ SegAgg s_prefix;
   __shared__ uint32_t s_base[TC + 1];      // row base of each chunk of the tile, relative to the tile
   __shared__ u32x4 s_desc[TC];            // regular chunk: first row; else slot row of the chunk
   __shared__ uint64_t s_c0[TC], s_len[TC];
@@ -437,25 +436,21 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   for (uint32_t k = 0; k < wave; ++k) wpre = seg_combine(wpre, s_wave[k]);
   inc = seg_combine(wpre, inc);
   SegAgg total = seg_combine(seg_combine(seg_combine(s_wave[0], s_wave[1]), s_wave[2]), s_wave[3]);
-  // publish the tile's aggregate, then find the prefix of the earlier tiles
-  uint64_t* g = a.tstate + 8ull * tile;
-  if (tid == 0) {
-    if (tile == 0) agg_put(g + 3, a.epoch, total);
-    else agg_put(g, a.epoch, total);
-  }
-  if (wave == 0) {
-    SegAgg P{0, 0, 0xFFFFFFFFu, 0};
-    if (tile > 0) {
-      if (lookback(a.tstate, a.epoch, tile, true, P)) {
-        if (lane == 0) agg_put(g + 3, a.epoch, seg_combine(P, total));
-      } else if (lane == 0) {
-        atomicOr(&a.ctr->any_invalid, 1u);  // gave up waiting: the repair path redoes the call
-      }
-    }
-    if (lane == 0) s_prefix = P;
-  }
-  __syncthreads();
-  const SegAgg P = s_prefix;
+  // Publish the tile's aggregate, then the prefix of the earlier tiles in two levels (every tile
+  // starts at about the same time, so a chained look-back would wait for its predecessors' own
+  // look-backs): the tiles of this tile's group of kFinGroup, then the groups before it, whose
+  // aggregates the last tile of each group publishes. Two round trips, whatever the tile's index.
+  const uint64_t ntiles = (a.total_chunks + TC - 1) / TC, grp = tile / kFinGroup;
+  uint64_t* st2 = a.tstate + 8ull * (ntiles + 1);  // group aggregates
+  if (tid == 0) agg_put(a.tstate + 8ull * tile, a.epoch, total);
+  SegAgg P1{0, 0, 0xFFFFFFFFu, 0}, P2{0, 0, 0xFFFFFFFFu, 0};
+  // (tile is the same in every thread: the barriers inside are uniform)
+  bool got = block_prefix(a.tstate, a.epoch, grp * kFinGroup, tile, P1);
+  if (got && tid == 0 && (tile % kFinGroup == kFinGroup - 1 || tile + 1 == ntiles))
+    agg_put(st2 + 8ull * grp, a.epoch, seg_combine(P1, total));
+  got = got && block_prefix(st2, a.epoch, 0, grp, P2);
+  if (!got && tid == 0) atomicOr(&a.ctr->any_invalid, 1u);  // gave up waiting: the repair path redoes the call
+  const SegAgg P = seg_combine(P2, P1);
   const SegAgg full = seg_combine(P, inc);  // inclusive prefix through this chunk
   const uint64_t base = full.rows - n;      // this chunk's first dense row
   // T[c]: max exit of the earlier chunks of this file. The lane before holds the tile's inclusive
@@ -493,16 +488,17 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   const uint64_t cap = a.row_cap;
   const uint64_t g0 = tile_lo >> 2, g1 = (tile_lo + tile_rows + 3) >> 2;
   const uint32_t nch = (uint32_t)((a.total_chunks - tile * TC) < TC ? (a.total_chunks - tile * TC) : TC);
+  const float per_row = (float)nch / (float)tile_rows;
   for (uint64_t grp = g0 + tid; grp < g1; grp += TC) {
     const uint64_t d0 = grp << 2;
     // chunk of the group's first row in the tile: last j with s_base[j] <= rel
     const uint64_t rel0 = d0 > tile_lo ? d0 - tile_lo : 0;
-    uint32_t lo = 0, hi = nch;  // s_base[lo] <= rel0 < s_base[hi]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (s_base[mid] <= rel0) lo = mid; else hi = mid;
-    }
-    uint32_t j = lo;
+    // the last chunk j with s_base[j] <= rel0: guessed from the tile's mean rows per chunk, then
+    // stepped (one or two LDS reads for tiles of similar chunks, not a binary search's eight)
+    uint32_t j = (uint32_t)((float)rel0 * per_row);  // (only a guess: corrected below)
+    j = j < nch ? j : nch - 1;
+    while (j > 0 && s_base[j] > rel0) --j;
+    while (j + 1 < nch && s_base[j + 1] <= rel0) ++j;
     uint64_t P4[4], S4[4];
     uint32_t V4[4], K4[4], T4[4];
     bool inr[4];

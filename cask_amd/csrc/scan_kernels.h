@@ -212,6 +212,7 @@ void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);
 constexpr uint32_t kFinTile = 256;  // chunks per k_finish tile (one per thread)
+constexpr uint32_t kFinGroup = 32;  // k_finish tiles per group of the two-level prefix
 void launch_finish(const ScanArgs& a, void* stream);
 void launch_err_dense(const ScanArgs& a, uint32_t fi, uint64_t row, uint32_t* out, void* stream);
 // k_keydir.hip: a shard's keydir block (keydir_format.h) from its dense rows

@@ -293,7 +293,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   if (!c->repair.ensure(runs_bytes + cerr_bytes + 2 * redo_bytes)) return CASK_E_NOMEM;
   if (!c->lq.ensure(8 * (lq_region_base(total_chunks, chunk, 32) + 1))) return CASK_E_NOMEM;
   bool fresh = false;  // k_finish look-back granules, 8 per tile
-  if (!c->tstate.ensure(64ull * (fin_tiles + 1), &fresh)) return CASK_E_NOMEM;
+  // (then the group aggregates of the two-level prefix)
+  if (!c->tstate.ensure(64ull * (fin_tiles + 1) + 64ull * (fin_tiles / kFinGroup + 2), &fresh)) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
