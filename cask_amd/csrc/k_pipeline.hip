@@ -398,21 +398,27 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
     s_long = 0u;
   }
   __syncthreads();
-  const uint64_t tile = s_tile;
+  const uint64_t tile = __builtin_amdgcn_readfirstlane(s_tile);
   const uint64_t c = tile * TC + tid;
   const bool act = c < a.total_chunks;
-  // the chunk's table entries
+  // the chunk's table entries, all loaded at once (the descriptor too: only regular chunks use it)
   uint32_t n = 0, cw = 0, fi = 0, cerr = 0xFFFFFFFFu, lr = 0xFFFFFFFFu;
   uint64_t e = 0, spec = kNone, c0 = 0, c1 = 0, len = 0;
+  u32x4 dsc = u32x4{0u, 0u, 0u, 0u};
   bool head = false;
+  // the file of the wave's first chunk (uniform: scalar loads), then each lane's own (a wave's
+  // chunks rarely cross a file boundary)
+  fi = find_file(a.files, a.nfiles, (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(tile * TC + wave * 64)));
   if (act) {
     cw = a.count[c];
     n = cw & kCountMask;
     spec = a.spec[c];
-    e = spec == kNone ? 0ull : a.exit[c];
+    const uint64_t ex = a.exit[c];
     cerr = a.cerr[c];
     lr = a.long_r[c];
-    fi = find_file(a.files, a.nfiles, c);
+    dsc = ((const u32x4*)a.desc)[c];
+    e = spec == kNone ? 0ull : ex;
+    while (fi + 1 < a.nfiles && a.files[fi + 1].first_chunk <= c) ++fi;
     const FileDesc fd = a.files[fi];
     c0 = (c - fd.first_chunk) * (uint64_t)a.chunk;
     c1 = (c0 + a.chunk < fd.len) ? c0 + a.chunk : fd.len;
@@ -481,7 +487,7 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   s_reg[tid] = act && (cw & kCountRegular);
   s_c0[tid] = c0;
   s_len[tid] = len;
-  if (act && (cw & kCountRegular)) s_desc[tid] = ((const u32x4*)a.desc)[c];
+  if (act && (cw & kCountRegular)) s_desc[tid] = dsc;
   __syncthreads();
   if (tid == 0 && s_long) a.ctr->long_pending = 1u;  // every writer stores the same value
   if (!tile_rows) return;
