@@ -577,7 +577,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_finish(a, st);
     L("k_finish");
     H(hipEventRecord(c->ev[3], st));
-    if (long_now) H(hipEventRecord(c->ev[4], st));
     read_call();
     if (!ok) return CASK_E_DEVICE;
   }
@@ -587,20 +586,21 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // every speculated start held: the rows are final but for the long records' checksums
     a.dense = 1;
     c->last_dense = 1;
+    // (no long records left: the call block read above already waited for everything; no
+    // further event or round trip)
     const bool more = !long_now && hc->long_pending;
     if (more) {
       launch_long(a, st);
       L("k_long");
+      H(hipEventRecord(c->ev[4], st));
+      read_call();
     }
-    if (!long_now) H(hipEventRecord(c->ev[4], st));
-    if (more) read_call();
-    else H(hipEventSynchronize(c->ev[4]), "event sync");
     if (!ok) return CASK_E_DEVICE;
     float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0;
-    (void)hipEventElapsedTime(&t_all, c->ev[1], c->ev[4]);
+    (void)hipEventElapsedTime(&t_all, c->ev[1], more ? c->ev[4] : c->ev[3]);
     (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
     (void)hipEventElapsedTime(&t_fin, c->ev[2], c->ev[3]);
-    (void)hipEventElapsedTime(&t_long, c->ev[3], c->ev[4]);
+    if (more) (void)hipEventElapsedTime(&t_long, c->ev[3], c->ev[4]);
     c->last_ms[0] = t_all;
     c->last_ms[1] = t_k1;
     c->last_ms[2] = t_long;
