@@ -30,8 +30,9 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md (8.0 TB/s spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    # (a step is ~1.7 ms: 100 steps keep host hiccups out of the number and still take 0.2 s)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--files", type=int, default=8, help="data files per GPU (configs[1]: 8)")
     ap.add_argument("--records-per-file", type=int, default=3_702_558)
     ap.add_argument("--no-cpu-baseline", action="store_true")
