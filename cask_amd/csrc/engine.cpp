@@ -464,7 +464,7 @@ struct EngineDev {
       return true;
     }
   } data, rows, hint;
-  static constexpr int kReaders = 8, kSlots = 2;
+  static constexpr int kReaders = 16, kSlots = 2;
   static constexpr size_t kSlotBytes = 32ull << 20;
   void* pin[kReaders][kSlots] = {};
   hipStream_t rs[kReaders] = {};
@@ -501,7 +501,10 @@ struct EngineDev {
     std::vector<Piece> pieces;
     for (uint32_t f = 0; f < v.size(); ++f)
       for (uint64_t o = 0; o < v[f].len; o += kSlotBytes) pieces.push_back(Piece{f, o, std::min<uint64_t>(kSlotBytes, v[f].len - o)});
-    const unsigned nt = std::max(1u, std::min<unsigned>((unsigned)kReaders, std::min<unsigned>(host_threads(), (unsigned)pieces.size())));
+    // CASK_OPEN_READERS (tuning knob): reader threads, at most kReaders (default: the host threads)
+    static const unsigned readers = getenv("CASK_OPEN_READERS") ? (unsigned)atoi(getenv("CASK_OPEN_READERS")) : 0u;
+    const unsigned want = readers ? std::min<unsigned>(readers, (unsigned)kReaders) : (unsigned)kReaders;
+    const unsigned nt = std::max(1u, std::min<unsigned>(want, std::min<unsigned>(host_threads(), (unsigned)pieces.size())));
     std::vector<int> status(nt, CASK_OK);
     parallel_for(nt, [&](unsigned t) {
       if (hipSetDevice(device) != hipSuccess) {
