@@ -550,6 +550,54 @@ struct EngineDev {
     return CASK_OK;
   }
 
+  // Device -> pageable host copy staged through the pinned slots: threads take every nt-th 32-MiB
+  // piece (CASK_STAGE_MIN=0 stages every copy: the tests run the small cases through it), the DMA of one piece into a slot overlapping the host copy of the previous piece out of
+  // the other (a copy to pageable memory straight from the device runs at ~10 GB/s). Small copies
+  // take cask_copy. The device work that produced `src` (on the context's stream) is waited for first.
+  int to_host(uint8_t* dst, const uint8_t* src, uint64_t n) {
+    const char* mv = getenv("CASK_STAGE_MIN");  // test knob: smallest copy staged (default 64 MiB)
+    if (n < (mv ? strtoull(mv, nullptr, 10) : (64ull << 20)) || !n) return cask_copy(ctx, dst, src, n);
+    if (hipSetDevice(device) != hipSuccess || hipStreamSynchronize((hipStream_t)cask_ctx_stream(ctx)) != hipSuccess)
+      return CASK_E_DEVICE;
+    const uint64_t np = (n + kSlotBytes - 1) / kSlotBytes;
+    const unsigned nt = std::max(1u, std::min<unsigned>((unsigned)kReaders, std::min<unsigned>(host_threads(), (unsigned)np)));
+    std::vector<int> status(nt, CASK_OK);
+    parallel_for(nt, [&](unsigned t) {
+      if (hipSetDevice(device) != hipSuccess) {
+        status[t] = CASK_E_DEVICE;
+        return;
+      }
+      uint64_t prev = ~0ull;
+      unsigned k = 0, pk = 0;
+      for (uint64_t j = t;; j += nt, k ^= 1) {
+        bool have = j < np;
+        if (have) {  // slot k is free: its last piece was copied out below, before this issue
+          const uint64_t off = j * kSlotBytes, m = std::min<uint64_t>(kSlotBytes, n - off);
+          if (hipMemcpyAsync(pin[t][k], src + off, m, hipMemcpyDeviceToHost, rs[t]) != hipSuccess ||
+              hipEventRecord(ev[t][k], rs[t]) != hipSuccess) {
+            status[t] = CASK_E_DEVICE;
+            have = false;
+          }
+        }
+        if (prev != ~0ull) {
+          if (hipEventSynchronize(ev[t][pk]) != hipSuccess) {
+            status[t] = CASK_E_DEVICE;
+            break;
+          }
+          const uint64_t off = prev * kSlotBytes;
+          memcpy(dst + off, pin[t][pk], std::min<uint64_t>(kSlotBytes, n - off));
+        }
+        if (!have) break;
+        prev = j;
+        pk = k;
+      }
+      if (hipStreamSynchronize(rs[t]) != hipSuccess) status[t] = CASK_E_DEVICE;
+    });
+    for (int st : status)
+      if (st != CASK_OK) return st;
+    return CASK_OK;
+  }
+
   // Device rows sized from a guess (average record >= 48 B), once more at the exact count if short.
   int scan(const std::vector<cask_file_view>& v, std::vector<uint64_t>& row_off, cask_scan_error& se) {
     uint64_t total = 0;
@@ -582,7 +630,7 @@ struct EngineDev {
     st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), hint.p, hint.cap, fo.data());
     if (st != CASK_OK) return st;
     if (!hbuf.resize(fo[v.size()])) return CASK_E_NOMEM;
-    if (!hbuf.empty() && cask_copy(ctx, hbuf.data(), hint.p, hbuf.size()) != CASK_OK) return CASK_E_DEVICE;
+    if (!hbuf.empty() && to_host(hbuf.data(), hint.p, hbuf.size()) != CASK_OK) return CASK_E_DEVICE;
     for (size_t k = 0; k < v.size(); ++k) {
       hs0[view_file[k]] = fo[k];
       hs1[view_file[k]] = fo[k + 1];
@@ -1350,7 +1398,7 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
         if (!ed->hint.ensure(total + 256)) return abort_with(CASK_E_NOMEM);
         st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), dst.data(),
                                 len32.data(), n, ed->hint.p);
-        if (st == CASK_OK) st = cask_copy(ed->ctx, host.get(), ed->hint.p, total);
+        if (st == CASK_OK) st = ed->to_host(host.get(), ed->hint.p, total);
         if (st != CASK_OK) return abort_with(st);
       }
       t_gather += ms_since(tg);
@@ -1921,7 +1969,7 @@ int64_t cask_log_write(const char* dir_c, uint32_t first_file_id, uint64_t max_f
               (!vend || hipMemcpy(d_vals, vals, vend, hipMemcpyHostToDevice) == hipSuccess);
     if (!ok) return CASK_E_DEVICE;
     st = cask_encode_device(ed->ctx, n, d_off, d_seq, d_ksz, d_vsz, d_keys, d_koff, d_vals, d_voff, ed->data.p);
-    if (st == CASK_OK) st = cask_copy(ed->ctx, host.get(), ed->data.p, total);
+    if (st == CASK_OK) st = ed->to_host(host.get(), ed->data.p, total);
     if (st != CASK_OK) return st;
   }
   // 3. each file's data bytes and hint file, files on threads

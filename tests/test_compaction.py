@@ -200,9 +200,12 @@ def _check_same(native_db, path, ref_db, ref):
 @pytest.mark.parametrize("seed,mfs", [(11, 64 << 10), (12, 1 << 20), (13, 4 << 10)])
 def test_engine_compact_files_matches_oracle(native, tmp_path, seed, mfs, threads, monkeypatch):
     """threaded: the open fold sharded by key hash and the liveness lookups on threads
-    (CASK_PAR_FOLD_MIN=0), against the same oracle."""
+    (CASK_PAR_FOLD_MIN=0), and every device-to-host copy staged through the pinned ring on threads
+    (CASK_STAGE_MIN=0), against the same oracle."""
     from cask_amd import CaskOptions
     monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if threads else str(1 << 62))
+    if threads:
+        monkeypatch.setenv("CASK_STAGE_MIN", "0")
     rng = random.Random(seed)
     path, ref = _both(tmp_path, _workload(rng, 6000, 700, vmax=500), mfs)
     rdb = R.replay(ref)

@@ -123,6 +123,8 @@ def test_golden_engine_open(native, case, tmp_path, monkeypatch, par_fold):
     fold on one thread and sharded by key hash over threads (CASK_PAR_FOLD_MIN=0 forces it)."""
     from cask_amd import CaskOptions, errors
     monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if par_fold else str(1 << 62))
+    if par_fold:  # and the hint bodies' copy to the host staged through the pinned ring
+        monkeypatch.setenv("CASK_STAGE_MIN", "0")
     exp = _expected(case)
     rep = exp["replay"]
     d = tmp_path / case
