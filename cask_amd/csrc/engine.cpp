@@ -29,6 +29,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include "../../include/cask_scan.h"
+#include "host_ring.h"
 #include "keydir_format.h"
 #include "xxh32.h"
 
@@ -358,40 +359,8 @@ bool find_data_files(const std::string& dir, std::vector<uint32_t>& out) {
   return true;
 }
 
-// Host threads for the fold and the compaction lookups: the CPUs this process may run on
-// (sched_getaffinity, so cgroup/affinity limits count), at most 16. CASK_HOST_THREADS (test and
-// tuning knob) sets the count, e.g. to force the threaded paths on a one-CPU machine.
-unsigned host_threads() {
-  if (const char* e = getenv("CASK_HOST_THREADS")) {
-    const int v = atoi(e);
-    if (v > 0) return (unsigned)std::min(v, 64);
-  }
-  unsigned k = 0;
-  cpu_set_t set;
-  CPU_ZERO(&set);
-  if (sched_getaffinity(0, sizeof(set), &set) == 0) k = (unsigned)CPU_COUNT(&set);
-  if (!k) k = std::thread::hardware_concurrency();
-  return std::max(1u, std::min(k, 16u));
-}
-
-// fn(t) for t in [0, nt): t = 1.. on threads of their own, t = 0 on the caller. A thread that cannot
-// be created (std::system_error) has its share run on the calling thread: no exception leaves the
-// C ABI, and the result does not depend on how many threads actually ran.
-template <class F>
-void parallel_for(unsigned nt, F fn) {
-  std::vector<std::thread> th;
-  std::vector<unsigned> here;
-  for (unsigned t = 1; t < nt; ++t) {
-    try {
-      th.emplace_back(fn, t);
-    } catch (...) {
-      here.push_back(t);
-    }
-  }
-  fn(0u);
-  for (unsigned t : here) fn(t);
-  for (auto& x : th) x.join();
-}
+using cask_host::host_threads;
+using cask_host::parallel_for;
 
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -464,11 +433,10 @@ struct EngineDev {
       return true;
     }
   } data, rows, hint;
-  static constexpr int kReaders = 16, kSlots = 2;
-  static constexpr size_t kSlotBytes = 32ull << 20;
-  void* pin[kReaders][kSlots] = {};
-  hipStream_t rs[kReaders] = {};
-  hipEvent_t ev[kReaders][kSlots] = {};
+  // pinned staging: reads of data files to the device, copies of results back to the host
+  cask_host::PinnedRing ring;
+  static constexpr int kReaders = cask_host::PinnedRing::kThreads;
+  static constexpr size_t kSlotBytes = cask_host::PinnedRing::kBytes;
   cask_rows r{};
 
   int prepare() {
@@ -478,17 +446,7 @@ struct EngineDev {
       ctx = cask_ctx_create(device, &st);
       if (!ctx) return st;
     }
-    for (int t = 0; t < kReaders; ++t) {
-      if (!rs[t] && hipStreamCreateWithFlags(&rs[t], hipStreamNonBlocking) != hipSuccess) return CASK_E_DEVICE;
-      for (int k = 0; k < kSlots; ++k) {
-        if (!pin[t][k] && hipHostMalloc(&pin[t][k], kSlotBytes, hipHostMallocDefault) != hipSuccess) {
-          pin[t][k] = nullptr;
-          return CASK_E_NOMEM;
-        }
-        if (!ev[t][k] && hipEventCreateWithFlags(&ev[t][k], hipEventDisableTiming) != hipSuccess) return CASK_E_DEVICE;
-      }
-    }
-    return CASK_OK;
+    return ring.init(device) ? CASK_OK : CASK_E_NOMEM;
   }
 
   // Reader thread t takes every kReaders-th 32-MiB piece of the files, alternating between its two
@@ -520,13 +478,13 @@ struct EngineDev {
           ok[pc.f] = 0;
           continue;
         }
-        if (hipEventSynchronize(ev[t][k]) != hipSuccess) {
+        if (hipEventSynchronize(ring.ev[t][k]) != hipSuccess) {
           status[t] = CASK_E_DEVICE;
           break;
         }
         uint64_t got = 0;
         while (got < pc.n) {
-          const ssize_t m = pread(fds[pc.f], (uint8_t*)pin[t][k] + got, pc.n - got, (off_t)(pc.off + got));
+          const ssize_t m = pread(fds[pc.f], (uint8_t*)ring.pin[t][k] + got, pc.n - got, (off_t)(pc.off + got));
           if (m < 0 && errno == EINTR) continue;
           if (m <= 0) break;
           got += (uint64_t)m;
@@ -535,15 +493,15 @@ struct EngineDev {
           ok[pc.f] = 0;
           continue;
         }
-        if (hipMemcpyAsync((uint8_t*)v[pc.f].data + pc.off, pin[t][k], pc.n, hipMemcpyHostToDevice, rs[t]) != hipSuccess ||
-            hipEventRecord(ev[t][k], rs[t]) != hipSuccess) {
+        if (hipMemcpyAsync((uint8_t*)v[pc.f].data + pc.off, ring.pin[t][k], pc.n, hipMemcpyHostToDevice, ring.rs[t]) != hipSuccess ||
+            hipEventRecord(ring.ev[t][k], ring.rs[t]) != hipSuccess) {
           status[t] = CASK_E_DEVICE;
           break;
         }
       }
       for (int fd : fds)
         if (fd >= 0) close(fd);
-      if (hipStreamSynchronize(rs[t]) != hipSuccess) status[t] = CASK_E_DEVICE;
+      if (hipStreamSynchronize(ring.rs[t]) != hipSuccess) status[t] = CASK_E_DEVICE;
     });
     for (int s : status)
       if (s != CASK_OK) return s;
@@ -559,43 +517,9 @@ struct EngineDev {
     if (n < (mv ? strtoull(mv, nullptr, 10) : (64ull << 20)) || !n) return cask_copy(ctx, dst, src, n);
     if (hipSetDevice(device) != hipSuccess || hipStreamSynchronize((hipStream_t)cask_ctx_stream(ctx)) != hipSuccess)
       return CASK_E_DEVICE;
-    const uint64_t np = (n + kSlotBytes - 1) / kSlotBytes;
-    const unsigned nt = std::max(1u, std::min<unsigned>((unsigned)kReaders, std::min<unsigned>(host_threads(), (unsigned)np)));
-    std::vector<int> status(nt, CASK_OK);
-    parallel_for(nt, [&](unsigned t) {
-      if (hipSetDevice(device) != hipSuccess) {
-        status[t] = CASK_E_DEVICE;
-        return;
-      }
-      uint64_t prev = ~0ull;
-      unsigned k = 0, pk = 0;
-      for (uint64_t j = t;; j += nt, k ^= 1) {
-        bool have = j < np;
-        if (have) {  // slot k is free: its last piece was copied out below, before this issue
-          const uint64_t off = j * kSlotBytes, m = std::min<uint64_t>(kSlotBytes, n - off);
-          if (hipMemcpyAsync(pin[t][k], src + off, m, hipMemcpyDeviceToHost, rs[t]) != hipSuccess ||
-              hipEventRecord(ev[t][k], rs[t]) != hipSuccess) {
-            status[t] = CASK_E_DEVICE;
-            have = false;
-          }
-        }
-        if (prev != ~0ull) {
-          if (hipEventSynchronize(ev[t][pk]) != hipSuccess) {
-            status[t] = CASK_E_DEVICE;
-            break;
-          }
-          const uint64_t off = prev * kSlotBytes;
-          memcpy(dst + off, pin[t][pk], std::min<uint64_t>(kSlotBytes, n - off));
-        }
-        if (!have) break;
-        prev = j;
-        pk = k;
-      }
-      if (hipStreamSynchronize(rs[t]) != hipSuccess) status[t] = CASK_E_DEVICE;
-    });
-    for (int st : status)
-      if (st != CASK_OK) return st;
-    return CASK_OK;
+    std::vector<cask_host::PinnedRing::Piece> ps;
+    cask_host::PinnedRing::split(dst, (uint8_t*)src, n, ps);
+    return ring.d2h(ps) ? CASK_OK : CASK_E_DEVICE;
   }
 
   // Device rows sized from a guess (average record >= 48 B), once more at the exact count if short.

@@ -7,11 +7,13 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <vector>
 
 #include "../../include/cask_scan.h"
+#include "host_ring.h"
 #include "scan_kernels.h"
 #include "xxh32.h"
 
@@ -108,6 +110,7 @@ struct cask_ctx {
   // host-scan staging
   DevBuf stage_data;
   DevBuf stage_rows;
+  std::unique_ptr<cask_host::PinnedRing> ring;  // cask_scan_host: pinned staging, made on first use
   int geo = -1;      // k_scan_chunks geometry: -1 picks one per call (CASK_SCAN_GEOMETRY forces one)
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
@@ -888,13 +891,28 @@ extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t
   if (!c->stage_rows.ensure(rcap * 23 + 5 * 256)) return CASK_E_NOMEM;
   std::vector<cask_file_view> dv(nfiles);
   uint8_t* d = c->stage_data.as<uint8_t>();
+  // Large inputs go through the pinned ring on host threads (CASK_STAGE_MIN: the smallest staged
+  // input, default 64 MiB; 0 stages everything — the tests' knob)
+  const char* mv = getenv("CASK_STAGE_MIN");
+  const bool staged = total && total >= (mv ? strtoull(mv, nullptr, 10) : (64ull << 20));
+  if (staged) {
+    if (!c->ring) c->ring.reset(new (std::nothrow) cask_host::PinnedRing());
+    if (!c->ring || !c->ring->init(c->device)) return CASK_E_NOMEM;
+    if (hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;  // stage_data is free
+  }
+  std::vector<cask_host::PinnedRing::Piece> ps;
   for (uint32_t i = 0; i < nfiles; ++i) {
     dv[i] = files[i];
     dv[i].flags = CASK_VIEW_DEVICE;
     dv[i].data = d + off[i];
-    if (files[i].len && hipMemcpyAsync(d + off[i], files[i].data, files[i].len, hipMemcpyHostToDevice, st) != hipSuccess)
+    if (staged) {
+      cask_host::PinnedRing::split((uint8_t*)files[i].data, d + off[i], files[i].len, ps);
+    } else if (files[i].len && hipMemcpyAsync(d + off[i], files[i].data, files[i].len, hipMemcpyHostToDevice, st) != hipSuccess) {
       return CASK_E_DEVICE;
+    }
   }
+  if (staged && !c->ring->h2d(ps)) return CASK_E_DEVICE;
+  (void)set_dev(c);  // (the calling thread's device, for the launches below)
   uint8_t* rb = c->stage_rows.as<uint8_t>();
   cask_rows dr{};
   dr.capacity = rcap;
@@ -910,6 +928,17 @@ extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t
   const uint64_t n = dr.count;
   bool ok = true;
   auto H = [&](hipError_t e) { ok = ok && (e == hipSuccess); };
+  if (n && staged) {  // the five row arrays through the ring too
+    H(hipStreamSynchronize(st));
+    std::vector<cask_host::PinnedRing::Piece> rp;
+    cask_host::PinnedRing::split((uint8_t*)rows->pos, (uint8_t*)dr.pos, n * 8, rp);
+    cask_host::PinnedRing::split((uint8_t*)rows->seq, (uint8_t*)dr.seq, n * 8, rp);
+    cask_host::PinnedRing::split((uint8_t*)rows->vsz, (uint8_t*)dr.vsz, n * 4, rp);
+    cask_host::PinnedRing::split((uint8_t*)rows->ksz, (uint8_t*)dr.ksz, n * 2, rp);
+    cask_host::PinnedRing::split(rows->status, dr.status, n, rp);
+    if (ok && !c->ring->d2h(rp)) ok = false;
+    return ok ? CASK_OK : CASK_E_DEVICE;
+  }
   if (n) {
     H(hipMemcpyAsync(rows->pos, dr.pos, n * 8, hipMemcpyDeviceToHost, st));
     H(hipMemcpyAsync(rows->seq, dr.seq, n * 8, hipMemcpyDeviceToHost, st));

@@ -25,11 +25,14 @@ def scan_mode(request, monkeypatch):
     """Every test here runs three times: the mode the library picks (k_scan_chunks for these mostly
     short records — with the short 1,008-B halo when the file heads hold short records — and the
     walk for the long-record cases), the walk mode forced (k_walk_runs), and the chunk scan forced
-    with the wide 4,080-B halo."""
+    with the wide 4,080-B halo (there host-resident inputs and rows also go through the pinned
+    staging ring, CASK_STAGE_MIN=0)."""
     if request.param == "auto":
         monkeypatch.delenv("CASK_SCAN_MODE", raising=False)
     else:
         monkeypatch.setenv("CASK_SCAN_MODE", request.param)
+    if request.param == "wide":  # host-resident scans staged through the pinned ring on threads
+        monkeypatch.setenv("CASK_STAGE_MIN", "0")
     return request.param
 
 
