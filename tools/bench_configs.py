@@ -141,14 +141,9 @@ def main():
     ap.add_argument("--files", type=int, default=4)
     ap.add_argument("--out", default="")
     ap.add_argument("--dir", default=None, help="parent directory of the compaction database")
-    ap.add_argument("--lib", default=os.environ.get("BENCH_LIB", ""),
-                    help="A/B only: another build of libcask_scan.so (env BENCH_LIB)")
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
-    if args.lib:
-        import cask_amd
-        cask_amd._lib.use_library(args.lib)
     from cask_amd import ScanContext
     ctx = ScanContext(0)
     results = []
