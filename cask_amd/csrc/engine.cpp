@@ -78,35 +78,6 @@ inline void stats_remove(StatsMap& st, const StatsMap* base, uint32_t file_id, u
   it->second.dead_bytes += size;
 }
 
-// The stats side of Index::update into a StatsMap (`base` as above).
-struct MapStats {
-  StatsMap& st;
-  const StatsMap* base;
-  void add(uint32_t f) { stats_add(st, f); }
-  void remove(uint32_t f, uint64_t size) { stats_remove(st, base, f, size); }
-};
-
-// The same rules into a dense per-file-id delta (a threaded fold's table; the file ids of a database
-// are few and small): a row exists once added to, or once removed from when `base_has` has it.
-// Two vector loads per record instead of hash-map lookups.
-struct DenseStats {
-  std::vector<StatsEntry> v;
-  std::vector<uint8_t> has;
-  const std::vector<uint8_t>* base_has = nullptr;
-  void add(uint32_t f) {
-    v[f].entries += 1;
-    has[f] = 1;
-  }
-  void remove(uint32_t f, uint64_t size) {
-    if (!has[f]) {
-      if (!(*base_has)[f]) return;  // "Tried to reclaim non-existant entry": warn only
-      has[f] = 1;
-    }
-    v[f].dead_entries += 1;
-    v[f].dead_bytes += size;
-  }
-};
-
 // One table of HashMap<Vec<u8>, IndexEntry> (cask.rs:28-31). Open addressing; keys live in an
 // append-only arena (the reference copies every key: hint.key.to_vec(), cask.rs:68).
 class KeyDir {
@@ -184,9 +155,8 @@ class KeyDir {
   }
 
   // Index::update (cask.rs:60-90). vsz_raw is the hint's value_size field.
-  template <class S>
   void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq,
-              uint64_t h, S& st) {
+              uint64_t h, StatsMap& st, const StatsMap* base) {
     const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
     cask_index_entry ie{};
     ie.file_id = file_id;
@@ -198,22 +168,22 @@ class KeyDir {
     if (f >= 0) {  // Occupied
       Slot& s = slots[f];
       if (s.e.sequence <= seq) {
-        st.remove(s.e.file_id, s.e.entry_size);
+        stats_remove(st, base, s.e.file_id, s.e.entry_size);
         if (deleted) {
           s.state = 2;
           --live;
         } else {
-          st.add(file_id);
+          stats_add(st, file_id);
           s.e = ie;
         }
       } else {
-        st.add(file_id);
-        st.remove(file_id, ie.entry_size);
+        stats_add(st, file_id);
+        stats_remove(st, base, file_id, ie.entry_size);
       }
       return;
     }
     if (deleted) return;  // Vacant + tombstone: nothing
-    st.add(file_id);
+    stats_add(st, file_id);
     insert_at((uint64_t)(-f - 1), key, ksz, h, ie);
   }
 
@@ -255,8 +225,7 @@ class Index {
   }
   void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
     const uint64_t h = hash_key(key, ksz);
-    MapStats ms{stats, nullptr};
-    sub[sub_of(h)].update(key, ksz, file_id, pos, vsz_raw, seq, h, ms);
+    sub[sub_of(h)].update(key, ksz, file_id, pos, vsz_raw, seq, h, stats, nullptr);
   }
   void update_kd(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
     const uint64_t h = hash_key(key, ksz);
@@ -636,40 +605,19 @@ void parallel_fold(FoldRec* recs, uint64_t n, Index& out) {
   constexpr unsigned S = Index::kSub;
   // 1. hashes, and per (range, table) lists of record indices, ranges in replay order
   std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(S));
-  std::vector<uint32_t> tmax(nt, 0);  // each range's largest file id
   parallel_for(nt, [&](unsigned t) {
     const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
     for (auto& l : lists[t]) l.reserve((hi - lo) / S + 16);
-    uint32_t mf = 0;
     for (uint64_t i = lo; i < hi; ++i) {
       FoldRec& r = recs[i];
       r.hash = hash_key(r.key, r.ksz);
-      mf = std::max(mf, r.file_id);
       lists[t][Index::sub_of(r.hash)].push_back((uint32_t)(i - lo));
     }
-    tmax[t] = mf;
   });
-  // 2. each table folds its keys in replay order, stats into its own delta (dense by file id when
-  // the ids are small, else a map)
-  uint32_t max_fid = *std::max_element(tmax.begin(), tmax.end());
-  for (const auto& kv : out.stats) max_fid = std::max(max_fid, kv.first);
-  const bool dense = max_fid < (1u << 20);
-  std::vector<uint8_t> base_has;
-  if (dense) {
-    base_has.assign((size_t)max_fid + 1, 0);
-    for (const auto& kv : out.stats) base_has[kv.first] = 1;
-  }
+  // 2. each table folds its keys in replay order, stats into its own delta map
   std::vector<StatsMap> delta(S);
-  std::vector<DenseStats> ddelta(dense ? S : 0);
   parallel_for(nt, [&](unsigned t) {
     for (unsigned q = t; q < S; q += nt) {
-      DenseStats* ds = dense ? &ddelta[q] : nullptr;
-      if (ds) {
-        ds->v.assign((size_t)max_fid + 1, StatsEntry{});
-        ds->has.assign((size_t)max_fid + 1, 0);
-        ds->base_has = &base_has;
-      }
-      MapStats ms{delta[q], &out.stats};
       KeyDir& kd = out.sub[q];
       uint64_t cnt = 0;
       for (unsigned g = 0; g < nt; ++g) cnt += lists[g][q].size();
@@ -688,15 +636,8 @@ void parallel_fold(FoldRec* recs, uint64_t n, Index& out) {
           }
           if (j + 4 < m) kd.prefetch_key(recs[lo + L[j + 4]].hash);
           const FoldRec& r = recs[lo + L[j]];
-          if (ds) kd.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, *ds);
-          else kd.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, ms);
+          kd.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, delta[q], &out.stats);
         }
-      }
-      if (ds) {  // the table's rows, as the map form would hold them
-        for (uint32_t f = 0; f <= max_fid; ++f)
-          if (ds->has[f]) delta[q][f] = ds->v[f];
-        ds->v = std::vector<StatsEntry>();
-        ds->has = std::vector<uint8_t>();
       }
     }
   });
