@@ -491,79 +491,93 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   __syncthreads();
   if (tid == 0 && s_long) a.ctr->long_pending = 1u;  // every writer stores the same value
   if (!tile_rows) return;
-  const uint64_t cap = a.row_cap;
-  const uint64_t g0 = tile_lo >> 2, g1 = (tile_lo + tile_rows + 3) >> 2;
   const uint32_t nch = (uint32_t)((a.total_chunks - tile * TC) < TC ? (a.total_chunks - tile * TC) : TC);
   const float per_row = (float)nch / (float)tile_rows;
-  for (uint64_t grp = g0 + tid; grp < g1; grp += TC) {
-    const uint64_t d0 = grp << 2;
-    // chunk of the group's first row in the tile: last j with s_base[j] <= rel
-    const uint64_t rel0 = d0 > tile_lo ? d0 - tile_lo : 0;
-    // the last chunk j with s_base[j] <= rel0: guessed from the tile's mean rows per chunk, then
-    // stepped (one or two LDS reads for tiles of similar chunks, not a binary search's eight)
-    uint32_t j = (uint32_t)((float)rel0 * per_row);  // (only a guess: corrected below)
-    j = j < nch ? j : nch - 1;
-    while (j > 0 && s_base[j] > rel0) --j;
-    while (j + 1 < nch && s_base[j + 1] <= rel0) ++j;
-    uint64_t P4[4], S4[4];
-    uint32_t V4[4], K4[4], T4[4];
-    bool inr[4];
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-      const uint64_t d = d0 + q;
-      inr[q] = d >= tile_lo && d < tile_lo + tile_rows;
-      P4[q] = 0; S4[q] = 0; V4[q] = 0; K4[q] = 0; T4[q] = 0;
-      if (!inr[q]) continue;
-      const uint32_t rel = (uint32_t)(d - tile_lo);
-      while (j + 1 < nch && s_base[j + 1] <= rel) ++j;
-      // skip chunks with no rows: s_base[j + 1] == s_base[j]
-      const uint32_t r = rel - s_base[j];
-      const uint64_t cc0 = s_c0[j];
-      if (s_reg[j]) {
-        const u32x4 w = s_desc[j];
-        const uint32_t ksz = w.w & 0xFFFFu;
-        const uint64_t rl = 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
-        P4[q] = cc0 + ((w.w >> 16) & 0x7FFFu) + (uint64_t)r * rl;
-        S4[q] = (((uint64_t)w.y << 32) | w.x) + r;
-        V4[q] = w.z;
-        K4[q] = ksz;
-        T4[q] = kRowOk;
-      } else {
-        const u32x4 w = *(const u32x4*)(a.slots + ((tile * TC + j) * (uint64_t)a.slot_cap + r) * 4);
-        const uint32_t ksz = w.w & 0xFFFFu;
-        const uint64_t p = cc0 + ((w.w >> 16) & 0x7FFFu);
-        const uint64_t hb = a.hint ? 22ull : 18ull;  // header bytes (a hint: data.rs:242-256)
-        const uint64_t end = p + hb + ksz + ((a.hint || w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
-        const uint64_t fl = s_len[j];
-        P4[q] = p;
-        S4[q] = ((uint64_t)w.y << 32) | w.x;
-        V4[q] = w.z;
-        K4[q] = ksz;
-        T4[q] = (p + hb > fl || end > fl) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
-      }
-    }
-    if (a.vec_ok && inr[0] && inr[3] && d0 + 3 < cap) {
-      typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-      const uint64_t kw = (uint64_t)(K4[0] & 0xFFFFu) | ((uint64_t)(K4[1] & 0xFFFFu) << 16) |
-                          ((uint64_t)(K4[2] & 0xFFFFu) << 32) | ((uint64_t)(K4[3] & 0xFFFFu) << 48);
-      const uint32_t tw = T4[0] | (T4[1] << 8) | (T4[2] << 16) | (T4[3] << 24);
-      *(u64x2*)(a.pos + d0) = u64x2{P4[0], P4[1]};
-      *(u64x2*)(a.pos + d0 + 2) = u64x2{P4[2], P4[3]};
-      *(u64x2*)(a.seq + d0) = u64x2{S4[0], S4[1]};
-      *(u64x2*)(a.seq + d0 + 2) = u64x2{S4[2], S4[3]};
-      *(u32x4*)(a.vsz + d0) = u32x4{V4[0], V4[1], V4[2], V4[3]};
-      *(uint64_t*)(a.ksz + d0) = kw;
-      *(uint32_t*)(a.status + d0) = tw;
+  const uint64_t hb = a.hint ? 22ull : 18ull;  // header bytes (a hint: data.rs:242-256)
+  // row d of the tile (tile_lo <= d < tile_lo + tile_rows); j: its chunk, advanced from the last one
+  auto row_at = [&](uint64_t d, uint32_t& j, uint64_t& P, uint64_t& S, uint32_t& V, uint32_t& K, uint32_t& T) {
+    const uint32_t rel = (uint32_t)(d - tile_lo);
+    while (j + 1 < nch && s_base[j + 1] <= rel) ++j;  // (skips chunks with no rows)
+    const uint32_t r = rel - s_base[j];
+    const uint64_t cc0 = s_c0[j];
+    if (s_reg[j]) {
+      const u32x4 w = s_desc[j];
+      const uint32_t ksz = w.w & 0xFFFFu;
+      const uint64_t rl = 18ull + ksz + ((w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+      P = cc0 + ((w.w >> 16) & 0x7FFFu) + (uint64_t)r * rl;
+      S = (((uint64_t)w.y << 32) | w.x) + r;
+      V = w.z;
+      K = ksz;
+      T = kRowOk;
     } else {
+      const u32x4 w = *(const u32x4*)(a.slots + ((tile * TC + j) * (uint64_t)a.slot_cap + r) * 4);
+      const uint32_t ksz = w.w & 0xFFFFu;
+      const uint64_t p = cc0 + ((w.w >> 16) & 0x7FFFu);
+      const uint64_t end = p + hb + ksz + ((a.hint || w.z == 0xFFFFFFFFu) ? 0ull : (uint64_t)w.z);
+      const uint64_t fl = s_len[j];
+      P = p;
+      S = ((uint64_t)w.y << 32) | w.x;
+      V = w.z;
+      K = ksz;
+      T = (p + hb > fl || end > fl) ? kRowEof : (w.w & kSlotBad) ? kRowChecksum : kRowOk;
+    }
+  };
+  // Blocks of 256 rows (aligned to the row index), one per wave at a time; in each half of a block
+  // lane l writes rows 2l and 2l + 1, so every store instruction covers one contiguous stretch of its
+  // array (1 KiB of pos or seq, 512 B of vsz, 256 B of ksz, 128 B of status): whole lines from
+  // every instruction, not halves of them completed by the next one.
+  const uint64_t lo = tile_lo, hi = tile_lo + tile_rows;
+  for (uint64_t blk = (lo >> 8) + wave; blk < ((hi + 255) >> 8); blk += TC / 64) {
 #pragma unroll
-      for (uint32_t q = 0; q < 4; ++q) {
-        const uint64_t d = d0 + q;
-        if (!inr[q] || d >= cap) continue;
-        a.pos[d] = P4[q];
-        a.seq[d] = S4[q];
-        a.vsz[d] = V4[q];
-        a.ksz[d] = (uint16_t)K4[q];
-        a.status[d] = (uint8_t)T4[q];
+    for (uint32_t h = 0; h < 2; ++h) {
+      const uint64_t d0 = (blk << 8) + 128u * h + 2u * lane;
+      const bool in0 = d0 >= lo && d0 < hi, in1 = d0 + 1 >= lo && d0 + 1 < hi;
+      if (!in0 && !in1) continue;
+      const uint64_t dfirst = in0 ? d0 : d0 + 1;
+      // the last chunk j with s_base[j] <= the first row: guessed from the tile's mean rows per
+      // chunk, then stepped (one or two LDS reads for tiles of similar chunks)
+      const uint32_t rel0 = (uint32_t)(dfirst - lo);
+      uint32_t j = (uint32_t)((float)rel0 * per_row);  // (only a guess: corrected below)
+      j = j < nch ? j : nch - 1;
+      while (j > 0 && s_base[j] > rel0) --j;
+      uint64_t P0 = 0, S0 = 0, P1 = 0, S1 = 0;
+      uint32_t V0 = 0, K0 = 0, T0 = 0, V1 = 0, K1 = 0, T1 = 0;
+      if (in0) row_at(d0, j, P0, S0, V0, K0, T0);
+      if (in1) row_at(d0 + 1, j, P1, S1, V1, K1, T1);
+      if (a.vec_ok && in0 && in1 && d0 + 1 < a.row_cap) {
+        typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+        typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+#ifdef CASK_FNT
+        __builtin_nontemporal_store(u64x2{P0, P1}, (u64x2*)(a.pos + d0));
+        __builtin_nontemporal_store(u64x2{S0, S1}, (u64x2*)(a.seq + d0));
+#else
+        *(u64x2*)(a.pos + d0) = u64x2{P0, P1};
+        *(u64x2*)(a.seq + d0) = u64x2{S0, S1};
+#endif
+#if defined(CASK_FNT) && CASK_FNT == 2
+        __builtin_nontemporal_store(u32x2{V0, V1}, (u32x2*)(a.vsz + d0));
+        __builtin_nontemporal_store((K0 & 0xFFFFu) | (K1 << 16), (uint32_t*)(a.ksz + d0));
+        __builtin_nontemporal_store((uint16_t)(T0 | (T1 << 8)), (uint16_t*)(a.status + d0));
+#else
+        *(u32x2*)(a.vsz + d0) = u32x2{V0, V1};
+        *(uint32_t*)(a.ksz + d0) = (K0 & 0xFFFFu) | (K1 << 16);
+        *(uint16_t*)(a.status + d0) = (uint16_t)(T0 | (T1 << 8));
+#endif
+      } else {
+        if (in0 && d0 < a.row_cap) {
+          a.pos[d0] = P0;
+          a.seq[d0] = S0;
+          a.vsz[d0] = V0;
+          a.ksz[d0] = (uint16_t)K0;
+          a.status[d0] = (uint8_t)T0;
+        }
+        if (in1 && d0 + 1 < a.row_cap) {
+          a.pos[d0 + 1] = P1;
+          a.seq[d0 + 1] = S1;
+          a.vsz[d0 + 1] = V1;
+          a.ksz[d0 + 1] = (uint16_t)K1;
+          a.status[d0 + 1] = (uint8_t)T1;
+        }
       }
     }
   }
