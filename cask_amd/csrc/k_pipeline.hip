@@ -547,22 +547,14 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
       if (a.vec_ok && in0 && in1 && d0 + 1 < a.row_cap) {
         typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
         typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
-#ifdef CASK_FNT
+        // pos and seq (16 of the 23 bytes) bypass the caches (nontemporal): no dirty lines left in
+        // the Infinity Cache for the next call's scan to write back; the narrow arrays keep the
+        // default policy (nontemporal stores of 2-8 B per lane ran slower)
         __builtin_nontemporal_store(u64x2{P0, P1}, (u64x2*)(a.pos + d0));
         __builtin_nontemporal_store(u64x2{S0, S1}, (u64x2*)(a.seq + d0));
-#else
-        *(u64x2*)(a.pos + d0) = u64x2{P0, P1};
-        *(u64x2*)(a.seq + d0) = u64x2{S0, S1};
-#endif
-#if defined(CASK_FNT) && CASK_FNT == 2
-        __builtin_nontemporal_store(u32x2{V0, V1}, (u32x2*)(a.vsz + d0));
-        __builtin_nontemporal_store((K0 & 0xFFFFu) | (K1 << 16), (uint32_t*)(a.ksz + d0));
-        __builtin_nontemporal_store((uint16_t)(T0 | (T1 << 8)), (uint16_t*)(a.status + d0));
-#else
         *(u32x2*)(a.vsz + d0) = u32x2{V0, V1};
         *(uint32_t*)(a.ksz + d0) = (K0 & 0xFFFFu) | (K1 << 16);
         *(uint16_t*)(a.status + d0) = (uint16_t)(T0 | (T1 << 8));
-#endif
       } else {
         if (in0 && d0 < a.row_cap) {
           a.pos[d0] = P0;
