@@ -17,7 +17,7 @@ if [ -z "$SKIP_BENCH" ]; then
   TAILN=1 step bench_full 600 python bench.py
 fi
 export TMPDIR=/tmp
-B="$R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-e2e --no-segmented"
+B="$R/bench.py --steps ${PSTEPS:-50} --warmup ${PWARM:-10} --no-cpu-baseline --no-e2e --no-segmented"
 rm -rf "$R/gpurun_out/prof_$TAG"
 TAILN=1 step prof_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG/kt" -o kt --output-format csv -- python3 $B
 step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_$TAG/fetch" -o fetch --output-format csv -- python3 $B
