@@ -399,6 +399,8 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   }
   __syncthreads();
   const uint64_t tile = __builtin_amdgcn_readfirstlane(s_tile);
+  if (tile == 0 && a.call_zero)  // the other call block, for the next call (no copy before it)
+    for (uint32_t i = tid; i < a.call_zero_words; i += TC) a.call_zero[i] = 0;
   const uint64_t c = tile * TC + tid;
   const bool act = c < a.total_chunks;
   // the chunk's table entries, all loaded at once (the descriptor too: only regular chunks use it)

@@ -124,6 +124,14 @@ struct cask_ctx {
   int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
   int last_walk = 0;   // the last call's speculative pass was k_walk_runs
   int last_geo = -1;   // the last call's k_scan_chunks geometry (-1: walk mode)
+  // The file table and two call blocks stay on the device between calls: a call whose file table is
+  // the last one's, and whose call block k_finish zeroed during the last call, needs no copy to the
+  // device before its first kernel.
+  std::vector<FileDesc> fd_last;
+  const void* fb_last = nullptr;
+  size_t callb_last = 0;
+  int cb_cur = 0;               // the call block the last call used
+  bool cb_zero[2] = {false, false};
   uint64_t probe_sig = 0;  // files of the last k_probe, and its answer
   bool probe_walk = false;
   bool probe_short = false;  // chunk mode: the short-halo geometry (kGeoShortHalo)
@@ -288,7 +296,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   const size_t sum_bytes = align_up(sum_words * 8, 256);
   const size_t callb = align_up(call_bytes, 256);
   const uint64_t C = total_chunks + 1;
-  if (!c->filebuf.ensure(fd_bytes + callb + 3 * pf_bytes + sum_bytes)) return CASK_E_NOMEM;
+  bool fb_fresh = false;  // (a new allocation may reuse the old address: never resident)
+  if (!c->filebuf.ensure(fd_bytes + 2 * callb + 3 * pf_bytes + sum_bytes, &fb_fresh)) return CASK_E_NOMEM;
   if (!c->chunk.ensure(C * (4 * 8 + 4 + 4 + 16 + 8) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
   if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
   const size_t runs_bytes = align_up(16ull * (total_chunks + 1), 256), cerr_bytes = align_up(4ull * (total_chunks + 1), 256),
@@ -301,11 +310,22 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
-  uint8_t* callp = fbase + fd_bytes;
-  unsigned long long* d_ferr = (unsigned long long*)(fbase + fd_bytes + callb);
-  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + callb + pf_bytes);
-  uint64_t* d_ftot = (uint64_t*)(fbase + fd_bytes + callb + 2 * pf_bytes);
-  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + callb + 3 * pf_bytes);
+  // call block: the other one than last time if that one is known zero and the file table is the
+  // same (then nothing is copied to the device before the first kernel), else block 0 with a copy
+  const bool fd_same = !fb_fresh && c->fb_last == fbase && c->callb_last == callb && c->fd_last.size() == nfiles &&
+                       (nfiles == 0 || !memcmp(c->fd_last.data(), fd, sizeof(FileDesc) * nfiles));
+  const bool resident = fd_same && c->cb_zero[c->cb_cur ^ 1];
+  const int cbi = resident ? (c->cb_cur ^ 1) : 0;
+  c->cb_zero[0] = c->cb_zero[1] = false;  // (set again only when this call completes on the dense path)
+  c->fd_last.assign(fd, fd + nfiles);
+  c->fb_last = fbase;
+  c->callb_last = callb;
+  c->cb_cur = cbi;
+  uint8_t* callp = fbase + fd_bytes + cbi * callb;
+  unsigned long long* d_ferr = (unsigned long long*)(fbase + fd_bytes + 2 * callb);
+  uint64_t* d_fbad = (uint64_t*)(fbase + fd_bytes + 2 * callb + pf_bytes);
+  uint64_t* d_ftot = (uint64_t*)(fbase + fd_bytes + 2 * callb + 2 * pf_bytes);
+  uint64_t* d_sum = (uint64_t*)(fbase + fd_bytes + 2 * callb + 3 * pf_bytes);
 
   uint64_t* cb = c->chunk.as<uint64_t>();
   ScanArgs a{};
@@ -350,6 +370,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.runs = nullptr;
   a.nruns_list = 0;
   a.tstate = c->tstate.as<uint64_t>();
+  a.call_zero = (uint64_t*)(fbase + fd_bytes + (cbi ^ 1) * callb);  // k_finish clears the other block
+  a.call_zero_words = (uint32_t)(callb / 8);
   if (rows) {
     a.pos = rows->pos;
     a.seq = rows->seq;
@@ -437,7 +459,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
 
   c->last_error[0] = 0;
   (void)hipGetLastError();  // drop any stale error another library left on this thread
-  H(hipMemcpyAsync(d_files, fd, fd_bytes + call_bytes, hipMemcpyHostToDevice, st), "file table H2D");
+  if (!resident) H(hipMemcpyAsync(d_files, fd, fd_bytes + call_bytes, hipMemcpyHostToDevice, st), "file table H2D");
   // Walk mode (k_walk_runs: header chase, long bodies read once, by k_long) when the records at the
   // heads of the files average kWalkMean bytes or more: k_probe, once per set of files (the answer
   // is cached on the context; it decides speed only). CASK_SCAN_MODE=walk|chunk (test and tuning
@@ -620,6 +642,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
         file_row_offset[f] = fd[f].nchunks ? h_rowoff[f] : file_row_offset[f + 1];
     }
     rows->count = total;
+    c->cb_zero[cbi ^ 1] = true;  // k_finish has run (and cleared the other call block)
     if (total > rows->capacity) return CASK_E_CAPACITY;
     if (err) {
       memset(err, 0, sizeof(*err));
