@@ -202,7 +202,10 @@ def main():
     achieved = bytes_per_step / (k1_avg * 1e-3) / 1e9  # algorithmic GB/s of the dominant kernel
     traffic, traffic_src = load_traffic()
 
-    extra = {"pipeline_breakdown_ms": ctx.last_timings()}
+    extra = {"pipeline_breakdown_ms": ctx.last_timings(),
+             # SURVEY §8d's definition: device time from the first to the last kernel of a step
+             # (HIP events), per GPU; `value` above is the wall clock, host gap included
+             "device_gibps_per_gpu": bytes_per_step / (sum(pipe_ms) / len(pipe_ms) * 1e-3) / 2 ** 30}
     counters = ctx.last_counters()
     # segmented output (no dense compaction; every slot row written), same files, same clock
     if not args.no_segmented:
