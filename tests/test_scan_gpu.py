@@ -219,6 +219,35 @@ def test_short_halo_records_crossing_the_window(gpu_ctx):
         assert cnt["geometry"] == 3 and cnt["long_records"] > 0, cnt
 
 
+def test_repeated_calls_alternating_file_sets(gpu_ctx):
+    """The file table and the call blocks stay on the device between calls (a call over the same
+    files as the last one copies nothing before its first kernel; k_finish clears the next call's
+    block): calls alternating between a clean set, a set with a checksum error and a set that
+    takes the repair path, each set's device buffers reused, must each give the oracle's rows."""
+    import torch
+    rng = random.Random(17)
+    clean = [make_records(rng, 3000, lambda r: 16, lambda r: 256, seq0=1 + 3000 * i) for i in range(3)]
+    bad = bytearray(make_records(rng, 2500, lambda r: r.randrange(1, 20), lambda r: r.randrange(0, 900)))
+    bad[len(bad) // 2] ^= 0x40
+    inner = [R.entry_new(10_000 + i, rng.randbytes(8), rng.randbytes(rng.randrange(0, 40))).write_bytes()
+             for i in range(64)]
+    adv = b"".join(R.entry_new(i + 1, b"outer%d" % i, b"".join(rng.choice(inner) for _ in range(rng.randrange(1, 30))))
+                   .write_bytes() for i in range(2000))
+    sets = {"clean": clean, "bad": [clean[0], bytes(bad)], "adv": [adv, clean[1]]}
+    dev = {k: [(i + 1, torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()) for i, b in enumerate(v)]
+           for k, v in sets.items()}
+    want = {k: [O.scan(b) for b in v] for k, v in sets.items()}
+    for k in ["clean", "clean", "bad", "clean", "adv", "adv", "clean", "bad", "bad", "clean", "clean"]:
+        res = gpu_ctx.scan_device(dev[k])
+        assert res.count == sum(len(w) for w in want[k]), k
+        for i, w in enumerate(want[k]):
+            sl = res.file_rows(i)
+            assert np.array_equal(res.pos[sl].cpu().numpy().astype(np.uint64), w["pos"]), (k, i)
+            assert np.array_equal(res.seq[sl].cpu().numpy().astype(np.uint64), w["seq"]), (k, i)
+            assert np.array_equal(res.status[sl].cpu().numpy(), w["status"].astype(np.uint8)), (k, i)
+        assert (res.error is None) == (k != "bad"), k
+
+
 def test_uniform_82_device(gpu_ctx):
     rng = random.Random(2)
     check_against_oracle(gpu_ctx, [make_records(rng, 60000, lambda r: 16, lambda r: 48)], device=True)
