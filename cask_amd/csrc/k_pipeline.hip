@@ -393,8 +393,10 @@ __global__ __launch_bounds__(256) void k_finish(ScanArgs a) {
   __shared__ uint32_t s_reg[TC];          // regular flag
   __shared__ uint32_t s_long;             // the tile has a record for k_long_hash
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // tiles by index when the whole grid is resident at once (a grid's worth of claims on one
+  // counter queue for microseconds), else claimed in order from the counter
   if (tid == 0) {
-    s_tile = atomicAdd(&a.ctr->tile_next, 1u);
+    s_tile = a.fin_static ? blockIdx.x : atomicAdd(&a.ctr->tile_next, 1u);
     s_long = 0u;
   }
   __syncthreads();
@@ -858,7 +860,9 @@ void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream) {
 void launch_finish(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
   const uint64_t tiles = (a.total_chunks + kFinTile - 1) / kFinTile;
-  hipLaunchKernelGGL(k_finish, dim3((uint32_t)tiles), dim3(kFinTile), 0, S(stream), a);
+  ScanArgs af = a;
+  af.fin_static = tiles <= 4ull * (uint64_t)device_cus() ? 1u : 0u;  // 4 of its workgroups fit a CU
+  hipLaunchKernelGGL(k_finish, dim3((uint32_t)tiles), dim3(kFinTile), 0, S(stream), af);
 }
 void launch_err_dense(const ScanArgs& a, uint32_t fi, uint64_t row, uint32_t* out, void* stream) {
   hipLaunchKernelGGL(k_err_dense, dim3(1), dim3(64), 0, S(stream), a, fi, row, out);

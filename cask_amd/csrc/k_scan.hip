@@ -552,9 +552,11 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
   };
   uint32_t my_claim = 0;  // thread kMetaT: the run claimed for after the current one
   bool publish = false;   // thread kMetaT: my_claim still to be published in L.claimed
+  // The first two runs of every workgroup are fixed by its index (a grid's worth of claims on one
+  // counter at once queue for tens of microseconds); later ones come from the counter.
   if (threadIdx.x == G::kMetaT) {
-    L.found = atomicAdd(&a.ctr->run_next, 1u);
-    L.claimed = atomicAdd(&a.ctr->run_next, 1u);
+    L.found = blockIdx.x;
+    L.claimed = blockIdx.x + gridDim.x;
   }
   BAR();
   const uint64_t r0 = L.found;
@@ -612,7 +614,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
         next_end = tn;
       }
       if (threadIdx.x == G::kMetaT && rn < nruns) {
-        my_claim = atomicAdd(&a.ctr->run_next, 1u);  // published at the next chunk's top
+        my_claim = 2u * gridDim.x + atomicAdd(&a.ctr->run_next, 1u);  // published at the next chunk's top
         publish = true;
       }
     }

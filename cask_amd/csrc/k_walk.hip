@@ -443,8 +443,9 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
   // a repair pass walks the stretches in a.runs from their exact starts (spec[first]); otherwise
   // runs of R chunks, each from a speculative start
   const uint64_t nruns = a.runs ? a.nruns_list : a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
-  for (;;) {
-    const uint64_t r = a.runs ? wave_claim(&a.ctr->run_next) : a.run_lo + wave_claim(&a.ctr->walk_next[a.grp]);
+  // the first run of every wave is fixed by its index, later ones come from the counter
+  for (uint64_t k = blockIdx.x;; k = gridDim.x + (a.runs ? wave_claim(&a.ctr->run_next) : wave_claim(&a.ctr->walk_next[a.grp]))) {
+    const uint64_t r = a.runs ? k : a.run_lo + k;
     if (r >= nruns) break;
     uint64_t t = a.runs ? a.runs[2ull * r] : (uint64_t)r * R;
     const uint64_t tend = a.runs ? a.runs[2ull * r + 1] : ((t + R < a.total_chunks) ? t + R : a.total_chunks);
@@ -475,8 +476,8 @@ __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* 
   __shared__ SearchLds L;
   const uint64_t R = a.run;
   const uint64_t nruns = a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
-  for (;;) {
-    const uint64_t r = a.run_lo + wave_claim(&a.ctr->search_next[a.grp]);
+  for (uint64_t k = blockIdx.x;; k = gridDim.x + wave_claim(&a.ctr->search_next[a.grp])) {
+    const uint64_t r = a.run_lo + k;
     if (r >= nruns) break;
     const uint64_t t = (uint64_t)r * R;
     const uint32_t fi = find_file(files, a.nfiles, t);

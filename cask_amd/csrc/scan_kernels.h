@@ -138,6 +138,7 @@ struct ScanArgs {
   uint32_t vec_ok;             // dense arrays aligned for the 4-row vector stores of k_finish
   uint32_t hint;               // 1: the files are hint-file bodies (cask_parse_hints_device), not data files
   uint32_t call_zero_words;    // k_finish: words of call_zero to clear
+  uint32_t fin_static;         // k_finish: tile = blockIdx.x (the grid fits the GPU at once)
   uint64_t* call_zero;         // k_finish: the call block the next call uses (null: none)
   uint32_t walk_pre;           // 1: k_walk_search left each run's speculative start in tin[first chunk]
   uint32_t grp;                // walk mode: the group of runs a launch covers (its claim counters)
