@@ -34,13 +34,15 @@ def child(path, steps, files, zipf_gib):
     views = [(f.file_id, f.data) for f in fs]
     rows = ctx.alloc_rows(n + 16)
     nbytes = sum(f.data.numel() for f in fs)
+    seg = os.environ.get("AB_SEGMENTED") == "1"  # time the segmented output instead
+    call = (lambda: ctx.scan_device_segmented(views)) if seg else (lambda: ctx.scan_device(views, rows))
     for _ in range(3):
-        ctx.scan_device(views, rows)
+        call()
     torch.cuda.synchronize()
     k = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        ctx.scan_device(views, rows)
+        call()
         k.append(ctx.last_timings()["chunk_scan_ms"])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
