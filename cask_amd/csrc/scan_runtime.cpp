@@ -415,7 +415,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.regular_ok = rows ? 1u : 0u;
   a.respec = 1u;
   // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
-  a.big = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
+  static const uint32_t big_env = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
+  a.big = big_env;
   if (a.big < kMinBigRec) a.big = kMinBigRec;  // the long-record queue's smallest length class
   a.win = chunk + geometry_halo(geo);
   // the dense path: CASK_DENSE=0 (tuning knob) sends every call through the repair path's k_compact
