@@ -108,6 +108,7 @@ SIGNATURES = [
     ("cask_scan_host", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                  C.POINTER(ScanError)]),
     ("cask_last_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
+    ("cask_last_timings8", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),
     ("cask_last_counters", C.c_int, [C.c_void_p, c_u64p]),
     ("cask_last_walk", C.c_int, [C.c_void_p]),
     ("cask_last_geometry", C.c_int, [C.c_void_p]),

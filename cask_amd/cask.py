@@ -214,6 +214,28 @@ class Cask:
             out[raw[off[i]:off[i] + kl[i]]] = IndexEntry(e.file_id, e.entry_pos, e.entry_size, e.sequence)
         return out
 
+    def export_arrays(self):
+        """The whole keydir as numpy arrays, keys in bytewise order (for keydirs too large for a
+        dict): (key_bytes uint8, key_off u64, key_len u64, entries) with entries a structured array
+        of file_id, entry_pos, entry_size, sequence."""
+        import numpy as np
+        lib = L.lib()
+        n = len(self)
+        total = lib.cask_db_export(self._handle(), None, 0, None, None, None, n)
+        if total < 0:
+            raise_status(int(total))
+        kb = np.zeros(max(total, 1), np.uint8)
+        off = np.zeros(max(n, 1), np.uint64)
+        kl = np.zeros(max(n, 1), np.uint64)
+        ents = np.zeros(max(n, 1), np.dtype([("file_id", "<u4"), ("pad", "<u4"), ("entry_pos", "<u8"),
+                                             ("entry_size", "<u8"), ("sequence", "<u8")]))
+        u64p = C.POINTER(C.c_uint64)
+        r = lib.cask_db_export(self._handle(), kb.ctypes.data, total, off.ctypes.data_as(u64p), kl.ctypes.data_as(u64p),
+                               ents.ctypes.data_as(C.POINTER(L.IndexEntry)), n)
+        if r < 0:
+            raise_status(int(r))
+        return kb[:total], off[:n], kl[:n], ents[:n]
+
     def keys(self) -> list[bytes]:
         """Cask::keys (cask.rs:668-671), sorted."""
         return list(self.index().keys())

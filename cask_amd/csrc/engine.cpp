@@ -1216,9 +1216,10 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
     return outs.size() - 1;
   };
   auto abort_with = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
-    for (OutFile& o : outs) {
+    for (OutFile& o : outs) {  // every file this call created, with any hint file already written
       if (o.fd >= 0) close(o.fd);
       (void)unlink(data_path(path, o.fid).c_str());
+      (void)unlink(hint_path(path, o.fid).c_str());
     }
     db->file_seq -= (uint32_t)outs.size();
     set_err(err, st, fid, pos, e, f);
@@ -1307,21 +1308,34 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
       // placement and the batch's bytes, gathered on the device in write order
       auto tg = std::chrono::steady_clock::now();
       std::vector<uint64_t> dst(n);
-      std::vector<uint32_t> len32(n);
       std::vector<size_t> oi(n);
+      // the gather's pieces: a record longer than kPiece (value sizes reach 0xFFFFFFFE B, data.rs:13)
+      // goes as several consecutive pieces of at most kPiece bytes
+      constexpr uint64_t kPiece = 1ull << 31;
+      std::vector<uint32_t> gsrc, glen;
+      std::vector<uint64_t> gpos, gdst;
+      gsrc.reserve(n);
+      glen.reserve(n);
+      gpos.reserve(n);
+      gdst.reserve(n);
       uint64_t total = 0;
       for (uint64_t k = 0; k < n; ++k) {
         oi[k] = place(len[k], true);
         dst[k] = total;
-        len32[k] = (uint32_t)len[k];
+        for (uint64_t o = 0; o < len[k]; o += kPiece) {
+          gsrc.push_back(src[k]);
+          gpos.push_back(pos[k] + o);
+          gdst.push_back(total + o);
+          glen.push_back((uint32_t)std::min<uint64_t>(kPiece, len[k] - o));
+        }
         total += len[k];
       }
       std::unique_ptr<uint8_t[]> host(new (std::nothrow) uint8_t[std::max<uint64_t>(total, 1)]);
       if (!host) return abort_with(CASK_E_NOMEM);
       if (total) {
         if (!ed->hint.ensure(total + 256)) return abort_with(CASK_E_NOMEM);
-        st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), dst.data(),
-                                len32.data(), n, ed->hint.p);
+        st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), gsrc.data(), gpos.data(), gdst.data(),
+                                glen.data(), (uint64_t)glen.size(), ed->hint.p);
         if (st == CASK_OK) st = ed->to_host(host.get(), ed->hint.p, total);
         if (st != CASK_OK) return abort_with(st);
       }
@@ -1506,11 +1520,27 @@ cask_db* cask_keydir_new(void) {
   return db;
 }
 
+static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes);
+
 int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
+  try {  // the block comes from a peer rank: no exception crosses the C ABI
+    return keydir_merge_impl(db, blk, bytes);
+  } catch (const std::bad_alloc&) {
+    return CASK_E_NOMEM;
+  } catch (...) {
+    return CASK_E_INVALID_ARG;
+  }
+}
+
+static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   using namespace cask_kd;
   if (!db || !db->merging || (bytes && !blk) || bytes < sizeof(ShardHeader)) return CASK_E_INVALID_ARG;
   ShardHeader hd;
   memcpy(&hd, blk, sizeof(hd));
+  // counts bounded by the block's size before any offset is derived from them (no wrap-around)
+  if (hd.nrec > (bytes - sizeof(ShardHeader)) / sizeof(ShardRec) ||
+      (uint64_t)hd.nfiles > (bytes - sizeof(ShardHeader)) / sizeof(ShardFileStat))
+    return CASK_E_INVALID_ARG;
   const uint64_t rec_at = sizeof(ShardHeader), fst_at = rec_at + sizeof(ShardRec) * hd.nrec,
                  key_at = fst_at + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
   if (hd.magic != kMagic || hd.version != kVersion || hd.bytes > bytes || key_at + hd.key_bytes > hd.bytes)
@@ -1925,6 +1955,11 @@ int64_t cask_log_write(const char* dir_c, uint32_t first_file_id, uint64_t max_f
           hb.insert(hb.end(), host.get() + goff[r] + 18, host.get() + goff[r] + 18 + ksz[r]);
         }
         ok = write_file_raw2(hint_path(dir, fid), hb.data(), hb.size(), cask_xxh::xxh32(hb.data(), hb.size(), 0));
+      } else if (ok) {
+        // no hints: a hint file left from an earlier file of this id would describe other bytes, and
+        // the next open would trust it (log.rs:121-135); the reference's HintWriter::new always
+        // truncates it (log.rs:373-380, util.rs:45-49)
+        if (unlink(hint_path(dir, fid).c_str()) != 0 && errno != ENOENT) ok = false;
       }
       fok[f] = ok;
     }

@@ -327,7 +327,8 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
              const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes, const uint64_t* key_at) {
   KdScratch& S_ = *(KdScratch*)scratch;
   hipStream_t st = S(stream);
-  if (n >= (1ull << 32)) return -10;  // row indices are 32-bit per shard
+  // row indices are 32-bit per shard and every hipCUB call below takes an int count
+  if (n > (uint64_t)INT32_MAX) return -12;  // CASK_E_CAPACITY: split the shard
   // temp storage sizes of the hipCUB calls
   size_t t_sort = 0, t_sel = 0, t_scan = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint32_t*)nullptr,
@@ -523,6 +524,7 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream) {
   KdScratch& S_ = *(KdScratch*)scratch;
   hipStream_t st = S(stream);
+  if (n > (uint64_t)INT32_MAX) return -12;  // CASK_E_CAPACITY: the scan takes an int count (callers batch files)
   size_t t_scan = 0;
   if (hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, (uint64_t*)nullptr, (uint64_t*)nullptr,
                                        (int)std::max<uint64_t>(n, 1), st) != hipSuccess)

@@ -229,6 +229,157 @@ __device__ __forceinline__ uint64_t walk_search(SearchLds& L, const uint8_t* dat
   return target;
 }
 
+// The same search with a cheaper pass A (k_walk_search's default): a record's value_size field ends
+// 17 bytes into its header, and a record that ends within the search horizon (or a tombstone) has a
+// last value_size byte of 0x00 (0xFF) — only offsets whose byte +17 is 0x00 or 0xFF are decoded,
+// found four at a time per aligned dword (SWAR zero-byte test), in 8-KiB windows. The short
+// candidates of a window are hashed 16 at a time in offset order (lane l scans the window's dwords
+// [32l, 32l + 32): lane order is offset order) until one verifies; long ones are listed for the hop
+// back. Same answer as walk_search for every input: the filter only skips offsets whose record
+// could neither be short nor end within the horizon.
+constexpr uint32_t kSwNL = 8, kSwWin = kSwNL * 1024, kSwUse = kSwWin - 16, kSwStep = kSwUse - 18;
+constexpr uint32_t kSwDw = 32;  // dwords of candidate bytes per lane per window (64 x 32 x 4 >= kSwStep)
+static_assert(64 * kSwDw * 4 >= kSwStep, "every candidate byte of a window is scanned");
+struct SearchLdsSw {
+  uint32_t win[kSwWin / 4 + 16];
+  uint32_t cand[16];
+  uint32_t nl;
+  uint32_t pad[3];
+  uint64_t lx[kLongList], le[kLongList];
+};
+__device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {  // 0x80 in each byte of w that is 0
+  return ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;
+}
+__device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t* data, uint64_t len, uint64_t b0,
+                                                   uint64_t b1) {
+  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
+  const uint64_t lim = (b1 + kSearchPast < len) ? b1 + kSearchPast : len;
+  uint64_t kA = kNone;
+  if (lane == 0) L.nl = 0;
+  bool over = false;
+  for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kSwStep) {
+    const uint32_t x0 = walk_stage<kSwNL>(L.win, data, len, wb);  // (its barriers also publish L.nl)
+    const uint64_t wend = (wb + kSwUse < len) ? wb + kSwUse : len;
+    // offsets o in [0, ostop) of this window are candidates (their 18-B header is staged)
+    const uint64_t oa = (lim - wb < kSwStep) ? lim - wb : kSwStep;
+    const uint64_t ob = (len - wb >= 18) ? len - wb - 17 : 0;
+    const uint32_t ostop = (uint32_t)(oa < ob ? oa : ob);
+    // phase 1: candidate bytes (+17) of lane's dwords; short candidates into a bit mask (bit 4k+b
+    // of sm[k>>3]), long ones appended to the list
+    // lane l: the 16-B aligned dwords [d0, d0 + 32) read as 8 ds_read_b128 (a lane-contiguous
+    // layout keeps lane order = offset order; 32 x ds_read_b32 at a 128-B lane stride hit one bank)
+    const uint32_t d0 = (((x0 + 17) >> 2) & ~3u) + kSwDw * lane;
+    uint32_t sm[kSwDw / 8] = {0u, 0u, 0u, 0u};
+    u32x4 wv[kSwDw / 4];
+#pragma unroll
+    for (uint32_t j = 0; j < kSwDw / 4; ++j) wv[j] = ((const u32x4*)L.win)[d0 / 4 + j];
+#pragma unroll
+    for (uint32_t k = 0; k < kSwDw; ++k) {
+      const uint32_t w = wv[k >> 2][k & 3];
+      uint32_t m = zero_bytes(w) | zero_bytes(~w);
+      while (m) {
+        const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
+        m &= m - 1;
+        const int64_t o = (int64_t)(4 * (d0 + k) + b) - 17 - (int64_t)x0;
+        if (o < 0 || o >= (int64_t)ostop) continue;
+        const uint64_t rl = lds_reclen(L.win, x0 + (uint32_t)o);
+        const uint64_t x = wb + (uint64_t)o;
+        if (rl <= kSearchShort) {
+          if (x + rl <= len) sm[k >> 3] |= 1u << (4 * (k & 7) + b);
+        } else if (x + rl <= lim) {
+          const uint32_t r = atomicAdd(&L.nl, 1u);
+          if (r < kLongList) {
+            L.lx[r] = x;
+            L.le[r] = x + rl;
+          } else {
+            over = true;
+          }
+        }
+      }
+    }
+    // phase 2: the short candidates in offset order, 16 per round (one per quad)
+    for (;;) {
+      const uint32_t mine = (uint32_t)__builtin_popcount(sm[0]) + __builtin_popcount(sm[1]) + __builtin_popcount(sm[2]) +
+                            __builtin_popcount(sm[3]);
+      // exclusive prefix of the counts over lanes (lane order is offset order)
+      uint32_t pre = mine;
+      for (int s = 1; s < 64; s <<= 1) {
+        const uint32_t u = __shfl_up(pre, s, 64);
+        if ((int)lane >= s) pre += u;
+      }
+      const uint32_t total = __shfl(pre, 63, 64);
+      pre -= mine;
+      if (!total) break;
+      // this lane's candidates with global rank < 16 go to cand[rank]
+      uint32_t r = pre;
+#pragma unroll
+      for (uint32_t g = 0; g < kSwDw / 8; ++g) {
+        while (sm[g] && r < 16) {
+          const uint32_t bit = (uint32_t)__builtin_ctz(sm[g]);
+          sm[g] &= sm[g] - 1;
+          const uint32_t k = 8 * g + (bit >> 2), b = bit & 3;
+          L.cand[r++] = 4 * (d0 + k) + b - 17 - x0;
+        }
+      }
+      __syncthreads();
+      const uint32_t nc = total < 16 ? total : 16u;
+      bool ok = false;
+      if (q < nc) {
+        const uint32_t ko = L.cand[q];
+        const uint64_t xc = wb + ko;
+        const uint64_t rlc = lds_reclen(L.win, x0 + ko);
+        const uint32_t st = lds_u32(L.win, x0 + ko);
+        const uint32_t h = (xc + rlc <= wend) ? quad_xxh32(L.win, x0 + ko + 4, (uint32_t)rlc - 4, qa)
+                                               : quad_gbl_xxh32<2>(data + xc + 4, rlc - 4, qa);
+        ok = qa == 0 && h == st;
+      }
+      const unsigned long long mo = __ballot(ok);
+      if (mo) kA = wb + L.cand[__builtin_ctzll(mo) >> 2];  // quads are in offset order
+      __syncthreads();
+      if (mo) break;
+    }
+  }
+  over = __any(over) || L.nl > kLongList;
+  if (kA == kNone) return kNone;
+  // hop back over long records ending exactly at the current target (lowest such offset)
+  uint64_t target = kA;
+  const uint32_t nlist = L.nl < kLongList ? L.nl : kLongList;
+  for (int it = 0; it < 64; ++it) {
+    uint64_t found = kNone;
+    if (!over) {
+      for (uint32_t i0 = 0; i0 < nlist; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        uint64_t x = (i < nlist && L.lx[i] < target && L.le[i] == target) ? L.lx[i] : kNone;
+        for (int s = 32; s; s >>= 1) {
+          const uint64_t y = __shfl_xor(x, s, 64);
+          x = y < x ? y : x;
+        }
+        found = x < found ? x : found;
+      }
+    } else {
+      for (uint64_t wb = b0; wb < target && found == kNone; wb += kStepB) {
+        const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
+        for (uint32_t k0 = 0; k0 < kStepB; k0 += 64) {
+          const uint64_t x = wb + k0 + lane;
+          bool hit = false;
+          if (k0 + lane < kStepB && x < target && x + 18 <= len) {
+            const uint64_t rl = lds_reclen(L.win, x0 + k0 + lane);
+            hit = rl > kSearchShort && x + rl == target;
+          }
+          const unsigned long long m = __ballot(hit);
+          if (m) {
+            found = wb + k0 + (uint64_t)__builtin_ctzll(m);
+            break;
+          }
+        }
+      }
+    }
+    if (found == kNone) break;
+    target = found;
+  }
+  return target;
+}
+
 // Hint-file bodies (cask_parse_hints_device): records `seq u64 | ksz u16 | vsz u32 | entry_pos u64 |
 // key` (Hint::write_bytes, data.rs:242-256), 22 + ksz bytes, no checksum of their own. A run's first
 // start is the lowest offset >= b0 whose record, and the two after it, have entry positions that
@@ -473,7 +624,7 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
 // starts a file needs none, and only the first segment of a run can. Kept out of k_walk_runs: the
 // search's registers would lower how many chasing waves fit on a CU.
 __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
-  __shared__ SearchLds L;
+  __shared__ SearchLdsSw L;
   const uint64_t R = a.run;
   const uint64_t nruns = a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
   for (uint64_t k = blockIdx.x;; k = gridDim.x + wave_claim(&a.ctr->search_next[a.grp])) {
@@ -487,7 +638,7 @@ __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* 
     const uint64_t se = fend < tend ? fend : tend;
     const uint64_t b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint64_t b1 = ((se - fd.first_chunk) * (uint64_t)a.chunk < fd.len) ? (se - fd.first_chunk) * (uint64_t)a.chunk : fd.len;
-    const uint64_t s0 = b0 == 0 ? 0 : walk_search(L, fd.data, fd.len, b0, b1);
+    const uint64_t s0 = b0 == 0 ? 0 : walk_search_sw(L, fd.data, fd.len, b0, b1);
     if (threadIdx.x == 0) a.tin[t] = s0;
   }
 }

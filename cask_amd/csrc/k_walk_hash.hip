@@ -1,0 +1,744 @@
+// k_walk_hash — walk mode in one pass, gfx950: a quad of lanes per run of chunks chases the record
+// chain (Entries::next, log.rs:403-429: each record starts where the previous one ends) and hashes
+// every record it visits straight from HBM (Entry::from_read's check, data.rs:185-198), so every
+// log byte is read once, by the quad that owns its record.
+//
+// Why a quad per run: XXH32's four stripe accumulators are the only parallelism inside a record
+// (one lane each); a log of long records needs thousands of records in flight at once to keep HBM
+// busy, and a run of chunks walked by one quad is one such stream. The previous walk mode chased
+// headers with a whole wave per run and left every record longer than its 1-KiB window to a second
+// kernel that read those bytes again (k_long_hash, behind a queue by length class).
+//
+// Per quad, one round of up to D 64-B blocks of its current record is in flight while it mixes the
+// round before: the loop waits for the round issued last iteration, decides the next round (the rest
+// of the record, or the next record, whose header was loaded one record ahead), issues it, then mixes.
+// A short record costs one iteration; the header of the record after it is always loaded with the
+// record's first round. The loads of an iteration are the same instructions for every quad (idle or
+// finished quads load one safe word), so the compiler's counted waits hold.
+//
+// Output: the chunk table and slot rows of k_scan_chunks / k_walk_runs (spec, exit, count, cerr,
+// long_r = none, slot rows with the checksum verdict): k_finish validates the speculated run starts
+// (k_walk_search, spec[c] == T[c]) and writes the dense rows, and the repair path runs unchanged.
+#include "device_util.h"
+
+#include <stdlib.h>
+
+namespace cask_dev {
+
+namespace {
+
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint64_t g_u64;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
+
+// The piece of a run inside one file: chunks [t0, t0 + nch) of the file at `data`.
+struct WSeg {
+  const uint8_t* data;
+  uint64_t len;
+  int64_t sl;      // the highest file offset a 16-B load may start at: such a load stays within the
+                   // 16-B granules that hold the file's bytes (sl < 0 for a file inside one granule)
+  uint64_t b0, b1; // the segment's file bytes
+  uint64_t t0;     // global index of its first chunk
+  uint32_t nch;
+};
+
+__device__ __forceinline__ u32x4 ld16(const WSeg& S, uint64_t o) {
+  const int64_t so = (int64_t)o < S.sl ? (int64_t)o : S.sl;
+  return gld16g((const g_u8*)(S.data + so));
+}
+__device__ __forceinline__ uint32_t ld4(const WSeg& S, uint64_t o) {
+  const int64_t lim = S.sl + 12;
+  const int64_t so = (int64_t)o < lim ? (int64_t)o : lim;
+  return gld4g((const g_u8*)(S.data + so));
+}
+
+// lane 0 of each quad to the whole quad (quad_perm [0,0,0,0])
+__device__ __forceinline__ uint32_t qb0(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t qb0_64(uint64_t v) {
+  return (uint64_t)qb0((uint32_t)v) | ((uint64_t)qb0((uint32_t)(v >> 32)) << 32);
+}
+
+// The 16 bytes of v from byte s on (s in 0..15), zero-filled past the end.
+__device__ __forceinline__ u32x4 shr_bytes(const u32x4& v, uint32_t s) {
+  const uint32_t k = s >> 2, b = s & 3;
+  const uint32_t w0 = k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
+  const uint32_t w1 = k == 0 ? v.y : k == 1 ? v.z : k == 2 ? v.w : 0u;
+  const uint32_t w2 = k == 0 ? v.z : k == 1 ? v.w : 0u;
+  const uint32_t w3 = k == 0 ? v.w : 0u;
+  return u32x4{fun(w0, w1, b), fun(w1, w2, b), fun(w2, w3, b), fun(w3, 0u, b)};
+}
+
+// One chunk's table entries (lane 0 of the quad).
+__device__ __forceinline__ void put_chunk(const ScanArgs& a, uint64_t t, uint64_t spec, uint64_t ex, uint32_t count,
+                                          uint32_t cerr) {
+  ((g_u64*)a.spec)[t] = spec;
+  ((g_u64*)a.exit)[t] = ex;
+  ((g_u32*)a.count)[t] = count;
+  ((g_u32*)a.long_r)[t] = 0xFFFFFFFFu;  // every record is hashed here: nothing left for k_long
+  ((g_u32*)a.cerr)[t] = cerr;
+}
+
+// A quad's walk state (every field the same in the quad's four lanes).
+struct Walk {
+  WSeg S;
+  uint64_t run_end;  // the run's end chunk (global)
+  // chunk state of the segment
+  uint32_t cj, cn, ccerr;
+  uint64_t cspec;
+};
+
+// The chain enters the record at `pos`: close the chunks it leaves, open its chunk; returns the
+// record's row within its chunk (and the chunk in *j).
+__device__ __forceinline__ uint32_t open_record(const ScanArgs& a, Walk& W, uint64_t pos, uint32_t csh, bool writer,
+                                                uint32_t* jout) {
+  const uint32_t j = (uint32_t)((pos - W.S.b0) >> csh);
+  if (j != W.cj) {
+    if (W.cj != kNoChunk && writer) put_chunk(a, W.S.t0 + W.cj, W.cspec, pos, W.cn, W.ccerr);
+    for (uint32_t k = W.cj == kNoChunk ? 0u : W.cj + 1; k < j; ++k)
+      if (writer) put_chunk(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
+    W.cj = j;
+    W.cn = 0;
+    W.ccerr = 0xFFFFFFFFu;
+    W.cspec = pos;
+  }
+  *jout = j;
+  return W.cn++;
+}
+
+// The segment ends: the chain leaves it at `ex` (kTerm after an EOF row).
+__device__ __forceinline__ void close_segment(const ScanArgs& a, Walk& W, uint64_t ex, bool writer) {
+  uint32_t k0 = 0;
+  if (W.cj != kNoChunk) {
+    if (writer) put_chunk(a, W.S.t0 + W.cj, W.cspec, ex, W.cn, W.ccerr);
+    k0 = W.cj + 1;
+  }
+  for (uint32_t k = k0; k < W.S.nch; ++k)
+    if (writer) put_chunk(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
+  W.cj = kNoChunk;
+}
+
+// The segment of chunks [t, min(file end, W.run_end)) of the file holding chunk t.
+__device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* files, Walk& W, uint64_t t) {
+  const uint32_t fi = find_file(files, a.nfiles, t);
+  const FileDesc fd = files[fi];
+  const uint64_t fend = fd.first_chunk + fd.nchunks;
+  const uint64_t se = fend < W.run_end ? fend : W.run_end;
+  W.S.data = fd.data;
+  W.S.len = fd.len;
+  const uintptr_t end16 = ((uintptr_t)(fd.data + fd.len) + 15) & ~(uintptr_t)15;
+  W.S.sl = (int64_t)(end16 - (uintptr_t)fd.data) - 16;
+  W.S.b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+  const uint64_t e = (se - fd.first_chunk) * (uint64_t)a.chunk;
+  W.S.b1 = e < fd.len ? e : fd.len;
+  W.S.t0 = t;
+  W.S.nch = (uint32_t)(se - t);
+  W.cj = kNoChunk;
+}
+
+}  // namespace
+
+// D: 64-B blocks per round (a quad keeps D * 64 B of its record in flight).
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_walk_hash(ScanArgs a, const FileDesc* __restrict__ files) {
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
+  const bool writer = q == 0;
+  const uint64_t R = a.run;
+  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
+  const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x >> 2);
+  const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
+  const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
+  g_u32* slots = (g_u32*)a.slots;
+
+  Walk W;
+  W.S.data = (const uint8_t*)files;  // (a safe address for the loads of a quad with no segment)
+  W.S.len = 16;
+  W.S.sl = 0;
+  W.S.b0 = W.S.b1 = 0;
+  W.S.t0 = 0;
+  W.S.nch = 0;
+  W.run_end = 0;
+  W.cj = kNoChunk;
+  W.cn = 0;
+  W.ccerr = 0xFFFFFFFFu;
+  W.cspec = 0;
+
+  // the record being hashed
+  bool cv = false;
+  uint64_t cp = 0, crl = 0, cseq = 0;
+  uint32_t cnblk = 0, crem = 0, cstored = 0, cksz = 0, cvsz = 0, cj_rec = 0, crow = 0, v = 0;
+  // the round in hand: blocks [rlb, rlb + rnl) of the record's full 64-B blocks; rfin: the record
+  // ends in it (its last partial block, if any, is in T); tclamp: that block's partial stripe could
+  // not be loaded whole (the file ends within its 16 bytes): read exactly when finishing
+  uint32_t rlb = 0, rnl = 0;
+  bool rfin = false, tclamp = false;
+  // the header at hp: in H/H4 when hv; to be loaded this iteration when hissue
+  uint64_t hp = 0;
+  bool hv = false, hissue = false;
+  bool active = true;
+
+  // Next segment of the run, or the next run (claimed); the chain's start in it goes to hp (header
+  // loaded at the next iteration), or the quad is done.
+  bool first_claim = true;
+  uint64_t tnext = 0;  // next chunk of the current run to set up
+  auto next_work = [&]() {
+    for (;;) {
+      if (tnext < W.run_end) {
+        const bool run_first = tnext % R == 0;  // (a run's later segments start files)
+        seg_setup(a, files, W, tnext);
+        tnext = W.S.t0 + W.S.nch;
+        uint64_t s = 0;
+        if (W.S.b0 != 0) s = run_first && a.walk_pre ? a.tin[W.S.t0] : kNone;
+        if (s == kNone || s >= W.S.b1) {  // no record starts in the segment (as found by the search)
+          close_segment(a, W, 0, writer);
+          continue;
+        }
+        hp = s;
+        hissue = true;
+        hv = false;
+        return;
+      }
+      uint64_t k;
+      if (first_claim) {
+        k = blockIdx.x * (uint64_t)(blockDim.x >> 2) + (threadIdx.x >> 2);
+        first_claim = false;
+      } else {
+        // every lane of the quad takes part (lane 0 adds 1): no lane-0 branch around the atomic
+        const uint32_t old = atomicAdd(&a.ctr->hash_next, q == 0 ? 1u : 0u);
+        k = nquads + qb0(old);
+      }
+      if (k >= nruns) {
+        active = false;
+        hv = hissue = false;
+        return;
+      }
+      tnext = k * R;
+      W.run_end = tnext + R < a.total_chunks ? tnext + R : a.total_chunks;
+    }
+  };
+  next_work();
+
+  u32x4 Ya[D], Yb[D], Ta, Tb, Ha, Hb;
+  uint32_t H4a = 0, H4b = 0;
+#pragma unroll
+  for (uint32_t d = 0; d < D; ++d) Ya[d] = Yb[d] = u32x4{0u, 0u, 0u, 0u};
+  Ta = Tb = Ha = Hb = u32x4{0u, 0u, 0u, 0u};
+
+  // One iteration: (Yi, Ti, Hi, H4i) hold what the last iteration loaded; this one loads (Yo, To,
+  // Ho, H4o).
+  auto body = [&](const u32x4* Yi, const u32x4& Ti, const u32x4& Hi, uint32_t H4i, u32x4* Yo, u32x4& To, u32x4& Ho,
+                  uint32_t& H4o) {
+    // ---- plan the next round
+    bool nrec = false, neof = false, nend = false, round2 = false, fin2 = false;
+    uint64_t base2 = 0, nrl = 0, hp2 = hp;
+    uint32_t lb2 = 0, nl2 = 0, nblk2 = 0, rb2 = 0;
+    if (cv && !rfin) {  // the rest of the current record
+      lb2 = rlb + D;
+      const uint32_t left = cnblk - lb2;
+      nl2 = left < D ? left : D;
+      fin2 = left < D || (left == D && crem == 0);
+      base2 = cp;
+      nblk2 = cnblk;
+      rb2 = crem;
+      round2 = true;
+    } else if (hv) {  // the next record: its header is in hand
+      if (hp >= W.S.b1) {
+        nend = true;
+      } else if (hp + 18 > W.S.len) {
+        neof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163)
+      } else {
+        const uint32_t vsz = H4i;
+        nrl = 18ull + (Hi.w & 0xFFFFu) + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+        if (hp + nrl > W.S.len) {
+          neof = true;  // key or value cut short (data.rs:172,181)
+        } else {
+          nrec = true;
+          nblk2 = (uint32_t)((nrl - 4) >> 6);
+          rb2 = (uint32_t)((nrl - 4) & 63);
+          nl2 = nblk2 < D ? nblk2 : D;
+          fin2 = nblk2 < D || (nblk2 == D && rb2 == 0);
+          base2 = hp;
+          round2 = true;
+          hp2 = hp + nrl;  // the header after it, loaded with its first round
+        }
+      }
+    }
+    // ---- issue: D blocks, the last partial block, the header (every quad issues every load)
+    const uint64_t blk0 = base2 + 4 + 64ull * lb2 + 16ull * q;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) Yo[d] = ld16(W.S, (round2 && d < nl2) ? blk0 + 64ull * d : 0ull);
+    const bool tail2 = round2 && fin2 && rb2 != 0 && nblk2 - lb2 < D;
+    const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);  // the partial stripe
+    const bool tclamp2 = tail2 && (rb2 & 15) != 0 && (int64_t)tpart > W.S.sl;
+    To = ld16(W.S, tail2 ? base2 + 4 + 64ull * nblk2 + 16ull * q : 0ull);
+    const bool hload = nrec || hissue || hv;
+    Ho = ld16(W.S, hload ? hp2 : 0ull);
+    H4o = ld4(W.S, hload ? hp2 + 14 : 0ull);
+    // ---- mix the round in hand
+    if (cv) {
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) {
+        u32x4 x = Yi[d];
+        quad_transpose(x, q);
+        const uint32_t w = xround(xround(xround(xround(v, x.x), x.y), x.z), x.w);
+        v = d < rnl ? w : v;
+      }
+      if (rfin) {  // the record's last partial block, merge, length, tail, avalanche (data.rs:185-198)
+        const uint32_t rem = crem >> 4, tb = crem & 15;
+        u32x4 t = Ti;
+        quad_transpose(t, q);
+        uint32_t vv = v;
+        vv = rem > 0 ? xround(vv, t.x) : vv;
+        vv = rem > 1 ? xround(vv, t.y) : vv;
+        vv = rem > 2 ? xround(vv, t.z) : vv;
+        uint32_t m = rotl_var(vv, mrot);
+        m += quad_xor1(m);
+        m += quad_xor2(m);
+        const uint64_t hl = crl - 4;
+        uint32_t h = (hl >= 16 ? m : P5) + (uint32_t)hl;
+        const int src = (int)((lane & ~3u) | rem);
+        u32x4 tw;
+        tw.x = (uint32_t)__shfl((int)Ti.x, src, 64);
+        tw.y = (uint32_t)__shfl((int)Ti.y, src, 64);
+        tw.z = (uint32_t)__shfl((int)Ti.z, src, 64);
+        tw.w = (uint32_t)__shfl((int)Ti.w, src, 64);
+        // The file ends within this stripe's 16 bytes: its lane loaded the file's last 16-B granule
+        // instead (ld16 clamps the address to W.S.sl), which holds the stripe's bytes from byte
+        // x - sl on. (No load here: a load in this branch would make every iteration wait for the
+        // next round's loads.)
+        const int64_t xs = (int64_t)(cp + 4 + 64ull * cnblk + 16ull * rem);
+        tw = shr_bytes(tw, tclamp ? (uint32_t)(xs - W.S.sl) : 0u);
+        const uint32_t n4 = tb >> 2, n1 = tb & 3;
+        h = n4 > 0 ? tail4(h, tw.x) : h;
+        h = n4 > 1 ? tail4(h, tw.y) : h;
+        h = n4 > 2 ? tail4(h, tw.z) : h;
+        const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
+        h = n1 > 0 ? tail1(h, lw & 0xFFu) : h;
+        h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
+        h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
+        h = avalanche(h);
+        const bool bad = h != cstored;  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
+        const uint32_t off = (uint32_t)(cp - W.S.b0 - ((uint64_t)cj_rec << csh));
+        if (writer)
+          *(g_u32x4*)(slots + ((W.S.t0 + cj_rec) * (uint64_t)a.slot_cap + crow) * 4) =
+              u32x4{(uint32_t)cseq, (uint32_t)(cseq >> 32), cvsz, cksz | (off << 16) | (bad ? kSlotBad : 0u)};
+        if (bad && crow < W.ccerr) W.ccerr = crow;
+      }
+    }
+    // ---- state for the next iteration
+    if (cv && rfin) cv = false;
+    if (cv) {  // the record goes on
+      rlb = lb2;
+      rnl = nl2;
+      rfin = fin2;
+      tclamp = tclamp2;
+    }
+    if (nrec) {
+      cv = true;
+      cp = hp;
+      crl = nrl;
+      cnblk = nblk2;
+      crem = rb2;
+      rlb = 0;
+      rnl = nl2;
+      rfin = fin2;
+      tclamp = tclamp2;
+      v = vinit;
+      cstored = Hi.x;
+      cseq = (uint64_t)Hi.y | ((uint64_t)Hi.z << 32);
+      cksz = Hi.w & 0xFFFFu;
+      cvsz = H4i;
+      crow = open_record(a, W, cp, csh, writer, &cj_rec);
+      hp = hp2;  // loaded this iteration
+      hv = true;
+    } else if (neof) {  // the chain ends with an UnexpectedEof row
+      uint32_t j = 0;
+      const uint32_t r = open_record(a, W, hp, csh, writer, &j);
+      const uint32_t off = (uint32_t)(hp - W.S.b0 - ((uint64_t)j << csh));
+      const bool hdr_ok = hp + 18 <= W.S.len;
+      const u32x4 row = hdr_ok ? u32x4{Hi.y, Hi.z, H4i, (Hi.w & 0xFFFFu) | (off << 16)} : u32x4{0u, 0u, 0u, off << 16};
+      if (writer) *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
+      if (r < W.ccerr) W.ccerr = r;
+      close_segment(a, W, kTerm, writer);
+      next_work();
+    } else if (nend) {  // the chain leaves the segment at hp
+      close_segment(a, W, hp, writer);
+      next_work();
+    } else if (hissue) {  // a segment's first header: loaded this iteration
+      hissue = false;
+      hv = true;
+    }
+  };
+
+  for (;;) {
+    if (!__any(active || cv)) break;
+    body(Ya, Ta, Ha, H4a, Yb, Tb, Hb, H4b);
+    if (!__any(active || cv)) break;
+    body(Yb, Tb, Hb, H4b, Ya, Ta, Ha, H4a);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split path, pass 1 — k_walk_chase: one lane per run of a.run chunks walks the record chain from
+// the run's speculative start (k_walk_search) reading only each record's 18-B header
+// (Entries::next, log.rs:403-429: each record starts where the previous one ends), and writes what
+// k_walk_runs would: slot rows (without the checksum verdict: k_run_hash adds it), the chunk table
+// (spec, exit, count, cerr, long_r = none) and, per chunk, the address of its first byte and of its
+// file's end (cdesc). A record cut short by the end of its file is its UnexpectedEof row (data.rs:163,
+// 172, 181) and ends the chain.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* __restrict__ files) {
+  const uint64_t R = a.run;
+  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
+  g_u32* slots = (g_u32*)a.slots;
+  g_u64* cd = (g_u64*)a.cdesc;
+  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nruns; k += (uint64_t)gridDim.x * blockDim.x) {
+    Walk W;
+    W.cn = 0;
+    W.ccerr = 0xFFFFFFFFu;
+    W.cspec = 0;
+    W.run_end = k * R + R < a.total_chunks ? k * R + R : a.total_chunks;
+    for (uint64_t t = k * R; t < W.run_end;) {
+      seg_setup(a, files, W, t);
+      t = W.S.t0 + W.S.nch;
+      const uint64_t fend = (uint64_t)(uintptr_t)(W.S.data + W.S.len);
+      for (uint32_t c = 0; c < W.S.nch; ++c) {
+        cd[2 * (W.S.t0 + c)] = (uint64_t)(uintptr_t)(W.S.data + W.S.b0 + ((uint64_t)c << csh));
+        cd[2 * (W.S.t0 + c) + 1] = fend;
+      }
+      // the run's first segment starts at its searched start; a later one starts a file (b0 == 0)
+      uint64_t p = W.S.b0 == 0 ? 0ull : a.walk_pre ? a.tin[W.S.t0] : kNone;
+      bool term = false;
+      while (p != kNone && p < W.S.b1) {
+        uint32_t j = 0;
+        if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
+          const uint32_t r = open_record(a, W, p, csh, true, &j);
+          const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
+          *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
+          if (r < W.ccerr) W.ccerr = r;
+          term = true;
+          break;
+        }
+        const u32x4 h = gld16g((const g_u8*)(W.S.data + p));
+        const uint32_t vsz = gld4g((const g_u8*)(W.S.data + p + 14));
+        const uint32_t ksz = h.w & 0xFFFFu;
+        const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+        const uint32_t r = open_record(a, W, p, csh, true, &j);
+        const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{h.y, h.z, vsz, ksz | (off << 16)};
+        if (p + rl > W.S.len) {  // key or value cut short (data.rs:172,181)
+          if (r < W.ccerr) W.ccerr = r;
+          term = true;
+          break;
+        }
+        p += rl;
+      }
+      close_segment(a, W, term ? kTerm : p, true);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Split path, pass 2 — k_run_hash: Entry::from_read's checksum (data.rs:185-198) of every record the
+// chase found. A wave claims runs and hands their records, in order, to its 16 quads: a quad hashes
+// its record straight from HBM (one round of up to D 64-B blocks in flight while it mixes the one
+// before; lane q keeps stripe accumulator q, quad_transpose), and takes the next record of the wave's
+// stream as it starts one (its slot row and chunk address arrive with the record's first round). A
+// failed record gets the bad bit in its slot row and lowers its chunk's first failing row (cerr),
+// which k_finish reads. The wave's stream runs on from one claimed run to the next, so no quad
+// waits for a run's last record.
+// ---------------------------------------------------------------------------------------------
+template <uint32_t D>
+__global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
+  constexpr uint32_t RT = kMaxRun + 1;
+  __shared__ uint32_t s_pf[4][2][RT];  // per wave, two runs: the exclusive prefix of their chunks' rows
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6;
+  const bool qlead = q == 0;
+  const uint64_t R = a.run;
+  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
+  const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
+  g_u32* slots = (g_u32*)a.slots;
+  const g_u64* cd = (const g_u64*)a.cdesc;
+  uint32_t* pf0 = s_pf[wv][0];
+  uint32_t* pf1 = s_pf[wv][1];
+  const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
+  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
+
+  // The wave's record stream (uniform): two run slots, the one records are handed out from (cs) and
+  // its cursor (cur); a slot is refilled from the claim counter once the other one runs low.
+  uint64_t rt0[2] = {0, 0};
+  uint32_t rn[2] = {0, 0}, rch[2] = {0, 0};
+  bool rfull[2] = {false, false};
+  uint32_t cs = 0, cur = 0;
+  bool first_claim = true, runs_left = true;
+  auto load_run = [&](uint32_t s) {
+    uint64_t k;
+    if (first_claim) {
+      k = blockIdx.x * 4ull + wv;
+      first_claim = false;
+    } else {  // (every lane takes part in the atomic, lane 0 adding 1: no lane-0 branch)
+      const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
+      k = (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old);
+    }
+    if (k >= nruns) {
+      runs_left = false;
+      return;
+    }
+    const uint64_t t0 = k * R;
+    const uint32_t nch = (uint32_t)(a.total_chunks - t0 < R ? a.total_chunks - t0 : R);
+    const uint32_t c = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
+    uint32_t inc = c;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if ((int)lane >= o) inc += u;
+    }
+    uint32_t* pf = s ? pf1 : pf0;
+    if (lane < nch) pf[lane + 1] = inc;
+    if (lane == 0) pf[0] = 0;
+    rt0[s] = t0;
+    rch[s] = nch;
+    rn[s] = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
+    rfull[s] = true;
+  };
+
+  // a quad's current record (cv) and the round of it in hand: blocks [rlb, rlb + rnl) of its full
+  // 64-B blocks, rfin if the record ends in this round (its partial block in T), head if it is the
+  // record's first (its stored checksum in xst); tclamp: the partial stripe is near the file end
+  bool cv = false, rfin = false, head = false, tclamp = false;
+  uint64_t cbase = 0, crl = 0, cend = 0, ct_t = 0;
+  uint32_t cnblk = 0, crem = 0, rlb = 0, rnl = 0, v = 0, cstored = 0, ct_r = 0, cw3 = 0;
+  // its next record: ns = 0 none, 1 slot row + chunk address loading (issued last iteration), 2 ready
+  uint32_t ns = 0;
+  uint64_t nt = 0;
+  uint32_t nr = 0;
+  u32x4 nrow = u32x4{0u, 0u, 0u, 0u}, ndesc = u32x4{0u, 0u, 0u, 0u};
+  u32x4 X[D], T = u32x4{0u, 0u, 0u, 0u};
+  uint32_t xst = 0;
+#pragma unroll
+  for (uint32_t d = 0; d < D; ++d) X[d] = u32x4{0u, 0u, 0u, 0u};
+
+  load_run(0);
+  for (;;) {
+    if (ns == 1) ns = 2;  // (every load of the last iteration has arrived)
+    if (runs_left && !rfull[cs ^ 1] && rn[cs] - cur < 16) load_run(cs ^ 1);
+    // ---- plan this quad's next round
+    bool promote = false, round2 = false, fin2 = false;
+    uint64_t base2 = 0, rl2 = 0, end2 = 0, pt = 0;
+    uint32_t lb2 = 0, nl2 = 0, nblk2 = 0, rb2 = 0, pr = 0, pw3 = 0;
+    const bool cont = cv && !rfin;
+    if (cont) {  // the rest of the current record
+      lb2 = rlb + D;
+      const uint32_t left = cnblk - lb2;
+      nl2 = left < D ? left : D;
+      fin2 = left < D || (left == D && crem == 0);
+      base2 = cbase;
+      rl2 = crl;
+      end2 = cend;
+      nblk2 = cnblk;
+      rb2 = crem;
+      round2 = true;
+    } else if (ns == 2) {  // the next record, from its slot row and its chunk's address
+      const uint32_t w3 = nrow.w, vsz = nrow.z;
+      const uint64_t b = ((uint64_t)ndesc.y << 32 | ndesc.x) + ((w3 >> 16) & 0x7FFFu);
+      const uint64_t e = (uint64_t)ndesc.w << 32 | ndesc.z;
+      const uint64_t rl = 18ull + (w3 & 0xFFFFu) + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+      promote = true;
+      ns = 0;
+      pt = nt;
+      pr = nr;
+      pw3 = w3;
+      if (b + rl <= e) {  // (an UnexpectedEof row, cut by the file's end, has failed already)
+        base2 = b;
+        rl2 = rl;
+        end2 = e;
+        nblk2 = (uint32_t)((rl - 4) >> 6);
+        rb2 = (uint32_t)((rl - 4) & 63);
+        nl2 = nblk2 < D ? nblk2 : D;
+        fin2 = nblk2 < D || (nblk2 == D && rb2 == 0);
+        round2 = true;
+      }
+    }
+    // ---- issue the round: D blocks, the last partial block, the stored checksum (first round)
+    u32x4 Y[D];
+    const g_u8* bp = (const g_u8*)(uintptr_t)(base2 + 4 + 64ull * lb2 + 16ull * q);
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) {
+      Y[d] = X[d];
+      if (round2 && d < nl2) Y[d] = gld16g(bp + 64 * d);
+    }
+    const bool tail2 = round2 && fin2 && rb2 != 0 && nblk2 - lb2 < D;
+    const uint64_t end16 = (end2 + 15) & ~15ull;
+    const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
+    const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);
+    const bool tclamp2 = tail2 && (rb2 & 15) != 0 && tpart + 16 > end16;
+    u32x4 T2 = T;
+    if (tail2) T2 = gld16g((const g_u8*)(uintptr_t)(tq + 16 <= end16 ? tq : end16 - 16));
+    uint32_t xst2 = xst;
+    if (round2 && !cont) xst2 = gld4g((const g_u8*)(uintptr_t)base2);
+    // ---- the stream's next records to the quads that have none (in lane order)
+    const bool want = ns == 0;
+    const unsigned long long wm = __ballot(qlead && want) & qmask;
+    const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
+    if (nw) {
+      const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (lane ? (~0ull >> (64 - (lane & ~3u))) : 0ull));
+      const uint32_t rem = rn[cs] - cur;
+      const uint32_t so = cs ^ 1;
+      const bool up = myrank >= rem;
+      const uint32_t idx = up ? myrank - rem : cur + myrank;
+      const bool ok = want && (up ? (rfull[so] && idx < rn[so]) : true);
+      if (ok) {
+        const uint32_t* pf = (up ? so : cs) ? pf1 : pf0;
+        uint32_t lo = 0, hi = up ? rch[so] : rch[cs];  // the last chunk j with pf[j] <= idx
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (pf[mid] <= idx) lo = mid; else hi = mid;
+        }
+        nt = (up ? rt0[so] : rt0[cs]) + lo;
+        nr = idx - pf[lo];
+        nrow = *(const g_u32x4*)(slots + (nt * (uint64_t)a.slot_cap + nr) * 4);
+        ndesc = *(const g_u32x4*)(cd + 2 * nt);
+        ns = 1;
+      }
+      const uint32_t avail = rem + (rfull[so] ? rn[so] : 0u);
+      const uint32_t used = nw < avail ? nw : avail;
+      if (used >= rem && rfull[so]) {  // the current run is handed out: the stream moves on
+        rfull[cs] = false;
+        cs = so;
+        cur = used - rem;
+      } else {
+        cur += used;
+      }
+    }
+    (void)below;
+    // ---- mix the round in hand
+    if (cv) {
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) {
+        u32x4 x = X[d];
+        quad_transpose(x, q);
+        const uint32_t w = xround(xround(xround(xround(v, x.x), x.y), x.z), x.w);
+        v = d < rnl ? w : v;
+      }
+      if (head) cstored = xst;
+      if (rfin) {  // the last partial block, merge, length, tail, avalanche (data.rs:185-198)
+        const uint32_t rem = crem >> 4, tb = crem & 15;
+        u32x4 t = T;
+        quad_transpose(t, q);
+        uint32_t vv = v;
+        vv = rem > 0 ? xround(vv, t.x) : vv;
+        vv = rem > 1 ? xround(vv, t.y) : vv;
+        vv = rem > 2 ? xround(vv, t.z) : vv;
+        uint32_t m = rotl_var(vv, mrot);
+        m += quad_xor1(m);
+        m += quad_xor2(m);
+        const uint64_t hl = crl - 4;
+        uint32_t h = (hl >= 16 ? m : P5) + (uint32_t)hl;
+        const int src = (int)((lane & ~3u) | rem);
+        u32x4 tw;
+        tw.x = (uint32_t)__shfl((int)T.x, src, 64);
+        tw.y = (uint32_t)__shfl((int)T.y, src, 64);
+        tw.z = (uint32_t)__shfl((int)T.z, src, 64);
+        tw.w = (uint32_t)__shfl((int)T.w, src, 64);
+        // the file ends within the partial stripe's 16 bytes: its lane loaded the file's last
+        // granule instead, which holds the stripe from byte xs - (e16 - 16) on
+        const uint64_t xs = cbase + 4 + 64ull * cnblk + 16ull * rem;
+        const uint64_t e16 = (cend + 15) & ~15ull;
+        tw = shr_bytes(tw, tclamp ? (uint32_t)(xs - (e16 - 16)) : 0u);
+        const uint32_t n4 = tb >> 2, n1 = tb & 3;
+        h = n4 > 0 ? tail4(h, tw.x) : h;
+        h = n4 > 1 ? tail4(h, tw.y) : h;
+        h = n4 > 2 ? tail4(h, tw.z) : h;
+        const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
+        h = n1 > 0 ? tail1(h, lw & 0xFFu) : h;
+        h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
+        h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
+        h = avalanche(h);
+        if (h != cstored && qlead) {  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
+          slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
+          atomicMin(&a.cerr[ct_t], ct_r);
+        }
+      }
+    }
+    // ---- state for the next iteration
+    if (cont) {
+      rlb = lb2;
+      rnl = nl2;
+      rfin = fin2;
+      tclamp = tclamp2;
+      head = false;
+    } else {
+      cv = promote && round2;
+      cbase = base2;
+      crl = rl2;
+      cend = end2;
+      cnblk = nblk2;
+      crem = rb2;
+      rlb = 0;
+      rnl = nl2;
+      rfin = fin2;
+      tclamp = tclamp2;
+      head = true;
+      v = vinit;
+      ct_t = pt;
+      ct_r = pr;
+      cw3 = pw3;
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) X[d] = Y[d];
+    T = T2;
+    xst = xst2;
+    const bool stream_left = rn[cs] != cur || (rfull[cs ^ 1] && rn[cs ^ 1] != 0) || runs_left;
+    if (!stream_left && !__any(cv || ns != 0)) break;
+  }
+}
+
+void launch_walk_hash(const ScanArgs& a, int depth, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  // CASK_HASH_WAVES (tuning knob): waves per CU of the grid (the runs beyond it are claimed)
+  static const uint32_t per_cu = getenv("CASK_HASH_WAVES") ? (uint32_t)atoi(getenv("CASK_HASH_WAVES")) : 8u;
+  uint64_t quads = (uint64_t)device_cus() * per_cu * 16u;
+  if (quads > nruns) quads = nruns;
+  const uint32_t grid = (uint32_t)((quads + 63) / 64);
+  hipStream_t s = (hipStream_t)stream;
+  if (depth == 8)
+    hipLaunchKernelGGL((k_walk_hash<8>), dim3(grid), dim3(256), 0, s, a, a.files);
+  else if (depth == 32)
+    hipLaunchKernelGGL((k_walk_hash<32>), dim3(grid), dim3(256), 0, s, a, a.files);
+  else
+    hipLaunchKernelGGL((k_walk_hash<16>), dim3(grid), dim3(256), 0, s, a, a.files);
+}
+
+
+void launch_walk_chase(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  const uint32_t grid = (uint32_t)((nruns + 255) / 256);
+  hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(256), 0, (hipStream_t)stream, a, a.files);
+}
+
+void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  // CASK_HASH_WAVES (tuning knob): waves per CU of the persistent grid (the runs beyond its first
+  // are claimed)
+  static const uint32_t per_cu = getenv("CASK_HASH_WAVES") ? (uint32_t)atoi(getenv("CASK_HASH_WAVES")) : 16u;
+  uint64_t waves = (uint64_t)device_cus() * per_cu;
+  if (waves > nruns) waves = nruns;
+  const uint32_t grid = (uint32_t)((waves + 3) / 4);
+  hipStream_t s = (hipStream_t)stream;
+  if (depth == 16)
+    hipLaunchKernelGGL((k_run_hash<16>), dim3(grid), dim3(256), 0, s, a);
+  else if (depth == 4)
+    hipLaunchKernelGGL((k_run_hash<4>), dim3(grid), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_run_hash<8>), dim3(grid), dim3(256), 0, s, a);
+}
+
+}  // namespace cask_dev

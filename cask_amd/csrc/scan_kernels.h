@@ -50,6 +50,7 @@ struct Counters {
   unsigned int lq_cnt[22];       // long-record queue: entries per length class 2^10 .. 2^31+
   unsigned int walk_next[8];     // k_walk_runs: next run of each walk group to hand out (kWalkGroups)
   unsigned int search_next[8];   // k_walk_search: the same, for the searches
+  unsigned int hash_next;        // k_walk_hash: next run to hand out (after the first by index)
 };
 
 // Layout of the call block: Counters, then row_off[nfiles + 1] (each file's first dense row,
@@ -149,6 +150,9 @@ struct ScanArgs {
   uint64_t t_lo, t_hi;
   const uint32_t* lq_lo;
   const uint32_t* lq_hi;
+  // walk mode, split path (k_walk_chase -> k_run_hash): per chunk, the address of its first byte and
+  // the end of its file's last 16-B granule (2 x u64), written by the chase
+  uint64_t* cdesc;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -233,6 +237,14 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: the walk-mode speculative pass
 void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each walk run's speculative start
+// k_walk_hash.hip: the walk mode in one pass (a quad per run chases and hashes every record);
+// depth = 64-B blocks per quad in flight (8, 16 or 32)
+void launch_walk_hash(const ScanArgs& a, int depth, void* stream);
+// k_walk_hash.hip, split path: k_walk_chase (a lane per run of a.run chunks chases the record
+// headers: slot rows, chunk table, cdesc), then k_run_hash (a wave per claimed run, a quad per record:
+// every record hashed from HBM; depth = 64-B blocks per quad in flight)
+void launch_walk_chase(const ScanArgs& a, void* stream);
+void launch_run_hash(const ScanArgs& a, int depth, void* stream);
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

@@ -98,6 +98,7 @@ struct cask_ctx {
   DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
   DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
   DevBuf lqsnap;     // walk groups: the long-record queue counts after each group's enqueue
+  DevBuf cdesc;      // walk mode, split path: per chunk its address and its file's end (2 x u64)
   uint32_t epoch = 0;
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
@@ -119,7 +120,7 @@ struct cask_ctx {
   // walk groups: group g walked (stream -> sides); sides done (-> stream); searches (both ways)
   hipEvent_t gev[kWalkGroups + 4] = {};
   void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
-  float last_ms[6] = {0, 0, 0, 0, 0, 0};
+  float last_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
   int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
   int last_walk = 0;   // the last call's speculative pass was k_walk_runs
@@ -227,7 +228,13 @@ uint32_t cask_xxh32(const uint8_t* data, uint64_t len) { return cask_xxh::xxh32(
 
 int cask_last_timings(const cask_ctx* c, float* ms6) {
   if (!c || !ms6) return CASK_E_INVALID_ARG;
-  memcpy(ms6, c->last_ms, sizeof(c->last_ms));
+  memcpy(ms6, c->last_ms, 6 * sizeof(float));
+  return CASK_OK;
+}
+
+int cask_last_timings8(const cask_ctx* c, float* ms8) {
+  if (!c || !ms8) return CASK_E_INVALID_ARG;
+  memcpy(ms8, c->last_ms, 8 * sizeof(float));
   return CASK_OK;
 }
 
@@ -526,7 +533,44 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // hash on HBM bandwidth). Long records hashed before k_finish mark their rows like any failed
   // check (slot bad bit, cerr), so k_finish sees them.
   bool long_pre = false;
-  if (walk && !hint) {
+  // Walk mode on data files. CASK_WALK_PATH (tuning knob) picks the path: "split" (default: every
+  // run's speculative start, k_walk_search; the header chase, k_walk_chase, a lane per run; then
+  // k_run_hash, a quad per record hashing it from HBM), "fused" (k_walk_hash: a quad per run chases
+  // and hashes) or "grouped" (k_walk_runs + the long-record queue + k_long_hash, in groups on two
+  // streams).
+  static const int walk_path = [] {
+    const char* v = getenv("CASK_WALK_PATH");
+    return !v ? 0 : !strcmp(v, "fused") ? 1 : !strcmp(v, "grouped") ? 2 : 0;
+  }();
+  // CASK_HASH_D (tuning knob): 64-B blocks in flight per quad of the hashing kernel
+  static const int hash_depth = getenv("CASK_HASH_D") ? atoi(getenv("CASK_HASH_D")) : (walk_path == 1 ? 16 : 8);
+  bool fused = false;
+  if (walk && !hint && walk_path != 2) {
+    fused = true;
+    const uint64_t nruns = (total_chunks + a.run - 1) / a.run;
+    ScanArgs as = a;
+    as.run_lo = 0;
+    as.run_hi = nruns;
+    launch_walk_search(as, st);
+    L("k_walk_search");
+    H(hipEventRecord(c->ev[6], st));
+    a.walk_pre = 1;
+    if (walk_path == 1) {
+      launch_walk_hash(a, hash_depth, st);
+      L("k_walk_hash");
+    } else {
+      if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
+      a.cdesc = c->cdesc.as<uint64_t>();
+      launch_walk_chase(a, st);
+      L("k_walk_chase");
+      H(hipEventRecord(c->ev[7], st));
+      launch_run_hash(a, hash_depth, st);
+      L("k_run_hash");
+    }
+    a.walk_pre = 0;
+    long_pre = true;
+    if (!ok) return CASK_E_DEVICE;
+  } else if (walk && !hint) {
     static const uint32_t groups_env = getenv("CASK_WALK_GROUPS") ? (uint32_t)atoi(getenv("CASK_WALK_GROUPS")) : 0u;
     const uint64_t nruns = (total_chunks + a.run - 1) / a.run;
     uint64_t G = groups_env ? groups_env : kWalkGroupsDefault;
@@ -623,9 +667,19 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       read_call();
     }
     if (!ok) return CASK_E_DEVICE;
-    float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0;
+    float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0, t_search = 0;
     (void)hipEventElapsedTime(&t_all, c->ev[1], more ? c->ev[4] : c->ev[3]);
-    (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
+    float t_chase = 0;
+    if (fused && walk_path == 1) {  // [1] is k_walk_hash alone, [6] the run searches before it
+      (void)hipEventElapsedTime(&t_search, c->ev[1], c->ev[6]);
+      (void)hipEventElapsedTime(&t_k1, c->ev[6], c->ev[2]);
+    } else if (fused) {  // [1] is k_run_hash alone, [6] the run searches, [7] the chase
+      (void)hipEventElapsedTime(&t_search, c->ev[1], c->ev[6]);
+      (void)hipEventElapsedTime(&t_chase, c->ev[6], c->ev[7]);
+      (void)hipEventElapsedTime(&t_k1, c->ev[7], c->ev[2]);
+    } else {
+      (void)hipEventElapsedTime(&t_k1, c->ev[1], c->ev[2]);
+    }
     (void)hipEventElapsedTime(&t_fin, c->ev[2], c->ev[3]);
     if (more) (void)hipEventElapsedTime(&t_long, c->ev[3], c->ev[4]);
     c->last_ms[0] = t_all;
@@ -634,6 +688,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     c->last_ms[3] = t_fin;
     c->last_ms[4] = 0.f;
     c->last_ms[5] = 0.f;
+    c->last_ms[6] = t_search;
+    c->last_ms[7] = t_chase;
     c->last_counters[0] = total_chunks;
     c->last_counters[1] = hc->nlong;
     c->last_counters[2] = c->last_counters[3] = c->last_counters[4] = 0;
@@ -825,6 +881,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   c->last_ms[3] = t_val;
   c->last_ms[4] = repair_ms;
   c->last_ms[5] = t_cmp;
+  c->last_ms[6] = 0.f;
+  c->last_ms[7] = 0.f;
   c->last_counters[0] = total_chunks;
   c->last_counters[1] = nlong_total;
   c->last_counters[2] = invalid_chunks;
@@ -997,8 +1055,33 @@ extern "C" int cask_hints_device(cask_ctx* c, const cask_file_view* files, uint3
   if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
   std::vector<FileDesc> fd(nfiles + 1);
   for (uint32_t i = 0; i < nfiles; ++i) fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
-  return hint_pack(c->kd, fd.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz, rows->status,
-                   rows->count, out, out ? cap : 0, file_hint_offset, c->stream);
+  if (rows->count <= (uint64_t)INT32_MAX)
+    return hint_pack(c->kd, fd.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz,
+                     rows->status, rows->count, out, out ? cap : 0, file_hint_offset, c->stream);
+  // more rows than one device scan takes (an int count): groups of whole files, bodies back to back
+  uint64_t at = 0;  // bytes of the bodies so far
+  int rc = CASK_OK;
+  for (uint32_t f0 = 0; f0 < nfiles;) {
+    const uint64_t r0 = file_row_offset[f0];
+    uint32_t f1 = f0 + 1;
+    while (f1 < nfiles && file_row_offset[f1 + 1] - r0 <= (uint64_t)INT32_MAX) ++f1;
+    const uint64_t n = file_row_offset[f1] - r0;
+    if (n > (uint64_t)INT32_MAX) return CASK_E_CAPACITY;  // one file of more than 2^31 records
+    std::vector<uint64_t> ro(f1 - f0 + 1), fs(f1 - f0 + 1);
+    for (uint32_t f = f0; f <= f1; ++f) ro[f - f0] = file_row_offset[f] - r0;
+    const bool room = out && at <= cap;
+    const int st = hint_pack(c->kd, fd.data() + f0, f1 - f0, ro.data(), rows->pos + r0, rows->seq + r0, rows->vsz + r0,
+                             rows->ksz + r0, rows->status + r0, n, room ? out + at : nullptr, room ? cap - at : 0,
+                             fs.data(), c->stream);
+    if (st != CASK_OK && st != CASK_E_CAPACITY) return st;
+    if (st == CASK_E_CAPACITY) rc = CASK_E_CAPACITY;
+    for (uint32_t f = f0; f < f1; ++f) file_hint_offset[f] = at + fs[f - f0];
+    at += fs[f1 - f0];
+    f0 = f1;
+  }
+  file_hint_offset[nfiles] = at;
+  if (out && at > cap) rc = CASK_E_CAPACITY;
+  return rc;
 }
 
 // The shard block of hint-file bodies (the hint fast path on the multi-GPU replay): rows as

@@ -233,12 +233,13 @@ class ScanContext:
         return v.decode() if v else ""
 
     def last_timings(self) -> dict[str, float]:
-        t = (C.c_float * 6)()
-        self.lib.cask_last_timings(self._h, t)
+        t = (C.c_float * 8)()
+        self.lib.cask_last_timings8(self._h, t)
         # validate_ms: k_finish on the dense path (validation + dense rows; compact_ms is then 0),
-        # the three validation launches on the repair path
+        # the three validation launches on the repair path; chunk_scan_ms is the first pass's kernel
+        # (k_scan_chunks, or k_walk_hash in walk mode, whose run searches are search_ms)
         return {"pipeline_ms": t[0], "chunk_scan_ms": t[1], "long_ms": t[2], "validate_ms": t[3],
-                "repair_ms": t[4], "compact_ms": t[5]}
+                "repair_ms": t[4], "compact_ms": t[5], "search_ms": t[6], "chase_ms": t[7]}
 
     def last_counters(self) -> dict[str, int]:
         c = (C.c_uint64 * 5)()

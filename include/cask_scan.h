@@ -145,6 +145,9 @@ int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
  * [0] whole device pipeline, [1] chunk-scan kernel, [2] long-record + summary kernels,
  * [3] validation kernels, [4] repair (0 when speculation held), [5] compaction. */
 int cask_last_timings(const cask_ctx* ctx, float* ms6);
+/* The same six, then, in walk mode, [6] the run searches (k_walk_search) and [7] the header chase
+ * (k_walk_chase); [1] is then the hashing kernel alone. */
+int cask_last_timings8(const cask_ctx* ctx, float* ms8);
 /* Counters of the last call: [0] chunks, [1] long records, [2] chunks from each file's first
  * invalid one on (0: speculation held), [3] local exact re-scans, [4] 1 if the serial boundary
  * walk ran. */

@@ -6,6 +6,7 @@
 #include "cask_oracle.h"
 
 #include <errno.h>
+#include <stdio.h>
 #include <fcntl.h>
 #include <stdlib.h>
 #include <string.h>
@@ -607,4 +608,365 @@ int orc_replay_buffer_fast(const uint8_t* buf, uint64_t len, uint32_t file_id, o
   }
   res->live_keys = orc_index_len(ix);
   return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Index lookup (Index::get, cask.rs:41-43)                                               */
+/* ------------------------------------------------------------------------------------ */
+int orc_index_get(const orc_index* ix, const uint8_t* key, uint16_t ksz, uint32_t* file_id, uint64_t* pos,
+                  uint64_t* size, uint64_t* seq) {
+  uint64_t h = key_hash(key, ksz);
+  uint64_t m = ix->cap - 1;
+  for (uint64_t i = h & m;; i = (i + 1) & m) {
+    const orc_slot* s = &ix->slots[i];
+    if (s->used == 0) return 0;
+    if (s->used == 1 && s->hash == h && s->ksz == ksz && (ksz == 0 || memcmp(s->key, key, ksz) == 0)) {
+      if (file_id) *file_id = s->file_id;
+      if (pos) *pos = s->pos;
+      if (size) *size = s->size;
+      if (seq) *seq = s->seq;
+      return 1;
+    }
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Compaction merge: Cask::compact_files_aux (cask.rs:451-523), fast restatement          */
+/* ------------------------------------------------------------------------------------ */
+static int read_whole(const char* path, uint8_t** out, uint64_t* len) {
+  int fd = open(path, O_RDONLY);
+  if (fd < 0) return -1;
+  off_t n = lseek(fd, 0, SEEK_END);
+  lseek(fd, 0, SEEK_SET);
+  uint8_t* b = (uint8_t*)malloc(n > 0 ? (size_t)n : 1);
+  uint64_t got = 0;
+  while (got < (uint64_t)n) {
+    ssize_t r = read(fd, b + got, (size_t)((uint64_t)n - got));
+    if (r < 0 && errno == EINTR) continue;
+    if (r <= 0) break;
+    got += (uint64_t)r;
+  }
+  close(fd);
+  *out = b;
+  *len = got;
+  return 0;
+}
+
+static void file_name(char* out, size_t cap, const char* dir, uint32_t id, const char* ext) {
+  /* get_data_file_path / hint path: "{:010}.cask.data" (log.rs:473-481) */
+  snprintf(out, cap, "%s/%010u.cask.%s", dir, id, ext);
+}
+
+/* LogWriter (log.rs:245-306) + EntryWriter (:317-358) + HintWriter (:360-395), buffered in memory
+ * and flushed when the writer moves on (the files are the same bytes the reference writes). */
+typedef struct {
+  const char* dir;
+  uint64_t max_file_size;
+  uint32_t seq;       /* Sequence (util.rs:55-65): the last id handed out */
+  int open;
+  uint32_t fid;
+  uint8_t* data;
+  uint64_t dlen, dcap;
+  uint8_t* hint;
+  uint64_t hlen, hcap;
+  int io_err;
+} orc_writer;
+
+static void grow_buf(uint8_t** b, uint64_t* cap, uint64_t need) {
+  if (need <= *cap) return;
+  uint64_t c = *cap ? *cap : 1 << 16;
+  while (c < need) c *= 2;
+  *b = (uint8_t*)realloc(*b, c);
+  *cap = c;
+}
+
+static int write_file(const char* path, const uint8_t* p, uint64_t n, const uint8_t* tail, size_t tn) {
+  int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+  if (fd < 0) return -1;
+  int rc = write_all_fd(fd, p, (size_t)n);
+  if (rc == 0 && tn) rc = write_all_fd(fd, tail, tn);
+  close(fd);
+  return rc;
+}
+
+static void writer_flush(orc_writer* w) {
+  if (!w->open) return;
+  char path[4096];
+  file_name(path, sizeof path, w->dir, w->fid, "data");
+  if (write_file(path, w->data, w->dlen, NULL, 0)) w->io_err = 1;
+  uint8_t tr[4];
+  wr32(tr, orc_xxh32(w->hint, w->hlen, 0)); /* HintWriter::drop: the trailer (log.rs:389-395) */
+  file_name(path, sizeof path, w->dir, w->fid, "hint");
+  if (write_file(path, w->hint, w->hlen, tr, 4)) w->io_err = 1;
+  w->open = 0;
+  w->dlen = w->hlen = 0;
+}
+
+/* LogWriter::write: a new file when there is none or data_file_pos + entry.size() > max_file_size
+ * (log.rs:282-306); returns 1 if this entry started a file (LogWrite::NewFile). */
+static int writer_write(orc_writer* w, uint64_t seq, const uint8_t* key, uint16_t ksz, const uint8_t* value,
+                        uint32_t vsz, int deleted) {
+  uint64_t size = 18 + (uint64_t)ksz + (deleted ? 0 : vsz); /* Entry::size (data.rs:63-65) */
+  int nf = 0;
+  if (!w->open || w->dlen + size > w->max_file_size) {
+    writer_flush(w);
+    w->fid = ++w->seq; /* Sequence::increment (util.rs:62-64) */
+    w->open = 1;
+    nf = 1;
+  }
+  uint64_t pos = w->dlen;
+  grow_buf(&w->data, &w->dcap, w->dlen + size);
+  orc_entry_encode(seq, key, ksz, value, vsz, deleted, w->data + w->dlen); /* Entry::write_bytes */
+  w->dlen += size;
+  grow_buf(&w->hint, &w->hcap, w->hlen + 22 + ksz);
+  /* Hint::new(entry, entry_pos) + Hint::write_bytes (data.rs:218-226, 242-256) */
+  w->hlen += orc_hint_encode(seq, ksz, deleted ? ORC_ENTRY_TOMBSTONE : vsz, pos, key, w->hint + w->hlen);
+  return nf;
+}
+
+/* deletes: HashMap<Vec<u8>, u64> (cask.rs:471, 487-499), kept in first-seen order (the reference
+ * iterates its RandomState HashMap: the order of its tombstone writes is unspecified) */
+typedef struct {
+  uint8_t* key;
+  uint64_t hash, seq;
+  uint16_t ksz;
+  uint8_t used;
+} del_slot;
+typedef struct {
+  del_slot* slots;
+  uint64_t cap, n;
+  uint64_t* order; /* slot indices in first-seen order */
+  uint64_t ocap;
+} del_map;
+
+static void del_put(del_map* d, const uint8_t* key, uint16_t ksz, uint64_t seq) {
+  if ((d->n + 1) * 2 > d->cap) {
+    del_slot* old = d->slots;
+    uint64_t oc = d->cap;
+    d->cap = oc ? oc * 2 : 1024;
+    d->slots = (del_slot*)calloc(d->cap, sizeof(del_slot));
+    for (uint64_t k = 0; k < d->n; ++k) { /* re-insert in first-seen order, indices rebuilt */
+      del_slot s = old[d->order[k]];
+      uint64_t j = s.hash & (d->cap - 1);
+      while (d->slots[j].used) j = (j + 1) & (d->cap - 1);
+      d->slots[j] = s;
+      d->order[k] = j;
+    }
+    free(old);
+  }
+  uint64_t h = key_hash(key, ksz);
+  uint64_t m = d->cap - 1;
+  uint64_t i = h & m;
+  for (;; i = (i + 1) & m) {
+    del_slot* s = &d->slots[i];
+    if (!s->used) break;
+    if (s->hash == h && s->ksz == ksz && (ksz == 0 || memcmp(s->key, key, ksz) == 0)) {
+      if (s->seq < seq) s->seq = seq; /* Occupied: keep the higher sequence (cask.rs:490-494) */
+      return;
+    }
+  }
+  del_slot* s = &d->slots[i];
+  s->used = 1;
+  s->hash = h;
+  s->ksz = ksz;
+  s->seq = seq;
+  s->key = (uint8_t*)malloc(ksz ? ksz : 1);
+  if (ksz) memcpy(s->key, key, ksz);
+  if (d->n == d->ocap) {
+    d->ocap = d->ocap ? d->ocap * 2 : 1024;
+    d->order = (uint64_t*)realloc(d->order, d->ocap * sizeof(uint64_t));
+  }
+  d->order[d->n++] = i;
+}
+
+static void set_cerr(orc_compact_result* r, int kind, uint32_t fid, uint64_t pos, uint32_t e, uint32_t f) {
+  r->err_kind = kind;
+  r->err_file_id = fid;
+  r->err_pos = pos;
+  r->err_expected = e;
+  r->err_found = f;
+}
+
+static int index_seq_of(const void* ix, const uint8_t* key, uint16_t ksz, uint64_t* seq) {
+  return orc_index_get((const orc_index*)ix, key, ksz, NULL, NULL, NULL, seq);
+}
+
+int orc_compact_files(const char* src_dir, const char* dst_dir, const orc_index* ix, const uint32_t* files,
+                      uint64_t nfiles, uint32_t file_id_seq, uint64_t max_file_size, uint32_t* out_ids,
+                      uint8_t* out_live, uint64_t cap, orc_compact_result* res) {
+  return orc_compact_files_fn(src_dir, dst_dir, index_seq_of, ix, files, nfiles, file_id_seq, max_file_size, out_ids,
+                              out_live, cap, res);
+}
+
+int orc_compact_files_fn(const char* src_dir, const char* dst_dir, orc_seq_fn seq_of, const void* ix,
+                         const uint32_t* files, uint64_t nfiles, uint32_t file_id_seq, uint64_t max_file_size,
+                         uint32_t* out_ids, uint8_t* out_live, uint64_t cap, orc_compact_result* res) {
+  memset(res, 0, sizeof(*res));
+  orc_writer w;
+  memset(&w, 0, sizeof w);
+  w.dir = dst_dir;
+  w.max_file_size = max_file_size;
+  w.seq = file_id_seq;
+  del_map dels;
+  memset(&dels, 0, sizeof dels);
+  uint64_t nout = 0;
+  int rc = 0;
+  char path[4096];
+  for (uint64_t fi = 0; fi < nfiles && !rc; ++fi) {
+    const uint32_t fid = files[fi];
+    /* Log::hints (log.rs:121-135): a missing or invalid hint file skips the file (cask.rs:456-468) */
+    file_name(path, sizeof path, src_dir, fid, "hint");
+    uint8_t* hb = NULL;
+    uint64_t hn = 0;
+    if (read_whole(path, &hb, &hn) != 0) continue;
+    if (hn < 4 || orc_xxh32(hb, hn - 4, 0) != rd32(hb + hn - 4)) { /* is_valid_hint_file (log.rs:512-539) */
+      free(hb);
+      continue;
+    }
+    const uint64_t body = hn - 4;
+    /* the data file, for Log::read_entry (log.rs:150-166) of its live entries */
+    file_name(path, sizeof path, src_dir, fid, "data");
+    uint8_t* db = NULL;
+    uint64_t dn = 0;
+    if (read_whole(path, &db, &dn) != 0) {
+      free(hb);
+      set_cerr(res, -1, fid, 0, 0, 0);
+      rc = -1;
+      break;
+    }
+    /* pass 1 (cask.rs:481-503): liveness of every hint, tombstones of absent keys */
+    uint64_t* ins = NULL;
+    uint64_t nins = 0, icap = 0;
+    for (uint64_t p = 0; p < body;) {
+      /* Hint::from_read (data.rs:258-276): seq u64 | ksz u16 | vsz u32 | pos u64 | key */
+      if (body - p < 22) {
+        set_cerr(res, ORC_ROW_EOF, fid, p, 0, 0);
+        rc = -1;
+        break;
+      }
+      const uint8_t* h = hb + p;
+      const uint64_t seq = rd64(h);
+      const uint16_t ksz = rd16(h + 8);
+      const uint32_t vsz = rd32(h + 10);
+      if (body - p - 22 < ksz) {
+        set_cerr(res, ORC_ROW_EOF, fid, p, 0, 0);
+        rc = -1;
+        break;
+      }
+      const uint8_t* key = h + 22;
+      uint64_t iseq = 0;
+      const int present = seq_of(ix, key, ksz, &iseq);
+      if (vsz == ORC_ENTRY_TOMBSTONE) {
+        if (!present) del_put(&dels, key, ksz, seq);
+      } else if (present && iseq == seq) { /* live iff the index holds this sequence (cask.rs:500) */
+        if (nins == icap) {
+          icap = icap ? icap * 2 : 1024;
+          ins = (uint64_t*)realloc(ins, icap * sizeof(uint64_t));
+        }
+        ins[nins++] = p;
+      }
+      p += 22 + (uint64_t)ksz;
+    }
+    /* pass 2 (cask.rs:505-513): read_entry + LogWriter::write of each live entry, in hint order */
+    for (uint64_t k = 0; k < nins && !rc; ++k) {
+      const uint8_t* h = hb + ins[k];
+      const uint64_t pos = rd64(h + 14);
+      /* Entry::from_read at pos (data.rs:161-206) */
+      if (pos > dn || dn - pos < 18) {
+        set_cerr(res, ORC_ROW_EOF, fid, pos, 0, 0);
+        rc = -1;
+        break;
+      }
+      const uint8_t* e = db + pos;
+      const uint16_t ksz = rd16(e + 12);
+      const uint32_t vraw = rd32(e + 14);
+      const int del = vraw == ORC_ENTRY_TOMBSTONE;
+      const uint64_t rl = 18 + (uint64_t)ksz + (del ? 0 : vraw);
+      if (dn - pos < rl) {
+        set_cerr(res, ORC_ROW_EOF, fid, pos, 0, 0);
+        rc = -1;
+        break;
+      }
+      const uint32_t found = orc_xxh32(e + 4, rl - 4, 0);
+      if (found != rd32(e)) {
+        set_cerr(res, ORC_ROW_CHECKSUM, fid, pos, rd32(e), found);
+        rc = -1;
+        break;
+      }
+      const int nf = writer_write(&w, rd64(e + 4), e + 18, ksz, e + 18 + ksz, del ? 0 : vraw, del);
+      if (nf) { /* LogWrite::NewFile -> new_files (cask.rs:510-512) */
+        if (nout < cap) {
+          out_ids[nout] = w.fid;
+          out_live[nout] = 1;
+        }
+        ++nout;
+        res->n_new++;
+      }
+      res->live_records++;
+      res->bytes_out += rl;
+    }
+    free(ins);
+    free(db);
+    free(hb);
+    if (!rc) res->n_compacted++;
+  }
+  /* the tombstone tail (cask.rs:518-520): files it starts are not in new_files */
+  for (uint64_t k = 0; k < dels.n && !rc; ++k) {
+    const del_slot* s = &dels.slots[dels.order[k]];
+    if (writer_write(&w, s->seq, s->key, s->ksz, NULL, 0, 1)) {
+      if (nout < cap) {
+        out_ids[nout] = w.fid;
+        out_live[nout] = 0;
+      }
+      ++nout;
+      res->n_tomb_only++;
+    }
+    res->tombstones++;
+    res->bytes_out += 18 + (uint64_t)s->ksz;
+  }
+  writer_flush(&w); /* the writers' Drop (log.rs:360-395) */
+  if (w.io_err && !rc) {
+    set_cerr(res, -1, 0, 0, 0, 0);
+    rc = -1;
+  }
+  for (uint64_t i = 0; i < dels.cap; ++i)
+    if (dels.slots && dels.slots[i].used) free(dels.slots[i].key);
+  free(dels.slots);
+  free(dels.order);
+  free(w.data);
+  free(w.hint);
+  res->n_out = nout;
+  res->file_id_seq = w.seq;
+  return rc;
+}
+
+uint64_t orc_index_digest(const orc_index* ix) {
+  uint64_t d = 0;
+  for (uint64_t i = 0; i < ix->cap; ++i) {
+    const orc_slot* s = &ix->slots[i];
+    if (s->used == 1) d += orc_entry_digest(s->key, s->ksz, s->file_id, s->pos, s->size, s->seq);
+  }
+  return d;
+}
+
+/* RecreateHints over a data file in memory (log.rs:137-148, 449-471; Hint::write_bytes, data.rs:242-256):
+ * one hint per Ok record in order, records after a checksum failure included (the drain of
+ * RecreateHints::drop), none after an EOF. Returns the body length (the trailer is not written), or
+ * -1 when cap is too small. */
+int64_t orc_hint_body(const uint8_t* buf, uint64_t len, uint8_t* out, uint64_t cap) {
+  uint64_t pos = 0, n = 0;
+  while (pos < len) {
+    if (len - pos < 18) break;
+    const uint8_t* h = buf + pos;
+    const uint16_t ksz = rd16(h + 12);
+    const uint32_t vsz = rd32(h + 14);
+    const uint64_t rl = 18 + (uint64_t)ksz + (vsz == ORC_ENTRY_TOMBSTONE ? 0 : vsz);
+    if (len - pos < rl) break;
+    if (orc_xxh32(h + 4, rl - 4, 0) == rd32(h)) {
+      if (n + 22 + ksz > cap) return -1;
+      n += orc_hint_encode(rd64(h + 4), ksz, vsz, pos, h + 18, out + n);
+    }
+    pos += rl;
+  }
+  return (int64_t)n;
 }

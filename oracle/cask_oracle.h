@@ -105,6 +105,83 @@ int orc_replay_file_faithful(const char* data_path, const char* hint_path, uint3
 int orc_replay_buffer_fast(const uint8_t* buf, uint64_t len, uint32_t file_id, orc_index* ix,
                            orc_replay_result* res);
 
+/* Index::get (cask.rs:41-43): 1 and the entry if the key is live, else 0. */
+int orc_index_get(const orc_index* ix, const uint8_t* key, uint16_t ksz, uint32_t* file_id, uint64_t* pos,
+                  uint64_t* size, uint64_t* seq);
+
+/* ---- compaction merge: Cask::compact_files_aux (cask.rs:451-523) ---- */
+typedef struct {
+  uint32_t n_compacted;  /* files with a valid hint file (compacted_files) */
+  uint32_t n_new;        /* files started by live records (new_files, cask.rs:510-512) */
+  uint32_t n_tomb_only;  /* files started by the tombstone tail (not in new_files, cask.rs:518-520) */
+  uint32_t file_id_seq;  /* the id sequence after the call (Sequence, util.rs:55-65) */
+  uint64_t n_out;        /* files written, in creation order (out_ids) */
+  uint64_t live_records, tombstones, bytes_out;
+  int32_t err_kind;      /* 0, ORC_ROW_CHECKSUM, ORC_ROW_EOF (read_entry / a hint cut short), -1 io */
+  uint32_t err_file_id;
+  uint64_t err_pos;
+  uint32_t err_expected, err_found;
+} orc_compact_result;
+
+/* compact_files_aux over `files` in the given order, reading data/hint files from src_dir and
+ * writing the new data/hint files (ids file_id_seq+1, ...) into dst_dir: per file with a valid hint
+ * file, every hint decides liveness against `ix` (index sequence == hint sequence, cask.rs:500) or
+ * records a tombstone of an absent key (highest sequence per key, cask.rs:487-499); the live
+ * entries are read back (Log::read_entry, log.rs:150-166: EOF / checksum errors end the call) and
+ * written through the LogWriter rollover (log.rs:282-306); the tombstones follow, in first-seen
+ * order (the reference's HashMap order is unspecified). out_ids/out_live (cap entries) receive the
+ * created files in order and whether a live record started each. Returns 0, or -1 with res->err_*.
+ * Nothing is removed from src_dir and `ix` is not updated. Test infrastructure only. */
+int orc_compact_files(const char* src_dir, const char* dst_dir, const orc_index* ix, const uint32_t* files,
+                      uint64_t nfiles, uint32_t file_id_seq, uint64_t max_file_size, uint32_t* out_ids,
+                      uint8_t* out_live, uint64_t cap, orc_compact_result* res);
+
+/* The same with liveness from any keydir: seq_of(ix, key, ksz, &seq) returns 1 and the key's
+ * sequence if the key is live (Index::get, cask.rs:41-43), else 0. */
+typedef int (*orc_seq_fn)(const void* ix, const uint8_t* key, uint16_t ksz, uint64_t* seq);
+int orc_compact_files_fn(const char* src_dir, const char* dst_dir, orc_seq_fn seq_of, const void* ix,
+                         const uint32_t* files, uint64_t nfiles, uint32_t file_id_seq, uint64_t max_file_size,
+                         uint32_t* out_ids, uint8_t* out_live, uint64_t cap, orc_compact_result* res);
+
+/* RecreateHints over one in-memory data file (log.rs:137-148, 449-471): the hint body (no trailer)
+ * into out; its length, or -1 if cap is too small. */
+int64_t orc_hint_body(const uint8_t* buf, uint64_t len, uint8_t* out, uint64_t cap);
+
+/* ---- Cask::open replay of many in-memory data files on host threads (cask_oracle_par.c) ---- */
+typedef struct {
+  uint64_t records;    /* rows folded */
+  uint64_t live;       /* keys in the keydir */
+  uint64_t max_seq;
+  uint64_t digest;     /* sum (mod 2^64) of orc_entry_digest over the keydir: order-independent */
+  uint64_t stats_rows; /* per-file Stats rows (may exceed the caller's cap) */
+  int32_t err_kind;    /* the first failure in replay order (0 none): open() stops there */
+  uint32_t err_file_id;
+  uint64_t err_pos;
+  uint32_t err_expected, err_found;
+} orc_parallel_result;
+
+/* One keydir entry's digest: splitmix64-chained over ksz, the key in 8-byte little-endian words
+ * (zero-padded), file_id, entry_pos, entry_size, sequence. orc_index_digest sums it over the live
+ * entries of an index. */
+uint64_t orc_entry_digest(const uint8_t* key, uint16_t ksz, uint32_t file_id, uint64_t pos, uint64_t size,
+                          uint64_t seq);
+uint64_t orc_index_digest(const orc_index* ix);
+
+/* The scan + Index::update fold of files bufs[0..nfiles) in that (replay) order, exactly as
+ * Cask::open without hint files (cask.rs:346-382, 60-90): files scanned on nthreads threads, the
+ * fold split by key over nthreads partitions. Stats rows (unsorted) go to st_* (st_cap entries). */
+int orc_replay_parallel(const uint8_t* const* bufs, const uint64_t* lens, const uint32_t* file_ids, uint32_t nfiles,
+                        uint32_t nthreads, orc_parallel_result* res, uint32_t* st_fid, uint64_t* st_e, uint64_t* st_d,
+                        uint64_t* st_b, uint64_t st_cap);
+/* The same, keeping the partitioned keydir for lookups (orc_pindex_seq, an orc_seq_fn) — e.g. the
+ * liveness of orc_compact_files_fn. */
+typedef struct orc_pindex orc_pindex;
+orc_pindex* orc_pindex_build(const uint8_t* const* bufs, const uint64_t* lens, const uint32_t* file_ids,
+                             uint32_t nfiles, uint32_t nthreads, orc_parallel_result* res, uint32_t* st_fid,
+                             uint64_t* st_e, uint64_t* st_d, uint64_t* st_b, uint64_t st_cap);
+int orc_pindex_seq(const void* pindex, const uint8_t* key, uint16_t ksz, uint64_t* seq);
+void orc_pindex_free(orc_pindex* p);
+
 #ifdef __cplusplus
 }
 #endif

@@ -204,3 +204,154 @@ def test_fold_random_cross_check(oracle_lib):
         py.update(R.Row(pos=pos, seq=seq, ksz=len(k), vsz_raw=vsz, key=k), fid)
     assert ix.export() == sorted([k.hex(), v.file_id, v.entry_pos, v.entry_size, v.sequence] for k, v in py.map.items())
     assert ix.stats() == sorted([f, *s] for f, s in py.stats.map.items())
+
+
+# ---------------------------------------------------------------------------------------------
+# The C oracle's compaction (orc_compact_files) and threaded replay (orc_replay_parallel), used as
+# the checkers of the full-size configs[3] / configs[4] GPU tests, pinned against the Python
+# restatement here at sizes it finishes in seconds.
+# ---------------------------------------------------------------------------------------------
+def _log_entries(rng, n, nkeys, p_del=0.1, vmax=300):
+    keys = [rng.randbytes(rng.randrange(1, 24)) for _ in range(nkeys)]
+    out = []
+    for i in range(n):
+        k = rng.choice(keys)
+        if rng.random() < p_del:
+            out.append(R.entry_deleted(i + 1, k))
+        else:
+            out.append(R.entry_new(i + 1, k, rng.randbytes(rng.randrange(0, vmax))))
+    return out
+
+
+def _py_index_to_oracle(db):
+    ix = O.Index()
+    # rebuild the keydir entries as they stand (one update per live key reproduces the entries)
+    for k, e in db.index.map.items():
+        ix.update(k, e.file_id, e.entry_pos, e.entry_size - 18 - len(k), e.sequence)
+    return ix
+
+
+@pytest.mark.parametrize("seed,mfs", [(1, 8 << 10), (2, 64 << 10), (3, 700)])
+def test_c_compaction_matches_restatement(oracle_lib, tmp_path, seed, mfs):
+    """orc_compact_files writes the same bytes as cask_ref.compact_files (both restate
+    compact_files_aux, cask.rs:451-523, with first-seen tombstone order): every new data and hint file,
+    the file ids and which files the live records started (new_files)."""
+    rng = random.Random(seed)
+    ents = _log_entries(rng, 4000, nkeys=600)
+    src, py = str(tmp_path / "src"), str(tmp_path / "py")
+    R.write_log(src, ents, max_file_size=mfs)
+    shutil.copytree(src, py)
+    db = R.replay(py)
+    ix = _py_index_to_oracle(db)
+    files = db.files[:-1] if len(db.files) > 1 else db.files
+    seq0 = db.file_id_seq
+    out = str(tmp_path / "c")
+    os.makedirs(out)
+    r, created = O.compact_files(src, out, ix, files, seq0, mfs)
+    assert r.err_kind == 0
+    compacted, new_files = R.compact_files(py, db, files, mfs)
+    assert r.n_compacted == len(compacted)
+    assert [f for f, live in created if live] == new_files
+    assert r.file_id_seq == db.file_id_seq
+    for fid, _ in created:
+        for ext in ("data", "hint"):
+            a = open(os.path.join(out, f"{fid:010}.cask.{ext}"), "rb").read()
+            b = open(os.path.join(py, f"{fid:010}.cask.{ext}"), "rb").read()
+            assert a == b, (fid, ext)
+
+
+def test_c_compaction_reports_corrupt_live_entry(oracle_lib, tmp_path):
+    """A live record whose bytes no longer verify ends compaction with InvalidChecksum at its
+    position (Log::read_entry, log.rs:150-166), as the restatement's read_entry does."""
+    rng = random.Random(5)
+    ents = _log_entries(rng, 1500, nkeys=200)
+    src = str(tmp_path / "src")
+    R.write_log(src, ents, max_file_size=16 << 10)
+    db = R.replay(src)
+    ix = _py_index_to_oracle(db)
+    fid = db.files[0]
+    live = [(k, e) for k, e in db.index.map.items() if e.file_id == fid]
+    k, e = live[len(live) // 2]
+    p = R.data_file_path(src, fid)
+    b = bytearray(open(p, "rb").read())
+    b[e.entry_pos + 18 + len(k) - 1 if e.entry_size == 18 + len(k) else e.entry_pos + e.entry_size - 1] ^= 0x40
+    open(p, "wb").write(bytes(b))
+    out = str(tmp_path / "c")
+    os.makedirs(out)
+    r, _ = O.compact_files(src, out, ix, [fid], db.file_id_seq, 16 << 10)
+    with pytest.raises(R.CaskError) as ex:
+        R.compact_files(src, R.replay(src, write_hints=False), [fid], 16 << 10)
+    err = ex.value
+    assert (r.err_kind, r.err_file_id) == ((1 if err.kind == "checksum" else 2), fid)
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_parallel_replay_matches_serial(oracle_lib, threads):
+    """orc_replay_parallel (scan on threads, fold split by key) equals the serial fold of the same
+    files in order: keydir digest, size, stats, max sequence — with overwrites, stale and
+    resurrecting tombstones across files — and stops at the first failure in replay order."""
+    rng = random.Random(100 + threads)
+    ents = _log_entries(rng, 6000, nkeys=400, p_del=0.15)
+    rng.shuffle(ents)  # sequences out of order across files: stale records and tombstones
+    bufs, fids = [], []
+    for i in range(0, len(ents), 700):
+        bufs.append(b"".join(e.write_bytes() for e in ents[i:i + 700]))
+        fids.append(len(fids) + 3)
+    ix = O.Index()
+    mx = 0
+    for b, f in zip(bufs, fids):
+        rr = O.replay_fast(np.frombuffer(b, np.uint8), f, ix)
+        assert rr.err_kind == 0
+        mx = max(mx, rr.max_seq)
+    r, stats = O.replay_parallel(bufs, fids, threads)
+    assert r.err_kind == 0 and r.records == len(ents)
+    assert (r.live, r.max_seq, r.digest) == (len(ix), mx, ix.digest())
+    assert stats == ix.stats()
+    # a corrupted record in file 3: the fold stops there (rows before it still count)
+    bad = bytearray(bufs[3])
+    bad[len(bad) // 2] ^= 0x01
+    bufs2 = bufs[:3] + [bytes(bad)] + bufs[4:]
+    r2, _ = O.replay_parallel(bufs2, fids, threads)
+    want = O.scan(bytes(bad))
+    first = want[want["status"] != 0][0]
+    assert (r2.err_kind, r2.err_file_id, r2.err_pos) == (int(first["status"]), fids[3], int(first["pos"]))
+
+
+def test_keydir_digest_numpy_equals_c(oracle_lib):
+    """The vectorised digest the GPU tests apply to a product export equals the C oracle's."""
+    rng = np.random.default_rng(3)
+    n = 1000
+    keys = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    fid = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    pos, size, seq = (rng.integers(0, 1 << 63, n, dtype=np.uint64) for _ in range(3))
+    want = 0
+    for i in range(n):
+        want = (want + O.entry_digest(keys[i].tobytes(), int(fid[i]), int(pos[i]), int(size[i]), int(seq[i]))) % (1 << 64)
+    got = O.keydir_digest_np(keys, np.full(n, 16), fid, pos, size, seq)
+    assert got == want
+
+
+def test_pindex_compaction_equals_serial_index(oracle_lib, tmp_path):
+    """Compaction with the threaded replay's keydir (orc_pindex) writes the same files as with the
+    serial one, and orc_hint_body reproduces the restatement's recreated hint bodies."""
+    rng = random.Random(21)
+    ents = _log_entries(rng, 3000, nkeys=500)
+    src = str(tmp_path / "src")
+    R.write_log(src, ents, max_file_size=8 << 10)
+    db = R.replay(src, write_hints=False)
+    bufs = [np.fromfile(R.data_file_path(src, f), np.uint8) for f in db.files]
+    for b, f in zip(bufs, db.files):
+        body = open(R.hint_file_path(src, f), "rb").read()[:-4]
+        assert O.hint_body(b).tobytes() == body
+    pix = O.PIndex(bufs, db.files, 4)
+    ix = _py_index_to_oracle(db)
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    os.makedirs(a)
+    os.makedirs(b)
+    r1, c1 = pix.compact_files(src, a, db.files, db.file_id_seq, 8 << 10)
+    r2, c2 = O.compact_files(src, b, ix, db.files, db.file_id_seq, 8 << 10)
+    assert r1.err_kind == r2.err_kind == 0 and c1 == c2 and r1.live_records == r2.live_records
+    assert sorted(os.listdir(a)) == sorted(os.listdir(b))
+    for f in os.listdir(a):
+        assert open(os.path.join(a, f), "rb").read() == open(os.path.join(b, f), "rb").read(), f
+    assert pix.result.live == len(db.index.map)

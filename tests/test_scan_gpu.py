@@ -325,7 +325,8 @@ def test_long_record_hash_every_length_residue(gpu_ctx):
 
 
 def test_records_past_walk_hash_limit(gpu_ctx):
-    """Records over 2 MiB (the walk leaves them to k_long_hash) between short ones, one corrupted."""
+    """Records over 2 MiB (the chunk scan leaves them to k_long_hash; k_walk_hash hashes them in
+    stride, past their run's end) between short ones, one corrupted."""
     rng = random.Random(48)
     recs = []
     for i, vsz in enumerate([40, 2_500_000, 17, 2_200_000, 3000, 2_097_200, 9]):
@@ -334,7 +335,8 @@ def test_records_past_walk_hash_limit(gpu_ctx):
             rec[18 + 16 + 777_777] ^= 0x10
         recs.append(bytes(rec))
     check_against_oracle(gpu_ctx, [b"".join(recs)], device=True)
-    assert gpu_ctx.last_counters()["long_records"] >= 3
+    cnt = gpu_ctx.last_counters()
+    assert cnt["long_records"] >= 3 or cnt["walk_mode"] == 1, cnt
 
 
 def test_many_files_empty_and_tiny(gpu_ctx):

@@ -106,3 +106,29 @@ def test_log_write_empty(tmp_path):
     from cask_amd.writer import log_write
     assert log_write(str(tmp_path), [], 1 << 20) == []
     assert os.listdir(str(tmp_path)) == []
+
+
+def test_log_write_no_hints_over_stale_hint_files(tmp_path):
+    """write_hints=False over a directory whose ids already have valid hint files (from other
+    data): those hint files go, so the next open scans the new data instead of trusting hints that
+    describe other bytes (the reference's HintWriter::new truncates them, log.rs:373-380)."""
+    from cask_amd import CaskOptions
+    from cask_amd.writer import log_write
+    rng = random.Random(11)
+    old = _entries(rng, 1500, nkeys=200)
+    new = _entries(random.Random(12), 1500, nkeys=900)
+    a, b = str(tmp_path / "a"), str(tmp_path / "b")
+    os.makedirs(a)
+    log_write(a, [(e.sequence, e.key, None if e.deleted else e.value) for e in old], 16 << 10)
+    assert any(f.endswith(".hint") for f in os.listdir(a))
+    log_write(a, [(e.sequence, e.key, None if e.deleted else e.value) for e in new], 16 << 10, write_hints=False)
+    R.write_log(b, new, max_file_size=16 << 10)
+    # files of the old log beyond the new one's ids keep their data and hints: drop them from both sides
+    keep = set(os.listdir(b)) | {f.replace(".hint", ".data") for f in os.listdir(b)}
+    for f in os.listdir(a):
+        if f.replace(".hint", ".data") not in keep:
+            os.remove(os.path.join(a, f))
+    with CaskOptions().max_file_size(16 << 10).open(a) as db:
+        rdb = R.replay(b)
+        assert {k: e.sequence for k, e in db.index().items()} == {k: v.sequence for k, v in rdb.index.map.items()}
+    assert _dir(a) == _dir(b)
