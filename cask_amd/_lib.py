@@ -146,6 +146,11 @@ SIGNATURES = [
     ("cask_shard_keydir", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                     C.POINTER(C.c_void_p), c_u64p]),
     ("cask_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_rccl_unique_id", C.c_int, [C.c_void_p]),
+    ("cask_rccl_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
+    ("cask_rccl_comm_destroy", C.c_int, [C.c_void_p]),
+    ("cask_keydir_gather_rccl", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_int, C.c_void_p,
+                                          c_u64p, c_u64p]),
     ("cask_hints_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                     C.c_void_p, C.c_uint64, c_u64p]),
     ("cask_keydir_new", C.c_void_p, []),

@@ -414,6 +414,17 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
       // the run's first segment starts at its searched start; a later one starts a file (b0 == 0)
       uint64_t p = W.S.b0 == 0 ? 0ull : a.walk_pre ? a.tin[W.S.t0] : kNone;
       bool term = false;
+      // The next record's header is loaded before this record's stores go out: a wait for a load
+      // also waits for every store issued before it (one vmcnt counts both), so loading after the
+      // stores would cost each hop a store round trip as well. Headers past the file's end are not
+      // read (an address inside the file is loaded instead).
+      const bool has = p != kNone && p < W.S.b1;
+      const uint64_t p0 = has && p + 18 <= W.S.len ? p : 0ull;
+      u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
+      uint32_t vsz = gld4g((const g_u8*)(W.S.data + p0 + 14));
+      // (waited for here, so that the loop's own wait counts the hop's load behind its stores: with
+      // this path arriving at the loop with loads outstanding, it would wait for everything)
+      asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w), "v"(vsz));
       while (p != kNone && p < W.S.b1) {
         uint32_t j = 0;
         if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
@@ -424,19 +435,22 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
           term = true;
           break;
         }
-        const u32x4 h = gld16g((const g_u8*)(W.S.data + p));
-        const uint32_t vsz = gld4g((const g_u8*)(W.S.data + p + 14));
         const uint32_t ksz = h.w & 0xFFFFu;
         const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+        const u32x4 row = u32x4{h.y, h.z, vsz, ksz};
+        const uint64_t pn = p + rl;
+        const uint64_t pl = pn + 18 <= W.S.len ? pn : 0ull;  // (pn < p: rl wrapped, impossible)
+        h = gld16g((const g_u8*)(W.S.data + pl));
+        vsz = gld4g((const g_u8*)(W.S.data + pl + 14));
         const uint32_t r = open_record(a, W, p, csh, true, &j);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{h.y, h.z, vsz, ksz | (off << 16)};
-        if (p + rl > W.S.len) {  // key or value cut short (data.rs:172,181)
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
+        if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
           if (r < W.ccerr) W.ccerr = r;
           term = true;
           break;
         }
-        p += rl;
+        p = pn;
       }
       close_segment(a, W, term ? kTerm : p, true);
     }
@@ -468,7 +482,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t* pf0 = s_pf[wv][0];
   uint32_t* pf1 = s_pf[wv][1];
   const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
-  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;
 
   // The wave's record stream (uniform): two run slots, the one records are handed out from (cs) and
   // its cursor (cur); a slot is refilled from the claim counter once the other one runs low.
@@ -586,7 +599,9 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     const unsigned long long wm = __ballot(qlead && want) & qmask;
     const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
     if (nw) {
-      const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (lane ? (~0ull >> (64 - (lane & ~3u))) : 0ull));
+      // quads before this one that want a record (the same in the quad's four lanes)
+      const uint32_t l0 = lane & ~3u;
+      const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (l0 ? (~0ull >> (64 - l0)) : 0ull));
       const uint32_t rem = rn[cs] - cur;
       const uint32_t so = cs ^ 1;
       const bool up = myrank >= rem;
@@ -615,7 +630,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         cur += used;
       }
     }
-    (void)below;
     // ---- mix the round in hand
     if (cv) {
 #pragma unroll

@@ -369,6 +369,23 @@ cask_db* cask_keydir_new(void);
 int cask_keydir_merge(cask_db* db, const uint8_t* block, uint64_t bytes);
 int cask_keydir_finish(cask_db* db);
 
+/* RCCL over xGMI (no torch needed): a communicator per rank from a unique id that one rank makes
+ * and the caller distributes (any side channel: MPI, a file, a TCP socket), then the rooted gather of
+ * the ranks' keydir blocks. Every rank calls cask_keydir_gather_rccl with its block (device memory,
+ * from cask_shard_keydir); the sizes go round by ncclAllGather, the blocks to `root` by grouped
+ * ncclSend/ncclRecv (one message per rank, each over its own xGMI link), the maximum sequence by
+ * ncclAllReduce(max) (*max_seq, on every rank, may be NULL). On `root`, `db` (cask_keydir_new) gets
+ * the blocks merged in rank order — rank order must be replay order (contiguous file-id ranges) —
+ * and the caller then calls cask_keydir_finish. *gathered: the bytes the root received (its own
+ * block's size elsewhere). Replaces rank 0's side of the replay loop (cask.rs:346-382) for a sharded
+ * open. */
+#define CASK_RCCL_ID_BYTES 128
+int cask_rccl_unique_id(uint8_t* id /* CASK_RCCL_ID_BYTES */);
+int cask_rccl_comm_init(const uint8_t* id, int nranks, int rank, int device, void** comm);
+int cask_rccl_comm_destroy(void* comm);
+int cask_keydir_gather_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, int root, cask_db* db,
+                            uint64_t* gathered, uint64_t* max_seq);
+
 /* Cask::open over several GPUs of this process (replaces cask.rs:346-382 like cask_db_open): the
  * data files are split into contiguous ranges, one per entry of `devices` (a device may appear more
  * than once: its shards run one after another); within a range, files with a valid hint file are
