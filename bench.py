@@ -2,14 +2,28 @@
 """Headline benchmark: device-resident Cask data-file scan (decode + XXH32 verify + row emit).
 
 Metric (BASELINE.json): GiB/s of log bytes checksum-verified + decoded, device-resident. A step is
-one pass of the scan over one batch: BASELINE configs[1] per GPU (8 data files x 1,073,741,820 B,
-3,702,558 records of 16 B key + 256 B value each), already resident in HBM. With N GPUs each rank
-scans its own 8 files (weak scaling; data files shard with no collective). Rank 0 prints one JSON
-line with the roofline of the dominant kernel (k_scan_chunks, HIP events inside the library) and
-the CPU baseline (the oracle's reference-faithful replay, timed on this host, rank 0, N=1 only).
+one pass of the scan (cask_scan_device: Entries::next + Entry::from_read, log.rs:403-429,
+data.rs:161-206) over one batch of data files already resident in HBM.
+
+  N = 1   BASELINE configs[2], the largest single-GPU configuration: 32 GiB of records with 16-B
+          keys and Zipf(1.1) value sizes 16 B .. 64 KiB, rolled over into files of at most 2 GiB
+          (the reference's default max_file_size, cask.rs:225; LogWriter rollover, log.rs:282-306).
+  N > 1   BASELINE configs[4]: 256 GiB across 256 data files over 8 GPUs, i.e. one shard of
+          32 x 1 GiB files per rank (the same record distribution as configs[2], so per-GPU work is
+          the same at every N: weak scaling). Data files shard with no collective; after the timed
+          loop each rank reduces its rows to a keydir block and the blocks meet on rank 0 over RCCL
+          through the library's C ABI (cask_keydir_gather_rccl), timed separately.
+
+Rank 0 prints one JSON line with the roofline of the dominant kernel (k_run_hash on these shapes,
+HIP events inside the library on the stream it launches on) and, at N = 1, the CPU baseline (the
+oracle's reference-faithful replay of a bounded sample of the same files, timed on this host).
+Secondary numbers (configs[1], host-resident end to end) go in extra keys, never in `value`.
 
   python bench.py [--gpus N] [--steps K] [--warmup W]
   torchrun --nproc-per-node N bench.py --gpus N ...      (driver, N>1)
+
+Every CASK_* variable in the environment is printed in the line; the library's tuning knobs are
+refused unless --allow-tuning is given (never for a headline).
 """
 from __future__ import annotations
 
@@ -25,70 +39,75 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md (8.0 TB/s spec)
+CFG2_GIB, CFG2_MAX_FILE = 32.0, 2 ** 31
+CFG4_FILES_PER_RANK, CFG4_FILE = 32, 2 ** 30
+SEQ_STRIDE = 1 << 40  # a rank's first sequence / key id (ranks' ranges disjoint and in rank order)
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # (a step is ~1.7 ms: 100 steps keep host hiccups out of the number and still take 0.2 s)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--files", type=int, default=8, help="data files per GPU (configs[1]: 8)")
-    ap.add_argument("--records-per-file", type=int, default=3_702_558)
+    # (a step is ~8 ms: 50 steps keep host hiccups out of the number and still take 0.4 s)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-files", type=int, default=1, help="files timed by the CPU baseline")
+    ap.add_argument("--cpu-sample-files", type=int, default=2, help="configs[2] files timed by the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (H2D+D2H) measurement")
-    ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--no-cfg1", action="store_true", help="skip the secondary configs[1] measurement")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the keydir gather + fold after the loop")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: gloo (blocks gathered through host memory)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (a one-GPU box)")
-    ap.add_argument("--no-segmented", action="store_true",
-                    help="skip the segmented-output measurement (profiling runs: dense-path launches only)")
+    ap.add_argument("--allow-tuning", action="store_true",
+                    help="run with CASK_* tuning variables set (diagnostics; the line says so)")
     return ap.parse_args()
 
 
-def cpu_baseline(files, nfiles: int):
+def cask_env(allow: bool) -> dict:
+    env = {k: v for k, v in sorted(os.environ.items()) if k.startswith("CASK_")}
+    if env and not allow:
+        raise SystemExit(f"bench.py: refusing to time with library tuning variables set: {env} "
+                         f"(unset them, or pass --allow-tuning for a diagnostic run)")
+    return env
+
+
+def cpu_baseline(files, nfiles: int, cfg: str):
     """The oracle's reference-faithful replay (read(2) per header/key/value, 5 write(2) per hint,
-    Index::update fold; 1 thread as in cask.rs:348) over `nfiles` of the workload's files."""
+    Index::update fold; 1 thread as in cask.rs:348) over `nfiles` of the workload's files, written
+    to memory-backed files first (the page cache of a real replay)."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_ffi as O
     O.load()
-    tmp = tempfile.mkdtemp(prefix="cask_cpu_")
+    tmp = tempfile.mkdtemp(prefix="cask_cpu_", dir="/dev/shm" if os.path.isdir("/dev/shm") else None)
     paths = []
     total = 0
-    for f in files[:nfiles]:
-        p = os.path.join(tmp, f"{f.file_id:010}.cask.data")
-        f.data.cpu().numpy().tofile(p)
-        paths.append((f.file_id, p))
-        total += f.data.numel()
-    # warm the page cache, as the reference's replay would read files already on disk
-    for _, p in paths:
-        with open(p, "rb") as fh:
-            while fh.read(1 << 24):
-                pass
-    ix = O.Index()
-    t0 = time.perf_counter()
-    recs = 0
-    for fid, p in paths:
-        r = O.replay_faithful(p, p.replace(".cask.data", ".cask.hint"), fid, ix)
-        assert r.err_kind == 0, r.err_kind
-        recs += r.records
-    dt = time.perf_counter() - t0
-    # fast restatement (context only): mmap-style tight loop, 1 core
-    buf = np.fromfile(paths[0][1], dtype=np.uint8)
-    ix2 = O.Index()
-    t1 = time.perf_counter()
-    O.replay_fast(buf, paths[0][0], ix2)
-    dt_fast = time.perf_counter() - t1
-    del ix, ix2
-    for _, p in paths:
-        os.remove(p)
-        h = p.replace(".cask.data", ".cask.hint")
-        if os.path.exists(h):
-            os.remove(h)
-    os.rmdir(tmp)
+    try:
+        for f in files[:nfiles]:
+            p = os.path.join(tmp, f"{f.file_id:010}.cask.data")
+            f.data.cpu().numpy().tofile(p)
+            paths.append((f.file_id, p))
+            total += f.data.numel()
+        ix = O.Index()
+        t0 = time.perf_counter()
+        recs = 0
+        for fid, p in paths:
+            r = O.replay_faithful(p, p.replace(".cask.data", ".cask.hint"), fid, ix)
+            assert r.err_kind == 0, r.err_kind
+            recs += r.records
+        dt = time.perf_counter() - t0
+        # fast restatement (context only): mmap-style tight loop over the first file, 1 core
+        buf = np.fromfile(paths[0][1], dtype=np.uint8)
+        ix2 = O.Index()
+        t1 = time.perf_counter()
+        O.replay_fast(buf, paths[0][0], ix2)
+        dt_fast = time.perf_counter() - t1
+        del ix, ix2, buf
+    finally:
+        for name in os.listdir(tmp):
+            os.remove(os.path.join(tmp, name))
+        os.rmdir(tmp)
     cpu = "unknown"
     try:
         with open("/proc/cpuinfo") as fh:
@@ -100,27 +119,88 @@ def cpu_baseline(files, nfiles: int):
         pass
     return {
         "value": total / dt / 2 ** 30, "unit": "GiB/s", "cores": 1, "kind": "port",
-        "sample": f"{nfiles} of the {len(files)} configs[1] files ({total} B, {recs} records) on disk, warm page "
-                  f"cache; oracle/cask_oracle.c orc_replay_file_faithful = Cask::open scan path without hint "
-                  f"files (3 read(2) + 5 write(2) + fold per record)",
+        "sample": f"{nfiles} of the {len(files)} {cfg} files ({total} B, {recs} records) in memory-backed "
+                  f"files (warm page cache); oracle/cask_oracle.c orc_replay_file_faithful = Cask::open's scan "
+                  f"path without hint files (3 read(2) + 5 write(2) + fold per record)",
         "seconds": dt, "host_cpu": cpu, "nproc": os.cpu_count(),
-        "fast_restatement_gibps_1core": buf.size / dt_fast / 2 ** 30,
+        "fast_restatement_gibps_1core": files[0].data.numel() / dt_fast / 2 ** 30,
     }
 
 
-def load_traffic():
-    """Per-launch HBM bytes of k_scan_chunks from the committed rocprofv3 PMC pass (see
-    profiles/README.md); null when absent."""
+def load_traffic(kernel: str):
+    """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/pmc_summary.py); null when absent."""
     p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None, None
     with open(p) as f:
         d = json.load(f)
-    return d.get("hbm_bytes_per_launch"), d.get("source")
+    k = d.get("kernels", {}).get(kernel)
+    if not k:
+        return None, None
+    return k.get("hbm_bytes_per_launch"), k.get("source")
+
+
+def check_rows(torch, rows, res, files, vsz, rl, first_seq):
+    """Parity gate before timing: every record found, in order, at its offset, with its sequence,
+    sizes and a passing checksum (the generator's own view of the files)."""
+    n = res.count
+    dev = rows["seq"].device
+    assert res.error is None
+    assert int((rows["status"][:n] != 0).sum().item()) == 0
+    seq = rows["seq"][:n].to(torch.int64)
+    assert bool((seq == torch.arange(first_seq, first_seq + n, device=dev)).all())
+    assert bool((rows["vsz"][:n].to(torch.int64) == vsz[:n].to(torch.int64)).all())
+    assert bool((rows["ksz"][:n].to(torch.int64) == 16).all())
+    for i, (_, idx) in enumerate(files):
+        rlf = rl[idx]
+        want = torch.cumsum(rlf, 0) - rlf
+        assert bool((rows["pos"][res.file_row_offset[i]:res.file_row_offset[i + 1]].to(torch.int64) == want).all()), i
+
+
+def time_loop(torch, dev, run, timings, steps, barrier, dist, backend):
+    tbuf = [(C.c_float * 8)() for _ in range(steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        run()
+        timings(tbuf[i])
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    return elapsed, [[float(x) for x in t] for t in tbuf]
+
+
+def cfg1_secondary(ctx, torch, dev, steps):
+    """configs[1] (8 x 1 GiB of fixed 290-B records): the regular-chunk path, for reference."""
+    from cask_amd.workloads import cfg2_files
+    fs = cfg2_files(ctx)
+    torch.cuda.synchronize(dev)
+    views = [(f.file_id, f.data) for f in fs]
+    n = sum(f.nrec for f in fs)
+    rows = ctx.alloc_rows(n)
+    res = ctx.scan_device(views, rows)
+    assert res.count == n and res.error is None
+    assert int((rows["status"][:n] != 0).sum().item()) == 0
+    run, timings = ctx.prepare_scan(views, rows)
+    for _ in range(3):
+        run()
+    el, tt = time_loop(torch, dev, run, timings, steps, lambda: torch.cuda.synchronize(dev), None, "nccl")
+    nb = sum(f.data.numel() for f in fs)
+    k = sum(t[1] for t in tt) / len(tt)
+    out = {"gibps": nb * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps, "kernel": "k_scan_chunks",
+           "kernel_ms_avg": k, "kernel_frac_of_8TBps": nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS, "bytes": nb}
+    del fs, views, rows
+    torch.cuda.empty_cache()
+    return out
 
 
 def main():
     args = parse()
+    env = cask_env(args.allow_tuning)
     import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -142,7 +222,7 @@ def main():
     import hashlib
     import cask_amd
     from cask_amd import ScanContext
-    from cask_amd.workloads import CFG2_KSZ, CFG2_VSZ, fixed_file
+    from cask_amd.workloads import zipf_files
     # only the in-tree product build is ever timed (no environment variable selects another)
     lib_path = cask_amd._lib.loaded_path()
     if lib_path != cask_amd.LIB_PATH:
@@ -151,25 +231,31 @@ def main():
         lib_sha = hashlib.sha256(fh.read()).hexdigest()
 
     ctx = ScanContext(dev.index)
-    rpf = args.records_per_file
-    rl = 18 + CFG2_KSZ + CFG2_VSZ
-    files = []
-    for i in range(args.files):
-        fid = rank * args.files + i + 1  # contiguous file-id range per rank
-        seq0 = 1 + (fid - 1) * rpf
-        files.append(fixed_file(ctx, fid, rpf, CFG2_KSZ, CFG2_VSZ, seq0, seq0, 0xC0FFEE + fid, device=dev))
+    if world == 1:
+        cfg = "configs[2]"
+        first_seq, first_key, first_fid = 1, 0, 1
+        files, vsz, n, rl = zipf_files(ctx, CFG2_GIB, CFG2_MAX_FILE)
+    else:  # one rank's shard of configs[4]: 32 x 1 GiB, file ids rank*32+1.., sequences after rank-1's
+        cfg = "configs[4]"
+        first_seq, first_key, first_fid = 1 + rank * SEQ_STRIDE, rank * SEQ_STRIDE, 1 + rank * CFG4_FILES_PER_RANK
+        files, vsz, n, rl = zipf_files(ctx, CFG4_FILES_PER_RANK * CFG4_FILE / 2 ** 30, CFG4_FILE,
+                                       seed=0x5A1F + rank, first_file_id=first_fid, first_seq=first_seq,
+                                       first_key=first_key)
     torch.cuda.synchronize(dev)
-    views = [(f.file_id, f.data) for f in files]
-    bytes_per_step = sum(f.data.numel() for f in files)
-    rows = ctx.alloc_rows(args.files * rpf)
+    views = [(f.file_id, f.data) for f, _ in files]
+    bytes_per_step = sum(f.data.numel() for f, _ in files)
+    nfiles = len(views)
+    rows = ctx.alloc_rows(n + 16)
 
-    # correctness gate before timing: every record verifies, count exact
+    # correctness gate before timing (every rank): rows equal the generator's records
     res = ctx.scan_device(views, rows)
-    assert res.count == args.files * rpf and res.error is None, (res.count, res.error)
-    assert int((rows["status"][:res.count] != 0).sum().item()) == 0
+    assert res.count == n, (res.count, n)
+    check_rows(torch, rows, res, files, vsz, rl, first_seq)
+    counters = ctx.last_counters()
 
+    run, timings = ctx.prepare_scan(views, rows)
     for _ in range(args.warmup):
-        ctx.scan_device(views, rows)
+        run()
 
     def barrier():
         torch.cuda.synchronize(dev)
@@ -179,48 +265,27 @@ def main():
 
     # the timed loop issues the same C call a compiled caller would (arguments built once); each
     # step's phase times (HIP events inside the library) are copied out of the context after it
-    run, timings = ctx.prepare_scan(views, rows)
-    tbuf = [(C.c_float * 6)() for _ in range(args.steps)]
-    barrier()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        run()
-        timings(tbuf[i])
-    barrier()
-    elapsed = time.perf_counter() - t0
-    k1_ms = [float(t[1]) for t in tbuf]  # cask_last_timings: [0] pipeline, [1] chunk scan
-    pipe_ms = [float(t[0]) for t in tbuf]
-    if dist is not None:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.dist_backend == "nccl" else "cpu")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed, tt = time_loop(torch, dev, run, timings, args.steps, barrier, dist, args.dist_backend)
     ms_per_step = elapsed * 1e3 / args.steps
-    total_bytes = bytes_per_step * world * args.steps
-    value = total_bytes / elapsed / 2 ** 30
+    value = bytes_per_step * world * args.steps / elapsed / 2 ** 30
 
-    k1_avg = sum(k1_ms) / len(k1_ms)
-    achieved = bytes_per_step / (k1_avg * 1e-3) / 1e9  # algorithmic GB/s of the dominant kernel
-    traffic, traffic_src = load_traffic()
-
-    extra = {"pipeline_breakdown_ms": ctx.last_timings(),
+    walk = bool(counters.get("walk_mode"))
+    kname = "k_run_hash" if walk else "k_scan_chunks"
+    k_avg = sum(t[1] for t in tt) / len(tt)
+    achieved = bytes_per_step / (k_avg * 1e-3) / 1e9  # algorithmic GB/s of the dominant kernel
+    traffic, traffic_src = load_traffic(kname)
+    names = ["pipeline_ms", "hash_or_chunk_scan_ms", "long_ms", "validate_ms", "repair_ms", "compact_ms",
+             "search_ms", "chase_ms"]
+    breakdown = {nm: sum(t[i] for t in tt) / len(tt) for i, nm in enumerate(names)}
+    extra = {"pipeline_breakdown_ms": breakdown,
              # SURVEY §8d's definition: device time from the first to the last kernel of a step
              # (HIP events), per GPU; `value` above is the wall clock, host gap included
-             "device_gibps_per_gpu": bytes_per_step / (sum(pipe_ms) / len(pipe_ms) * 1e-3) / 2 ** 30}
-    counters = ctx.last_counters()
-    # segmented output (no dense compaction; every slot row written), same files, same clock
-    if not args.no_segmented:
-        ctx.scan_device_segmented(views)
-        barrier()
-        ts = time.perf_counter()
-        for _ in range(args.steps):
-            ctx.scan_device_segmented(views)
-        barrier()
-        extra["segmented_gibps"] = bytes_per_step * world * args.steps / (time.perf_counter() - ts) / 2 ** 30
-    # keydir block of this rank's files, and the blocks gathered on rank 0 over RCCL,
-    # reported separately from the metric; any failure here is reported, not fatal to the line
+             "device_gibps_per_gpu": bytes_per_step / (breakdown["pipeline_ms"] * 1e-3) / 2 ** 30}
+
+    # N>1: this rank's keydir block and the blocks' gather + rank-0 fold over RCCL through the C ABI
+    # (cask_keydir_gather_rccl), reported apart from the metric; a failure is reported, not fatal
     if dist is not None and not args.no_gather:
         try:
-            from cask_amd.distributed import gather_blocks
             from cask_amd.keydir import shard_keydir
             res = ctx.scan_device(views, rows)
             barrier()
@@ -228,45 +293,75 @@ def main():
             blk = shard_keydir(ctx, views, rows, res.count, res.file_row_offset)
             barrier()
             tg = time.perf_counter()
-            got = gather_blocks(blk if args.dist_backend == "nccl" else blk.cpu(), dst=0)
-            barrier()
-            te = time.perf_counter()
-            extra["keydir_block_ms"] = (tg - tb) * 1e3
-            extra["keydir_gather_ms"] = (te - tg) * 1e3
-            extra["keydir_block_bytes_per_rank"] = int(blk.numel())
-            if rank == 0:
-                extra["keydir_gathered_bytes"] = int(sum(b.numel() for b in got))
-                # rank 0's fold of the blocks in rank order (host keydir, exact stats)
+            if args.dist_backend == "nccl" and not args.same_device:
+                from cask_amd.distributed import gather_fold_rccl, rccl_comm_from_dist
+                comm = rccl_comm_from_dist(dev.index)
+                barrier()
+                tg = time.perf_counter()
+                db, got, mx = gather_fold_rccl(ctx, comm, blk, root=0)
+                barrier()
+                te = time.perf_counter()
+                comm.close()
+                extra["keydir_gather"] = "cask_keydir_gather_rccl (RCCL over xGMI, C ABI; fold on rank 0 included)"
+            else:  # rehearsal: torch.distributed point-to-point, then the fold
+                from cask_amd.distributed import allreduce_max_seq, gather_blocks
                 from cask_amd.keydir import KeydirFold
-                tf = time.perf_counter()
-                fold = KeydirFold()
-                for b in got:
-                    fold.merge(b.cpu())
-                db = fold.finish()
-                extra["keydir_fold_ms"] = (time.perf_counter() - tf) * 1e3
+                got_b = gather_blocks(blk if args.dist_backend == "nccl" else blk.cpu(), dst=0)
+                mx = allreduce_max_seq(first_seq + n - 1, dev if args.dist_backend == "nccl" else "cpu")
+                db, got = None, sum(int(b.numel()) for b in got_b) if got_b else int(blk.numel())
+                if rank == 0:
+                    fold = KeydirFold()
+                    for b in got_b:
+                        fold.merge(b.cpu())
+                    db = fold.finish()
+                barrier()
+                te = time.perf_counter()
+                extra["keydir_gather"] = f"torch.distributed {args.dist_backend} rehearsal"
+            extra["keydir_block_ms"] = (tg - tb) * 1e3
+            extra["keydir_gather_fold_ms"] = (te - tg) * 1e3
+            extra["keydir_block_bytes_per_rank"] = int(blk.numel())
+            extra["keydir_max_seq"] = int(mx)
+            if rank == 0:
+                extra["keydir_gathered_bytes"] = int(got)
                 extra["keydir_live_keys"] = len(db)
+                # unique keys: every record of every rank is live
+                extra["keydir_ok"] = len(db) == n * world and db.current_sequence == int(mx) + 1
                 db.close()
-            del blk, got
+            del blk
         except Exception as e:  # noqa: BLE001 - reported in the line
             extra["keydir_gather_error"] = f"{type(e).__name__}: {e}"[:300]
 
-    # end-to-end: host-resident files -> H2D -> scan -> rows D2H (cask_scan_host)
+    # end-to-end: host-resident files -> H2D -> scan -> rows D2H (cask_scan_host), first 2 files
     if rank == 0 and not args.no_e2e:
-        host = [(f.file_id, f.data.cpu().numpy()) for f in files]
+        host = [(f.file_id, f.data.cpu().numpy()) for f, _ in files[:2]]
         ctx.scan_host(host[:1])
         te = time.perf_counter()
         hr = ctx.scan_host(host)
         e2e = time.perf_counter() - te
-        assert hr.count == args.files * rpf
-        extra["e2e_host_scan_gibps"] = bytes_per_step / e2e / 2 ** 30
-        extra["e2e_note"] = "cask_scan_host: pageable host buffers -> H2D -> scan -> 5 row arrays D2H, 1 GPU"
+        assert hr.count == res.file_row_offset[2] - res.file_row_offset[0]
+        extra["e2e_host_scan_gibps"] = sum(b.size for _, b in host) / e2e / 2 ** 30
+        extra["e2e_note"] = (f"cask_scan_host over the first 2 {cfg} files: pageable host buffers -> H2D -> "
+                             f"scan -> 5 row arrays D2H, 1 GPU")
         del host, hr
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(files, max(1, min(args.cpu_sample_files, len(files))))
+        cpu = cpu_baseline([f for f, _ in files], max(1, min(args.cpu_sample_files, len(files))), cfg)
+
+    if rank == 0 and world == 1 and not args.no_cfg1:
+        del res
+        rows = views = None
+        files = None
+        torch.cuda.empty_cache()
+        extra["configs1_secondary"] = cfg1_secondary(ctx, torch, dev, max(10, args.steps))
 
     if rank == 0:
+        if world == 1:
+            workload = ("configs[2]: 32 GiB, 16-B keys, Zipf(1.1) value sizes 16 B-64 KiB, files of <= 2 GiB "
+                        "(LogWriter rollover at the default max_file_size), 1-GPU device-resident scan")
+        else:
+            workload = (f"configs[4]: 32 x 1 GiB data files per GPU ({world} GPUs, {32 * world} files), "
+                        f"configs[2]'s record distribution, unique keys, device-resident scan per rank")
         line = {
             "metric": "GiB/s of log bytes CRC-verified+decoded, device-resident, at 1/2/4/8 GPUs",
             "value": value,
@@ -281,11 +376,10 @@ def main():
             "dtype": "u32",
             "data": "synthetic (device-generated records: splitmix64 keys/values, XXH32 seed 0 checksums)",
             "config": {
-                "workload": "configs[1]: 8 GiB across 8 data files, fixed 16B keys / 256B values, 1-GPU "
-                            "device-resident scan (per GPU; N GPUs scan N x 8 files)",
-                "files_per_gpu": args.files,
-                "records_per_file": rpf,
-                "record_bytes": rl,
+                "workload": workload,
+                "files_per_gpu": nfiles,
+                "records_per_gpu": n,
+                "mean_record_bytes": bytes_per_step / n,
                 "bytes_per_gpu": bytes_per_step,
                 "chunk_bytes": ctx.chunk_bytes(),
                 "checksum": "XXH32 seed 0 (the reference's twox-hash, not CRC32: SURVEY.md §0)",
@@ -293,19 +387,19 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_scan_chunks",
+                "kernel": kname,
                 "achieved": achieved,
                 "peak": HBM_PEAK_GBPS,
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": traffic,
                 "traffic_source": traffic_src,
-                "kernel_ms_avg": k1_avg,
+                "kernel_ms_avg": k_avg,
                 "algorithmic_bytes_per_launch": bytes_per_step,
-                "pipeline_ms_avg": sum(pipe_ms) / len(pipe_ms),
             },
             "cpu_baseline": cpu,
             "counters": counters,
+            "cask_env": env,
             "library": {"path": os.path.relpath(lib_path, ROOT), "sha256": lib_sha},
         }
         line.update(extra)

@@ -616,8 +616,13 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         }
         nt = (up ? rt0[so] : rt0[cs]) + lo;
         nr = idx - pf[lo];
-        nrow = *(const g_u32x4*)(slots + (nt * (uint64_t)a.slot_cap + nr) * 4);
-        ndesc = *(const g_u32x4*)(cd + 2 * nt);
+        // both addresses in registers before either load: otherwise the second address may be built
+        // in the first load's destination, a write that waits for every load in flight (the round)
+        uint64_t arow = (uint64_t)(uintptr_t)(slots + (nt * (uint64_t)a.slot_cap + nr) * 4);
+        uint64_t adesc = (uint64_t)(uintptr_t)(cd + 2 * nt);
+        asm volatile("" : "+v"(arow), "+v"(adesc));
+        nrow = *(const g_u32x4*)(uintptr_t)arow;
+        ndesc = *(const g_u32x4*)(uintptr_t)adesc;
         ns = 1;
       }
       const uint32_t avail = rem + (rfull[so] ? rn[so] : 0u);
@@ -737,22 +742,34 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(256), 0, (hipStream_t)stream, a, a.files);
 }
 
+template <uint32_t D>
+static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
+  // A persistent grid of exactly the resident workgroups: a workgroup beyond them would start only
+  // as the first ones finish, holding its first run (claimed by block index) until the end.
+  // CASK_HASH_WAVES (tuning knob) overrides the waves per CU.
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (getenv("CASK_HASH_WAVES")) per_cu = atoi(getenv("CASK_HASH_WAVES"));
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash<D>, 256, 0) == hipSuccess && nb > 0)
+      per_cu = 4 * nb;
+    if (per_cu <= 0) per_cu = 8;
+  }
+  uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
+  if (waves > nruns) waves = nruns;
+  hipLaunchKernelGGL((k_run_hash<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+}
+
 void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
   if (!a.total_chunks) return;
   const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
-  // CASK_HASH_WAVES (tuning knob): waves per CU of the persistent grid (the runs beyond its first
-  // are claimed)
-  static const uint32_t per_cu = getenv("CASK_HASH_WAVES") ? (uint32_t)atoi(getenv("CASK_HASH_WAVES")) : 16u;
-  uint64_t waves = (uint64_t)device_cus() * per_cu;
-  if (waves > nruns) waves = nruns;
-  const uint32_t grid = (uint32_t)((waves + 3) / 4);
   hipStream_t s = (hipStream_t)stream;
   if (depth == 16)
-    hipLaunchKernelGGL((k_run_hash<16>), dim3(grid), dim3(256), 0, s, a);
+    run_hash_at<16>(a, nruns, s);
   else if (depth == 4)
-    hipLaunchKernelGGL((k_run_hash<4>), dim3(grid), dim3(256), 0, s, a);
+    run_hash_at<4>(a, nruns, s);
   else
-    hipLaunchKernelGGL((k_run_hash<8>), dim3(grid), dim3(256), 0, s, a);
+    run_hash_at<8>(a, nruns, s);
 }
 
 }  // namespace cask_dev

@@ -115,7 +115,8 @@ class ScanContext:
         """A repeatable cask_scan_device call on the same device-resident files and rows, its ctypes
         arguments built once (what a compiled caller of the C ABI pays per call: the call itself).
         Returns (run, timings): run() issues the scan and returns the row count (raising on any
-        error); timings(out) copies the call's six phase times (ms) into a float array."""
+        error); timings(out) copies the call's eight phase times (ms, last_timings' order) into a
+        float array of 8."""
         n = len(files)
         views = (L.FileView * max(n, 1))()
         for i, (fid, t) in enumerate(files):
@@ -141,7 +142,7 @@ class ScanContext:
             return r.count
 
         def timings(out):
-            lib.cask_last_timings(h, out)
+            lib.cask_last_timings8(h, out)
 
         return run, timings
 

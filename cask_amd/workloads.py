@@ -84,11 +84,13 @@ def zipf_sizes(n: int, s: float = 1.1, kmax: int = 4096, seed: int = 0x5A1F, dev
     return (kk * 16).to(torch.int32)
 
 
-def zipf_files(ctx: ScanContext, total_gib: float = 32.0, max_file: int = 2 ** 31, seed: int = 0x5A1F):
+def zipf_files(ctx: ScanContext, total_gib: float = 32.0, max_file: int = 2 ** 31, seed: int = 0x5A1F,
+               first_file_id: int = 1, first_seq: int = 1, first_key: int = 0):
     """BASELINE configs[2]: ~total_gib GiB of records with 16 B keys and Zipf(1.1) value sizes
-    (16 B .. 64 KiB), sequences 1.., in files rolled over as LogWriter does (a new file when
-    pos + size > max_file_size, log.rs:282-306). Returns ([(DataFile, record indices)], vsz, n,
-    record lengths) — the generator's own view, for checking rows."""
+    (16 B .. 64 KiB), sequences first_seq.., key ids first_key.. (unique), in files rolled over as
+    LogWriter does (a new file when pos + size > max_file_size, log.rs:282-306), file ids
+    first_file_id... Returns ([(DataFile, record indices)], vsz, n, record lengths) — the
+    generator's own view, for checking rows (record i has sequence first_seq + i)."""
     torch = _torch()
     dev = torch.device("cuda", ctx.device)
     target = int(total_gib * 2 ** 30)
@@ -104,7 +106,8 @@ def zipf_files(ctx: ScanContext, total_gib: float = 32.0, max_file: int = 2 ** 3
         r1 = min(max(r1, r0 + 1), n)
         idx = torch.arange(r0, r1, dtype=torch.int64, device=dev)
         ks = torch.full((r1 - r0,), 16, dtype=torch.int16, device=dev)
-        f = variable_file(ctx, len(files) + 1, ks, vsz[r0:r1].clone(), idx + 1, idx, seed + len(files))
+        f = variable_file(ctx, first_file_id + len(files), ks, vsz[r0:r1].clone(), idx + first_seq,
+                          idx + first_key, seed + len(files))
         files.append((f, idx))
         base = int(cum[r1 - 1].item())
         r0 = r1

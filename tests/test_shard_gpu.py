@@ -214,3 +214,35 @@ def test_sharded_keydir_unique_keys_large(gpu_ctx):
         assert (e.file_id, e.entry_pos, e.entry_size, e.sequence) == (6, 580, 290, 1 + 5 * nrec + 2)
     del files
     torch.cuda.empty_cache()
+
+
+def test_rccl_c_abi_gather_single_rank(gpu_ctx, tmp_path):
+    """cask_keydir_gather_rccl on a one-rank communicator made through the C ABI (unique id, comm
+    init): the rank's block goes to itself and is folded there; keydir, stats and sequence equal the
+    replay, and the gathered byte count and max sequence are reported. (Two or more ranks need as
+    many GPUs: bench.py --gpus N runs it on the driver's node.)"""
+    import torch
+    from cask_amd.distributed import RcclComm, gather_fold_rccl, rccl_unique_id
+    path = str(tmp_path / "db")
+    _make_db(path, 9, nfiles=3)
+    files = _files(path)
+    want = _want(path)
+    tens = [(fid, torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()) for fid, b in files]
+    res = gpu_ctx.scan_device(tens)
+    assert res.error is None
+    from cask_amd.keydir import shard_keydir
+    blk = shard_keydir(gpu_ctx, tens, {"pos": res.pos, "seq": res.seq, "vsz": res.vsz, "ksz": res.ksz,
+                                       "status": res.status}, res.count, res.file_row_offset)
+    comm = RcclComm(rccl_unique_id(), 1, 0, gpu_ctx.device)
+    try:
+        db, got, mx = gather_fold_rccl(gpu_ctx, comm, blk, root=0)
+        with db:
+            assert _got(db) == want
+            assert mx == want[2] - 1
+        assert got == (blk.numel() + 255) // 256 * 256
+        # an empty block from the rank (no files) folds to an empty keydir
+        db2, got2, _ = gather_fold_rccl(gpu_ctx, comm, torch.empty(0, dtype=torch.uint8, device=blk.device))
+        with db2:
+            assert len(db2) == 0 and got2 == 0
+    finally:
+        comm.close()

@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call: full bench line, rocprofv3 kernel-trace stats, and two PMC passes (FETCH_SIZE,
-# WRITE_SIZE) for the HBM traffic of k_scan_chunks. Outputs under gpurun_out/; tools/pmc_summary.py
+# WRITE_SIZE) for the HBM traffic of the headline's dominant kernel (bench.py: configs[2]). Outputs under gpurun_out/; tools/pmc_summary.py
 # turns them into profiles/.
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out
@@ -17,7 +17,7 @@ if [ -z "$SKIP_BENCH" ]; then
   TAILN=1 step bench_full 600 python bench.py
 fi
 export TMPDIR=/tmp
-B="$R/bench.py --steps ${PSTEPS:-50} --warmup ${PWARM:-10} --no-cpu-baseline --no-e2e --no-segmented"
+B="$R/bench.py --steps ${PSTEPS:-20} --warmup ${PWARM:-3} --no-cpu-baseline --no-e2e --no-cfg1"
 rm -rf "$R/gpurun_out/prof_$TAG"
 TAILN=1 step prof_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG/kt" -o kt --output-format csv -- python3 $B
 step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_$TAG/fetch" -o fetch --output-format csv -- python3 $B

@@ -47,16 +47,22 @@ def main():
         lines.append(f"{k},{nf.get(k, 0)},{avg:.0f},{f2:.0f},{w:.0f},{f2 + w:.0f}")
     with open(os.path.join(out, f"{tag}_pmc_traffic.csv"), "w") as f:
         f.write("\n".join(lines) + "\n")
-    if len(sys.argv) > 2 and sys.argv[2] == "--no-json":  # another workload (e.g. configs[2]): tables only
-        print("\n".join(lines))
-        return
-    scan = next(k for k in table if k.startswith("k_scan_chunks"))
-    with open(os.path.join(out, "pmc_traffic.json"), "w") as f:
-        json.dump({"kernel": scan, "hbm_bytes_per_launch": table[scan]["hbm_bytes"],
-                   "fetch_bytes_per_launch": table[scan]["fetch_bytes"],
-                   "write_bytes_per_launch": table[scan]["write_bytes"],
-                   "source": f"profiles/{tag}_pmc_traffic.csv (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
-                             f"separate passes, bench.py configs[1])"}, f, indent=1)
+    # profiles/pmc_traffic.json: per kernel (short name without template arguments), merged into
+    # what is there; tools/pmc_summary.py TAG [WORKLOAD] [KERNEL,...]
+    workload = sys.argv[2] if len(sys.argv) > 2 else "bench.py"
+    want = sys.argv[3].split(",") if len(sys.argv) > 3 else ["k_run_hash", "k_scan_chunks"]
+    jp = os.path.join(out, "pmc_traffic.json")
+    doc = json.load(open(jp)) if os.path.exists(jp) else {}
+    kern = doc.get("kernels", {})
+    for k, t in table.items():
+        base = k.split("<")[0]
+        if base in want:
+            kern[base] = {"kernel": k, "hbm_bytes_per_launch": t["hbm_bytes"], "fetch_bytes_per_launch": t["fetch_bytes"],
+                          "write_bytes_per_launch": t["write_bytes"], "avg_ns": t["avg_ns"],
+                          "source": f"profiles/{tag}_pmc_traffic.csv (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, "
+                                    f"separate passes, {workload})"}
+    with open(jp, "w") as f:
+        json.dump({"kernels": kern}, f, indent=1)
     print("\n".join(lines))
 
 
