@@ -626,11 +626,11 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
 __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
   __shared__ SearchLdsSw L;
   const uint64_t R = a.run;
-  const uint64_t nruns = a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
+  const uint64_t nruns = a.wruns ? a.nwruns : a.run_hi ? a.run_hi : (a.total_chunks + R - 1) / R;
   for (uint64_t k = blockIdx.x;; k = gridDim.x + wave_claim(&a.ctr->search_next[a.grp])) {
-    const uint64_t r = a.run_lo + k;
+    const uint64_t r = a.wruns ? k : a.run_lo + k;
     if (r >= nruns) break;
-    const uint64_t t = (uint64_t)r * R;
+    const uint64_t t = (a.wruns ? a.wruns[r] : r) * R;
     const uint32_t fi = find_file(files, a.nfiles, t);
     const FileDesc fd = files[fi];
     const uint64_t fend = fd.first_chunk + fd.nchunks;
@@ -668,9 +668,73 @@ __global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long lo
   }
 }
 
+// Record lengths at kProbeRegions points of every file (one wave per file and point), for the scan
+// mode of each region (speed only: every mode reads every file correctly). Point 0 is the file's
+// head, walked exactly; point s > 0 is s/kProbeRegions of the way in, where the first offset of a
+// 4-KiB window from which four headers chain plausibly (key <= 4 KiB, value inside the file,
+// each record inside the file) is taken as a record start. Up to 32 records are walked from it:
+// out[3 * (f * kProbeRegions + s)] = {bytes, records, longest}. No start in the window (a record
+// longer than it covers the point): {window, 0, window}.
+__device__ __forceinline__ bool probe_chain(const uint8_t* d, uint64_t len, uint64_t p) {
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    if (p == len) return j > 0;  // the file ends exactly at a record boundary
+    if (p + 18 > len) return false;
+    const uint32_t b3 = gld4(d + p + 12);
+    const uint32_t ksz = b3 & 0xFFFFu;
+    const uint32_t vsz = (b3 >> 16) | ((uint32_t)d[p + 16] << 16) | ((uint32_t)d[p + 17] << 24);
+    if (ksz > 4096u) return false;
+    const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+    if (p + rl > len) return false;
+    p += rl;
+  }
+  return true;
+}
+
+__global__ __launch_bounds__(64) void k_probe_regions(const FileDesc* __restrict__ files, uint32_t nfiles,
+                                                      unsigned long long* __restrict__ out) {
+  const uint32_t f = blockIdx.x / kProbeRegions, s = blockIdx.x % kProbeRegions, lane = threadIdx.x;
+  if (f >= nfiles) return;
+  const FileDesc fd = files[f];
+  const uint64_t x = fd.len * s / kProbeRegions;
+  constexpr uint32_t kWin = 4096;
+  uint64_t p0 = kNone;
+  if (s == 0) {
+    p0 = 0;
+  } else {
+    for (uint32_t i = 0; i < kWin / 64 && p0 == kNone; ++i) {
+      const uint64_t p = x + 64ull * i + lane;
+      const bool ok = p < fd.len && probe_chain(fd.data, fd.len, p);
+      const unsigned long long b = __ballot(ok);
+      if (b) p0 = x + 64ull * i + (uint64_t)__builtin_ctzll(b);
+    }
+  }
+  if (lane) return;
+  uint64_t bytes = 0, recs = 0, mx = 0;
+  if (p0 == kNone) {
+    bytes = kWin;
+    mx = kWin;
+  } else {
+    uint64_t p = p0;
+    for (int k = 0; k < 32 && p + 18 <= fd.len; ++k) {
+      const uint64_t rl = g_reclen(fd.data + p);
+      if (p + rl > fd.len) break;
+      bytes += rl;
+      ++recs;
+      mx = rl > mx ? rl : mx;
+      p += rl;
+    }
+  }
+  unsigned long long* o = out + 3ull * blockIdx.x;
+  o[0] = bytes;
+  o[1] = recs;
+  o[2] = mx;
+}
+
 // Runs a launch covers: its group's, or the repair pass's list.
 static uint64_t launch_runs(const ScanArgs& a) {
   if (a.runs) return a.nruns_list;
+  if (a.wruns) return a.nwruns;
   const uint64_t hi = a.run_hi ? a.run_hi : (a.total_chunks + a.run - 1) / a.run;
   return hi > a.run_lo ? hi - a.run_lo : 0;
 }
@@ -696,6 +760,12 @@ void launch_walk_search(const ScanArgs& a, void* stream) {
 
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {
   hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, files, nfiles, out);
+}
+
+void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {
+  if (!nfiles) return;
+  hipLaunchKernelGGL(k_probe_regions, dim3(nfiles * kProbeRegions), dim3(64), 0, (hipStream_t)stream, files, nfiles,
+                     out);
 }
 
 }  // namespace cask_dev

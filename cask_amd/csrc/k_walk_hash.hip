@@ -393,11 +393,12 @@ __global__ __launch_bounds__(256) void k_walk_hash(ScanArgs a, const FileDesc* _
 // ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* __restrict__ files) {
   const uint64_t R = a.run;
-  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
   const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   g_u32* slots = (g_u32*)a.slots;
   g_u64* cd = (g_u64*)a.cdesc;
-  for (uint64_t k = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; k < nruns; k += (uint64_t)gridDim.x * blockDim.x) {
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nruns; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t k = a.wruns ? a.wruns[i] : i;
     Walk W;
     W.cn = 0;
     W.ccerr = 0xFFFFFFFFu;
@@ -474,7 +475,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6;
   const bool qlead = q == 0;
   const uint64_t R = a.run;
-  const uint64_t nruns = (a.total_chunks + R - 1) / R;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
   const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
   const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
   g_u32* slots = (g_u32*)a.slots;
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       runs_left = false;
       return;
     }
-    const uint64_t t0 = k * R;
+    const uint64_t t0 = (a.wruns ? a.wruns[k] : k) * R;
     const uint32_t nch = (uint32_t)(a.total_chunks - t0 < R ? a.total_chunks - t0 : R);
     const uint32_t c = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
     uint32_t inc = c;
@@ -737,7 +738,8 @@ void launch_walk_hash(const ScanArgs& a, int depth, void* stream) {
 
 void launch_walk_chase(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
-  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
+  if (!nruns) return;
   const uint32_t grid = (uint32_t)((nruns + 255) / 256);
   hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(256), 0, (hipStream_t)stream, a, a.files);
 }
@@ -762,7 +764,8 @@ static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
 
 void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
   if (!a.total_chunks) return;
-  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
+  if (!nruns) return;
   hipStream_t s = (hipStream_t)stream;
   if (depth == 16)
     run_hash_at<16>(a, nruns, s);

@@ -153,6 +153,11 @@ struct ScanArgs {
   // walk mode, split path (k_walk_chase -> k_run_hash): per chunk, the address of its first byte and
   // the end of its file's last 16-B granule (2 x u64), written by the chase
   uint64_t* cdesc;
+  // a call whose runs are split between the modes (per region of each file: k_probe_regions): the
+  // walk-mode runs, by index (k_walk_search, k_walk_chase, k_run_hash; null: every run); the
+  // chunk-mode runs go to k_scan_chunks as a.runs stretches
+  const uint64_t* wruns;
+  uint64_t nwruns;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -170,7 +175,7 @@ __host__ __device__ __forceinline__ bool lds_hashed(uint64_t p, uint64_t rl, uin
 constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // Walk mode (k_walk.hip): chunks per run, and the mean record length (bytes, sampled at the heads
 // of the files by k_probe) from which a call takes it.
-constexpr uint32_t kWalkRun = 64, kWalkMean = 1024;
+constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk runs 2 % faster than 64)
 // Chunk mode: the short-halo geometry (kGeoShortHalo, a 1,008-B halo) when the records at the file
 // heads average at most kShortHaloMean bytes and none is longer than kShortHaloMax; else the wide
 // halo (kDefaultGeometry, 4,080 B). Speed only: a record that crosses the window goes to k_long.
@@ -246,6 +251,9 @@ void launch_walk_hash(const ScanArgs& a, int depth, void* stream);
 void launch_walk_chase(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, int depth, void* stream);
 void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
+// k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
+constexpr uint32_t kProbeRegions = 8;
+void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,
                          const uint16_t* ksz, const uint32_t* vsz_raw, const uint64_t* key_id,

@@ -99,6 +99,8 @@ struct cask_ctx {
   DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
   DevBuf lqsnap;     // walk groups: the long-record queue counts after each group's enqueue
   DevBuf cdesc;      // walk mode, split path: per chunk its address and its file's end (2 x u64)
+  DevBuf probe;      // k_probe_regions: 3 u64 per region of each file
+  DevBuf mruns;      // mixed call: walk-mode run indices | chunk-mode [first, end) stretches
   uint32_t epoch = 0;
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
@@ -133,9 +135,15 @@ struct cask_ctx {
   size_t callb_last = 0;
   int cb_cur = 0;               // the call block the last call used
   bool cb_zero[2] = {false, false};
-  uint64_t probe_sig = 0;  // files of the last k_probe, and its answer
-  bool probe_walk = false;
+  uint64_t probe_sig = 0;  // files of the last k_probe_regions, and its answer
+  bool probe_walk = false;   // every region of every file reads fastest in walk mode
+  bool probe_mixed = false;  // some regions in walk mode, some in chunk mode
   bool probe_short = false;  // chunk mode: the short-halo geometry (kGeoShortHalo)
+  std::vector<uint8_t> probe_region;     // per file and region (kProbeRegions): 1 = walk mode
+  std::vector<unsigned long long> probe_host;
+  uint64_t mixed_key = 0;                // the run lists in mruns: for this probe and run length
+  uint64_t mixed_nw = 0, mixed_nc = 0;   // walk-mode runs, chunk-mode runs
+  std::vector<uint64_t> mruns_host;
   std::mutex mu;
   char last_error[256] = {0};
   ~cask_ctx() {
@@ -469,13 +477,23 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   c->last_error[0] = 0;
   (void)hipGetLastError();  // drop any stale error another library left on this thread
   if (!resident) H(hipMemcpyAsync(d_files, fd, fd_bytes + call_bytes, hipMemcpyHostToDevice, st), "file table H2D");
-  // Walk mode (k_walk_runs: header chase, long bodies read once, by k_long) when the records at the
-  // heads of the files average kWalkMean bytes or more: k_probe, once per set of files (the answer
-  // is cached on the context; it decides speed only). CASK_SCAN_MODE=walk|chunk (test and tuning
-  // knob) forces a mode.
+  // The scan mode, per region of each file (speed only: both modes read any file correctly). Walk
+  // mode (k_walk_search -> k_walk_chase -> k_run_hash: the record chain followed header to header,
+  // every record hashed from HBM) where the records average kWalkMean bytes or more; chunk mode
+  // (k_scan_chunks: every chunk staged through LDS, its records found by search and hashed there)
+  // elsewhere. k_probe_regions samples kProbeRegions points of every file once per set of files
+  // (the answer is cached on the context). A call whose regions differ runs both, on their own runs.
+  // CASK_SCAN_MODE=walk|chunk (test and tuning knob) forces a mode for the whole call.
   // The chunk scan's halo comes from the same probe: CASK_SCAN_MODE=wide|narrow forces the chunk
   // mode with the wide (4,080-B) or the short (1,008-B) halo.
-  bool walk = false;
+  // CASK_WALK_PATH (tuning knob) picks the walk path: "split" (default, above), "fused" (k_walk_hash:
+  // a quad per run chases and hashes) or "grouped" (k_walk_runs + the long-record queue +
+  // k_long_hash, in groups on two streams); a mixed call needs the split path (else: chunk mode).
+  static const int walk_path = [] {
+    const char* v = getenv("CASK_WALK_PATH");
+    return !v ? 0 : !strcmp(v, "fused") ? 1 : !strcmp(v, "grouped") ? 2 : 0;
+  }();
+  bool walk = false, mixed = false;
   int halo_pick = 0;  // 1: wide, 2: short (forced); 0: from the probe
   if (hint) {
     walk = true;  // hint bodies are always walked (k_walk_runs' hint mode)
@@ -498,34 +516,97 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
         sig ^= sig >> 31;
       }
       if (sig != c->probe_sig) {
-        unsigned long long* d = c->err2.as<unsigned long long>();
-        unsigned long long hp[3] = {0, 0, 0};
-        H(hipMemsetAsync(d, 0, 24, st), "probe memset");
-        launch_probe(d_files, nfiles, d, st);
-        L("k_probe");
-        H(hipMemcpyAsync(hp, d, 24, hipMemcpyDeviceToHost, st), "probe D2H");
+        const uint64_t np = (uint64_t)nfiles * kProbeRegions;
+        if (!c->probe.ensure(24 * np)) return CASK_E_NOMEM;
+        c->probe_host.assign(3 * np, 0ull);
+        launch_probe_regions(d_files, nfiles, c->probe.as<unsigned long long>(), st);
+        L("k_probe_regions");
+        H(hipMemcpyAsync(c->probe_host.data(), c->probe.p, 24 * np, hipMemcpyDeviceToHost, st), "probe D2H");
         H(hipStreamSynchronize(st), "probe sync");
         if (!ok) return CASK_E_DEVICE;
+        c->probe_region.assign(np, 0);
+        uint64_t nw = 0, nreg = 0, cb = 0, cr = 0, cm = 0;
+        for (uint64_t i = 0; i < np; ++i) {
+          const unsigned long long b = c->probe_host[3 * i], r = c->probe_host[3 * i + 1], m = c->probe_host[3 * i + 2];
+          if (!b) continue;  // an empty file
+          ++nreg;
+          // no record start in the probe window (a longer record covers the point), or long records
+          const bool w = r == 0 || b >= (unsigned long long)kWalkMean * r;
+          c->probe_region[i] = w ? 1 : 0;
+          if (w) {
+            ++nw;
+          } else {
+            cb += b;
+            cr += r;
+            cm = m > cm ? m : cm;
+          }
+        }
         c->probe_sig = sig;
-        c->probe_walk = hp[1] && hp[0] >= kWalkMean * hp[1];
-        c->probe_short = hp[1] && hp[0] <= kShortHaloMean * hp[1] && hp[2] <= kShortHaloMax;
+        c->probe_walk = nreg && nw == nreg;
+        c->probe_mixed = nw && nw < nreg;
+        c->probe_short = cr && cb <= kShortHaloMean * cr && cm <= kShortHaloMax;
+        c->mixed_key = 0;
       }
       walk = c->probe_walk;
+      mixed = c->probe_mixed && walk_path == 0;
       halo_pick = c->probe_short ? 2 : 1;
     }
   }
-  if (c->geo < 0 && !walk && halo_pick == 2) {
+  if (mixed) {
+    // Each run of kWalkRun chunks in the mode of the region its first chunk lies in: the walk-mode
+    // runs by index, the chunk-mode runs as [first, end) stretches for k_scan_chunks (a.runs). Built
+    // and copied to the device once per set of files.
+    const char* wr = getenv("CASK_WALK_RUN");
+    a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : kWalkRun;
+    a.run_tail = ~0ull;
+    const uint64_t R = a.run, nr = (total_chunks + R - 1) / R;
+    const uint64_t key = (c->probe_sig ^ (R << 1) ^ (total_chunks << 20)) | 1ull;
+    if (c->mixed_key != key) {
+      c->mruns_host.assign(3 * nr, 0ull);
+      uint64_t* wl = c->mruns_host.data();
+      uint64_t* cl = wl + nr;
+      uint64_t nw = 0, nc = 0;
+      uint32_t fi = 0;
+      for (uint64_t r = 0; r < nr; ++r) {
+        const uint64_t t = r * R;
+        while (fi + 1 < nfiles && (fd[fi].nchunks == 0 || t >= fd[fi].first_chunk + fd[fi].nchunks)) ++fi;
+        const uint64_t reg = fd[fi].nchunks ? (t - fd[fi].first_chunk) * kProbeRegions / fd[fi].nchunks : 0;
+        if (c->probe_region[(uint64_t)fi * kProbeRegions + std::min<uint64_t>(reg, kProbeRegions - 1)]) {
+          wl[nw++] = r;
+        } else {
+          cl[2 * nc] = t;
+          cl[2 * nc + 1] = std::min<uint64_t>(t + R, total_chunks);
+          ++nc;
+        }
+      }
+      if (nw && nc) {
+        memmove(wl + nw, cl, 16 * nc);
+        if (!c->mruns.ensure(8 * (nw + 2 * nc))) return CASK_E_NOMEM;
+        H(hipMemcpyAsync(c->mruns.p, wl, 8 * (nw + 2 * nc), hipMemcpyHostToDevice, st), "run lists H2D");
+        H(hipStreamSynchronize(st), "run lists sync");
+        if (!ok) return CASK_E_DEVICE;
+      }
+      c->mixed_nw = nw;
+      c->mixed_nc = nc;
+      c->mixed_key = key;
+    }
+    if (!c->mixed_nw || !c->mixed_nc) {  // (every run's first chunk fell in one mode)
+      mixed = false;
+      walk = c->mixed_nw != 0;
+    }
+  }
+  if (c->geo < 0 && (!walk || mixed) && halo_pick == 2) {
     geo = kGeoShortHalo;  // same chunk size: only the window (and the kernel) change
     a.win = chunk + geometry_halo(geo);
   }
-  c->last_geo = walk ? -1 : geo;
-  if (walk && !hint) a.big = kWalkHashMax;  // the walker hashes what fits its window, k_long the rest
-  if (walk) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
+  c->last_geo = walk && !mixed ? -1 : geo;
+  if (walk && !hint && !mixed) a.big = kWalkHashMax;  // the walker hashes what fits its window, k_long the rest
+  if (walk && !mixed) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
     const char* wr = getenv("CASK_WALK_RUN");
     a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : hint ? kHintRun : kWalkRun;
     a.run_tail = ~0ull;  // (the chunk scan's short tail runs were sized for its own run length)
   }
-  c->last_walk = walk ? 1 : 0;
+  c->last_walk = mixed ? 2 : walk ? 1 : 0;
   H(hipEventRecord(c->ev[1], st));
   // walk mode on data files: the runs in G groups; per group the walk (which hashes the records
   // that fit its window) and the long records' queueing on the call's stream, then their hashing
@@ -533,19 +614,33 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // hash on HBM bandwidth). Long records hashed before k_finish mark their rows like any failed
   // check (slot bad bit, cerr), so k_finish sees them.
   bool long_pre = false;
-  // Walk mode on data files. CASK_WALK_PATH (tuning knob) picks the path: "split" (default: every
-  // run's speculative start, k_walk_search; the header chase, k_walk_chase, a lane per run; then
-  // k_run_hash, a quad per record hashing it from HBM), "fused" (k_walk_hash: a quad per run chases
-  // and hashes) or "grouped" (k_walk_runs + the long-record queue + k_long_hash, in groups on two
-  // streams).
-  static const int walk_path = [] {
-    const char* v = getenv("CASK_WALK_PATH");
-    return !v ? 0 : !strcmp(v, "fused") ? 1 : !strcmp(v, "grouped") ? 2 : 0;
-  }();
   // CASK_HASH_D (tuning knob): 64-B blocks in flight per quad of the hashing kernel
-  static const int hash_depth = getenv("CASK_HASH_D") ? atoi(getenv("CASK_HASH_D")) : (walk_path == 1 ? 16 : 8);
+  static const int hash_depth = getenv("CASK_HASH_D") ? atoi(getenv("CASK_HASH_D")) : 16;  // (16: 5 % faster than 8)
   bool fused = false;
-  if (walk && !hint && walk_path != 2) {
+  if (mixed) {  // the walk-mode runs (split path), then the chunk-mode runs, then k_finish for all
+    fused = true;
+    ScanArgs aw = a;
+    aw.wruns = c->mruns.as<uint64_t>();
+    aw.nwruns = c->mixed_nw;
+    launch_walk_search(aw, st);
+    L("k_walk_search");
+    H(hipEventRecord(c->ev[6], st));
+    aw.walk_pre = 1;
+    if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
+    aw.cdesc = c->cdesc.as<uint64_t>();
+    launch_walk_chase(aw, st);
+    L("k_walk_chase");
+    H(hipEventRecord(c->ev[7], st));
+    launch_run_hash(aw, hash_depth, st);
+    L("k_run_hash");
+    ScanArgs ac = a;
+    ac.runs = c->mruns.as<uint64_t>() + c->mixed_nw;
+    ac.nruns_list = c->mixed_nc;
+    launch_scan_chunks(ac, geo, st);
+    L("k_scan_chunks");
+    // (the chunk-mode runs' long records go to k_long after k_finish, as in a chunk-mode call)
+    if (!ok) return CASK_E_DEVICE;
+  } else if (walk && !hint && walk_path != 2) {
     fused = true;
     const uint64_t nruns = (total_chunks + a.run - 1) / a.run;
     ScanArgs as = a;

@@ -245,6 +245,8 @@ def test_repeated_calls_alternating_file_sets(gpu_ctx):
             assert np.array_equal(res.pos[sl].cpu().numpy().astype(np.uint64), w["pos"]), (k, i)
             assert np.array_equal(res.seq[sl].cpu().numpy().astype(np.uint64), w["seq"]), (k, i)
             assert np.array_equal(res.status[sl].cpu().numpy(), w["status"].astype(np.uint8)), (k, i)
+            assert np.array_equal(res.vsz[sl].cpu().numpy().astype(np.uint32), w["vsz_raw"].astype(np.uint32)), (k, i)
+            assert np.array_equal(res.ksz[sl].cpu().numpy().astype(np.uint16), w["ksz"].astype(np.uint16)), (k, i)
         assert (res.error is None) == (k != "bad"), k
 
 
@@ -266,7 +268,7 @@ def test_variable_sizes_with_long_records(gpu_ctx):
     buf = make_records(rng, 3000, lambda r: r.randrange(0, 40), vsz, tomb_p=0.1)
     check_against_oracle(gpu_ctx, [buf])
     cnt = gpu_ctx.last_counters()
-    assert cnt["long_records"] > 0 or cnt["walk_mode"] == 1, cnt  # k_long_hash, or the walk hashed them
+    assert cnt["long_records"] > 0 or cnt["walk_mode"] >= 1, cnt  # k_long_hash, or the walk hashed them
 
 
 def _zipf_vsz(rng, s=1.1, kmax=4096):
@@ -293,8 +295,30 @@ def test_zipf_sizes_long_records(gpu_ctx, seed):
     buf = make_records(rng, 4000, lambda r: 16, _zipf_vsz(rng), tomb_p=0.02)
     check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 3]], device=True)
     cnt = gpu_ctx.last_counters()
-    assert cnt["long_records"] > 0 or cnt["walk_mode"] == 1, cnt
+    assert cnt["long_records"] > 0 or cnt["walk_mode"] >= 1, cnt
     assert cnt["walked"] == 0, cnt
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_mixed_modes_in_one_call(gpu_ctx, corrupt):
+    """One call over a file of fixed 290-B records (configs[1] shape), a file of Zipf-length records
+    (configs[2] shape) and a file with a short-record head and a long-record body: the library picks
+    the mode per region of each file (chunk mode for the short records, walk mode for the long ones,
+    walk_mode == 2), and the rows equal the oracle's row for row — with a flipped byte in the short
+    and in the long regions too."""
+    rng = random.Random(61)
+    a = bytearray(make_records(rng, 29000, lambda r: 16, lambda r: 256))
+    b = bytearray(make_records(rng, 5000, lambda r: 16, _zipf_vsz(rng), seq0=100_000, tomb_p=0.02))
+    head = make_records(rng, 25000, lambda r: 16, lambda r: r.randrange(40, 160), seq0=200_000)
+    body = make_records(rng, 2600, lambda r: 16, _zipf_vsz(rng), seq0=300_000)
+    c = bytearray(head + body)
+    if corrupt:
+        a[len(a) // 2] ^= 0x08
+        c[len(c) - len(body) // 3] ^= 0x80
+    check_against_oracle(gpu_ctx, [bytes(a), bytes(b), bytes(c)], device=True)
+    cnt = gpu_ctx.last_counters()
+    if os.environ.get("CASK_SCAN_MODE") is None:
+        assert cnt["walk_mode"] == 2, cnt
 
 
 def test_zipf_sizes_corrupt(gpu_ctx):
@@ -320,7 +344,7 @@ def test_long_record_hash_every_length_residue(gpu_ctx):
     buf = b"".join(recs)
     res = check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 2]], device=True)
     cnt = gpu_ctx.last_counters()
-    assert cnt["long_records"] > 0 or cnt["walk_mode"] == 1, cnt
+    assert cnt["long_records"] > 0 or cnt["walk_mode"] >= 1, cnt
     assert res.error is not None
 
 
@@ -336,7 +360,7 @@ def test_records_past_walk_hash_limit(gpu_ctx):
         recs.append(bytes(rec))
     check_against_oracle(gpu_ctx, [b"".join(recs)], device=True)
     cnt = gpu_ctx.last_counters()
-    assert cnt["long_records"] >= 3 or cnt["walk_mode"] == 1, cnt
+    assert cnt["long_records"] >= 3 or cnt["walk_mode"] >= 1, cnt
 
 
 def test_many_files_empty_and_tiny(gpu_ctx):

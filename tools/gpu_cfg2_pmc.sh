@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r03a}
 O="$R/gpurun_out/pmc_$TAG"
 rm -rf "$O"; mkdir -p "$O"
-C="$R/tools/bench_configs.py cfg3 --steps ${STEPS:-2}"
+C="${PMC_CMD:-$R/tools/bench_configs.py cfg3 --steps ${STEPS:-2}}"
 timeout -s KILL 60 rocprofv3 -L > "$O/counters.txt" 2>&1 || true
 have() { grep -q -w "$1" "$O/counters.txt"; }
 pass() {  # pass NAME COUNTER...
@@ -31,5 +31,7 @@ pass occ SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_
 pass mem SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_WR GRBM_COUNT
 pass lds SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SMEM SQ_INST_CYCLES_VMEM_RD SQ_WAIT_INST_ANY SQ_INSTS_VALU_MUL_I32 SQ_ACTIVE_INST_MISC GRBM_GUI_ACTIVE
 pass ta TA_BUSY_avr TA_TA_BUSY_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
+pass tlb TCP_UTCL1_REQUEST_sum TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_THRASHING_STALL_sum GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE
+pass tlb2 TCP_UTCL1_STALL_UTCL2_REQ_OUT_OF_CREDITS_sum TCP_UTCL1_TRANSLATION_MISS_UNDER_MISS_sum TCP_UTCL1_STALL_INFLIGHT_MAX_sum TCP_CLIENT_UTCL1_INFLIGHT_sum
 if [ -z "$NO_FETCH" ]; then pass fetch FETCH_SIZE; pass write WRITE_SIZE; fi
 ls "$O"

@@ -31,6 +31,8 @@ def per_kernel(path, counter):
 def main():
     tag = sys.argv[1] if len(sys.argv) > 1 else "r01"
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
+    if not os.path.isdir(src):  # tools/gpu_cfg2_pmc.sh's layout
+        src = os.path.join(ROOT, "gpurun_out", f"pmc_{tag}")
     out = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(out, f"{tag}_kernel_stats.csv"))
     fetch, nf = per_kernel(os.path.join(src, "fetch", "fetch_counter_collection.csv"), "FETCH_SIZE")

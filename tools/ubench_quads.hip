@@ -1,0 +1,108 @@
+// Design microbenchmark (not part of the product): HBM read rate of the k_run_hash access pattern —
+// every quad of lanes streams its own contiguous segment (a "record") in rounds of D 64-B blocks
+// (one 16-B load per lane per block), the next round's loads in flight while the current one is
+// mixed — by segment size, waves per CU, depth, with XXH32 mixing (quad_transpose + 4 rounds per
+// block) or a plain XOR, and with the quads of a wave on adjacent or on scattered segments.
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 tools/ubench_quads.hip -o tools/ubench_quads
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../cask_amd/csrc/device_util.h"
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1);} } while (0)
+
+using namespace cask_dev;
+
+// nseg segments of S bytes at base + perm(seg) * S + 4 (the body of a record: 4 B past its start);
+// quad k of the grid takes segments k, k + Q, k + 2Q, ... (Q = quads in the grid).
+template <uint32_t D, bool HASH>
+__global__ __launch_bounds__(256) void k_quads(const uint8_t* __restrict__ base, uint64_t nseg, uint32_t S,
+                                               uint32_t scatter, uint32_t* __restrict__ sink) {
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
+  const uint64_t Q = (uint64_t)gridDim.x * 64, qid = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
+  const uint32_t nblk = (S - 64) / 64;  // full blocks of a segment's body
+  for (uint64_t k = qid; k < nseg; k += Q) {
+    const uint64_t seg = scatter ? (k * 0x9E3779B97F4A7C15ull) % nseg : k;  // (nseg odd: a permutation)
+    const g_u8* lp = (const g_u8*)(base + seg * S + 4 + 16 * q);
+    u32x4 A[D], B[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) A[d] = gld16g(lp + 64 * d);
+    uint32_t b = D;
+    for (;;) {
+      const bool more = b + D <= nblk;
+      if (more) {
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) B[d] = gld16g(lp + 64 * (b + d));
+      }
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) {
+        u32x4 x = A[d];
+        if (HASH) {
+          quad_transpose(x, q);
+          v = xround(xround(xround(xround(v, x.x), x.y), x.z), x.w);
+        } else {
+          v ^= x.x ^ x.y ^ x.z ^ x.w;
+        }
+      }
+      if (!more) break;
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) A[d] = B[d];
+      b += D;
+    }
+  }
+  if (v == 0x12345678u) sink[0] = v;
+}
+
+template <uint32_t D, bool HASH>
+static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_per_cu, uint32_t scatter, int cus,
+                 uint32_t* sink) {
+  uint64_t nseg = bytes / S;
+  if (!(nseg & 1)) --nseg;
+  const uint32_t grid = (uint32_t)(cus * waves_per_cu / 4);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink);
+  CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int it = 0; it < 3; ++it) {
+    CK(hipEventRecord(a));
+    hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    best = ms < best ? ms : best;
+  }
+  // bytes actually read: nblk full blocks of each segment
+  const double rd = (double)nseg * (double)((S - 64) / 64 * 64);
+  printf("D=%2u %s S=%6u waves/CU=%2u %s: %.3f ms %.0f GB/s\n", D, HASH ? "hash" : "xor ", S, waves_per_cu,
+         scatter ? "scattered" : "adjacent ", best, rd / best / 1e6);
+  fflush(stdout);
+  return best;
+}
+
+int main() {
+  int cus = 0;
+  CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+  const uint64_t bytes = 16ull << 30;
+  uint8_t* buf;
+  CK(hipMalloc(&buf, bytes + 4096));
+  CK(hipMemset(buf, 0x5A, bytes + 4096));
+  uint32_t* sink;
+  CK(hipMalloc(&sink, 64));
+  for (uint32_t S : {4096u, 65536u}) {
+    for (uint32_t sc : {0u, 1u}) {
+      for (uint32_t w : {8u, 16u, 32u}) {
+        run<8, false>(buf, bytes, S, w, sc, cus, sink);
+        run<16, false>(buf, bytes, S, w, sc, cus, sink);
+        run<8, true>(buf, bytes, S, w, sc, cus, sink);
+        run<16, true>(buf, bytes, S, w, sc, cus, sink);
+      }
+    }
+  }
+  return 0;
+}
