@@ -158,6 +158,10 @@ struct ScanArgs {
   // chunk-mode runs go to k_scan_chunks as a.runs stretches
   const uint64_t* wruns;
   uint64_t nwruns;
+  // k_walk_search: candidates of at most this many bytes are verified by their checksum, longer
+  // ones are listed for the hop back (kSearchShort; CASK_SEARCH_SHORT tuning knob)
+  uint32_t search_short;
+  uint32_t search_mode;  // k_walk_search: 0 checksum-verified candidates, 1 chain plausibility first
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,

@@ -155,11 +155,12 @@ int cask_last_counters(const cask_ctx* ctx, uint64_t* c5);
 /* 1 if the last cask_scan_device / cask_scan_host call took the two-kernel dense path (k_scan_chunks
  * + k_finish: every speculated chunk start held), 0 if it went through the repair path. */
 int cask_last_dense(const cask_ctx* ctx);
-/* 1 if the last call's speculative pass was the walk mode (k_walk_runs: record headers chased from
- * HBM, chosen when the records at the heads of the files average >= 1 KiB), 0 for k_scan_chunks. */
+/* The last call's scan mode: 1 walk mode (record headers chased from HBM, every record hashed from
+ * HBM: picked where the records sampled at 8 points of each file average >= 1 KiB), 0 chunk mode
+ * (k_scan_chunks), 2 both in one call (each run of chunks in the mode of its file region). */
 int cask_last_walk(const cask_ctx* ctx);
 /* The last call's k_scan_chunks geometry: 0 for the wide 4,080-B halo, 3 for the short 1,008-B halo
- * (picked when the records at the heads of the files are short), -1 when the walk mode ran. */
+ * (picked when the sampled chunk-mode records are short), -1 when only the walk mode ran. */
 int cask_last_geometry(const cask_ctx* ctx);
 
 /* ------------------------------------------------------------------------------------------ */
