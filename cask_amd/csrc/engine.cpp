@@ -13,6 +13,8 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cerrno>
 #include <chrono>
 #include <cstdio>
@@ -435,6 +437,7 @@ struct EngineDev {
   } data, rows, hint;
   // pinned staging: reads of data files to the device, copies of results back to the host
   cask_host::PinnedRing ring;
+  cask_host::PinnedRing ring_out;  // open(): hint bodies back to the host while `ring` reads files in
   static constexpr int kReaders = cask_host::PinnedRing::kThreads;
   static constexpr size_t kSlotBytes = cask_host::PinnedRing::kBytes;
   cask_rows r{};
@@ -446,7 +449,7 @@ struct EngineDev {
       ctx = cask_ctx_create(device, &st);
       if (!ctx) return st;
     }
-    return ring.init(device) ? CASK_OK : CASK_E_NOMEM;
+    return ring.init(device) && ring_out.init(device) ? CASK_OK : CASK_E_NOMEM;
   }
 
   // Reader thread t takes every kReaders-th 32-MiB piece of the files, alternating between its two
@@ -512,14 +515,14 @@ struct EngineDev {
   // piece (CASK_STAGE_MIN=0 stages every copy: the tests run the small cases through it), the DMA of one piece into a slot overlapping the host copy of the previous piece out of
   // the other (a copy to pageable memory straight from the device runs at ~10 GB/s). Small copies
   // take cask_copy. The device work that produced `src` (on the context's stream) is waited for first.
-  int to_host(uint8_t* dst, const uint8_t* src, uint64_t n) {
+  int to_host(uint8_t* dst, const uint8_t* src, uint64_t n, cask_host::PinnedRing* rg = nullptr) {
     const char* mv = getenv("CASK_STAGE_MIN");  // test knob: smallest copy staged (default 64 MiB)
     if (n < (mv ? strtoull(mv, nullptr, 10) : (64ull << 20)) || !n) return cask_copy(ctx, dst, src, n);
     if (hipSetDevice(device) != hipSuccess || hipStreamSynchronize((hipStream_t)cask_ctx_stream(ctx)) != hipSuccess)
       return CASK_E_DEVICE;
     std::vector<cask_host::PinnedRing::Piece> ps;
     cask_host::PinnedRing::split(dst, (uint8_t*)src, n, ps);
-    return ring.d2h(ps) ? CASK_OK : CASK_E_DEVICE;
+    return (rg ? rg : &ring)->d2h(ps) ? CASK_OK : CASK_E_DEVICE;
   }
 
   // Device rows sized from a guess (average record >= 48 B), once more at the exact count if short.
@@ -545,20 +548,18 @@ struct EngineDev {
     return CASK_E_DEVICE;
   }
 
+  // The hint bodies of the scanned files v (rows of the last scan) into hbuf, file k's at
+  // [fo[k], fo[k + 1]); copied back through ring_out (open() reads the next files through `ring`).
   int hints(const std::vector<cask_file_view>& v, const std::vector<uint64_t>& row_off, RawBytes& hbuf,
-            std::vector<uint64_t>& hs0, std::vector<uint64_t>& hs1, const std::vector<uint32_t>& view_file) {
-    std::vector<uint64_t> fo(v.size() + 1, 0);
+            std::vector<uint64_t>& fo) {
+    fo.assign(v.size() + 1, 0);
     int st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), nullptr, 0, fo.data());
     if (st != CASK_E_CAPACITY && st != CASK_OK) return st;
     if (!hint.ensure(fo[v.size()] + 256)) return CASK_E_NOMEM;
     st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), hint.p, hint.cap, fo.data());
     if (st != CASK_OK) return st;
     if (!hbuf.resize(fo[v.size()])) return CASK_E_NOMEM;
-    if (!hbuf.empty() && to_host(hbuf.data(), hint.p, hbuf.size()) != CASK_OK) return CASK_E_DEVICE;
-    for (size_t k = 0; k < v.size(); ++k) {
-      hs0[view_file[k]] = fo[k];
-      hs1[view_file[k]] = fo[k + 1];
-    }
+    if (!hbuf.empty() && to_host(hbuf.data(), hint.p, hbuf.size(), &ring_out) != CASK_OK) return CASK_E_DEVICE;
     return CASK_OK;
   }
 };
@@ -788,75 +789,153 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     scan_idx.push_back((uint32_t)i);
   }
 
-  // The scanned files: read from disk straight to the device through pinned buffers (file reads on
-  // host threads overlapped with the copies), scanned there, and their hint bodies built there
-  // (cask_hints_device) and brought back: the host never holds the data bytes, only the hint
-  // records it writes and folds.
-  RawBytes hbuf;                             // hint bodies of the scanned files, file after file
-  std::vector<uint64_t> hs0(nf, 0), hs1(nf, 0);  // body of scanned file i: hbuf[hs0[i], hs1[i])
-  cask_scan_error se{};
-  uint32_t err_file = UINT32_MAX;            // index into files of the scan's first failure
+  // The scanned files, in batches of consecutive files (an eighth of their bytes each, at least
+  // 1 GiB): a reader thread reads batch b + 1 from disk straight to the device (host threads,
+  // pinned buffers) while a device thread scans batch b and brings its hint bodies back (built on
+  // the device, cask_hints_device), and this thread replays the batches before it in file order —
+  // the fold and the hint files. The host never holds the data bytes, only the hint records it
+  // writes and folds.
   std::vector<cask_file_view> views;
   std::vector<uint32_t> view_file;
+  std::vector<int64_t> view_of(nf, -1);
   for (uint32_t i : scan_idx)
     if (data_ok[i]) {
+      view_of[i] = (int64_t)views.size();
       views.push_back(cask_file_view{db->files[i], CASK_VIEW_DEVICE, nullptr, flen[i]});
       view_file.push_back(i);
     }
-  double t_read = 0;
-  auto t1 = std::chrono::steady_clock::now();
+  std::vector<size_t> vcut{0};
+  {
+    uint64_t all = 0, acc = 0;
+    for (const auto& v : views) all += v.len;
+    // CASK_OPEN_BATCH (test and tuning knob): bytes per batch (1: every file a batch of its own)
+    const uint64_t bb_env = getenv("CASK_OPEN_BATCH") ? strtoull(getenv("CASK_OPEN_BATCH"), nullptr, 10) : 0ull;
+    const uint64_t bb = bb_env ? bb_env : std::max<uint64_t>(1ull << 30, all / 8);
+    for (size_t v = 0; v < views.size(); ++v) {
+      acc += views[v].len;
+      if (acc >= bb && v + 1 < views.size()) {
+        vcut.push_back(v + 1);
+        acc = 0;
+      }
+    }
+    vcut.push_back(views.size());
+  }
+  const size_t nbat = vcut.size() - 1;
+  struct Batch {
+    RawBytes hb;                // hint bodies of the batch's files
+    std::vector<uint64_t> fo;   // view k of the batch: hb[fo[k], fo[k + 1])
+    cask_scan_error se{};
+    int st = CASK_OK;
+    bool read_done = false, ready = false;
+  };
+  std::vector<Batch> bat(nbat);
+  std::mutex bm;
+  std::condition_variable bcv;
+  std::atomic<bool> stop{false};
+  double t_read = 0, t_dev = 0;
+  EngineDev* ed = nullptr;
+  std::unique_lock<std::mutex> edlock;
+  int dst = CASK_OK;
   if (!views.empty()) {
-    EngineDev* ed = engine_dev(opts.device);
+    ed = engine_dev(opts.device);
     if (!ed) {
       delete db;
       set_err(err, CASK_E_DEVICE);
       return nullptr;
     }
-    std::lock_guard<std::mutex> g(ed->mu);
-    int st = ed->prepare();
+    edlock = std::unique_lock<std::mutex>(ed->mu);
+    dst = ed->prepare();
     std::vector<uint64_t> doff(views.size() + 1, 0);
     for (size_t v = 0; v < views.size(); ++v) doff[v + 1] = doff[v] + ((views[v].len + 255) & ~255ull);
-    if (st == CASK_OK && !ed->data.ensure(doff.back() + 256)) st = CASK_E_NOMEM;
-    if (st == CASK_OK) {
+    if (dst == CASK_OK && !ed->data.ensure(doff.back() + 256)) dst = CASK_E_NOMEM;
+    if (dst == CASK_OK)
       for (size_t v = 0; v < views.size(); ++v) views[v].data = ed->data.p + doff[v];
-      std::vector<std::string> paths;
-      for (uint32_t i : view_file) paths.push_back(data_path(path, db->files[i]));
-      std::vector<char> ok(views.size(), 1);
-      st = ed->read_to_device(paths, views, ok);
-      for (size_t v = 0; v < views.size(); ++v)
-        if (!ok[v]) {  // the file could not be read whole: Log::entries' Io error when its turn comes
-          data_ok[view_file[v]] = 0;
-          views[v].len = 0;
-        }
-    }
-    t_read = ms_since(t1);
-    std::vector<uint64_t> row_off(views.size() + 1);
-    if (st == CASK_OK) st = ed->scan(views, row_off, se);
-    if (st == CASK_OK) st = ed->hints(views, row_off, hbuf, hs0, hs1, view_file);
-    if (st != CASK_OK) {
-      delete db;
-      set_err(err, st);
-      return nullptr;
-    }
-    if (se.kind) {
-      for (size_t v = 0; v < views.size(); ++v)
-        if (views[v].file_id == se.file_id) err_file = view_file[v];
-    }
   }
-  db->timings[0] = ms_since(t0) - ms_since(t1) + t_read;
-  db->timings[1] = ms_since(t1) - t_read;
+  auto mark = [&](size_t b, int st, bool ready) {
+    {
+      std::lock_guard<std::mutex> g(bm);
+      if (st != CASK_OK && bat[b].st == CASK_OK) bat[b].st = st;
+      (ready ? bat[b].ready : bat[b].read_done) = true;
+    }
+    bcv.notify_all();
+  };
+  auto reader = [&]() {
+    const auto tr = std::chrono::steady_clock::now();
+    for (size_t b = 0; b < nbat; ++b) {
+      int st = dst;
+      if (st == CASK_OK && !stop.load() && vcut[b + 1] > vcut[b]) {
+        std::vector<std::string> paths;
+        std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
+        for (size_t v = vcut[b]; v < vcut[b + 1]; ++v) paths.push_back(data_path(path, db->files[view_file[v]]));
+        std::vector<char> ok(vb.size(), 1);
+        st = ed->read_to_device(paths, vb, ok);
+        for (size_t k = 0; k < vb.size(); ++k)
+          if (!ok[k]) {  // the file could not be read whole: Log::entries' Io error when its turn comes
+            data_ok[view_file[vcut[b] + k]] = 0;
+            views[vcut[b] + k].len = 0;
+          }
+      }
+      mark(b, st, false);
+    }
+    t_read = ms_since(tr);
+  };
+  auto device = [&]() {
+    for (size_t b = 0; b < nbat; ++b) {
+      {
+        std::unique_lock<std::mutex> lk(bm);
+        bcv.wait(lk, [&] { return bat[b].read_done; });
+      }
+      const auto td = std::chrono::steady_clock::now();
+      int st = bat[b].st;
+      if (st == CASK_OK && !stop.load() && vcut[b + 1] > vcut[b]) {
+        std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
+        std::vector<uint64_t> ro(vb.size() + 1);
+        st = ed->scan(vb, ro, bat[b].se);
+        if (st == CASK_OK) st = ed->hints(vb, ro, bat[b].hb, bat[b].fo);
+      }
+      t_dev += ms_since(td);
+      mark(b, st, true);
+    }
+  };
+  std::thread th_read, th_dev;
+  bool threaded = false;
+  if (!views.empty()) {
+    try {
+      th_read = std::thread(reader);
+      try {
+        th_dev = std::thread(device);
+        threaded = true;
+      } catch (...) {
+        stop = true;  // (the reader marks every batch and ends)
+        th_read.join();
+      }
+    } catch (...) {
+    }
+    if (!threaded) {  // no threads to be had: the same steps, one after the other
+      stop = false;
+      for (auto& bt : bat) bt = Batch();
+      reader();
+      device();
+    }
+  } else {
+    for (size_t b = 0; b < nbat; ++b) bat[b].read_done = bat[b].ready = true;
+  }
+  auto join_all = [&]() {
+    stop = true;
+    if (th_read.joinable()) th_read.join();
+    if (th_dev.joinable()) th_dev.join();
+  };
+  db->timings[0] = ms_since(t0);  // (until the replay starts; the reads' own span is added below)
 
-  // Replay in ascending file order (cask.rs:348-369); the first Err aborts open(). Hint files of the
-  // scanned files up to that point are written on threads: each is its body + XXH32 trailer
-  // (RecreateHints keeps draining after an error, so a failing file's hint file has every Ok row).
-  double t_fold = 0;
-  std::unique_ptr<FoldRec[]> recs;  // the replay's fold, in order (parallel_fold); not zero-filled
-  std::vector<uint32_t> to_write;
+  // Replay in ascending file order (cask.rs:348-369), batch after batch; the first Err aborts open().
+  // Hint files of the scanned files up to that point are written on threads: each is its body +
+  // XXH32 trailer (RecreateHints keeps draining after an error, so a failing file's hint file has
+  // every Ok row).
+  double t_fold = 0, t_hint = 0;
   int fail = CASK_OK;
   uint32_t fail_fid = 0;
   uint64_t fail_pos = 0;
   uint32_t fail_e = 0, fail_f = 0;
-  auto tf = std::chrono::steady_clock::now();
   // each file's hint body (a hint file's, or the one built for a scanned file), walked on threads:
   // its record count, highest sequence and first short read (Hints::next / Hint::from_read,
   // log.rs:437-447; data.rs:258-276)
@@ -865,115 +944,145 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     uint64_t n = 0, cnt = 0, max_seq = 0, bad = UINT64_MAX, base = 0;
   };
   std::vector<Body> bodies(nf);
-  for (size_t i = 0; i < nf; ++i) {
-    if (use_hint[i]) {
-      bodies[i].b = hints[i].data();
-      bodies[i].n = hints[i].size() - 4;  // Take(size - 4) (log.rs:129)
-    } else if (data_ok[i]) {
-      bodies[i].b = hbuf.data() + hs0[i];
-      bodies[i].n = hs1[i] - hs0[i];
-    }
-  }
   const unsigned ntb = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)std::max<size_t>(nf, 1)));
-  parallel_for(ntb, [&](unsigned t) {
-    for (size_t i = t; i < nf; i += ntb) {
-      Body& B = bodies[i];
-      for (uint64_t p = 0; p < B.n;) {
-        if (B.n - p < 22 || B.n - p - 22 < rd16(B.b + p + 8)) {
-          B.bad = p;
-          break;
-        }
-        B.max_seq = std::max(B.max_seq, rd64(B.b + p));
-        ++B.cnt;
-        p += 22ull + rd16(B.b + p + 8);
-      }
+  size_t fi = 0;  // the next file to replay
+  for (size_t b = 0; b < nbat && fail == CASK_OK; ++b) {
+    {
+      std::unique_lock<std::mutex> lk(bm);
+      bcv.wait(lk, [&] { return bat[b].ready; });
     }
-  });
-  // replay in ascending file order (cask.rs:348-369): the first Err aborts
-  size_t nrep = 0;
-  uint64_t total = 0;
-  for (size_t i = 0; i < nf && fail == CASK_OK; ++i) {
-    const uint32_t fid = db->files[i];
-    if (!use_hint[i]) {
-      if (!data_ok[i]) {
-        // HintWriter::new truncated the hint file before Log::entries failed; its Drop then wrote
-        // the trailer of an empty body (log.rs:141-142, 389-395).
-        if (opts.write_hints) write_file(hint_path(path, fid), {}, cask_xxh::xxh32(nullptr, 0, 0));
-        fail = CASK_E_IO;
-        fail_fid = fid;
-        break;
-      }
-      if (opts.write_hints) to_write.push_back((uint32_t)i);
-      if (err_file == i) {  // the scan's first failing record is in this file
-        fail = se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF;
-        fail_fid = fid;
-        fail_pos = se.pos;
-        fail_e = se.expected;
-        fail_f = se.found;
-        break;
-      }
-    }
-    if (bodies[i].bad != UINT64_MAX) {
-      fail = CASK_E_EOF;
-      fail_fid = fid;
-      fail_pos = bodies[i].bad;
+    if (bat[b].st != CASK_OK) {
+      fail = bat[b].st;
       break;
     }
-    if (bodies[i].cnt && bodies[i].max_seq > db->sequence) db->sequence = bodies[i].max_seq;
-    bodies[i].base = total;
-    total += bodies[i].cnt;
-    nrep = i + 1;
-  }
-  if (fail == CASK_OK) {  // the fold's records, file by file on threads
-    recs.reset(new (std::nothrow) FoldRec[std::max<uint64_t>(total, 1)]);
-    if (!recs) fail = CASK_E_NOMEM;
-  }
-  if (fail == CASK_OK) {
-    parallel_for(ntb, [&](unsigned t) {
-      for (size_t i = t; i < nrep; i += ntb) {
-        const Body& B = bodies[i];
-        FoldRec* out = recs.get() + B.base;
-        for (uint64_t p = 0, j = 0; j < B.cnt; ++j) {
-          const uint8_t* h = B.b + p;
-          const uint16_t k = rd16(h + 8);
-          out[j] = FoldRec{h + 22, rd64(h + 14), rd64(h), 0, db->files[i], rd32(h + 10), k};
-          p += 22ull + k;
+    const size_t fe = b + 1 < nbat ? (size_t)view_file[vcut[b + 1] - 1] + 1 : nf;
+    uint32_t err_file = UINT32_MAX;  // the batch's first failing record is in this file
+    if (bat[b].se.kind)
+      for (size_t v = vcut[b]; v < vcut[b + 1]; ++v)
+        if (views[v].file_id == bat[b].se.file_id) err_file = view_file[v];
+    auto tf = std::chrono::steady_clock::now();
+    for (size_t i = fi; i < fe; ++i) {
+      if (use_hint[i]) {
+        bodies[i].b = hints[i].data();
+        bodies[i].n = hints[i].size() - 4;  // Take(size - 4) (log.rs:129)
+      } else if (data_ok[i] && view_of[i] >= 0) {
+        const size_t k = (size_t)view_of[i] - vcut[b];
+        bodies[i].b = bat[b].hb.data() + bat[b].fo[k];
+        bodies[i].n = bat[b].fo[k + 1] - bat[b].fo[k];
+      }
+    }
+    const unsigned nt = std::max(1u, std::min<unsigned>(ntb, (unsigned)std::max<size_t>(fe - fi, 1)));
+    parallel_for(nt, [&](unsigned t) {
+      for (size_t i = fi + t; i < fe; i += nt) {
+        Body& B = bodies[i];
+        for (uint64_t p = 0; p < B.n;) {
+          if (B.n - p < 22 || B.n - p - 22 < rd16(B.b + p + 8)) {
+            B.bad = p;
+            break;
+          }
+          B.max_seq = std::max(B.max_seq, rd64(B.b + p));
+          ++B.cnt;
+          p += 22ull + rd16(B.b + p + 8);
         }
       }
     });
-  }
-  t_fold += ms_since(tf);
-  auto th = std::chrono::steady_clock::now();
-  {
-    std::vector<char> wok(to_write.size(), 1);
-    const unsigned nt = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)to_write.size()));
-    parallel_for(nt, [&](unsigned t) {
-      for (size_t j = t; j < to_write.size(); j += nt) {
-        const uint32_t i = to_write[j];
-        const uint8_t* b = hbuf.data() + hs0[i];
-        const uint64_t n = hs1[i] - hs0[i];
-        wok[j] = write_file_raw2(hint_path(path, db->files[i]), b, n, cask_xxh::xxh32(b, n, 0));
+    size_t nrep = fi;  // files of the batch replayed: [fi, nrep)
+    uint64_t total = 0;
+    std::vector<uint32_t> to_write;
+    for (size_t i = fi; i < fe && fail == CASK_OK; ++i) {
+      const uint32_t fid = db->files[i];
+      if (!use_hint[i]) {
+        if (!data_ok[i]) {
+          // HintWriter::new truncated the hint file before Log::entries failed; its Drop then wrote
+          // the trailer of an empty body (log.rs:141-142, 389-395).
+          if (opts.write_hints) write_file(hint_path(path, fid), {}, cask_xxh::xxh32(nullptr, 0, 0));
+          fail = CASK_E_IO;
+          fail_fid = fid;
+          break;
+        }
+        if (opts.write_hints) to_write.push_back((uint32_t)i);
+        if (err_file == i) {
+          const cask_scan_error& se = bat[b].se;
+          fail = se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF;
+          fail_fid = fid;
+          fail_pos = se.pos;
+          fail_e = se.expected;
+          fail_f = se.found;
+          break;
+        }
       }
-    });
-    for (size_t j = 0; j < to_write.size() && fail == CASK_OK; ++j)
-      if (!wok[j]) {
-        fail = CASK_E_IO;
-        fail_fid = db->files[to_write[j]];
+      if (bodies[i].bad != UINT64_MAX) {
+        fail = CASK_E_EOF;
+        fail_fid = fid;
+        fail_pos = bodies[i].bad;
+        break;
       }
+      if (bodies[i].cnt && bodies[i].max_seq > db->sequence) db->sequence = bodies[i].max_seq;
+      bodies[i].base = total;
+      total += bodies[i].cnt;
+      nrep = i + 1;
+    }
+    std::unique_ptr<FoldRec[]> recs;  // the batch's fold, in order (parallel_fold); not zero-filled
+    if (fail == CASK_OK) {
+      recs.reset(new (std::nothrow) FoldRec[std::max<uint64_t>(total, 1)]);
+      if (!recs) fail = CASK_E_NOMEM;
+    }
+    if (fail == CASK_OK) {  // the fold's records, file by file on threads
+      parallel_for(nt, [&](unsigned t) {
+        for (size_t i = fi + t; i < nrep; i += nt) {
+          const Body& B = bodies[i];
+          FoldRec* out = recs.get() + B.base;
+          for (uint64_t p = 0, j = 0; j < B.cnt; ++j) {
+            const uint8_t* h = B.b + p;
+            const uint16_t k = rd16(h + 8);
+            out[j] = FoldRec{h + 22, rd64(h + 14), rd64(h), 0, db->files[i], rd32(h + 10), k};
+            p += 22ull + k;
+          }
+        }
+      });
+    }
+    t_fold += ms_since(tf);
+    auto th = std::chrono::steady_clock::now();
+    {
+      std::vector<char> wok(to_write.size(), 1);
+      const unsigned nw = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)to_write.size()));
+      parallel_for(nw, [&](unsigned t) {
+        for (size_t j = t; j < to_write.size(); j += nw) {
+          const Body& B = bodies[to_write[j]];
+          wok[j] = write_file_raw2(hint_path(path, db->files[to_write[j]]), B.b, B.n, cask_xxh::xxh32(B.b, B.n, 0));
+        }
+      });
+      for (size_t j = 0; j < to_write.size() && fail == CASK_OK; ++j)
+        if (!wok[j]) {
+          fail = CASK_E_IO;
+          fail_fid = db->files[to_write[j]];
+        }
+    }
+    t_hint += ms_since(th);
+    if (fail != CASK_OK) break;
+    // Index::update + Stats over the batch's records (their keys stay in hints[] / the batch's
+    // bodies until here)
+    auto tf2 = std::chrono::steady_clock::now();
+    parallel_fold(recs.get(), total, db->index);
+    t_fold += ms_since(tf2);
+    recs.reset();
+    RawBytes().p.swap(bat[b].hb.p);  // (the batch's bodies are no longer needed)
+    for (size_t i = fi; i < fe; ++i)
+      if (use_hint[i]) std::vector<uint8_t>().swap(hints[i]);
+    fi = fe;
   }
-  db->timings[2] = ms_since(th);
+  join_all();
+  edlock = std::unique_lock<std::mutex>();
+  db->timings[0] = t_read;
+  db->timings[1] = t_dev;
+  db->timings[2] = t_hint;
+  db->timings[3] = t_fold;
+  db->timings[4] = ms_since(t0);
   if (fail != CASK_OK) {
     delete db;
     set_err(err, fail, fail_fid, fail_pos, fail_e, fail_f);
     return nullptr;
   }
-  {  // Index::update + Stats over every record (the keys stay in hints[] / hbuf until here)
-    auto tf2 = std::chrono::steady_clock::now();
-    parallel_fold(recs.get(), total, db->index);
-    t_fold += ms_since(tf2);
-  }
-  db->timings[3] = t_fold;
-  db->timings[4] = ms_since(t0);
   return db;
 }
 

@@ -123,11 +123,13 @@ def test_golden_rows_device(gpu_ctx, case):
 @pytest.mark.parametrize("case", golden_cases())
 def test_golden_engine_open(native, case, tmp_path, monkeypatch, par_fold):
     """Cask::open on the fixture directory: keydir, stats, sequence or error, hint files — with the
-    fold on one thread and sharded by key hash over threads (CASK_PAR_FOLD_MIN=0 forces it)."""
+    fold on one thread and sharded by key hash over threads (CASK_PAR_FOLD_MIN=0 forces it), the
+    latter with every data file a pipeline batch of its own (read, scanned and folded in turn)."""
     from cask_amd import CaskOptions, errors
     monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if par_fold else str(1 << 62))
     if par_fold:  # and the hint bodies' copy to the host staged through the pinned ring
         monkeypatch.setenv("CASK_STAGE_MIN", "0")
+        monkeypatch.setenv("CASK_OPEN_BATCH", "1")
     exp = _expected(case)
     rep = exp["replay"]
     d = tmp_path / case
