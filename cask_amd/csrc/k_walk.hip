@@ -235,8 +235,10 @@ __device__ __forceinline__ uint64_t walk_search(SearchLds& L, const uint8_t* dat
 // found four at a time per aligned dword (SWAR zero-byte test), in 8-KiB windows. The short
 // candidates of a window are hashed 16 at a time in offset order (lane l scans the window's dwords
 // [32l, 32l + 32): lane order is offset order) until one verifies; long ones are listed for the hop
-// back. Same answer as walk_search for every input: the filter only skips offsets whose record
-// could neither be short nor end within the horizon.
+// back. Same answer as walk_search for every input whose keys are at most 4,351 B: the filter skips
+// offsets whose record could neither be short nor end within the horizon, and offsets whose
+// key_size is larger (a run start after such a key is found later and k_finish's check sends the
+// run to the repair: speed only).
 constexpr uint32_t kSwNL = 8, kSwWin = kSwNL * 1024, kSwUse = kSwWin - 16, kSwStep = kSwUse - 18;
 constexpr uint32_t kSwDw = 32;  // dwords of candidate bytes per lane per window (64 x 32 x 4 >= kSwStep)
 static_assert(64 * kSwDw * 4 >= kSwStep, "every candidate byte of a window is scanned");
@@ -271,34 +273,46 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
     const uint64_t ob = (len - wb >= 18) ? len - wb - 17 : 0;
     const uint32_t ostop = (uint32_t)(oa < ob ? oa : ob);
     // phase 1: candidate bytes (+17) of lane's dwords; short candidates into a bit mask (bit 4k+b
-    // of sm[k>>3]), long ones appended to the list
-    // lane l: the 16-B aligned dwords [d0, d0 + 32) read as 8 ds_read_b128 (a lane-contiguous
-    // layout keeps lane order = offset order; 32 x ds_read_b32 at a 128-B lane stride hit one bank)
+    // of sm[k>>4], k = the dword), long ones appended to the list. A candidate's key_size high byte
+    // (+13, the same byte of the dword before) must be at most 0x10: keys over 4,351 B are left to
+    // the repair (speed only), random bytes pass 1 time in 15.
+    // lane l: the 16-B aligned dwords [d0, d0 + 32) (a lane-contiguous layout keeps lane order =
+    // offset order), read as 8 ds_read_b128 in an order rotated by the lane — piece (j + l) % 8 at
+    // read j — so that the 8 lanes of each LDS cycle hit 8 different bank quads (in plain order a
+    // 128-B lane stride put every lane on 2 of them)
     const uint32_t d0 = (((x0 + 17) >> 2) & ~3u) + kSwDw * lane;
-    uint32_t sm[kSwDw / 8] = {0u, 0u, 0u, 0u};
+    uint64_t sm[2] = {0ull, 0ull};
     u32x4 wv[kSwDw / 4];
+    const uint32_t dprev = L.win[d0 - 1];  // (x0 + 17 >= 17: d0 >= 4)
 #pragma unroll
-    for (uint32_t j = 0; j < kSwDw / 4; ++j) wv[j] = ((const u32x4*)L.win)[d0 / 4 + j];
+    for (uint32_t j = 0; j < kSwDw / 4; ++j) wv[j] = ((const u32x4*)L.win)[d0 / 4 + ((j + lane) & 7)];
 #pragma unroll
-    for (uint32_t k = 0; k < kSwDw; ++k) {
-      const uint32_t w = wv[k >> 2][k & 3];
-      uint32_t m = zero_bytes(w) | zero_bytes(~w);
-      while (m) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
-        m &= m - 1;
-        const int64_t o = (int64_t)(4 * (d0 + k) + b) - 17 - (int64_t)x0;
-        if (o < 0 || o >= (int64_t)ostop) continue;
-        const uint64_t rl = lds_reclen(L.win, x0 + (uint32_t)o);
-        const uint64_t x = wb + (uint64_t)o;
-        if (rl <= sshort) {
-          if (x + rl <= len) sm[k >> 3] |= 1u << (4 * (k & 7) + b);
-        } else if (x + rl <= lim) {
-          const uint32_t r = atomicAdd(&L.nl, 1u);
-          if (r < kLongList) {
-            L.lx[r] = x;
-            L.le[r] = x + rl;
-          } else {
-            over = true;
+    for (uint32_t j = 0; j < kSwDw / 4; ++j) {
+      const uint32_t pc = (j + lane) & 7;  // the piece in wv[j]
+#pragma unroll
+      for (uint32_t e = 0; e < 4; ++e) {
+        const uint32_t w = wv[j][e];
+        const uint32_t wp = e ? wv[j][e - 1] : (pc ? wv[(j + 7) & 7][3] : dprev);
+        const uint32_t kszhi_small = ~(((wp & 0x7F7F7F7Fu) + 0x6F6F6F6Fu) | wp) & 0x80808080u;  // byte < 0x11
+        uint32_t m = (zero_bytes(w) | zero_bytes(~w)) & kszhi_small;
+        const uint32_t k = 4 * pc + e;
+        while (m) {
+          const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
+          m &= m - 1;
+          const int64_t o = (int64_t)(4 * (d0 + k) + b) - 17 - (int64_t)x0;
+          if (o < 0 || o >= (int64_t)ostop) continue;
+          const uint64_t rl = lds_reclen(L.win, x0 + (uint32_t)o);
+          const uint64_t x = wb + (uint64_t)o;
+          if (rl <= sshort) {
+            if (x + rl <= len) sm[k >> 4] |= 1ull << (4 * (k & 15) + b);
+          } else if (x + rl <= lim) {
+            const uint32_t r = atomicAdd(&L.nl, 1u);
+            if (r < kLongList) {
+              L.lx[r] = x;
+              L.le[r] = x + rl;
+            } else {
+              over = true;
+            }
           }
         }
       }
@@ -308,8 +322,7 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
     // phase 2: the short candidates in offset order, 16 per round (one per quad)
     for (;;) {
       WCNT(6)
-      const uint32_t mine = (uint32_t)__builtin_popcount(sm[0]) + __builtin_popcount(sm[1]) + __builtin_popcount(sm[2]) +
-                            __builtin_popcount(sm[3]);
+      const uint32_t mine = (uint32_t)__builtin_popcountll(sm[0]) + (uint32_t)__builtin_popcountll(sm[1]);
       // exclusive prefix of the counts over lanes (lane order is offset order)
       uint32_t pre = mine;
       for (int s = 1; s < 64; s <<= 1) {
@@ -322,11 +335,11 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
       // this lane's candidates with global rank < 16 go to cand[rank]
       uint32_t r = pre;
 #pragma unroll
-      for (uint32_t g = 0; g < kSwDw / 8; ++g) {
+      for (uint32_t g = 0; g < 2; ++g) {
         while (sm[g] && r < 16) {
-          const uint32_t bit = (uint32_t)__builtin_ctz(sm[g]);
+          const uint32_t bit = (uint32_t)__builtin_ctzll(sm[g]);
           sm[g] &= sm[g] - 1;
-          const uint32_t k = 8 * g + (bit >> 2), b = bit & 3;
+          const uint32_t k = 16 * g + (bit >> 2), b = bit & 3;
           L.cand[r++] = 4 * (d0 + k) + b - 17 - x0;
         }
       }
@@ -634,112 +647,11 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
 #endif
 }
 
-// The same speculative start found by chain plausibility instead of checksums (k_walk_search with
-// ScanArgs::search_mode 1): the lowest offset >= b0 whose header and the next kChainHops headers of
-// its chain are plausible — key at most kChainKey bytes, value_size below 2^24 (or a tombstone), the
-// record inside the file — or whose chain ends exactly at the file's end. Offsets are pre-filtered
-// as in walk_search_sw (byte +17 is 0x00 or 0xFF), their headers decoded from the staged window,
-// and the plausible ones chained 64 at a time in offset order (one per lane; hops past the window
-// read from HBM). No record is hashed and no hop back is needed: the true first start of a chain of
-// such records is itself a candidate. Speed only: k_finish checks the start like any other, and
-// a log whose records break the plausibility rule falls back to walk_search_sw per run.
-constexpr uint32_t kChainHops = 3, kChainKey = 4096;
-struct SearchLdsCh {
-  uint32_t win[kSwWin / 4 + 16];
-  uint32_t cand[64];
-};
-__device__ __forceinline__ bool hdr_plausible(uint32_t ksz, uint32_t vsz, uint64_t y, uint64_t rl, uint64_t len) {
-  return ksz <= kChainKey && (vsz == 0xFFFFFFFFu || vsz < (1u << 24)) && y + rl <= len;
-}
-__device__ __forceinline__ bool chain_plausible(const uint8_t* data, uint64_t len, uint64_t y) {
-#pragma unroll 1
-  for (uint32_t h = 0; h < kChainHops; ++h) {
-    if (y == len) return true;
-    if (y + 18 > len) return false;
-    const uint32_t w3 = gld4(data + y + 12), vsz = gld4(data + y + 14);
-    const uint32_t ksz = w3 & 0xFFFFu;
-    const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-    if (!hdr_plausible(ksz, vsz, y, rl, len)) return false;
-    y += rl;
-  }
-  return true;
-}
-__device__ __forceinline__ uint64_t walk_search_chain(SearchLdsCh& L, const uint8_t* data, uint64_t len, uint64_t b0,
-                                                      uint64_t b1) {
-  const uint32_t lane = threadIdx.x;
-  const uint64_t lim = (b1 + kSearchPast < len) ? b1 + kSearchPast : len;
-  for (uint64_t wb = b0; wb < lim; wb += kSwStep) {
-    const uint32_t x0 = walk_stage<kSwNL>(L.win, data, len, wb);
-    const uint64_t oa = (lim - wb < kSwStep) ? lim - wb : kSwStep;
-    const uint64_t ob = (len - wb >= 18) ? len - wb - 17 : 0;
-    const uint32_t ostop = (uint32_t)(oa < ob ? oa : ob);
-    // phase 1: plausible headers among the lane's candidate bytes (bit 4k+b of sm[k>>3])
-    const uint32_t d0 = (((x0 + 17) >> 2) & ~3u) + kSwDw * lane;
-    uint32_t sm[kSwDw / 8] = {0u, 0u, 0u, 0u};
-    u32x4 wv[kSwDw / 4];
-#pragma unroll
-    for (uint32_t j = 0; j < kSwDw / 4; ++j) wv[j] = ((const u32x4*)L.win)[d0 / 4 + j];
-#pragma unroll
-    for (uint32_t k = 0; k < kSwDw; ++k) {
-      const uint32_t w = wv[k >> 2][k & 3];
-      uint32_t m = zero_bytes(w) | zero_bytes(~w);
-      while (m) {
-        const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
-        m &= m - 1;
-        const int64_t o = (int64_t)(4 * (d0 + k) + b) - 17 - (int64_t)x0;
-        if (o < 0 || o >= (int64_t)ostop) continue;
-        const uint32_t xo = x0 + (uint32_t)o;
-        const uint32_t i = (xo + 12) >> 2, sh = xo & 3;
-        const uint32_t e0 = L.win[i], e1 = L.win[i + 1], e2 = L.win[i + 2];
-        const uint32_t w3 = fun(e0, e1, sh), w4 = fun(e1, e2, sh);
-        const uint32_t ksz = w3 & 0xFFFFu, vsz = (w3 >> 16) | (w4 << 16);
-        const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-        if (hdr_plausible(ksz, vsz, wb + (uint64_t)o, rl, len)) sm[k >> 3] |= 1u << (4 * (k & 7) + b);
-      }
-    }
-    // phase 2: the plausible headers in offset order, 64 per round, each lane chaining one
-    for (;;) {
-      const uint32_t mine = (uint32_t)__builtin_popcount(sm[0]) + __builtin_popcount(sm[1]) + __builtin_popcount(sm[2]) +
-                            __builtin_popcount(sm[3]);
-      uint32_t pre = mine;
-      for (int s = 1; s < 64; s <<= 1) {
-        const uint32_t u = __shfl_up(pre, s, 64);
-        if ((int)lane >= s) pre += u;
-      }
-      const uint32_t total = __shfl(pre, 63, 64);
-      pre -= mine;
-      if (!total) break;
-      uint32_t r = pre;
-#pragma unroll
-      for (uint32_t g = 0; g < kSwDw / 8; ++g) {
-        while (sm[g] && r < 64) {
-          const uint32_t bit = (uint32_t)__builtin_ctz(sm[g]);
-          sm[g] &= sm[g] - 1;
-          const uint32_t k = 8 * g + (bit >> 2), b = bit & 3;
-          L.cand[r++] = 4 * (d0 + k) + b - 17 - x0;
-        }
-      }
-      __syncthreads();
-      const uint32_t nc = total < 64 ? total : 64u;
-      bool ok = false;
-      if (lane < nc) ok = chain_plausible(data, len, wb + L.cand[lane] + lds_reclen(L.win, x0 + L.cand[lane]));
-      const unsigned long long mo = __ballot(ok);
-      const uint64_t found = mo ? wb + L.cand[__builtin_ctzll(mo)] : kNone;
-      __syncthreads();
-      if (mo) return found;
-    }
-  }
-  return kNone;
-}
-
 // Each walk run's speculative first start (walk_search), ahead of the chase: a run whose first chunk
 // starts a file needs none, and only the first segment of a run can. Kept out of k_walk_runs: the
 // search's registers would lower how many chasing waves fit on a CU.
 __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
-  __shared__ union {
-    SearchLdsSw sw;
-    SearchLdsCh ch;
-  } L;
+  __shared__ SearchLdsSw L;
   uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)wst;
   const uint64_t R = a.run;
@@ -755,16 +667,7 @@ __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* 
     const uint64_t se = fend < tend ? fend : tend;
     const uint64_t b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint64_t b1 = ((se - fd.first_chunk) * (uint64_t)a.chunk < fd.len) ? (se - fd.first_chunk) * (uint64_t)a.chunk : fd.len;
-    uint64_t s0 = 0;
-    if (b0 != 0 && a.search_mode == 1) {
-      s0 = walk_search_chain(L.ch, fd.data, fd.len, b0, b1);
-      if (s0 == kNone) {
-        __syncthreads();
-        s0 = walk_search_sw(L.sw, fd.data, fd.len, b0, b1, wst, a.search_short);
-      }
-    } else if (b0 != 0) {
-      s0 = walk_search_sw(L.sw, fd.data, fd.len, b0, b1, wst, a.search_short);
-    }
+    const uint64_t s0 = b0 == 0 ? 0 : walk_search_sw(L, fd.data, fd.len, b0, b1, wst, a.search_short);
     if (threadIdx.x == 0) a.tin[t] = s0;
   }
 #ifdef CASK_STAMPS

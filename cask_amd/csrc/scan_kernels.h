@@ -161,7 +161,7 @@ struct ScanArgs {
   // k_walk_search: candidates of at most this many bytes are verified by their checksum, longer
   // ones are listed for the hop back (kSearchShort; CASK_SEARCH_SHORT tuning knob)
   uint32_t search_short;
-  uint32_t search_mode;  // k_walk_search: 0 checksum-verified candidates, 1 chain plausibility first
+  uint32_t pad_ss;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,

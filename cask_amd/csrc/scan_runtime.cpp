@@ -437,9 +437,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // CASK_SEARCH_SHORT (tuning knob): k_walk_search verifies candidates up to this long by checksum
   static const uint32_t ss_env = getenv("CASK_SEARCH_SHORT") ? (uint32_t)atoi(getenv("CASK_SEARCH_SHORT")) : 2048u;
   a.search_short = ss_env < 64 ? 64 : ss_env > 2048 ? 2048 : ss_env;
-  // CASK_SEARCH=hash|chain (tuning knob): how k_walk_search verifies a run's speculative start
-  static const uint32_t sm_env = getenv("CASK_SEARCH") && !strcmp(getenv("CASK_SEARCH"), "chain") ? 1u : 0u;
-  a.search_mode = sm_env;
   // the dense path: CASK_DENSE=0 (tuning knob) sends every call through the repair path's k_compact
   static const bool dense_on = !(getenv("CASK_DENSE") && atoi(getenv("CASK_DENSE")) == 0);
   const bool dense = rows != nullptr && dense_on && total_chunks > 0;
