@@ -25,6 +25,16 @@
 
 namespace cask_dev {
 
+#ifdef CASK_STAMPS  // diagnostic build: k_run_hash phase cycle sums -> a.stamps[8..15] (tools/hash_stamps.py)
+#define HST(v) const uint64_t v = __builtin_amdgcn_s_memtime();
+#define HADD(i, v) hst[i] += __builtin_amdgcn_s_memtime() - (v);
+#define HCNT(i) hst[i] += 1;
+#else
+#define HST(v)
+#define HADD(i, v)
+#define HCNT(i)
+#endif
+
 namespace {
 
 typedef __attribute__((address_space(1))) uint32_t g_u32;
@@ -461,12 +471,20 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
 // ---------------------------------------------------------------------------------------------
 // Split path, pass 2 — k_run_hash: Entry::from_read's checksum (data.rs:185-198) of every record the
 // chase found. A wave claims runs and hands their records, in order, to its 16 quads: a quad hashes
-// its record straight from HBM (one round of up to D 64-B blocks in flight while it mixes the one
-// before; lane q keeps stripe accumulator q, quad_transpose), and takes the next record of the wave's
-// stream as it starts one (its slot row and chunk address arrive with the record's first round). A
-// failed record gets the bad bit in its slot row and lowers its chunk's first failing row (cerr),
-// which k_finish reads. The wave's stream runs on from one claimed run to the next, so no quad
+// its record straight from HBM (lane q keeps stripe accumulator q, quad_transpose), and takes the next
+// record of the wave's stream as it starts one (its slot row and chunk address are loaded one
+// iteration ahead). A failed record gets the bad bit in its slot row and lowers its chunk's first
+// failing row (cerr), which k_finish reads. The wave's stream runs on from one claimed run to the
+// next (the next run's row counts are loaded one iteration before they are needed), so no quad
 // waits for a run's last record.
+//
+// The pipeline: iteration i issues round i (up to D 64-B blocks of each quad's record, its partial
+// last stripe, the stored checksum of a record's first round) and then mixes round i - 1. Every
+// quad issues every one of those loads (a quad with nothing to load reads one safe line), and the
+// two rounds live in two register sets used in turn (the loop body twice, no copies), so the
+// compiler's counted waits wait for round i - 1 only and round i stays in flight while it is mixed.
+// The loads whose results the next iteration's bookkeeping needs (slot rows, chunk addresses, the
+// next run's counts) are issued before the round's, so waiting for them never waits for the round.
 // ---------------------------------------------------------------------------------------------
 template <uint32_t D>
 __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
@@ -480,46 +498,50 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
   g_u32* slots = (g_u32*)a.slots;
   const g_u64* cd = (const g_u64*)a.cdesc;
-  uint32_t* pf0 = s_pf[wv][0];
-  uint32_t* pf1 = s_pf[wv][1];
+  uint32_t* pfA = s_pf[wv][0];  // the run records are handed out from (A) and the one after it (B)
+  uint32_t* pfB = s_pf[wv][1];
   const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
+  const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;      // a line every idle load may read
 
-  // The wave's record stream (uniform): two run slots, the one records are handed out from (cs) and
-  // its cursor (cur); a slot is refilled from the claim counter once the other one runs low.
-  uint64_t rt0[2] = {0, 0};
-  uint32_t rn[2] = {0, 0}, rch[2] = {0, 0};
-  bool rfull[2] = {false, false};
-  uint32_t cs = 0, cur = 0;
-  bool first_claim = true, runs_left = true;
-  auto load_run = [&](uint32_t s) {
-    uint64_t k;
-    if (first_claim) {
-      k = blockIdx.x * 4ull + wv;
-      first_claim = false;
-    } else {  // (every lane takes part in the atomic, lane 0 adding 1: no lane-0 branch)
-      const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
-      k = (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old);
-    }
-    if (k >= nruns) {
-      runs_left = false;
-      return;
-    }
-    const uint64_t t0 = (a.wruns ? a.wruns[k] : k) * R;
+  // The wave's record stream (uniform): two runs, A (records are handed out from it, at cursor
+  // cur) and B (the next one, once loaded: fullB), each as its first chunk, chunk count and row
+  // count. B is refilled from the claim counter as soon as it is free (at the top of an iteration:
+  // the wait for the claim also waits for the round in flight, once a run). (Plain variables, not
+  // arrays indexed by the slot: those go to scratch memory, whose loads wait for every load.)
+  uint64_t rtA = 0, rtB = 0;
+  uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
+  bool fullB = false;
+  uint32_t cur = 0;
+  bool runs_left = true;
+  auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
+  // run k's chunk-row prefix into LDS and its bounds into A or B; false if there is no run k (the
+  // flags are set by the callers: a store to one of two flags chosen at run time is what the
+  // compiler merges into a store through a selected pointer, which keeps both in scratch memory)
+  auto load_run = [&](bool intoA, uint64_t k) __attribute__((always_inline)) -> bool {
+    if (k >= nruns) return false;
+    const uint64_t t0 = run_start(k);
     const uint32_t nch = (uint32_t)(a.total_chunks - t0 < R ? a.total_chunks - t0 : R);
-    const uint32_t c = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
-    uint32_t inc = c;
+    uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
       if ((int)lane >= o) inc += u;
     }
-    uint32_t* pf = s ? pf1 : pf0;
+    uint32_t* pf = intoA ? pfA : pfB;
     if (lane < nch) pf[lane + 1] = inc;
     if (lane == 0) pf[0] = 0;
-    rt0[s] = t0;
-    rch[s] = nch;
-    rn[s] = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
-    rfull[s] = true;
+    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
+    if (intoA) {
+      rtA = t0;
+      rchA = nch;
+      rnA = n;
+    } else {
+      rtB = t0;
+      rchB = nch;
+      rnB = n;
+    }
+    return true;
   };
+  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first run, by its index
 
   // a quad's current record (cv) and the round of it in hand: blocks [rlb, rlb + rnl) of its full
   // 64-B blocks, rfin if the record ends in this round (its partial block in T), head if it is the
@@ -532,123 +554,144 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint64_t nt = 0;
   uint32_t nr = 0;
   u32x4 nrow = u32x4{0u, 0u, 0u, 0u}, ndesc = u32x4{0u, 0u, 0u, 0u};
-  u32x4 X[D], T = u32x4{0u, 0u, 0u, 0u};
-  uint32_t xst = 0;
+  // where they are read from: every iteration reloads them (a quad that has claimed a record it
+  // cannot start yet reads the same slot row again; one with no record reads the safe line)
+  uint64_t carow = safe, cadesc = safe;
+  u32x4 XA[D], XB[D], TA = u32x4{0u, 0u, 0u, 0u}, TB = u32x4{0u, 0u, 0u, 0u};
+  uint32_t sA = 0, sB = 0;
 #pragma unroll
-  for (uint32_t d = 0; d < D; ++d) X[d] = u32x4{0u, 0u, 0u, 0u};
+  for (uint32_t d = 0; d < D; ++d) XA[d] = XB[d] = u32x4{0u, 0u, 0u, 0u};
 
-  load_run(0);
-  for (;;) {
-    if (ns == 1) ns = 2;  // (every load of the last iteration has arrived)
-    if (runs_left && !rfull[cs ^ 1] && rn[cs] - cur < 16) load_run(cs ^ 1);
-    // ---- plan this quad's next round
-    bool promote = false, round2 = false, fin2 = false;
-    uint64_t base2 = 0, rl2 = 0, end2 = 0, pt = 0;
-    uint32_t lb2 = 0, nl2 = 0, nblk2 = 0, rb2 = 0, pr = 0, pw3 = 0;
+  uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  (void)hst;
+  HST(h_all)
+  // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi). False: done.
+  auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi)
+                  __attribute__((always_inline)) -> bool {
+    HCNT(6)
+    HST(h0)
+    if (ns == 1) ns = 2;
+    if (runs_left && !fullB) {  // (every lane takes part in the atomic, lane 0 adding 1)
+      const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
+      const bool got = load_run(false, (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old));
+      runs_left = got;
+      fullB = got;
+    }
+    // ---- plan this quad's next round: the rest of its record, or the next record from its slot row
+    // and its chunk's address (branch-free: every lane computes both and selects, so the counted
+    // waits see one path)
     const bool cont = cv && !rfin;
-    if (cont) {  // the rest of the current record
-      lb2 = rlb + D;
-      const uint32_t left = cnblk - lb2;
-      nl2 = left < D ? left : D;
-      fin2 = left < D || (left == D && crem == 0);
-      base2 = cbase;
-      rl2 = crl;
-      end2 = cend;
-      nblk2 = cnblk;
-      rb2 = crem;
-      round2 = true;
-    } else if (ns == 2) {  // the next record, from its slot row and its chunk's address
-      const uint32_t w3 = nrow.w, vsz = nrow.z;
-      const uint64_t b = ((uint64_t)ndesc.y << 32 | ndesc.x) + ((w3 >> 16) & 0x7FFFu);
-      const uint64_t e = (uint64_t)ndesc.w << 32 | ndesc.z;
-      const uint64_t rl = 18ull + (w3 & 0xFFFFu) + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-      promote = true;
-      ns = 0;
-      pt = nt;
-      pr = nr;
-      pw3 = w3;
-      if (b + rl <= e) {  // (an UnexpectedEof row, cut by the file's end, has failed already)
-        base2 = b;
-        rl2 = rl;
-        end2 = e;
-        nblk2 = (uint32_t)((rl - 4) >> 6);
-        rb2 = (uint32_t)((rl - 4) & 63);
-        nl2 = nblk2 < D ? nblk2 : D;
-        fin2 = nblk2 < D || (nblk2 == D && rb2 == 0);
-        round2 = true;
-      }
-    }
-    // ---- issue the round: D blocks, the last partial block, the stored checksum (first round)
-    u32x4 Y[D];
-    const g_u8* bp = (const g_u8*)(uintptr_t)(base2 + 4 + 64ull * lb2 + 16ull * q);
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) {
-      Y[d] = X[d];
-      if (round2 && d < nl2) Y[d] = gld16g(bp + 64 * d);
-    }
-    const bool tail2 = round2 && fin2 && rb2 != 0 && nblk2 - lb2 < D;
-    const uint64_t end16 = (end2 + 15) & ~15ull;
-    const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
-    const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);
-    const bool tclamp2 = tail2 && (rb2 & 15) != 0 && tpart + 16 > end16;
-    u32x4 T2 = T;
-    if (tail2) T2 = gld16g((const g_u8*)(uintptr_t)(tq + 16 <= end16 ? tq : end16 - 16));
-    uint32_t xst2 = xst;
-    if (round2 && !cont) xst2 = gld4g((const g_u8*)(uintptr_t)base2);
+    const bool promote = !cont && ns == 2;
+    const uint32_t w3n = nrow.w, vszn = nrow.z;
+    const uint64_t bn = ((uint64_t)ndesc.y << 32 | ndesc.x) + ((w3n >> 16) & 0x7FFFu);
+    const uint64_t en = (uint64_t)ndesc.w << 32 | ndesc.z;
+    const uint64_t rln = 18ull + (w3n & 0xFFFFu) + (vszn == 0xFFFFFFFFu ? 0ull : (uint64_t)vszn);
+    // (an UnexpectedEof row, cut by the file's end, has failed already: nothing to hash)
+    const bool round2 = cont || (promote && bn + rln <= en);
+    const uint32_t lb2 = cont ? rlb + D : 0u;
+    const uint64_t base2 = cont ? cbase : bn, rl2 = cont ? crl : rln, end2 = cont ? cend : en;
+    const uint32_t nblk2 = cont ? cnblk : (uint32_t)((rln - 4) >> 6);
+    const uint32_t rb2 = cont ? crem : (uint32_t)((rln - 4) & 63);
+    const uint32_t left = nblk2 - lb2;
+    const uint32_t nl2 = round2 ? (left < D ? left : D) : 0u;
+    const bool fin2 = round2 && (left < D || (left == D && rb2 == 0));
+    const uint64_t pt = nt;
+    const uint32_t pr = nr, pw3 = w3n;
+    ns = promote ? 0u : ns;
+    HADD(1, h0)
+    HST(h1)
     // ---- the stream's next records to the quads that have none (in lane order)
     const bool want = ns == 0;
     const unsigned long long wm = __ballot(qlead && want) & qmask;
     const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
+    // every lane loads a slot row and a chunk address every iteration (the safe line when it takes
+    // no record): a load into a loop-carried register only under a branch is a copy after the
+    // merge, and the copy waits for every load in flight
+    // (branch-free for the lanes: the rank, chunk search and addresses are computed by every lane)
+    const uint32_t l0 = lane & ~3u;
+    const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (l0 ? (~0ull >> (64 - l0)) : 0ull));
+    const uint32_t rem = rnA - cur;
+    const bool up = myrank >= rem;
+    const uint32_t idx = up ? myrank - rem : cur + myrank;
+    const bool claimed = want && (up ? (fullB && idx < rnB) : true);
+    const uint32_t* pf = up ? pfB : pfA;
+    uint32_t lo = 0, hi = up ? rchB : rchA;  // the last chunk j with pf[j] <= idx
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {  // (a run is at most 64 chunks)
+      const uint32_t mid = (lo + hi) >> 1;
+      const bool go = hi - lo > 1;
+      const bool le = go && pf[mid] <= idx;
+      lo = le ? mid : lo;
+      hi = go && !le ? mid : hi;
+    }
+    const uint64_t ntc = (up ? rtB : rtA) + lo;
+    const uint32_t nrc = idx - pf[lo];
+    nt = claimed ? ntc : nt;
+    nr = claimed ? nrc : nr;
+    carow = claimed ? (uint64_t)(uintptr_t)(slots + (ntc * (uint64_t)a.slot_cap + nrc) * 4) : promote ? safe : carow;
+    cadesc = claimed ? (uint64_t)(uintptr_t)(cd + 2 * ntc) : promote ? safe : cadesc;
+    uint64_t arow = carow, adesc = cadesc;
     if (nw) {
-      // quads before this one that want a record (the same in the quad's four lanes)
-      const uint32_t l0 = lane & ~3u;
-      const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (l0 ? (~0ull >> (64 - l0)) : 0ull));
-      const uint32_t rem = rn[cs] - cur;
-      const uint32_t so = cs ^ 1;
-      const bool up = myrank >= rem;
-      const uint32_t idx = up ? myrank - rem : cur + myrank;
-      const bool ok = want && (up ? (rfull[so] && idx < rn[so]) : true);
-      if (ok) {
-        const uint32_t* pf = (up ? so : cs) ? pf1 : pf0;
-        uint32_t lo = 0, hi = up ? rch[so] : rch[cs];  // the last chunk j with pf[j] <= idx
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (pf[mid] <= idx) lo = mid; else hi = mid;
-        }
-        nt = (up ? rt0[so] : rt0[cs]) + lo;
-        nr = idx - pf[lo];
-        // both addresses in registers before either load: otherwise the second address may be built
-        // in the first load's destination, a write that waits for every load in flight (the round)
-        uint64_t arow = (uint64_t)(uintptr_t)(slots + (nt * (uint64_t)a.slot_cap + nr) * 4);
-        uint64_t adesc = (uint64_t)(uintptr_t)(cd + 2 * nt);
-        asm volatile("" : "+v"(arow), "+v"(adesc));
-        nrow = *(const g_u32x4*)(uintptr_t)arow;
-        ndesc = *(const g_u32x4*)(uintptr_t)adesc;
-        ns = 1;
-      }
-      const uint32_t avail = rem + (rfull[so] ? rn[so] : 0u);
+      const uint32_t avail = rem + (fullB ? rnB : 0u);
       const uint32_t used = nw < avail ? nw : avail;
-      if (used >= rem && rfull[so]) {  // the current run is handed out: the stream moves on
-        rfull[cs] = false;
-        cs = so;
+      if (used >= rem && fullB) {  // run A is handed out: the stream moves on to B
+        rtA = rtB;
+        rnA = rnB;
+        rchA = rchB;
+        uint32_t* t = pfA;
+        pfA = pfB;
+        pfB = t;
+        fullB = false;
         cur = used - rem;
       } else {
         cur += used;
       }
     }
+    ns = claimed ? 1u : ns;
+    // ---- issue the round: D blocks, the last partial block, the stored checksum (first round);
+    // every quad issues every load (the ones it does not need read the safe line). Every address
+    // of the iteration's loads is in a register before the first load issues: an address built
+    // after a load may be built in that load's destination, a write that waits for every load in
+    // flight.
+    const uint64_t bpa = base2 + 4 + 64ull * lb2 + 16ull * q;
+    uint64_t ya[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;
+    const bool tail2 = round2 && fin2 && rb2 != 0;  // (then nblk2 - lb2 < D)
+    const uint64_t end16 = (end2 + 15) & ~15ull;
+    const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
+    const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);
+    const bool tclamp2 = tail2 && (rb2 & 15) != 0 && tpart + 16 > end16;
+    uint64_t ta = tail2 ? (tq + 16 <= end16 ? tq : end16 - 16) : safe;
+    uint64_t sa = round2 && !cont ? base2 : safe;
+    asm volatile("" : "+v"(arow), "+v"(adesc), "+v"(ta), "+v"(sa));
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
+    nrow = *(const g_u32x4*)(uintptr_t)arow;
+    ndesc = *(const g_u32x4*)(uintptr_t)adesc;
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16g((const g_u8*)(uintptr_t)ya[d]);
+    Ti = gld16g((const g_u8*)(uintptr_t)ta);
+    xi = gld4g((const g_u8*)(uintptr_t)sa);
+    // the round in hand's tail and checksum are used from here on: nothing that reads them (nor the
+    // wait for them, one counted past this round's loads) is scheduled above the loads
+    asm volatile("" : "+v"(Tm.x), "+v"(Tm.y), "+v"(Tm.z), "+v"(Tm.w), "+v"(xm)::"memory");
+    HADD(2, h1)
+    HST(h2)
     // ---- mix the round in hand
     if (cv) {
 #pragma unroll
       for (uint32_t d = 0; d < D; ++d) {
-        u32x4 x = X[d];
+        u32x4 x = Xm[d];
         quad_transpose(x, q);
         const uint32_t w = xround(xround(xround(xround(v, x.x), x.y), x.z), x.w);
         v = d < rnl ? w : v;
       }
-      if (head) cstored = xst;
+      if (head) cstored = xm;
+      HST(h3)
       if (rfin) {  // the last partial block, merge, length, tail, avalanche (data.rs:185-198)
         const uint32_t rem = crem >> 4, tb = crem & 15;
-        u32x4 t = T;
+        u32x4 t = Tm;
         quad_transpose(t, q);
         uint32_t vv = v;
         vv = rem > 0 ? xround(vv, t.x) : vv;
@@ -661,10 +704,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         uint32_t h = (hl >= 16 ? m : P5) + (uint32_t)hl;
         const int src = (int)((lane & ~3u) | rem);
         u32x4 tw;
-        tw.x = (uint32_t)__shfl((int)T.x, src, 64);
-        tw.y = (uint32_t)__shfl((int)T.y, src, 64);
-        tw.z = (uint32_t)__shfl((int)T.z, src, 64);
-        tw.w = (uint32_t)__shfl((int)T.w, src, 64);
+        tw.x = (uint32_t)__shfl((int)Tm.x, src, 64);
+        tw.y = (uint32_t)__shfl((int)Tm.y, src, 64);
+        tw.z = (uint32_t)__shfl((int)Tm.z, src, 64);
+        tw.w = (uint32_t)__shfl((int)Tm.w, src, 64);
         // the file ends within the partial stripe's 16 bytes: its lane loaded the file's last
         // granule instead, which holds the stripe from byte xs - (e16 - 16) on
         const uint64_t xs = cbase + 4 + 64ull * cnblk + 16ull * rem;
@@ -684,7 +727,9 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
           atomicMin(&a.cerr[ct_t], ct_r);
         }
       }
+      HADD(4, h3)
     }
+    HADD(3, h2)
     // ---- state for the next iteration
     if (cont) {
       rlb = lb2;
@@ -709,13 +754,18 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       ct_r = pr;
       cw3 = pw3;
     }
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) X[d] = Y[d];
-    T = T2;
-    xst = xst2;
-    const bool stream_left = rn[cs] != cur || (rfull[cs ^ 1] && rn[cs ^ 1] != 0) || runs_left;
-    if (!stream_left && !__any(cv || ns != 0)) break;
+    const bool stream_left = rnA != cur || (fullB && rnB != 0) || runs_left;
+    return stream_left || __any(cv || ns != 0);
+  };
+  for (;;) {
+    if (!step(XA, TA, sA, XB, TB, sB)) break;
+    if (!step(XB, TB, sB, XA, TA, sA)) break;
   }
+#ifdef CASK_STAMPS
+  HADD(0, h_all)
+  if (a.stamps && lane == 0)
+    for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[8 + i], (unsigned long long)hst[i]);
+#endif
 }
 
 void launch_walk_hash(const ScanArgs& a, int depth, void* stream) {

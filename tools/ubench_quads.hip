@@ -56,6 +56,76 @@ __global__ __launch_bounds__(256) void k_quads(const uint8_t* __restrict__ base,
   if (v == 0x12345678u) sink[0] = v;
 }
 
+// The same segments, one lane per segment (all four XXH32 accumulators in the lane, no transpose):
+// lane k of the grid takes segments k, k + N, ... (N = lanes in the grid), D 16-B loads per round.
+template <uint32_t D, bool HASH>
+__global__ __launch_bounds__(256) void k_lanes(const uint8_t* __restrict__ base, uint64_t nseg, uint32_t S,
+                                               uint32_t scatter, uint32_t* __restrict__ sink) {
+  const uint64_t N = (uint64_t)gridDim.x * 256, lid = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint32_t v0 = P1 + P2, v1 = P2, v2 = 0u, v3 = 0u - P1;
+  const uint32_t nstr = (S - 64) / 16;  // full stripes read of a segment's body
+  for (uint64_t k = lid; k < nseg; k += N) {
+    const uint64_t seg = scatter ? (k * 0x9E3779B97F4A7C15ull) % nseg : k;
+    const g_u8* lp = (const g_u8*)(base + seg * S + 4);
+    u32x4 A[D], B[D];
+#pragma unroll
+    for (uint32_t d = 0; d < D; ++d) A[d] = gld16g(lp + 16 * d);
+    uint32_t b = D;
+    for (;;) {
+      const bool more = b + D <= nstr;
+      if (more) {
+#pragma unroll
+        for (uint32_t d = 0; d < D; ++d) B[d] = gld16g(lp + 16 * (b + d));
+      }
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) {
+        const u32x4 x = A[d];
+        if (HASH) {
+          v0 = xround(v0, x.x);
+          v1 = xround(v1, x.y);
+          v2 = xround(v2, x.z);
+          v3 = xround(v3, x.w);
+        } else {
+          v0 ^= x.x ^ x.y ^ x.z ^ x.w;
+        }
+      }
+      if (!more) break;
+#pragma unroll
+      for (uint32_t d = 0; d < D; ++d) A[d] = B[d];
+      b += D;
+    }
+  }
+  if ((v0 ^ v1 ^ v2 ^ v3) == 0x12345678u) sink[0] = v0;
+}
+
+template <uint32_t D, bool HASH>
+static float run_lanes(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_per_cu, uint32_t scatter, int cus,
+                       uint32_t* sink) {
+  uint64_t nseg = bytes / S;
+  if (!(nseg & 1)) --nseg;
+  const uint32_t grid = (uint32_t)(cus * waves_per_cu / 4);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  hipLaunchKernelGGL((k_lanes<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink);
+  CK(hipDeviceSynchronize());
+  float best = 1e30f;
+  for (int it = 0; it < 3; ++it) {
+    CK(hipEventRecord(a));
+    hipLaunchKernelGGL((k_lanes<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    best = ms < best ? ms : best;
+  }
+  const double rd = (double)nseg * (double)((S - 64) / 16 * 16);
+  printf("lanes D=%2u %s S=%6u waves/CU=%2u %s: %.3f ms %.0f GB/s\n", D, HASH ? "hash" : "xor ", S, waves_per_cu,
+         scatter ? "scattered" : "adjacent ", best, rd / best / 1e6);
+  fflush(stdout);
+  return best;
+}
+
 template <uint32_t D, bool HASH>
 static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_per_cu, uint32_t scatter, int cus,
                  uint32_t* sink) {
@@ -94,13 +164,14 @@ int main() {
   CK(hipMemset(buf, 0x5A, bytes + 4096));
   uint32_t* sink;
   CK(hipMalloc(&sink, 64));
-  for (uint32_t S : {4096u, 65536u}) {
-    for (uint32_t sc : {0u, 1u}) {
-      for (uint32_t w : {8u, 16u, 32u}) {
-        run<8, false>(buf, bytes, S, w, sc, cus, sink);
+  for (uint32_t S : {8192u, 65536u}) {
+    for (uint32_t sc : {1u}) {
+      for (uint32_t w : {8u, 16u, 24u}) {
         run<16, false>(buf, bytes, S, w, sc, cus, sink);
-        run<8, true>(buf, bytes, S, w, sc, cus, sink);
         run<16, true>(buf, bytes, S, w, sc, cus, sink);
+        run_lanes<8, false>(buf, bytes, S, w, sc, cus, sink);
+        run_lanes<8, true>(buf, bytes, S, w, sc, cus, sink);
+        run_lanes<16, true>(buf, bytes, S, w, sc, cus, sink);
       }
     }
   }
