@@ -490,6 +490,7 @@ template <uint32_t D>
 __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   constexpr uint32_t RT = kMaxRun + 1;
   __shared__ uint32_t s_pf[4][2][RT];  // per wave, two runs: the exclusive prefix of their chunks' rows
+  __shared__ uint64_t s_cd[4][2][2 * kMaxRun];  // and their chunks' first-byte and file-end addresses
   const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6;
   const bool qlead = q == 0;
   const uint64_t R = a.run;
@@ -500,6 +501,8 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   const g_u64* cd = (const g_u64*)a.cdesc;
   uint32_t* pfA = s_pf[wv][0];  // the run records are handed out from (A) and the one after it (B)
   uint32_t* pfB = s_pf[wv][1];
+  uint64_t* cdA = s_cd[wv][0];
+  uint64_t* cdB = s_cd[wv][1];
   const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
   const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;      // a line every idle load may read
 
@@ -529,6 +532,11 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     uint32_t* pf = intoA ? pfA : pfB;
     if (lane < nch) pf[lane + 1] = inc;
     if (lane == 0) pf[0] = 0;
+    uint64_t* cdt = intoA ? cdA : cdB;
+    if (lane < nch) {
+      cdt[2 * lane] = cd[2 * (t0 + lane)];
+      cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
+    }
     const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
     if (intoA) {
       rtA = t0;
@@ -553,10 +561,11 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t ns = 0;
   uint64_t nt = 0;
   uint32_t nr = 0;
-  u32x4 nrow = u32x4{0u, 0u, 0u, 0u}, ndesc = u32x4{0u, 0u, 0u, 0u};
-  // where they are read from: every iteration reloads them (a quad that has claimed a record it
+  u32x4 nrow = u32x4{0u, 0u, 0u, 0u};
+  uint64_t ncb = 0, nce = 0;  // its chunk's first byte and its file's end (from the run's LDS table)
+  // where the slot row is read from: every iteration reloads it (a quad that has claimed a record it
   // cannot start yet reads the same slot row again; one with no record reads the safe line)
-  uint64_t carow = safe, cadesc = safe;
+  uint64_t carow = safe;
   u32x4 XA[D], XB[D], TA = u32x4{0u, 0u, 0u, 0u}, TB = u32x4{0u, 0u, 0u, 0u};
   uint32_t sA = 0, sB = 0;
 #pragma unroll
@@ -565,9 +574,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)hst;
   HST(h_all)
-  // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi). False: done.
-  auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi)
-                  __attribute__((always_inline)) -> bool {
+  // One iteration: round in hand in (Xm, xm), the next round into (Xi, xi). In a record's last
+  // round the partial last block is loaded into X[D - 1] (that round has at most D - 1 full
+  // blocks). False: done.
+  auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
     HCNT(6)
     HST(h0)
     if (ns == 1) ns = 2;
@@ -583,8 +593,8 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     const bool cont = cv && !rfin;
     const bool promote = !cont && ns == 2;
     const uint32_t w3n = nrow.w, vszn = nrow.z;
-    const uint64_t bn = ((uint64_t)ndesc.y << 32 | ndesc.x) + ((w3n >> 16) & 0x7FFFu);
-    const uint64_t en = (uint64_t)ndesc.w << 32 | ndesc.z;
+    const uint64_t bn = ncb + ((w3n >> 16) & 0x7FFFu);
+    const uint64_t en = nce;
     const uint64_t rln = 18ull + (w3n & 0xFFFFu) + (vszn == 0xFFFFFFFFu ? 0ull : (uint64_t)vszn);
     // (an UnexpectedEof row, cut by the file's end, has failed already: nothing to hash)
     const bool round2 = cont || (promote && bn + rln <= en);
@@ -628,9 +638,12 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     const uint32_t nrc = idx - pf[lo];
     nt = claimed ? ntc : nt;
     nr = claimed ? nrc : nr;
+    const uint64_t* cdt = up ? cdB : cdA;
+    const uint64_t cbc = cdt[2 * lo], cec = cdt[2 * lo + 1];
+    ncb = claimed ? cbc : ncb;
+    nce = claimed ? cec : nce;
     carow = claimed ? (uint64_t)(uintptr_t)(slots + (ntc * (uint64_t)a.slot_cap + nrc) * 4) : promote ? safe : carow;
-    cadesc = claimed ? (uint64_t)(uintptr_t)(cd + 2 * ntc) : promote ? safe : cadesc;
-    uint64_t arow = carow, adesc = cadesc;
+    uint64_t arow = carow;
     if (nw) {
       const uint32_t avail = rem + (fullB ? rnB : 0u);
       const uint32_t used = nw < avail ? nw : avail;
@@ -641,6 +654,9 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         uint32_t* t = pfA;
         pfA = pfB;
         pfB = t;
+        uint64_t* tc = cdA;
+        cdA = cdB;
+        cdB = tc;
         fullB = false;
         cur = used - rem;
       } else {
@@ -657,24 +673,23 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     uint64_t ya[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;
-    const bool tail2 = round2 && fin2 && rb2 != 0;  // (then nblk2 - lb2 < D)
+    const bool tail2 = round2 && fin2 && rb2 != 0;  // (then nl2 <= D - 1: the partial block in X[D - 1])
     const uint64_t end16 = (end2 + 15) & ~15ull;
     const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
     const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);
     const bool tclamp2 = tail2 && (rb2 & 15) != 0 && tpart + 16 > end16;
     uint64_t ta = tail2 ? (tq + 16 <= end16 ? tq : end16 - 16) : safe;
     uint64_t sa = round2 && !cont ? base2 : safe;
-    asm volatile("" : "+v"(arow), "+v"(adesc), "+v"(ta), "+v"(sa));
+    asm volatile("" : "+v"(arow), "+v"(sa), "+v"(ta));
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
     nrow = *(const g_u32x4*)(uintptr_t)arow;
-    ndesc = *(const g_u32x4*)(uintptr_t)adesc;
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16g((const g_u8*)(uintptr_t)ya[d]);
     Ti = gld16g((const g_u8*)(uintptr_t)ta);
     xi = gld4g((const g_u8*)(uintptr_t)sa);
-    // the round in hand's tail and checksum are used from here on: nothing that reads them (nor the
-    // wait for them, one counted past this round's loads) is scheduled above the loads
+    // the round in hand's last block and checksum are used from here on: nothing that reads them
+    // (nor the wait for them, one counted past this round's loads) is scheduled above the loads
     asm volatile("" : "+v"(Tm.x), "+v"(Tm.y), "+v"(Tm.z), "+v"(Tm.w), "+v"(xm)::"memory");
     HADD(2, h1)
     HST(h2)
@@ -691,7 +706,8 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       HST(h3)
       if (rfin) {  // the last partial block, merge, length, tail, avalanche (data.rs:185-198)
         const uint32_t rem = crem >> 4, tb = crem & 15;
-        u32x4 t = Tm;
+        const u32x4 T = Tm;
+        u32x4 t = T;
         quad_transpose(t, q);
         uint32_t vv = v;
         vv = rem > 0 ? xround(vv, t.x) : vv;
@@ -704,10 +720,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         uint32_t h = (hl >= 16 ? m : P5) + (uint32_t)hl;
         const int src = (int)((lane & ~3u) | rem);
         u32x4 tw;
-        tw.x = (uint32_t)__shfl((int)Tm.x, src, 64);
-        tw.y = (uint32_t)__shfl((int)Tm.y, src, 64);
-        tw.z = (uint32_t)__shfl((int)Tm.z, src, 64);
-        tw.w = (uint32_t)__shfl((int)Tm.w, src, 64);
+        tw.x = (uint32_t)__shfl((int)T.x, src, 64);
+        tw.y = (uint32_t)__shfl((int)T.y, src, 64);
+        tw.z = (uint32_t)__shfl((int)T.z, src, 64);
+        tw.w = (uint32_t)__shfl((int)T.w, src, 64);
         // the file ends within the partial stripe's 16 bytes: its lane loaded the file's last
         // granule instead, which holds the stripe from byte xs - (e16 - 16) on
         const uint64_t xs = cbase + 4 + 64ull * cnblk + 16ull * rem;

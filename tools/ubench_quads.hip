@@ -19,23 +19,27 @@ using namespace cask_dev;
 // quad k of the grid takes segments k, k + Q, k + 2Q, ... (Q = quads in the grid).
 template <uint32_t D, bool HASH>
 __global__ __launch_bounds__(256) void k_quads(const uint8_t* __restrict__ base, uint64_t nseg, uint32_t S,
-                                               uint32_t scatter, uint32_t* __restrict__ sink) {
+                                               uint32_t scatter, uint32_t* __restrict__ sink, uint32_t idle = 0,
+                                               uint32_t extra = 0) {
   const uint32_t lane = threadIdx.x & 63, q = lane & 3;
   const uint64_t Q = (uint64_t)gridDim.x * 64, qid = (uint64_t)blockIdx.x * 64 + (threadIdx.x >> 2);
+  const bool idleq = ((threadIdx.x >> 2) & 3) < idle;  // this quad reads the safe line only
   uint32_t v = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
   const uint32_t nblk = (S - 64) / 64;  // full blocks of a segment's body
   for (uint64_t k = qid; k < nseg; k += Q) {
     const uint64_t seg = scatter ? (k * 0x9E3779B97F4A7C15ull) % nseg : k;  // (nseg odd: a permutation)
-    const g_u8* lp = (const g_u8*)(base + seg * S + 4 + 16 * q);
+    const g_u8* lp = idleq ? (const g_u8*)(base + 16 * q) - 64 * 0 : (const g_u8*)(base + seg * S + 4 + 16 * q);
+    const int64_t step = idleq ? 0 : 64;
     u32x4 A[D], B[D];
 #pragma unroll
-    for (uint32_t d = 0; d < D; ++d) A[d] = gld16g(lp + 64 * d);
+    for (uint32_t d = 0; d < D; ++d) A[d] = gld16g(lp + step * d);
     uint32_t b = D;
     for (;;) {
       const bool more = b + D <= nblk;
       if (more) {
 #pragma unroll
-        for (uint32_t d = 0; d < D; ++d) B[d] = gld16g(lp + 64 * (b + d));
+        for (uint32_t d = 0; d < D; ++d) B[d] = gld16g(lp + step * (int64_t)(b + d));
+        for (uint32_t e = 0; e < extra; ++e) B[0].x ^= gld4g(lp + 4 * e);
       }
 #pragma unroll
       for (uint32_t d = 0; d < D; ++d) {
@@ -128,29 +132,29 @@ static float run_lanes(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t 
 
 template <uint32_t D, bool HASH>
 static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_per_cu, uint32_t scatter, int cus,
-                 uint32_t* sink) {
+                 uint32_t* sink, uint32_t idle = 0, uint32_t extra = 0) {
   uint64_t nseg = bytes / S;
   if (!(nseg & 1)) --nseg;
   const uint32_t grid = (uint32_t)(cus * waves_per_cu / 4);
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink);
+  hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink, idle, extra);
   CK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int it = 0; it < 3; ++it) {
     CK(hipEventRecord(a));
-    hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink);
+    hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink, idle, extra);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     best = ms < best ? ms : best;
   }
-  // bytes actually read: nblk full blocks of each segment
-  const double rd = (double)nseg * (double)((S - 64) / 64 * 64);
-  printf("D=%2u %s S=%6u waves/CU=%2u %s: %.3f ms %.0f GB/s\n", D, HASH ? "hash" : "xor ", S, waves_per_cu,
-         scatter ? "scattered" : "adjacent ", best, rd / best / 1e6);
+  // useful bytes: nblk full blocks of each segment the non-idle quads read
+  const double rd = (double)nseg * (double)((S - 64) / 64 * 64) * (4 - idle) / 4.0;
+  printf("D=%2u %s S=%6u waves/CU=%2u %s idle=%u/4 extra=%u: %.3f ms %.0f GB/s useful\n", D, HASH ? "hash" : "xor ", S,
+         waves_per_cu, scatter ? "scattered" : "adjacent ", idle, extra, best, rd / best / 1e6);
   fflush(stdout);
   return best;
 }
@@ -165,15 +169,11 @@ int main() {
   uint32_t* sink;
   CK(hipMalloc(&sink, 64));
   for (uint32_t S : {8192u, 65536u}) {
-    for (uint32_t sc : {1u}) {
-      for (uint32_t w : {8u, 16u, 24u}) {
-        run<16, false>(buf, bytes, S, w, sc, cus, sink);
-        run<16, true>(buf, bytes, S, w, sc, cus, sink);
-        run_lanes<8, false>(buf, bytes, S, w, sc, cus, sink);
-        run_lanes<8, true>(buf, bytes, S, w, sc, cus, sink);
-        run_lanes<16, true>(buf, bytes, S, w, sc, cus, sink);
-      }
-    }
+    run<16, true>(buf, bytes, S, 8, 1, cus, sink, 0, 0);
+    run<16, true>(buf, bytes, S, 8, 1, cus, sink, 1, 0);
+    run<16, true>(buf, bytes, S, 8, 1, cus, sink, 2, 0);
+    run<16, true>(buf, bytes, S, 8, 1, cus, sink, 0, 2);
+    run<16, true>(buf, bytes, S, 8, 1, cus, sink, 0, 4);
   }
   return 0;
 }
