@@ -2094,6 +2094,14 @@ int cask_db_get_entry(const cask_db* db, const uint8_t* key, uint64_t ksz, cask_
 int64_t cask_db_export(const cask_db* db, uint8_t* key_bytes, uint64_t key_cap, uint64_t* key_off,
                        uint64_t* key_len, cask_index_entry* entries, uint64_t nkeys) {
   if (!db) return CASK_E_INVALID_ARG;
+  if (!key_bytes && !key_off && !key_len && !entries) {  // sizing call: no order needed
+    uint64_t total = 0, n = 0;
+    db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& s) {
+      total += s.ksz;
+      ++n;
+    });
+    return nkeys < n ? CASK_E_CAPACITY : (int64_t)total;
+  }
   struct Ref {
     const uint8_t* key;
     uint32_t ksz;

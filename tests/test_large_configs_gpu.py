@@ -17,7 +17,9 @@ over host threads, orc_replay_parallel).
 """
 import os
 import shutil
+import sys
 import tempfile
+import time
 
 import numpy as np
 import pytest
@@ -28,6 +30,37 @@ pytestmark = pytest.mark.gpu
 
 RPF = 3_702_558  # records of 290 B per 1,073,741,820-B file (configs[1] / configs[3] / configs[4])
 THREADS = 16
+
+
+_T0 = time.time()
+
+
+def _say(msg):
+    """Progress line (run with -s): the GPU harness kills a command that is silent for 3 minutes."""
+    print(f"[{time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+def _beat(label, fn, *args):
+    """fn(*args) on a worker thread (ctypes calls drop the GIL) with a progress line every 30 s."""
+    import threading
+    out = {}
+
+    def run():
+        try:
+            out["v"] = fn(*args)
+        except BaseException as e:  # re-raised on the caller's thread
+            out["e"] = e
+
+    t = threading.Thread(target=run, daemon=True)
+    t.start()
+    while True:
+        t.join(30)
+        if not t.is_alive():
+            break
+        _say(f"{label}: running")
+    if "e" in out:
+        raise out["e"]
+    return out["v"]
 
 
 def _shm_dir(prefix):
@@ -79,10 +112,13 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
             f = variable_file(ctx, i + 1, ks, vsz[sl].clone(), idx + 1, kid[sl].clone(), 0xC0FFEE + i)
             f.data.cpu().numpy().tofile(os.path.join(path, f"{i + 1:010}.cask.data"))
             del f
+            if i % 8 == 7:
+                _say(f"cfg3: wrote {i + 1} files")
         del kid, vsz
         torch.cuda.empty_cache()
         ids = list(range(1, nfiles + 1))
         # the product's open: scan on the device, hint files recreated (they must be the oracle's)
+        _say("cfg3: product open")
         with CaskOptions().max_file_size(1 << 30).open(path) as db:
             assert len(db) == live_want
             maps = [np.memmap(os.path.join(path, f"{i:010}.cask.data"), np.uint8, "r") for i in ids]
@@ -91,22 +127,26 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
                 body = O.hint_body(m)
                 assert hb[:-4].tobytes() == body.tobytes(), i
                 assert int.from_bytes(hb[-4:].tobytes(), "little") == O.xxh32(body.tobytes()), i
+            _say("cfg3: hint files checked; oracle replay")
             # the oracle's keydir (threaded replay) and its compaction of the same files, first
-            pix = O.PIndex(maps, ids, THREADS)
+            pix = _beat("cfg3 oracle replay", O.PIndex, maps, ids, THREADS)
             assert pix.result.err_kind == 0 and pix.result.live == live_want
             assert pix.stats == _stats_rows(db)
             want_dir = os.path.join(work, "oracle")
             os.makedirs(want_dir)
-            r, created = pix.compact_files(path, want_dir, ids, nfiles, 1 << 30)
+            _say("cfg3: oracle compaction")
+            r, created = _beat("cfg3 oracle compaction", pix.compact_files, path, want_dir, ids, nfiles, 1 << 30)
             assert r.err_kind == 0 and r.live_records == live_want
             pix.close()
             del maps
             # the product's compaction in place
-            rep = db.compact_files(ids)
+            _say("cfg3: product compaction")
+            rep = _beat("cfg3 product compaction", db.compact_files, ids)
             assert rep["live_records"] == live_want and rep["tombstones"] == r.tombstones
             assert len(db) == live_want
         # every file the compaction created: same ids, same bytes (the live records in file order;
         # a tombstone tail that differs in order only is compared as a multiset over all files)
+        _say("cfg3: comparing files")
         got = sorted(f for f in os.listdir(path) if f.endswith(".cask.data"))
         assert got == sorted(f"{fid:010}.cask.data" for fid, _ in created)
         tomb_a, tomb_b = [], []
@@ -133,12 +173,13 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
         assert sorted(tomb_a) == sorted(tomb_b)
         # reopen (hint fast path): keydir and stats equal the oracle's replay of the new files
         new_ids = sorted(fid for fid, _ in created)
+        _say("cfg3: oracle replay of the new files; reopen")
         maps = [np.memmap(os.path.join(path, f"{i:010}.cask.data"), np.uint8, "r") for i in new_ids]
-        want, want_stats = O.replay_parallel(maps, new_ids, THREADS)
+        want, want_stats = _beat("cfg3 oracle replay (new files)", O.replay_parallel, maps, new_ids, THREADS)
         del maps
         assert want.err_kind == 0 and want.live == live_want
         with CaskOptions().max_file_size(1 << 30).open(path) as db:
-            dg, nk = _digest_of_export(db)
+            dg, nk = _beat("cfg3 export + digest", _digest_of_export, db)
             assert nk == live_want and dg == want.digest
             assert _stats_rows(db) == want_stats
             assert db.current_sequence == want.max_seq + 1
@@ -174,15 +215,19 @@ def test_cfg4_two_rank_shards_fold_against_oracle(gpu_ctx):
             ids.append(f.file_id)
         del files, views, rows, blk, res
         torch.cuda.empty_cache()
-    want, want_stats = O.replay_parallel(hosts, ids, THREADS)
+        _say(f"cfg4: rank {rank} shard scanned and folded")
+    _say("cfg4: oracle replay")
+    want, want_stats = _beat("cfg4 oracle replay", O.replay_parallel, hosts, ids, THREADS)
+    _say("cfg4: oracle done")
     del hosts
     assert want.err_kind == 0 and want.records == 2 * per_rank * RPF
-    db = fold.finish()
+    db = _beat("cfg4 fold finish", fold.finish)
+    _say("cfg4: finished; stats")
     try:
         assert len(db) == want.live == 2 * per_rank * RPF  # unique keys: every record is live
         assert db.current_sequence == want.max_seq + 1
         assert _stats_rows(db) == want_stats
-        dg, _ = _digest_of_export(db)
+        dg, _ = _beat("cfg4 export + digest", _digest_of_export, db)
         assert dg == want.digest
     finally:
         db.close()
