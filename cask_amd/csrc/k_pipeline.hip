@@ -759,12 +759,6 @@ void launch_long(const ScanArgs& a, void* stream, bool enqueue) {
   if (enqueue) launch_long_enqueue(a, stream);
   launch_long_hash(a, stream);
 }
-__global__ void k_lq_snap(const Counters* ctr, uint32_t* out) {
-  if (threadIdx.x < kLqClasses) out[threadIdx.x] = ctr->lq_cnt[threadIdx.x];
-}
-void launch_lq_snap(const ScanArgs& a, uint32_t* out, void* stream) {
-  hipLaunchKernelGGL(k_lq_snap, dim3(1), dim3(64), 0, S(stream), a.ctr, out);
-}
 void launch_validate(const ScanArgs& a, void* stream) {
   if (!a.nfiles) return;
   // k_val_files runs even with no tiles at all (every file empty): it writes the file totals

@@ -676,30 +676,6 @@ __global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* 
 #endif
 }
 
-// Record lengths at the head of each file (at most 64 files, 32 records each, exact from offset
-// 0): out[0] bytes, out[1] records, out[2] the longest. The host picks the walk mode and the chunk
-// scan's halo from it.
-__global__ void k_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out) {
-  const uint32_t f = threadIdx.x;
-  uint64_t bytes = 0, recs = 0, mx = 0;
-  if (f < nfiles && f < 64) {
-    const FileDesc fd = files[(uint64_t)f * nfiles / (nfiles < 64 ? nfiles : 64)];
-    uint64_t p = 0;
-    for (int k = 0; k < 32 && p + 18 <= fd.len; ++k) {
-      const uint64_t rl = g_reclen(fd.data + p);
-      if (p + rl > fd.len) break;
-      bytes += rl;
-      ++recs;
-      mx = rl > mx ? rl : mx;
-      p += rl;
-    }
-  }
-  if (recs) {
-    atomicAdd(&out[0], (unsigned long long)bytes);
-    atomicAdd(&out[1], (unsigned long long)recs);
-    atomicMax(&out[2], (unsigned long long)mx);
-  }
-}
 
 // Record lengths at kProbeRegions points of every file (one wave per file and point), for the scan
 // mode of each region (speed only: every mode reads every file correctly). Point 0 is the file's
@@ -791,9 +767,6 @@ void launch_walk_search(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(k_walk_search, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
 }
 
-void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {
-  hipLaunchKernelGGL(k_probe, dim3(1), dim3(64), 0, (hipStream_t)stream, files, nfiles, out);
-}
 
 void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream) {
   if (!nfiles) return;

@@ -1,24 +1,21 @@
-// k_walk_hash — walk mode in one pass, gfx950: a quad of lanes per run of chunks chases the record
-// chain (Entries::next, log.rs:403-429: each record starts where the previous one ends) and hashes
-// every record it visits straight from HBM (Entry::from_read's check, data.rs:185-198), so every
-// log byte is read once, by the quad that owns its record.
+// Walk mode, gfx950 (the scan of logs of long records): every log byte read once, by the quad of
+// lanes that hashes its record.
 //
-// Why a quad per run: XXH32's four stripe accumulators are the only parallelism inside a record
+//   k_walk_search (k_walk.hip)  each run of a.run chunks gets a speculative first record start
+//   k_walk_chase                one lane per run follows the record chain header to header
+//                               (Entries::next, log.rs:403-429) and writes slot rows + chunk table
+//   k_run_hash                  Entry::from_read's checksum (data.rs:185-198) of every record the
+//                               chase found, a quad of lanes per record, straight from HBM
+//   k_finish (k_pipeline.hip)   validates the speculated starts (spec[c] == T[c]) and writes rows
+//
+// Why a quad per record: XXH32's four stripe accumulators are the only parallelism inside a record
 // (one lane each); a log of long records needs thousands of records in flight at once to keep HBM
-// busy, and a run of chunks walked by one quad is one such stream. The previous walk mode chased
-// headers with a whole wave per run and left every record longer than its 1-KiB window to a second
-// kernel that read those bytes again (k_long_hash, behind a queue by length class).
+// busy. Why split the chase from the hash: the chase is a chain of dependent 18-B loads (latency
+// bound, ~0.5 ms for configs[2]) and the hash a stream (HBM bound); in one kernel (a quad per run
+// chasing and hashing, round 3's first walk) each quad's stream stalled on its own header chain.
 //
-// Per quad, one round of up to D 64-B blocks of its current record is in flight while it mixes the
-// round before: the loop waits for the round issued last iteration, decides the next round (the rest
-// of the record, or the next record, whose header was loaded one record ahead), issues it, then mixes.
-// A short record costs one iteration; the header of the record after it is always loaded with the
-// record's first round. The loads of an iteration are the same instructions for every quad (idle or
-// finished quads load one safe word), so the compiler's counted waits hold.
-//
-// Output: the chunk table and slot rows of k_scan_chunks / k_walk_runs (spec, exit, count, cerr,
-// long_r = none, slot rows with the checksum verdict): k_finish validates the speculated run starts
-// (k_walk_search, spec[c] == T[c]) and writes the dense rows, and the repair path runs unchanged.
+// Output: the chunk table and slot rows of k_scan_chunks (spec, exit, count, cerr, long_r = none,
+// slot rows with the checksum verdict), so k_finish and the repair path run unchanged.
 #include "device_util.h"
 
 #include <stdlib.h>
@@ -53,24 +50,6 @@ struct WSeg {
   uint64_t t0;     // global index of its first chunk
   uint32_t nch;
 };
-
-__device__ __forceinline__ u32x4 ld16(const WSeg& S, uint64_t o) {
-  const int64_t so = (int64_t)o < S.sl ? (int64_t)o : S.sl;
-  return gld16g((const g_u8*)(S.data + so));
-}
-__device__ __forceinline__ uint32_t ld4(const WSeg& S, uint64_t o) {
-  const int64_t lim = S.sl + 12;
-  const int64_t so = (int64_t)o < lim ? (int64_t)o : lim;
-  return gld4g((const g_u8*)(S.data + so));
-}
-
-// lane 0 of each quad to the whole quad (quad_perm [0,0,0,0])
-__device__ __forceinline__ uint32_t qb0(uint32_t v) {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
-}
-__device__ __forceinline__ uint64_t qb0_64(uint64_t v) {
-  return (uint64_t)qb0((uint32_t)v) | ((uint64_t)qb0((uint32_t)(v >> 32)) << 32);
-}
 
 // The 16 bytes of v from byte s on (s in 0..15), zero-filled past the end.
 __device__ __forceinline__ u32x4 shr_bytes(const u32x4& v, uint32_t s) {
@@ -150,247 +129,6 @@ __device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* fil
 }
 
 }  // namespace
-
-// D: 64-B blocks per round (a quad keeps D * 64 B of its record in flight).
-template <uint32_t D>
-__global__ __launch_bounds__(256) void k_walk_hash(ScanArgs a, const FileDesc* __restrict__ files) {
-  const uint32_t lane = threadIdx.x & 63, q = lane & 3;
-  const bool writer = q == 0;
-  const uint64_t R = a.run;
-  const uint64_t nruns = (a.total_chunks + R - 1) / R;
-  const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
-  const uint64_t nquads = (uint64_t)gridDim.x * (blockDim.x >> 2);
-  const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
-  const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
-  g_u32* slots = (g_u32*)a.slots;
-
-  Walk W;
-  W.S.data = (const uint8_t*)files;  // (a safe address for the loads of a quad with no segment)
-  W.S.len = 16;
-  W.S.sl = 0;
-  W.S.b0 = W.S.b1 = 0;
-  W.S.t0 = 0;
-  W.S.nch = 0;
-  W.run_end = 0;
-  W.cj = kNoChunk;
-  W.cn = 0;
-  W.ccerr = 0xFFFFFFFFu;
-  W.cspec = 0;
-
-  // the record being hashed
-  bool cv = false;
-  uint64_t cp = 0, crl = 0, cseq = 0;
-  uint32_t cnblk = 0, crem = 0, cstored = 0, cksz = 0, cvsz = 0, cj_rec = 0, crow = 0, v = 0;
-  // the round in hand: blocks [rlb, rlb + rnl) of the record's full 64-B blocks; rfin: the record
-  // ends in it (its last partial block, if any, is in T); tclamp: that block's partial stripe could
-  // not be loaded whole (the file ends within its 16 bytes): read exactly when finishing
-  uint32_t rlb = 0, rnl = 0;
-  bool rfin = false, tclamp = false;
-  // the header at hp: in H/H4 when hv; to be loaded this iteration when hissue
-  uint64_t hp = 0;
-  bool hv = false, hissue = false;
-  bool active = true;
-
-  // Next segment of the run, or the next run (claimed); the chain's start in it goes to hp (header
-  // loaded at the next iteration), or the quad is done.
-  bool first_claim = true;
-  uint64_t tnext = 0;  // next chunk of the current run to set up
-  auto next_work = [&]() {
-    for (;;) {
-      if (tnext < W.run_end) {
-        const bool run_first = tnext % R == 0;  // (a run's later segments start files)
-        seg_setup(a, files, W, tnext);
-        tnext = W.S.t0 + W.S.nch;
-        uint64_t s = 0;
-        if (W.S.b0 != 0) s = run_first && a.walk_pre ? a.tin[W.S.t0] : kNone;
-        if (s == kNone || s >= W.S.b1) {  // no record starts in the segment (as found by the search)
-          close_segment(a, W, 0, writer);
-          continue;
-        }
-        hp = s;
-        hissue = true;
-        hv = false;
-        return;
-      }
-      uint64_t k;
-      if (first_claim) {
-        k = blockIdx.x * (uint64_t)(blockDim.x >> 2) + (threadIdx.x >> 2);
-        first_claim = false;
-      } else {
-        // every lane of the quad takes part (lane 0 adds 1): no lane-0 branch around the atomic
-        const uint32_t old = atomicAdd(&a.ctr->hash_next, q == 0 ? 1u : 0u);
-        k = nquads + qb0(old);
-      }
-      if (k >= nruns) {
-        active = false;
-        hv = hissue = false;
-        return;
-      }
-      tnext = k * R;
-      W.run_end = tnext + R < a.total_chunks ? tnext + R : a.total_chunks;
-    }
-  };
-  next_work();
-
-  u32x4 Ya[D], Yb[D], Ta, Tb, Ha, Hb;
-  uint32_t H4a = 0, H4b = 0;
-#pragma unroll
-  for (uint32_t d = 0; d < D; ++d) Ya[d] = Yb[d] = u32x4{0u, 0u, 0u, 0u};
-  Ta = Tb = Ha = Hb = u32x4{0u, 0u, 0u, 0u};
-
-  // One iteration: (Yi, Ti, Hi, H4i) hold what the last iteration loaded; this one loads (Yo, To,
-  // Ho, H4o).
-  auto body = [&](const u32x4* Yi, const u32x4& Ti, const u32x4& Hi, uint32_t H4i, u32x4* Yo, u32x4& To, u32x4& Ho,
-                  uint32_t& H4o) {
-    // ---- plan the next round
-    bool nrec = false, neof = false, nend = false, round2 = false, fin2 = false;
-    uint64_t base2 = 0, nrl = 0, hp2 = hp;
-    uint32_t lb2 = 0, nl2 = 0, nblk2 = 0, rb2 = 0;
-    if (cv && !rfin) {  // the rest of the current record
-      lb2 = rlb + D;
-      const uint32_t left = cnblk - lb2;
-      nl2 = left < D ? left : D;
-      fin2 = left < D || (left == D && crem == 0);
-      base2 = cp;
-      nblk2 = cnblk;
-      rb2 = crem;
-      round2 = true;
-    } else if (hv) {  // the next record: its header is in hand
-      if (hp >= W.S.b1) {
-        nend = true;
-      } else if (hp + 18 > W.S.len) {
-        neof = true;  // header cut short: Io(UnexpectedEof) (data.rs:163)
-      } else {
-        const uint32_t vsz = H4i;
-        nrl = 18ull + (Hi.w & 0xFFFFu) + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-        if (hp + nrl > W.S.len) {
-          neof = true;  // key or value cut short (data.rs:172,181)
-        } else {
-          nrec = true;
-          nblk2 = (uint32_t)((nrl - 4) >> 6);
-          rb2 = (uint32_t)((nrl - 4) & 63);
-          nl2 = nblk2 < D ? nblk2 : D;
-          fin2 = nblk2 < D || (nblk2 == D && rb2 == 0);
-          base2 = hp;
-          round2 = true;
-          hp2 = hp + nrl;  // the header after it, loaded with its first round
-        }
-      }
-    }
-    // ---- issue: D blocks, the last partial block, the header (every quad issues every load)
-    const uint64_t blk0 = base2 + 4 + 64ull * lb2 + 16ull * q;
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) Yo[d] = ld16(W.S, (round2 && d < nl2) ? blk0 + 64ull * d : 0ull);
-    const bool tail2 = round2 && fin2 && rb2 != 0 && nblk2 - lb2 < D;
-    const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);  // the partial stripe
-    const bool tclamp2 = tail2 && (rb2 & 15) != 0 && (int64_t)tpart > W.S.sl;
-    To = ld16(W.S, tail2 ? base2 + 4 + 64ull * nblk2 + 16ull * q : 0ull);
-    const bool hload = nrec || hissue || hv;
-    Ho = ld16(W.S, hload ? hp2 : 0ull);
-    H4o = ld4(W.S, hload ? hp2 + 14 : 0ull);
-    // ---- mix the round in hand
-    if (cv) {
-#pragma unroll
-      for (uint32_t d = 0; d < D; ++d) {
-        u32x4 x = Yi[d];
-        quad_transpose(x, q);
-        const uint32_t w = xround(xround(xround(xround(v, x.x), x.y), x.z), x.w);
-        v = d < rnl ? w : v;
-      }
-      if (rfin) {  // the record's last partial block, merge, length, tail, avalanche (data.rs:185-198)
-        const uint32_t rem = crem >> 4, tb = crem & 15;
-        u32x4 t = Ti;
-        quad_transpose(t, q);
-        uint32_t vv = v;
-        vv = rem > 0 ? xround(vv, t.x) : vv;
-        vv = rem > 1 ? xround(vv, t.y) : vv;
-        vv = rem > 2 ? xround(vv, t.z) : vv;
-        uint32_t m = rotl_var(vv, mrot);
-        m += quad_xor1(m);
-        m += quad_xor2(m);
-        const uint64_t hl = crl - 4;
-        uint32_t h = (hl >= 16 ? m : P5) + (uint32_t)hl;
-        const int src = (int)((lane & ~3u) | rem);
-        u32x4 tw;
-        tw.x = (uint32_t)__shfl((int)Ti.x, src, 64);
-        tw.y = (uint32_t)__shfl((int)Ti.y, src, 64);
-        tw.z = (uint32_t)__shfl((int)Ti.z, src, 64);
-        tw.w = (uint32_t)__shfl((int)Ti.w, src, 64);
-        // The file ends within this stripe's 16 bytes: its lane loaded the file's last 16-B granule
-        // instead (ld16 clamps the address to W.S.sl), which holds the stripe's bytes from byte
-        // x - sl on. (No load here: a load in this branch would make every iteration wait for the
-        // next round's loads.)
-        const int64_t xs = (int64_t)(cp + 4 + 64ull * cnblk + 16ull * rem);
-        tw = shr_bytes(tw, tclamp ? (uint32_t)(xs - W.S.sl) : 0u);
-        const uint32_t n4 = tb >> 2, n1 = tb & 3;
-        h = n4 > 0 ? tail4(h, tw.x) : h;
-        h = n4 > 1 ? tail4(h, tw.y) : h;
-        h = n4 > 2 ? tail4(h, tw.z) : h;
-        const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
-        h = n1 > 0 ? tail1(h, lw & 0xFFu) : h;
-        h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
-        h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
-        h = avalanche(h);
-        const bool bad = h != cstored;  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
-        const uint32_t off = (uint32_t)(cp - W.S.b0 - ((uint64_t)cj_rec << csh));
-        if (writer)
-          *(g_u32x4*)(slots + ((W.S.t0 + cj_rec) * (uint64_t)a.slot_cap + crow) * 4) =
-              u32x4{(uint32_t)cseq, (uint32_t)(cseq >> 32), cvsz, cksz | (off << 16) | (bad ? kSlotBad : 0u)};
-        if (bad && crow < W.ccerr) W.ccerr = crow;
-      }
-    }
-    // ---- state for the next iteration
-    if (cv && rfin) cv = false;
-    if (cv) {  // the record goes on
-      rlb = lb2;
-      rnl = nl2;
-      rfin = fin2;
-      tclamp = tclamp2;
-    }
-    if (nrec) {
-      cv = true;
-      cp = hp;
-      crl = nrl;
-      cnblk = nblk2;
-      crem = rb2;
-      rlb = 0;
-      rnl = nl2;
-      rfin = fin2;
-      tclamp = tclamp2;
-      v = vinit;
-      cstored = Hi.x;
-      cseq = (uint64_t)Hi.y | ((uint64_t)Hi.z << 32);
-      cksz = Hi.w & 0xFFFFu;
-      cvsz = H4i;
-      crow = open_record(a, W, cp, csh, writer, &cj_rec);
-      hp = hp2;  // loaded this iteration
-      hv = true;
-    } else if (neof) {  // the chain ends with an UnexpectedEof row
-      uint32_t j = 0;
-      const uint32_t r = open_record(a, W, hp, csh, writer, &j);
-      const uint32_t off = (uint32_t)(hp - W.S.b0 - ((uint64_t)j << csh));
-      const bool hdr_ok = hp + 18 <= W.S.len;
-      const u32x4 row = hdr_ok ? u32x4{Hi.y, Hi.z, H4i, (Hi.w & 0xFFFFu) | (off << 16)} : u32x4{0u, 0u, 0u, off << 16};
-      if (writer) *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = row;
-      if (r < W.ccerr) W.ccerr = r;
-      close_segment(a, W, kTerm, writer);
-      next_work();
-    } else if (nend) {  // the chain leaves the segment at hp
-      close_segment(a, W, hp, writer);
-      next_work();
-    } else if (hissue) {  // a segment's first header: loaded this iteration
-      hissue = false;
-      hv = true;
-    }
-  };
-
-  for (;;) {
-    if (!__any(active || cv)) break;
-    body(Ya, Ta, Ha, H4a, Yb, Tb, Hb, H4b);
-    if (!__any(active || cv)) break;
-    body(Yb, Tb, Hb, H4b, Ya, Ta, Ha, H4a);
-  }
-}
 
 // ---------------------------------------------------------------------------------------------
 // Split path, pass 1 — k_walk_chase: one lane per run of a.run chunks walks the record chain from
@@ -783,24 +521,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[8 + i], (unsigned long long)hst[i]);
 #endif
 }
-
-void launch_walk_hash(const ScanArgs& a, int depth, void* stream) {
-  if (!a.total_chunks) return;
-  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
-  // CASK_HASH_WAVES (tuning knob): waves per CU of the grid (the runs beyond it are claimed)
-  static const uint32_t per_cu = getenv("CASK_HASH_WAVES") ? (uint32_t)atoi(getenv("CASK_HASH_WAVES")) : 8u;
-  uint64_t quads = (uint64_t)device_cus() * per_cu * 16u;
-  if (quads > nruns) quads = nruns;
-  const uint32_t grid = (uint32_t)((quads + 63) / 64);
-  hipStream_t s = (hipStream_t)stream;
-  if (depth == 8)
-    hipLaunchKernelGGL((k_walk_hash<8>), dim3(grid), dim3(256), 0, s, a, a.files);
-  else if (depth == 32)
-    hipLaunchKernelGGL((k_walk_hash<32>), dim3(grid), dim3(256), 0, s, a, a.files);
-  else
-    hipLaunchKernelGGL((k_walk_hash<16>), dim3(grid), dim3(256), 0, s, a, a.files);
-}
-
 
 void launch_walk_chase(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;

@@ -223,7 +223,6 @@ int device_cus();  // compute units of the current device (cached per device)
 void launch_long(const ScanArgs& a, void* stream, bool enqueue = true);  // k_long_enqueue + k_long_hash
 void launch_long_enqueue(const ScanArgs& a, void* stream);
 void launch_long_hash(const ScanArgs& a, void* stream);
-void launch_lq_snap(const ScanArgs& a, uint32_t* out, void* stream);  // out[c] = ctr->lq_cnt[c]
 void launch_validate(const ScanArgs& a, void* stream);
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream);
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream);
@@ -244,17 +243,13 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
               const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz, const uint16_t* ksz, const uint8_t* status,
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
-void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: the walk-mode speculative pass
+void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: hint bodies (cask_parse_hints_device)
 void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each walk run's speculative start
-// k_walk_hash.hip: the walk mode in one pass (a quad per run chases and hashes every record);
-// depth = 64-B blocks per quad in flight (8, 16 or 32)
-void launch_walk_hash(const ScanArgs& a, int depth, void* stream);
-// k_walk_hash.hip, split path: k_walk_chase (a lane per run of a.run chunks chases the record
+// k_walk_hash.hip: k_walk_chase (a lane per run of a.run chunks chases the record
 // headers: slot rows, chunk table, cdesc), then k_run_hash (a wave per claimed run, a quad per record:
 // every record hashed from HBM; depth = 64-B blocks per quad in flight)
 void launch_walk_chase(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, int depth, void* stream);
-void launch_probe(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
 constexpr uint32_t kProbeRegions = 8;
 void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);

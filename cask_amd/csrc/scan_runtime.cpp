@@ -97,7 +97,6 @@ struct cask_ctx {
   DevBuf lq;         // long-record queue (slot indices by length class)
   DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
   DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
-  DevBuf lqsnap;     // walk groups: the long-record queue counts after each group's enqueue
   DevBuf cdesc;      // walk mode, split path: per chunk its address and its file's end (2 x u64)
   DevBuf probe;      // k_probe_regions: 3 u64 per region of each file
   DevBuf mruns;      // mixed call: walk-mode run indices | chunk-mode [first, end) stretches
@@ -117,15 +116,11 @@ struct cask_ctx {
   int geo = -1;      // k_scan_chunks geometry: -1 picks one per call (CASK_SCAN_GEOMETRY forces one)
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
-  hipStream_t side = nullptr;   // walk mode: the long-record hashing of each walked group
-  hipStream_t side2 = nullptr;  // walk mode: the short-record hashing of each walked group
-  // walk groups: group g walked (stream -> sides); sides done (-> stream); searches (both ways)
-  hipEvent_t gev[kWalkGroups + 4] = {};
   void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
   float last_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
   int last_dense = 0;  // the last call's rows came from k_finish (every speculated start held)
-  int last_walk = 0;   // the last call's speculative pass was k_walk_runs
+  int last_walk = 0;   // the last call's mode: 0 chunk, 1 walk, 2 mixed
   int last_geo = -1;   // the last call's k_scan_chunks geometry (-1: walk mode)
   // The file table and two call blocks stay on the device between calls: a call whose file table is
   // the last one's, and whose call block k_finish zeroed during the last call, needs no copy to the
@@ -149,14 +144,8 @@ struct cask_ctx {
   ~cask_ctx() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
-    if (side) (void)hipStreamSynchronize(side);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
-    for (auto& e : gev)
-      if (e) (void)hipEventDestroy(e);
-    if (side2) (void)hipStreamSynchronize(side2);
-    if (side) (void)hipStreamDestroy(side);
-    if (side2) (void)hipStreamDestroy(side2);
     if (evw) (void)hipEventDestroy(evw);
     if (kd) kd_scratch_destroy(kd);
     if (own) (void)hipStreamDestroy(own);
@@ -489,13 +478,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // CASK_SCAN_MODE=walk|chunk (test and tuning knob) forces a mode for the whole call.
   // The chunk scan's halo comes from the same probe: CASK_SCAN_MODE=wide|narrow forces the chunk
   // mode with the wide (4,080-B) or the short (1,008-B) halo.
-  // CASK_WALK_PATH (tuning knob) picks the walk path: "split" (default, above), "fused" (k_walk_hash:
-  // a quad per run chases and hashes) or "grouped" (k_walk_runs + the long-record queue +
-  // k_long_hash, in groups on two streams); a mixed call needs the split path (else: chunk mode).
-  static const int walk_path = [] {
-    const char* v = getenv("CASK_WALK_PATH");
-    return !v ? 0 : !strcmp(v, "fused") ? 1 : !strcmp(v, "grouped") ? 2 : 0;
-  }();
   bool walk = false, mixed = false;
   int halo_pick = 0;  // 1: wide, 2: short (forced); 0: from the probe
   if (hint) {
@@ -551,7 +533,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
         c->mixed_key = 0;
       }
       walk = c->probe_walk;
-      mixed = c->probe_mixed && walk_path == 0;
+      mixed = c->probe_mixed;
       halo_pick = c->probe_short ? 2 : 1;
     }
   }
@@ -643,7 +625,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     L("k_scan_chunks");
     // (the chunk-mode runs' long records go to k_long after k_finish, as in a chunk-mode call)
     if (!ok) return CASK_E_DEVICE;
-  } else if (walk && !hint && walk_path != 2) {
+  } else if (walk && !hint) {
     fused = true;
     const uint64_t nruns = (total_chunks + a.run - 1) / a.run;
     ScanArgs as = a;
@@ -653,81 +635,13 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     L("k_walk_search");
     H(hipEventRecord(c->ev[6], st));
     a.walk_pre = 1;
-    if (walk_path == 1) {
-      launch_walk_hash(a, hash_depth, st);
-      L("k_walk_hash");
-    } else {
-      if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
-      a.cdesc = c->cdesc.as<uint64_t>();
-      launch_walk_chase(a, st);
-      L("k_walk_chase");
-      H(hipEventRecord(c->ev[7], st));
-      launch_run_hash(a, hash_depth, st);
-      L("k_run_hash");
-    }
-    a.walk_pre = 0;
-    long_pre = true;
-    if (!ok) return CASK_E_DEVICE;
-  } else if (walk && !hint) {
-    static const uint32_t groups_env = getenv("CASK_WALK_GROUPS") ? (uint32_t)atoi(getenv("CASK_WALK_GROUPS")) : 0u;
-    const uint64_t nruns = (total_chunks + a.run - 1) / a.run;
-    uint64_t G = groups_env ? groups_env : kWalkGroupsDefault;
-    G = std::max<uint64_t>(1, std::min<uint64_t>({G, (uint64_t)kWalkGroups, nruns}));
-    if (!c->side) {
-      if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
-          hipStreamCreateWithFlags(&c->side2, hipStreamNonBlocking) != hipSuccess) {
-        snprintf(c->last_error, sizeof(c->last_error), "side stream create failed");
-        return CASK_E_DEVICE;  // (the destructor releases whichever was made)
-      }
-      for (auto& e : c->gev) H(hipEventCreateWithFlags(&e, hipEventDisableTiming), "event create");
-      if (!ok) return CASK_E_DEVICE;
-    }
-    if (!c->lqsnap.ensure(4ull * 32 * kWalkGroups)) return CASK_E_NOMEM;
-    uint32_t* snap = c->lqsnap.as<uint32_t>();
-    // the speculative starts: group 0's first, then (on the second side stream, while group 0 is
-    // walked) every other group's in one launch — a search's latency (a stretch of long records to
-    // cross) does not shrink with the group, so a launch per group would pay the longest each time
-    {
-      ScanArgs as = a;
-      as.run_hi = nruns / G;
-      launch_walk_search(as, st);
-      L("k_walk_search");
-      H(hipEventRecord(c->gev[kWalkGroups + 2], st), "event record");
-      H(hipStreamWaitEvent(c->side2, c->gev[kWalkGroups + 2], 0), "stream wait");
-      as.run_lo = nruns / G;
-      as.run_hi = nruns;
-      as.grp = 1;  // (its claim counter: group 1's, unused by the walk groups' searches)
-      launch_walk_search(as, c->side2);
-      L("k_walk_search (side)");
-      H(hipEventRecord(c->gev[kWalkGroups + 3], c->side2), "event record");
-    }
-    a.walk_pre = 1;
-    for (uint64_t g = 0; g < G && ok; ++g) {
-      ScanArgs ag = a;
-      ag.grp = (uint32_t)g;
-      ag.run_lo = nruns * g / G;
-      ag.run_hi = nruns * (g + 1) / G;
-      ag.t_lo = ag.run_lo * a.run;
-      ag.t_hi = std::min<uint64_t>(ag.run_hi * a.run, total_chunks);
-      if (g == 1) H(hipStreamWaitEvent(st, c->gev[kWalkGroups + 3], 0), "stream wait");  // the other searches
-      launch_walk_runs(ag, st);
-      L("k_walk_runs");
-      launch_long_enqueue(ag, st);
-      L("k_long_enqueue");
-      launch_lq_snap(ag, snap + 32 * g, st);
-      L("k_lq_snap");
-      H(hipEventRecord(c->gev[g], st), "event record");
-      H(hipStreamWaitEvent(c->side, c->gev[g], 0), "stream wait");
-      ScanArgs al = a;
-      al.lq_lo = g ? snap + 32 * (g - 1) : nullptr;
-      al.lq_hi = snap + 32 * g;
-      launch_long_hash(al, c->side);
-      L("k_long_hash (side)");
-    }
-    H(hipEventRecord(c->gev[kWalkGroups], c->side), "event record");
-    H(hipEventRecord(c->gev[kWalkGroups + 1], c->side2), "event record");
-    H(hipStreamWaitEvent(st, c->gev[kWalkGroups], 0), "stream wait");
-    H(hipStreamWaitEvent(st, c->gev[kWalkGroups + 1], 0), "stream wait");
+    if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
+    a.cdesc = c->cdesc.as<uint64_t>();
+    launch_walk_chase(a, st);
+    L("k_walk_chase");
+    H(hipEventRecord(c->ev[7], st));
+    launch_run_hash(a, hash_depth, st);
+    L("k_run_hash");
     a.walk_pre = 0;
     long_pre = true;
     if (!ok) return CASK_E_DEVICE;
@@ -768,10 +682,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0, t_search = 0;
     (void)hipEventElapsedTime(&t_all, c->ev[1], more ? c->ev[4] : c->ev[3]);
     float t_chase = 0;
-    if (fused && walk_path == 1) {  // [1] is k_walk_hash alone, [6] the run searches before it
-      (void)hipEventElapsedTime(&t_search, c->ev[1], c->ev[6]);
-      (void)hipEventElapsedTime(&t_k1, c->ev[6], c->ev[2]);
-    } else if (fused) {  // [1] is k_run_hash alone, [6] the run searches, [7] the chase
+    if (fused) {  // [1] is k_run_hash alone, [6] the run searches, [7] the chase
       (void)hipEventElapsedTime(&t_search, c->ev[1], c->ev[6]);
       (void)hipEventElapsedTime(&t_chase, c->ev[6], c->ev[7]);
       (void)hipEventElapsedTime(&t_k1, c->ev[7], c->ev[2]);
