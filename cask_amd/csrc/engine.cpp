@@ -9,6 +9,7 @@
 #include <fcntl.h>
 #include <sched.h>
 #include <sys/file.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
@@ -17,6 +18,7 @@
 #include <condition_variable>
 #include <cerrno>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -69,40 +71,112 @@ using StatsMap = std::unordered_map<uint32_t, StatsEntry>;
 // Stats::add_entry / remove_entry (stats.rs:23-48) into `st`. A fold on threads keeps per-table
 // deltas: then `base` is the map entering the fold, and a remove of a file absent from the delta
 // still counts when that file has a row there (remove_entry only skips files with no row at all).
-inline void stats_add(StatsMap& st, uint32_t file_id) { st[file_id].entries += 1; }
-inline void stats_remove(StatsMap& st, const StatsMap* base, uint32_t file_id, uint64_t size) {
-  auto it = st.find(file_id);
-  if (it == st.end()) {
-    if (!base || !base->count(file_id)) return;  // "Tried to reclaim non-existant entry": warn only
-    it = st.emplace(file_id, StatsEntry{}).first;
+// The rows a fold touches are few (the files of the replay) and each is touched by most records: a
+// 16-entry cache of row pointers by file id (unordered_map elements never move) keeps the map
+// lookups off the per-record path.
+class StatsDelta {
+ public:
+  StatsDelta(StatsMap& st, const StatsMap* base) : st_(st), base_(base) {}
+  void add(uint32_t file_id) { get(file_id, true)->entries += 1; }
+  void remove(uint32_t file_id, uint64_t size) {
+    StatsEntry* e = get(file_id, false);
+    if (!e) return;  // "Tried to reclaim non-existant entry": warn only
+    e->dead_entries += 1;
+    e->dead_bytes += size;
   }
-  it->second.dead_entries += 1;
-  it->second.dead_bytes += size;
-}
 
-// One table of HashMap<Vec<u8>, IndexEntry> (cask.rs:28-31). Open addressing; keys live in an
-// append-only arena (the reference copies every key: hint.key.to_vec(), cask.rs:68).
+ private:
+  StatsEntry* get(uint32_t fid, bool create) {
+    const unsigned c = fid & 15u;
+    if (ce_[c] && cf_[c] == fid) return ce_[c];
+    auto it = st_.find(fid);
+    if (it == st_.end()) {
+      if (!create && !(base_ && base_->count(fid))) return nullptr;
+      it = st_.emplace(fid, StatsEntry{}).first;
+    }
+    cf_[c] = fid;
+    ce_[c] = &it->second;
+    return ce_[c];
+  }
+  StatsMap& st_;
+  const StatsMap* base_;
+  uint32_t cf_[16] = {};
+  StatsEntry* ce_[16] = {};
+};
+
+// Allocator for large tables: 2-MiB-aligned and advised as transparent huge pages (a keydir fold
+// hits random slots of tables of tens of MB; with 4-KiB pages nearly every access also misses the
+// TLB). Small allocations take the ordinary heap.
+template <class T>
+struct HugeAlloc {
+  using value_type = T;
+  HugeAlloc() = default;
+  template <class U>
+  HugeAlloc(const HugeAlloc<U>&) {}
+  static constexpr size_t kHuge = 2ull << 20;
+  T* allocate(size_t n) {
+    const size_t b = n * sizeof(T);
+    if (b < kHuge) {
+      void* p = ::operator new(b, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
+      return static_cast<T*>(p);
+    }
+    const size_t r = (b + kHuge - 1) & ~(kHuge - 1);
+    void* p = std::aligned_alloc(kHuge, r);
+    if (!p) throw std::bad_alloc();
+    (void)madvise(p, r, MADV_HUGEPAGE);
+    return static_cast<T*>(p);
+  }
+  void deallocate(T* p, size_t n) {
+    if (n * sizeof(T) < kHuge) ::operator delete(p, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
+    else std::free(p);
+  }
+  template <class U>
+  bool operator==(const HugeAlloc<U>&) const { return true; }
+  template <class U>
+  bool operator!=(const HugeAlloc<U>&) const { return false; }
+};
+
+// One table of HashMap<Vec<u8>, IndexEntry> (cask.rs:28-31). Open addressing over 64-B slots (one
+// cache line each); a key of up to 16 bytes lives in its slot, a longer one in an append-only arena
+// (the reference copies every key: hint.key.to_vec(), cask.rs:68). A fold touches one line per
+// record for short keys: the slot holds hash, entry and key.
 class KeyDir {
  public:
-  struct Slot {
+  static constexpr uint32_t kInline = 16;
+  struct alignas(64) Slot {
     uint64_t hash;
-    uint64_t key_off;
+    cask_index_entry e;
     uint32_t ksz;
     uint32_t state;  // 0 empty, 1 live, 2 deleted
-    cask_index_entry e;
+    union {
+      uint8_t kin[kInline];  // ksz <= kInline
+      uint64_t key_off;      // else: the key's offset in the arena
+    };
   };
-  std::vector<Slot> slots;
+  static_assert(sizeof(Slot) == 64, "a slot is one cache line");
+  std::vector<Slot, HugeAlloc<Slot>> slots;
   std::vector<uint8_t> arena;
   uint64_t live = 0, used = 0;
 
   KeyDir() { slots.assign(256, Slot{}); }
 
-  const uint8_t* key_of(const Slot& s) const { return arena.data() + s.key_off; }
+  const uint8_t* key_of(const Slot& s) const { return s.ksz <= kInline ? s.kin : arena.data() + s.key_off; }
   void prefetch(uint64_t h) const { __builtin_prefetch(&slots[h & (slots.size() - 1)]); }
-  // the key bytes of the slot h lands on, once that slot is in cache (prefetch() a few records before)
+  // the arena bytes of a long key on the slot h lands on, once that slot is in cache (prefetch() a
+  // few records before)
   void prefetch_key(uint64_t h) const {
     const Slot& s = slots[h & (slots.size() - 1)];
-    if (s.state == 1 && s.hash == h) __builtin_prefetch(arena.data() + s.key_off);
+    if (s.state == 1 && s.hash == h && s.ksz > kInline) __builtin_prefetch(arena.data() + s.key_off);
+  }
+
+  bool key_eq(const Slot& s, const uint8_t* k, uint32_t n) const {
+    if (n == kInline) {  // (the common fixed-size key: two word compares, no call)
+      uint64_t a[2], b[2];
+      memcpy(a, s.kin, 16);
+      memcpy(b, k, 16);
+      return a[0] == b[0] && a[1] == b[1];
+    }
+    return n == 0 || memcmp(key_of(s), k, n) == 0;
   }
 
   int64_t find(const uint8_t* k, uint32_t n, uint64_t h) const {
@@ -110,7 +184,7 @@ class KeyDir {
     for (uint64_t i = h & m;; i = (i + 1) & m) {
       const Slot& s = slots[i];
       if (s.state == 0) return -(int64_t)i - 1;
-      if (s.state == 1 && s.hash == h && s.ksz == n && (n == 0 || memcmp(key_of(s), k, n) == 0)) return (int64_t)i;
+      if (s.state == 1 && s.hash == h && s.ksz == n && key_eq(s, k, n)) return (int64_t)i;
     }
   }
 
@@ -119,7 +193,7 @@ class KeyDir {
     uint64_t cap = slots.size();
     while (cap * 3 < (std::max(n, live) + 1) * 4) cap *= 2;
     if (cap == slots.size() && (used + 1) * 4 <= cap * 3) return;
-    std::vector<Slot> old;
+    std::vector<Slot, HugeAlloc<Slot>> old;
     old.swap(slots);
     slots.assign(cap, Slot{});
     used = 0;
@@ -158,7 +232,7 @@ class KeyDir {
 
   // Index::update (cask.rs:60-90). vsz_raw is the hint's value_size field.
   void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq,
-              uint64_t h, StatsMap& st, const StatsMap* base) {
+              uint64_t h, StatsDelta& sd) {
     const bool deleted = vsz_raw == CASK_ENTRY_TOMBSTONE;
     cask_index_entry ie{};
     ie.file_id = file_id;
@@ -170,22 +244,22 @@ class KeyDir {
     if (f >= 0) {  // Occupied
       Slot& s = slots[f];
       if (s.e.sequence <= seq) {
-        stats_remove(st, base, s.e.file_id, s.e.entry_size);
+        sd.remove(s.e.file_id, s.e.entry_size);
         if (deleted) {
           s.state = 2;
           --live;
         } else {
-          stats_add(st, file_id);
+          sd.add(file_id);
           s.e = ie;
         }
       } else {
-        stats_add(st, file_id);
-        stats_remove(st, base, file_id, ie.entry_size);
+        sd.add(file_id);
+        sd.remove(file_id, ie.entry_size);
       }
       return;
     }
     if (deleted) return;  // Vacant + tombstone: nothing
-    stats_add(st, file_id);
+    sd.add(file_id);
     insert_at((uint64_t)(-f - 1), key, ksz, h, ie);
   }
 
@@ -193,11 +267,15 @@ class KeyDir {
   void insert_at(uint64_t i, const uint8_t* key, uint32_t ksz, uint64_t h, const cask_index_entry& e) {
     Slot& s = slots[i];
     s.hash = h;
-    s.key_off = arena.size();
     s.ksz = ksz;
     s.state = 1;
     s.e = e;
-    arena.insert(arena.end(), key, key + ksz);
+    if (ksz <= kInline) {
+      if (ksz) memcpy(s.kin, key, ksz);
+    } else {
+      s.key_off = arena.size();
+      arena.insert(arena.end(), key, key + ksz);
+    }
     ++live;
     ++used;
   }
@@ -227,7 +305,8 @@ class Index {
   }
   void update(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
     const uint64_t h = hash_key(key, ksz);
-    sub[sub_of(h)].update(key, ksz, file_id, pos, vsz_raw, seq, h, stats, nullptr);
+    StatsDelta sd(stats, nullptr);
+    sub[sub_of(h)].update(key, ksz, file_id, pos, vsz_raw, seq, h, sd);
   }
   void update_kd(const uint8_t* key, uint32_t ksz, uint32_t file_id, uint64_t pos, uint32_t vsz_raw, uint64_t seq) {
     const uint64_t h = hash_key(key, ksz);
@@ -576,69 +655,145 @@ EngineDev* engine_dev(int device) {
   return devs[device];
 }
 
-// One record of the replay fold (a hint, or an Ok row of a scanned file), in replay order.
-struct FoldRec {
-  const uint8_t* key;
-  uint64_t pos, seq, hash;
-  uint32_t file_id, vsz_raw;
-  uint32_t ksz;
+constexpr uint64_t kFoldPiece = 1ull << 19;  // records per fold source (pass 1's unit of work)
+
+// A stretch of a hint body (Hint::write_bytes records, data.rs:242-256: seq u64, ksz u16, vsz u32,
+// pos u64, key) holding `cnt` whole records, all of one file: what the replay folds, in order.
+struct FoldSrc {
+  const uint8_t* b;
+  uint64_t n, cnt;
+  uint32_t file_id;
 };
 
-// Index::update over records in replay order (the open replay, cask.rs:346-382; compact_files'
-// re-index, cask.rs:528-536), on threads by key-hash table. Index::update's outcome for a key depends
-// only on that key's records in order, and each table sees its keys' records in replay order. Stats
+// One record on its way to its keydir table: everything Index::update reads, key bytes included
+// when short, so the table's fold streams its list and touches only its own slots.
+struct FoldItem {
+  uint64_t hash, seq, pos;
+  uint32_t file_id, vsz_raw, ksz, pad;
+  union {
+    uint8_t kin[KeyDir::kInline];
+    const uint8_t* kp;  // ksz > kInline: the key in its hint body
+  };
+  const uint8_t* key() const { return ksz <= KeyDir::kInline ? kin : kp; }
+};
+
+// Index::update over the hint records of `src` in order (the open replay, cask.rs:346-382;
+// compact_files' re-index, cask.rs:528-536), on threads by key-hash table. Index::update's outcome
+// for a key depends only on that key's records in order, and each table sees its keys' records in
+// replay order. Pass 1 (threads by source) hashes every key and appends the record to its
+// (source, table) list; pass 2 (threads by table) folds each table's lists in source order. Stats
 // rows are per-file counters (order-free sums): each table keeps deltas, summed at the end; a remove
 // counts when its file has a row in the delta or in the map entering the fold. The two differ from
 // one serial fold only if a key's entry pointed at a file with no stats row, which cannot happen:
 // every entry's file got its row when the entry was written, and compaction drops a file's row only
 // after re-indexing all of its live entries elsewhere. Small replays fold on the calling thread.
-void parallel_fold(FoldRec* recs, uint64_t n, Index& out) {
+// Pass 1's lists, kept across the batches of one open() so that later batches reuse their pages.
+struct FoldScratch {
+  std::vector<std::vector<FoldItem>> lists;
+  std::vector<uint8_t> hll;
+};
+
+void parallel_fold(const std::vector<FoldSrc>& src, Index& out, FoldScratch* keep = nullptr) {
+  uint64_t n = 0;
+  for (const FoldSrc& f : src) n += f.cnt;
   const char* mv = getenv("CASK_PAR_FOLD_MIN");  // tuning/test knob: smallest replay folded in parallel
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
   const unsigned nt = std::min(host_threads(), Index::kSub);
   if (n < min_par || nt == 1) {
-    for (uint64_t i = 0; i < n; ++i) {
-      const FoldRec& r = recs[i];
-      out.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq);
-    }
+    StatsDelta sd(out.stats, nullptr);
+    for (const FoldSrc& f : src)
+      for (uint64_t p = 0, j = 0; j < f.cnt; ++j) {
+        const uint8_t* h = f.b + p;
+        const uint16_t k = rd16(h + 8);
+        const uint64_t hs = hash_key(h + 22, k);
+        out.sub[Index::sub_of(hs)].update(h + 22, k, f.file_id, rd64(h + 14), rd32(h + 10), rd64(h), hs, sd);
+        p += 22ull + k;
+      }
     return;
   }
   constexpr unsigned S = Index::kSub;
-  // 1. hashes, and per (range, table) lists of record indices, ranges in replay order
-  std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(S));
-  parallel_for(nt, [&](unsigned t) {
-    const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    for (auto& l : lists[t]) l.reserve((hi - lo) / S + 16);
-    for (uint64_t i = lo; i < hi; ++i) {
-      FoldRec& r = recs[i];
-      r.hash = hash_key(r.key, r.ksz);
-      lists[t][Index::sub_of(r.hash)].push_back((uint32_t)(i - lo));
+  const size_t ns = src.size();
+  // 1. per (source, table) lists, sources claimed by threads
+  FoldScratch local;
+  FoldScratch& fs = keep ? *keep : local;
+  if (fs.lists.size() < ns * S) fs.lists.resize(ns * S);
+  std::vector<std::vector<FoldItem>>& lists = fs.lists;
+  // and per (source, table) a 256-register HyperLogLog sketch of the keys (hash bits below the
+  // table's), so that each table is sized once for the keys it will hold: a table sized from the
+  // record count instead (configs[3]: 5 records per key) costs pass 2 a third more in page faults
+  // and cache misses, one sized too small a rehash per doubling.
+  constexpr unsigned kReg = 256;
+  std::vector<uint8_t>& hll = fs.hll;
+  hll.assign(ns * S * kReg, 0);
+  std::atomic<size_t> next{0};
+  parallel_for(nt, [&](unsigned) {
+    for (size_t k; (k = next.fetch_add(1)) < ns;) {
+      const FoldSrc& f = src[k];
+      std::vector<FoldItem>* L = &lists[k * S];
+      for (unsigned q = 0; q < S; ++q) {
+        L[q].clear();
+        L[q].reserve(f.cnt / S + f.cnt / (4 * S) + 16);
+      }
+      for (uint64_t p = 0, j = 0; j < f.cnt; ++j) {
+        const uint8_t* h = f.b + p;
+        FoldItem it;
+        it.ksz = rd16(h + 8);
+        it.hash = hash_key(h + 22, it.ksz);
+        it.seq = rd64(h);
+        it.pos = rd64(h + 14);
+        it.file_id = f.file_id;
+        it.vsz_raw = rd32(h + 10);
+        it.pad = 0;
+        if (it.ksz <= KeyDir::kInline) {  // (16 bytes at once unless that would pass the body's end)
+          if (p + 22 + KeyDir::kInline <= f.n) memcpy(it.kin, h + 22, KeyDir::kInline);
+          else memcpy(it.kin, h + 22, it.ksz);
+        } else {
+          it.kp = h + 22;
+        }
+        const unsigned q = Index::sub_of(it.hash);
+        L[q].push_back(it);
+        uint8_t& reg = hll[(k * S + q) * kReg + ((it.hash >> 50) & (kReg - 1))];
+        const uint8_t rank = (uint8_t)(__builtin_clzll((it.hash << 14) | (1ull << 13)) + 1);
+        reg = rank > reg ? rank : reg;
+        p += 22ull + it.ksz;
+      }
     }
   });
-  // 2. each table folds its keys in replay order, stats into its own delta map
+  // 2. each table folds its lists in source order, stats into its own delta map
   std::vector<StatsMap> delta(S);
   parallel_for(nt, [&](unsigned t) {
     for (unsigned q = t; q < S; q += nt) {
       KeyDir& kd = out.sub[q];
       uint64_t cnt = 0;
-      for (unsigned g = 0; g < nt; ++g) cnt += lists[g][q].size();
-      kd.reserve(kd.live + cnt / 2);
-      for (unsigned g = 0; g < nt; ++g) {
-        const uint64_t lo = n * g / nt;
-        const std::vector<uint32_t>& L = lists[g][q];
-        const size_t m = L.size();
-        for (size_t j = 0; j < m; ++j) {  // the record 16 ahead, the slot and key of the one 8 ahead,
-                                          // the keydir's copy of the key of the one 4 ahead
-          if (j + 16 < m) __builtin_prefetch(&recs[lo + L[j + 16]]);
-          if (j + 8 < m) {
-            const FoldRec& a = recs[lo + L[j + 8]];
-            kd.prefetch(a.hash);
-            __builtin_prefetch(a.key);
-          }
-          if (j + 4 < m) kd.prefetch_key(recs[lo + L[j + 4]].hash);
-          const FoldRec& r = recs[lo + L[j]];
-          kd.update(r.key, r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, delta[q], &out.stats);
+      for (size_t k = 0; k < ns; ++k) cnt += lists[k * S + q].size();
+      {  // the sketches of the table's lists merged: an estimate of its distinct keys (+-7 %)
+        uint8_t m[kReg] = {};
+        for (size_t k = 0; k < ns; ++k) {
+          const uint8_t* r = &hll[(k * S + q) * kReg];
+          for (unsigned j = 0; j < kReg; ++j) m[j] = r[j] > m[j] ? r[j] : m[j];
         }
+        double z = 0;
+        unsigned zeros = 0;
+        for (unsigned j = 0; j < kReg; ++j) {
+          z += std::ldexp(1.0, -(int)m[j]);
+          zeros += m[j] == 0;
+        }
+        double est = 0.7213 / (1 + 1.079 / kReg) * kReg * kReg / z;
+        if (est < 2.5 * kReg && zeros) est = kReg * std::log((double)kReg / zeros);
+        const uint64_t want = std::min<uint64_t>(cnt, (uint64_t)(est * 1.15) + 64);
+        kd.reserve(kd.live + want);
+      }
+      StatsDelta sd(delta[q], &out.stats);
+      for (size_t k = 0; k < ns; ++k) {
+        const std::vector<FoldItem>& L = lists[k * S + q];
+        const size_t m = L.size();
+        for (size_t j = 0; j < m; ++j) {  // the slot of the record 8 ahead, a long key 4 ahead
+          if (j + 16 < m) kd.prefetch(L[j + 16].hash);
+          if (j + 4 < m) kd.prefetch_key(L[j + 4].hash);
+          const FoldItem& r = L[j];
+          kd.update(r.key(), r.ksz, r.file_id, r.pos, r.vsz_raw, r.seq, r.hash, sd);
+        }
+        if (!keep) std::vector<FoldItem>().swap(lists[k * S + q]);
       }
     }
   });
@@ -941,11 +1096,14 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   // log.rs:437-447; data.rs:258-276)
   struct Body {
     const uint8_t* b = nullptr;
-    uint64_t n = 0, cnt = 0, max_seq = 0, bad = UINT64_MAX, base = 0;
+    uint64_t n = 0, cnt = 0, max_seq = 0, bad = UINT64_MAX;
+    std::vector<uint64_t> cut;  // the offset of every kPiece-th record: the fold's sources
   };
+  constexpr uint64_t kPiece = kFoldPiece;
   std::vector<Body> bodies(nf);
   const unsigned ntb = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)std::max<size_t>(nf, 1)));
   size_t fi = 0;  // the next file to replay
+  FoldScratch fscratch;
   for (size_t b = 0; b < nbat && fail == CASK_OK; ++b) {
     {
       std::unique_lock<std::mutex> lk(bm);
@@ -975,11 +1133,13 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     parallel_for(nt, [&](unsigned t) {
       for (size_t i = fi + t; i < fe; i += nt) {
         Body& B = bodies[i];
+        B.cut.clear();
         for (uint64_t p = 0; p < B.n;) {
           if (B.n - p < 22 || B.n - p - 22 < rd16(B.b + p + 8)) {
             B.bad = p;
             break;
           }
+          if (!(B.cnt & (kPiece - 1))) B.cut.push_back(p);
           B.max_seq = std::max(B.max_seq, rd64(B.b + p));
           ++B.cnt;
           p += 22ull + rd16(B.b + p + 8);
@@ -987,7 +1147,6 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
       }
     });
     size_t nrep = fi;  // files of the batch replayed: [fi, nrep)
-    uint64_t total = 0;
     std::vector<uint32_t> to_write;
     for (size_t i = fi; i < fe && fail == CASK_OK; ++i) {
       const uint32_t fid = db->files[i];
@@ -1018,29 +1177,19 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
         break;
       }
       if (bodies[i].cnt && bodies[i].max_seq > db->sequence) db->sequence = bodies[i].max_seq;
-      bodies[i].base = total;
-      total += bodies[i].cnt;
       nrep = i + 1;
     }
-    std::unique_ptr<FoldRec[]> recs;  // the batch's fold, in order (parallel_fold); not zero-filled
-    if (fail == CASK_OK) {
-      recs.reset(new (std::nothrow) FoldRec[std::max<uint64_t>(total, 1)]);
-      if (!recs) fail = CASK_E_NOMEM;
-    }
-    if (fail == CASK_OK) {  // the fold's records, file by file on threads
-      parallel_for(nt, [&](unsigned t) {
-        for (size_t i = fi + t; i < nrep; i += nt) {
-          const Body& B = bodies[i];
-          FoldRec* out = recs.get() + B.base;
-          for (uint64_t p = 0, j = 0; j < B.cnt; ++j) {
-            const uint8_t* h = B.b + p;
-            const uint16_t k = rd16(h + 8);
-            out[j] = FoldRec{h + 22, rd64(h + 14), rd64(h), 0, db->files[i], rd32(h + 10), k};
-            p += 22ull + k;
-          }
+    // the batch's fold sources, in order: pieces of kPiece records of each replayed file's body
+    std::vector<FoldSrc> srcs;
+    if (fail == CASK_OK)
+      for (size_t i = fi; i < nrep; ++i) {
+        const Body& B = bodies[i];
+        for (size_t c = 0; c < B.cut.size(); ++c) {
+          const uint64_t e = c + 1 < B.cut.size() ? B.cut[c + 1] : B.n;
+          const uint64_t k = c + 1 < B.cut.size() ? kPiece : B.cnt - c * kPiece;
+          srcs.push_back(FoldSrc{B.b + B.cut[c], e - B.cut[c], k, db->files[i]});
         }
-      });
-    }
+      }
     t_fold += ms_since(tf);
     auto th = std::chrono::steady_clock::now();
     {
@@ -1063,9 +1212,8 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     // Index::update + Stats over the batch's records (their keys stay in hints[] / the batch's
     // bodies until here)
     auto tf2 = std::chrono::steady_clock::now();
-    parallel_fold(recs.get(), total, db->index);
+    parallel_fold(srcs, db->index, &fscratch);
     t_fold += ms_since(tf2);
-    recs.reset();
     RawBytes().p.swap(bat[b].hb.p);  // (the batch's bodies are no longer needed)
     for (size_t i = fi; i < fe; ++i)
       if (use_hint[i]) std::vector<uint8_t>().swap(hints[i]);
@@ -1527,19 +1675,23 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
   // files' stats, swap the file sets
   auto t4 = std::chrono::steady_clock::now();
   {
-    std::vector<FoldRec> recs;
-    recs.reserve(ins.size());
+    std::vector<FoldSrc> srcs;
     for (uint32_t fid : new_files) {
       const OutFile& o = *std::find_if(outs.begin(), outs.end(), [&](const OutFile& x) { return x.fid == fid; });
       const std::vector<uint8_t>& hb = o.hints;
+      uint64_t p0 = 0, k = 0;
       for (uint64_t p = 0; p < hb.size();) {
-        const uint8_t* h = hb.data() + p;
-        const uint16_t k = rd16(h + 8);
-        recs.push_back(FoldRec{h + 22, rd64(h + 14), rd64(h), 0, fid, rd32(h + 10), k});
-        p += 22ull + k;
+        if (k == kFoldPiece) {
+          srcs.push_back(FoldSrc{hb.data() + p0, p - p0, k, fid});
+          p0 = p;
+          k = 0;
+        }
+        p += 22ull + rd16(hb.data() + p + 8);
+        ++k;
       }
+      if (k) srcs.push_back(FoldSrc{hb.data() + p0, hb.size() - p0, k, fid});
     }
-    parallel_fold(recs.data(), recs.size(), db->index);
+    parallel_fold(srcs, db->index);
   }
   for (uint32_t fid : compacted) db->index.stats.erase(fid);  // Stats::remove_files (stats.rs:50-54)
   {  // Log::swap_files (log.rs:198-217): the compacted files removed (on threads; the first failure
