@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <sched.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <cstdint>
@@ -50,6 +51,26 @@ void parallel_for(unsigned nt, F fn) {
   for (auto& x : th) x.join();
 }
 
+// Page-locked host memory the device can DMA to and from: an anonymous mapping populated when it is
+// made (huge pages where the kernel has them) and then registered. hipHostMalloc's memory is
+// mapped into the process lazily instead: the first host write to each 4-KiB page faults, which
+// cost the first open() of a process ~1 s per GiB of staging (tools/read_bench.cpp).
+inline void* pinned_alloc(size_t n) {
+  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  (void)madvise(p, n, MADV_HUGEPAGE);
+  memset(p, 0, n);  // (populated now, on huge pages if any: MAP_POPULATE would fault in 4-KiB pages first)
+  if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
+    munmap(p, n);
+    return nullptr;
+  }
+  return p;
+}
+inline void pinned_free(void* p, size_t n) {
+  (void)hipHostUnregister(p);
+  munmap(p, n);
+}
+
 // kThreads x 2 pinned buffers of kBytes, a stream per thread, an event per buffer. Thread t takes
 // every nt-th piece and alternates between its two buffers, so the DMA of one piece overlaps the
 // host copy of the next (host -> device) or of the previous one (device -> host).
@@ -82,10 +103,7 @@ struct PinnedRing {
     for (int t = 0; t < kThreads; ++t) {
       if (!rs[t] && hipStreamCreateWithFlags(&rs[t], hipStreamNonBlocking) != hipSuccess) return false;
       for (int k = 0; k < kSlots; ++k) {
-        if (!pin[t][k] && hipHostMalloc(&pin[t][k], kBytes, hipHostMallocDefault) != hipSuccess) {
-          pin[t][k] = nullptr;
-          return false;
-        }
+        if (!pin[t][k] && !(pin[t][k] = pinned_alloc(kBytes))) return false;
         if (!ev[t][k] && hipEventCreateWithFlags(&ev[t][k], hipEventDisableTiming) != hipSuccess) return false;
       }
     }
@@ -96,7 +114,7 @@ struct PinnedRing {
     for (int t = 0; t < kThreads; ++t) {
       if (rs[t]) (void)hipStreamSynchronize(rs[t]);
       for (int k = 0; k < kSlots; ++k) {
-        if (pin[t][k]) (void)hipHostFree(pin[t][k]);
+        if (pin[t][k]) pinned_free(pin[t][k], kBytes);
         if (ev[t][k]) (void)hipEventDestroy(ev[t][k]);
         pin[t][k] = nullptr;
         ev[t][k] = nullptr;

@@ -312,9 +312,12 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)hst;
   HST(h_all)
-  // One iteration: round in hand in (Xm, xm), the next round into (Xi, xi). In a record's last
-  // round the partial last block is loaded into X[D - 1] (that round has at most D - 1 full
-  // blocks). False: done.
+#ifdef CASK_STAMPS
+  const uint64_t wid = blockIdx.x * 4ull + wv;
+  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+  // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi): D full blocks
+  // in X, a record's partial last block in T, its stored checksum in x. False: done.
   auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
     HCNT(6)
     HST(h0)
@@ -411,7 +414,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     uint64_t ya[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;
-    const bool tail2 = round2 && fin2 && rb2 != 0;  // (then nl2 <= D - 1: the partial block in X[D - 1])
+    const bool tail2 = round2 && fin2 && rb2 != 0;  // the record's partial last block, into T
     const uint64_t end16 = (end2 + 15) & ~15ull;
     const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
     const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);
@@ -428,7 +431,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     xi = gld4g((const g_u8*)(uintptr_t)sa);
     // the round in hand's last block and checksum are used from here on: nothing that reads them
     // (nor the wait for them, one counted past this round's loads) is scheduled above the loads
-    asm volatile("" : "+v"(Tm.x), "+v"(Tm.y), "+v"(Tm.z), "+v"(Tm.w), "+v"(xm)::"memory");
+    asm volatile("" : "+v"(xm)::"memory");
     HADD(2, h1)
     HST(h2)
     // ---- mix the round in hand
@@ -509,16 +512,23 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       cw3 = pw3;
     }
     const bool stream_left = rnA != cur || (fullB && rnB != 0) || runs_left;
-    return stream_left || __any(cv || ns != 0);
+    // (uniform by construction, and made visibly so: a loop exit the compiler must treat as divergent
+    // becomes an exec-mask loop in which the exit after the first step also reaches the loop header,
+    // so the header's waits count the first step's loads as possibly in flight and wait for them)
+    return __builtin_amdgcn_readfirstlane((int)(stream_left || __any(cv || ns != 0))) != 0;
   };
+  // (one exit, after the second step: a wave that finishes in the first step runs the second as a
+  // no-op — nothing left to claim or load but safe lines — so that no path from the middle of the
+  // body reaches the loop header with the first step's loads in flight)
   for (;;) {
-    if (!step(XA, TA, sA, XB, TB, sB)) break;
+    (void)step(XA, TA, sA, XB, TB, sB);
     if (!step(XB, TB, sB, XA, TA, sA)) break;
   }
 #ifdef CASK_STAMPS
   HADD(0, h_all)
   if (a.stamps && lane == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[8 + i], (unsigned long long)hst[i]);
+  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[17 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
 #endif
 }
 

@@ -112,7 +112,8 @@ struct ScanArgs {
   uint16_t* ksz;
   uint8_t* status;
   uint64_t row_cap;
-  unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums
+  unsigned long long* stamps;  // diagnostic builds only (-DCASK_STAMPS): per-phase cycle sums, then
+                               // k_run_hash's per-wave start/end real times ([16 + 2 w], [17 + 2 w])
   uint32_t run;                // k_scan_chunks: consecutive chunks a workgroup walks with a carry
   uint32_t run_small;          // k_scan_chunks: chunks per run from run_tail on
   uint64_t run_tail;           // k_scan_chunks: first chunk of the short runs (a multiple of run;
@@ -252,6 +253,7 @@ void launch_walk_chase(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, int depth, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
 constexpr uint32_t kProbeRegions = 8;
+constexpr uint32_t kStampWaves = 8192;  // diagnostic builds: waves with start/end stamps
 void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

@@ -438,7 +438,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
   a.epoch = ++c->epoch;
 #ifdef CASK_STAMPS
-  if (c->stamps.ensure(16 * 8)) a.stamps = c->stamps.as<unsigned long long>();
+  if (c->stamps.ensure(8ull * (16 + 2 * kStampWaves))) a.stamps = c->stamps.as<unsigned long long>();
 #endif
 
   bool ok = true;
@@ -738,7 +738,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
     H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
     H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
-    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 16 * 8, st));
+    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 8ull * (16 + 2 * kStampWaves), st));
   };
   uint64_t nlong_total = 0;  // records hashed by k_long over all passes (each pass queues only chunks it scanned)
   // validation, long records and summary after a scan of the chunks (events 2..4 when timed)
@@ -1249,13 +1249,19 @@ extern "C" int cask_debug_stamps(cask_ctx* c, uint64_t* out16) {
   if (hipMemcpy(out16, c->stamps.p, 16 * 8, hipMemcpyDeviceToHost) != hipSuccess) return CASK_E_DEVICE;
   return CASK_OK;
 }
+// Diagnostic build only: k_run_hash's per-wave start/end real times (2 per wave, kStampWaves waves).
+extern "C" int cask_debug_wave_stamps(cask_ctx* c, uint64_t* out, uint64_t n) {
+  if (!c || !c->stamps.p || n > 2ull * kStampWaves) return CASK_E_INVALID_ARG;
+  if (hipMemcpy(out, (uint8_t*)c->stamps.p + 16 * 8, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return CASK_E_DEVICE;
+  return CASK_OK;
+}
 // Diagnostic build only: per-chunk spec / exit / tin / count of the last (unrepaired) pass.
 extern "C" int cask_debug_chunks(cask_ctx* c, uint64_t* spec, uint64_t* exitv, uint64_t* tin, uint32_t* count, uint64_t n) {
   if (!c || !c->dbg_spec || n > c->dbg_n) return CASK_E_INVALID_ARG;
-  hipMemcpy(spec, c->dbg_spec, n * 8, hipMemcpyDeviceToHost);
-  hipMemcpy(exitv, c->dbg_exit, n * 8, hipMemcpyDeviceToHost);
-  hipMemcpy(tin, c->dbg_tin, n * 8, hipMemcpyDeviceToHost);
-  hipMemcpy(count, c->dbg_count, n * 4, hipMemcpyDeviceToHost);
-  return CASK_OK;
+  const bool ok = hipMemcpy(spec, c->dbg_spec, n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(exitv, c->dbg_exit, n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(tin, c->dbg_tin, n * 8, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(count, c->dbg_count, n * 4, hipMemcpyDeviceToHost) == hipSuccess;
+  return ok ? CASK_OK : CASK_E_DEVICE;
 }
 #endif

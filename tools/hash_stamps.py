@@ -39,6 +39,24 @@ def main():
     print(f"shares: plan+issue {h[1] / tot:.3f} claim {h[2] / tot:.3f} mix {h[3] / tot:.3f} (finalize {h[4] / tot:.3f}) "
           f"wait {h[5] / tot:.3f}; per iteration {h[0] / max(h[6], 1):.0f} cycles; iterations {h[6]}")
     print("timings", ctx.last_timings(), "rows", res.count)
+    # per-wave start/end (100 MHz real-time clock) of the last call's k_run_hash
+    nw = 8192
+    L.cask_debug_wave_stamps.restype = C.c_int
+    L.cask_debug_wave_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64]
+    ws = (C.c_uint64 * (2 * nw))()
+    L.cask_debug_wave_stamps(ctx._h, ws, 2 * nw)
+    import numpy as np
+    a = np.frombuffer(ws, np.uint64).reshape(nw, 2).astype(np.int64)
+    a = a[a[:, 1] > 0]
+    if a.size:
+        t0 = a[:, 0].min()
+        st, en = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0  # us
+        span = en.max()
+        q = np.percentile(en, [0, 10, 50, 90, 99, 100])
+        print(f"waves {len(a)}: span {span:.1f} us; start spread {st.max():.1f} us; end percentiles "
+              f"0/10/50/90/99/100 = {' / '.join(f'{x:.1f}' for x in q)} us")
+        print(f"idle after finishing: {np.mean(span - en) / span:.3f} of wave-time; "
+              f"tail (max - median end) {span - q[2]:.1f} us")
 
 
 if __name__ == "__main__":
