@@ -139,71 +139,113 @@ __device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* fil
 // file's end (cdesc). A record cut short by the end of its file is its UnexpectedEof row (data.rs:163,
 // 172, 181) and ends the chain.
 // ---------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* __restrict__ files) {
-  const uint64_t R = a.run;
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
+// Chunks [tb, te) of one run (te <= the run's end): the chain enters the range's first segment at
+// p_in (ignored when the segment starts a file: the chain starts there at 0); returns the position
+// it leaves the range at (kTerm once an EOF row ended it, kNone if it never had a start). Chasing a
+// run as [t0, tm) and then [tm, t1) from the first range's exit writes exactly what one range
+// [t0, t1) writes: the chain is one walk either way.
+__device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t tb, uint64_t te,
+                                uint64_t p_in) {
   const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   g_u32* slots = (g_u32*)a.slots;
   g_u64* cd = (g_u64*)a.cdesc;
-  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nruns; i += (uint64_t)gridDim.x * blockDim.x) {
-    const uint64_t k = a.wruns ? a.wruns[i] : i;
-    Walk W;
-    W.cn = 0;
-    W.ccerr = 0xFFFFFFFFu;
-    W.cspec = 0;
-    W.run_end = k * R + R < a.total_chunks ? k * R + R : a.total_chunks;
-    for (uint64_t t = k * R; t < W.run_end;) {
-      seg_setup(a, files, W, t);
-      t = W.S.t0 + W.S.nch;
-      const uint64_t fend = (uint64_t)(uintptr_t)(W.S.data + W.S.len);
-      for (uint32_t c = 0; c < W.S.nch; ++c) {
-        cd[2 * (W.S.t0 + c)] = (uint64_t)(uintptr_t)(W.S.data + W.S.b0 + ((uint64_t)c << csh));
-        cd[2 * (W.S.t0 + c) + 1] = fend;
-      }
-      // the run's first segment starts at its searched start; a later one starts a file (b0 == 0)
-      uint64_t p = W.S.b0 == 0 ? 0ull : a.walk_pre ? a.tin[W.S.t0] : kNone;
-      bool term = false;
-      // The next record's header is loaded before this record's stores go out: a wait for a load
-      // also waits for every store issued before it (one vmcnt counts both), so loading after the
-      // stores would cost each hop a store round trip as well. Headers past the file's end are not
-      // read (an address inside the file is loaded instead).
-      const bool has = p != kNone && p < W.S.b1;
-      const uint64_t p0 = has && p + 18 <= W.S.len ? p : 0ull;
-      u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
-      uint32_t vsz = gld4g((const g_u8*)(W.S.data + p0 + 14));
-      // (waited for here, so that the loop's own wait counts the hop's load behind its stores: with
-      // this path arriving at the loop with loads outstanding, it would wait for everything)
-      asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w), "v"(vsz));
-      while (p != kNone && p < W.S.b1) {
-        uint32_t j = 0;
-        if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
-          const uint32_t r = open_record(a, W, p, csh, true, &j);
-          const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-          *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
-          if (r < W.ccerr) W.ccerr = r;
-          term = true;
-          break;
-        }
-        const uint32_t ksz = h.w & 0xFFFFu;
-        const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-        const u32x4 row = u32x4{h.y, h.z, vsz, ksz};
-        const uint64_t pn = p + rl;
-        const uint64_t pl = pn + 18 <= W.S.len ? pn : 0ull;  // (pn < p: rl wrapped, impossible)
-        h = gld16g((const g_u8*)(W.S.data + pl));
-        vsz = gld4g((const g_u8*)(W.S.data + pl + 14));
+  Walk W;
+  W.cn = 0;
+  W.ccerr = 0xFFFFFFFFu;
+  W.cspec = 0;
+  W.run_end = te;
+  uint64_t p = p_in;
+  bool term = false;
+  for (uint64_t t = tb; t < te;) {
+    seg_setup(a, files, W, t);
+    t = W.S.t0 + W.S.nch;
+    const uint64_t fend = (uint64_t)(uintptr_t)(W.S.data + W.S.len);
+    for (uint32_t c = 0; c < W.S.nch; ++c) {
+      cd[2 * (W.S.t0 + c)] = (uint64_t)(uintptr_t)(W.S.data + W.S.b0 + ((uint64_t)c << csh));
+      cd[2 * (W.S.t0 + c) + 1] = fend;
+    }
+    // the range's first segment starts at p_in; a later one starts a file (b0 == 0)
+    if (W.S.b0 == 0) p = 0ull;
+    else if (W.S.t0 != tb) p = kNone;  // (unreachable: a later segment starts a file)
+    term = false;
+    // The next record's header is loaded before this record's stores go out: a wait for a load
+    // also waits for every store issued before it (one vmcnt counts both), so loading after the
+    // stores would cost each hop a store round trip as well. Headers past the file's end are not
+    // read (an address inside the file is loaded instead).
+    const bool has = p != kNone && p < W.S.b1;
+    const uint64_t p0 = has && p + 18 <= W.S.len ? p : 0ull;
+    u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
+    uint32_t vsz = gld4g((const g_u8*)(W.S.data + p0 + 14));
+    // (waited for here, so that the loop's own wait counts the hop's load behind its stores: with
+    // this path arriving at the loop with loads outstanding, it would wait for everything)
+    asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w), "v"(vsz));
+    while (p != kNone && p < W.S.b1) {
+      uint32_t j = 0;
+      if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
         const uint32_t r = open_record(a, W, p, csh, true, &j);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
-        if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
-          if (r < W.ccerr) W.ccerr = r;
-          term = true;
-          break;
-        }
-        p = pn;
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
+        if (r < W.ccerr) W.ccerr = r;
+        term = true;
+        break;
       }
-      close_segment(a, W, term ? kTerm : p, true);
+      const uint32_t ksz = h.w & 0xFFFFu;
+      const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+      const u32x4 row = u32x4{h.y, h.z, vsz, ksz};
+      const uint64_t pn = p + rl;
+      const uint64_t pl = pn + 18 <= W.S.len ? pn : 0ull;  // (pn < p: rl wrapped, impossible)
+      h = gld16g((const g_u8*)(W.S.data + pl));
+      vsz = gld4g((const g_u8*)(W.S.data + pl + 14));
+      const uint32_t r = open_record(a, W, p, csh, true, &j);
+      const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
+      *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
+      if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
+        if (r < W.ccerr) W.ccerr = r;
+        term = true;
+        break;
+      }
+      p = pn;
     }
+    close_segment(a, W, term ? kTerm : p, true);
+    if (term) p = kTerm;
   }
+  return p;
+}
+
+// The chunk range of walk run i (an index into a.wruns, or the run itself): [t0, t1).
+__device__ __forceinline__ void walk_run_chunks(const ScanArgs& a, uint64_t i, uint64_t* t0, uint64_t* t1) {
+  const uint64_t R = a.run;
+  const uint64_t k = a.wruns ? a.wruns[i] : i;
+  *t0 = k * R;
+  *t1 = k * R + R < a.total_chunks ? k * R + R : a.total_chunks;
+}
+
+__global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* __restrict__ files) {
+  const uint64_t R = a.run;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
+  for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nruns; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t t0, t1;
+    walk_run_chunks(a, i, &t0, &t1);
+    (void)chase_range(a, files, t0, t1, a.walk_pre ? a.tin[t0] : kNone);
+  }
+}
+
+// A single-wave claim of the next item of a work counter (every lane takes part in the atomic, lane 0
+// adding 1; no lane-0 branch, which the compiler could thread into the claiming loop's back edge).
+__device__ __forceinline__ uint32_t wave_claim_next(unsigned int* ctr) {
+  const uint32_t old = atomicAdd(ctr, (threadIdx.x & 63) == 0 ? 1u : 0u);
+  return __builtin_amdgcn_readfirstlane(old);
+}
+
+// Fused chase (k_run_hash with a.chase_flag): the chasing wave has written the slot rows, chunk table
+// and cdesc of its 64 runs up to `stage` (1: the first a.hash_h0 chunks of each, 2: all of them).
+// Every store of the wave drained, the XCD's L2 written back (agent release), then the item's flag,
+// tagged with the call's epoch (no clearing between calls). Every lane stores the same word.
+__device__ __forceinline__ void chase_publish(const ScanArgs& a, uint32_t it, uint32_t stage) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&a.chase_flag[it], (a.epoch << 8) | stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -233,6 +275,14 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   const bool qlead = q == 0;
   const uint64_t R = a.run;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
+  // Hash units: with 0 < a.hash_h0 < R, unit u < nruns is the first hash_h0 chunks of run u and unit
+  // nruns + k the rest of run k (the first parts of every run are handed out first: with the chase
+  // fused in, they are the parts chased first); else unit k is run k.
+  const uint64_t H0 = a.hash_h0;
+  const bool split = H0 != 0 && H0 < R;
+  const uint64_t nunits = split ? 2 * nruns : nruns;
+  const uint64_t nitems = (nruns + 63) / 64;  // fused chase: items of 64 runs, a lane each
+  bool chased = a.chase_flag == nullptr;      // every chase item is known done (and visible)
   const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
   const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
   g_u32* slots = (g_u32*)a.slots;
@@ -255,13 +305,41 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t cur = 0;
   bool runs_left = true;
   auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
-  // run k's chunk-row prefix into LDS and its bounds into A or B; false if there is no run k (the
+  // Fused chase: wait until chase item `item` has published `stage`, then an agent acquire (this CU's
+  // L1 invalidated) so the rows, chunk table and cdesc it wrote are read fresh. Once every item has
+  // finished (chase_done), one acquire covers the rest of the wave's units. A poll that never
+  // matches gives up after ~0.2 s, once per wave (a protocol fault then shows as wrong rows, not as
+  // a hung GPU).
+  auto wait_chase = [&](uint64_t item, uint32_t stage) __attribute__((always_inline)) {
+    const uint32_t done = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&a.ctr->chase_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (done >= nitems) {
+      chased = true;
+    } else {
+      uint32_t polls = 0;
+      for (; polls < (1u << 22); ++polls) {
+        const uint32_t f = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&a.chase_flag[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if ((f >> 8) == a.epoch && (f & 0xFFu) >= stage) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      if (polls == (1u << 22)) chased = true;  // (gave up: never wait again, so the grid drains)
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  // unit u's chunk-row prefix into LDS and its bounds into A or B; false if there is no unit u (the
   // flags are set by the callers: a store to one of two flags chosen at run time is what the
   // compiler merges into a store through a selected pointer, which keeps both in scratch memory)
-  auto load_run = [&](bool intoA, uint64_t k) __attribute__((always_inline)) -> bool {
-    if (k >= nruns) return false;
-    const uint64_t t0 = run_start(k);
-    const uint32_t nch = (uint32_t)(a.total_chunks - t0 < R ? a.total_chunks - t0 : R);
+  auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
+    if (u >= nunits) return false;
+    const bool rest = split && u >= nruns;
+    const uint64_t k = rest ? u - nruns : u;
+    if (!chased) wait_chase(k / 64, rest || !split ? 2u : 1u);
+    const uint64_t tr = run_start(k);
+    const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
+    const uint64_t t0 = rest ? tr + H0 : tr;
+    const uint32_t nch = (uint32_t)(!split ? nk : rest ? (nk > H0 ? nk - H0 : 0ull) : (nk < H0 ? nk : H0));
     uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
@@ -287,7 +365,36 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     }
     return true;
   };
-  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first run, by its index
+  // Fused chase (a.chase_flag): the first waves to start each take items of 64 runs and chase them
+  // (a lane per run) before they hash: first parts, publish, the rest from where the first part
+  // left the chain, publish. Waiting hashing waves only ever wait for items already claimed by a
+  // running wave (every wave claims chase items before it hashes), so the grid cannot deadlock,
+  // whatever the residency.
+#ifdef CASK_STAMPS
+  const uint64_t wid = blockIdx.x * 4ull + wv;
+  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+  if (a.chase_flag) {
+    for (;;) {
+      const uint32_t it = wave_claim_next(&a.ctr->chase_next);
+      if (it >= nitems) break;
+      const uint64_t i = (uint64_t)it * 64 + lane;
+      uint64_t t0 = 0, t1 = 0;
+      if (i < nruns) walk_run_chunks(a, i, &t0, &t1);
+      const uint64_t tm = split && t0 + H0 < t1 ? t0 + H0 : t1;
+      uint64_t p = i < nruns ? a.tin[t0] : kNone;
+      for (uint32_t st = split ? 1u : 2u; st <= 2u; ++st) {
+        const uint64_t tb = st == 1u ? t0 : tm, te = st == 1u ? tm : t1;
+        if (i < nruns && tb < te) p = chase_range(a, a.files, tb, te, p);
+        chase_publish(a, it, st);
+#ifdef CASK_STAMPS  // (every lane stores the same time: no lane-0 branch in the claiming loop)
+        if (a.stamps && it < kStampChase) a.stamps[16 + 2 * kStampWaves + 2 * it + st - 1] = __builtin_amdgcn_s_memrealtime();
+#endif
+      }
+      atomicAdd(&a.ctr->chase_done, lane == 0 ? 1u : 0u);
+    }
+  }
+  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first unit, by its index
 
   // a quad's current record (cv) and the round of it in hand: blocks [rlb, rlb + rnl) of its full
   // 64-B blocks, rfin if the record ends in this round (its partial block in T), head if it is the
@@ -312,10 +419,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)hst;
   HST(h_all)
-#ifdef CASK_STAMPS
-  const uint64_t wid = blockIdx.x * 4ull + wv;
-  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
-#endif
   // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi): D full blocks
   // in X, a record's partial last block in T, its stored checksum in x. False: done.
   auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
@@ -554,7 +657,7 @@ static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
     if (per_cu <= 0) per_cu = 8;
   }
   uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
-  if (waves > nruns) waves = nruns;
+  if (waves > nruns) waves = nruns;  // (nruns <= the units: every wave's first unit exists)
   hipLaunchKernelGGL((k_run_hash<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
 }
 

@@ -35,9 +35,21 @@ THREADS = 16
 _T0 = time.time()
 
 
+_PROGRESS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
+                         "progress_large_configs.log")
+
+
 def _say(msg):
-    """Progress line (run with -s): the GPU harness kills a command that is silent for 3 minutes."""
-    print(f"[{time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
+    """Progress line on stderr (seen with -s) and appended to gpurun_out/ (seen under pytest's capture):
+    the GPU harness kills a command that writes nothing for 3 minutes."""
+    line = f"[{time.time() - _T0:7.1f}s] {msg}"
+    print(line, file=sys.stderr, flush=True)
+    try:
+        os.makedirs(os.path.dirname(_PROGRESS), exist_ok=True)
+        with open(_PROGRESS, "a") as f:
+            f.write(line + "\n")
+    except OSError:
+        pass
 
 
 def _beat(label, fn, *args):
@@ -127,6 +139,8 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
                 body = O.hint_body(m)
                 assert hb[:-4].tobytes() == body.tobytes(), i
                 assert int.from_bytes(hb[-4:].tobytes(), "little") == O.xxh32(body.tobytes()), i
+                if i % 16 == 0:
+                    _say(f"cfg3: hint file {i} checked")
             _say("cfg3: hint files checked; oracle replay")
             # the oracle's keydir (threaded replay) and its compaction of the same files, first
             pix = _beat("cfg3 oracle replay", O.PIndex, maps, ids, THREADS)
