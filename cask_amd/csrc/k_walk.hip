@@ -31,7 +31,7 @@ constexpr uint32_t kSearchShort = 2048;               // pass A verifies records
 constexpr uint32_t kStepA = kWalkUse - 18;            // candidate offsets per pass-A window
 constexpr uint32_t kStepB = kWalkUse - 18;            // candidate offsets per hop-back window
 constexpr uint32_t kSearchPast = 1u << 20;            // pass A looks this far past the run's end
-constexpr uint32_t kLongList = 256;                   // pass A's long candidates kept for the hop back
+constexpr uint32_t kLongList = 256;  // pass A's long candidates kept for the hop back (64: no faster)
 #ifdef CASK_STAMPS  // diagnostic build: per-wave s_memtime sums -> a.stamps[0..7] (tools/walk_stamps.py)
 #define WST(v) const uint64_t v = __builtin_amdgcn_s_memtime();
 #define WADD(i, v) wst[i] += __builtin_amdgcn_s_memtime() - (v);
@@ -261,6 +261,8 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
   uint64_t kA = kNone;
   if (lane == 0) L.nl = 0;
   bool over = false;
+  // (staging the next window into registers while this one is searched measured no faster: 207
+  // VGPRs, 2 waves per SIMD instead of 3)
   for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kSwStep) {
     WST(tw0)
     const uint32_t x0 = walk_stage<kSwNL>(L.win, data, len, wb);  // (its barriers also publish L.nl)

@@ -173,12 +173,20 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
     // stores would cost each hop a store round trip as well. Headers past the file's end are not
     // read (an address inside the file is loaded instead).
     const bool has = p != kNone && p < W.S.b1;
+#ifndef CASK_CHASE_TWOLOADS
+    // one 16-B load per hop, of header bytes 2..17 (seq, key size, value size; the checksum's first
+    // two bytes are not needed)
+    const uint64_t p0 = has && p + 18 <= W.S.len ? p + 2 : 0ull;
+    u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
+    asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
+#else
     const uint64_t p0 = has && p + 18 <= W.S.len ? p : 0ull;
     u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
     uint32_t vsz = gld4g((const g_u8*)(W.S.data + p0 + 14));
     // (waited for here, so that the loop's own wait counts the hop's load behind its stores: with
     // this path arriving at the loop with loads outstanding, it would wait for everything)
     asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w), "v"(vsz));
+#endif
     while (p != kNone && p < W.S.b1) {
       uint32_t j = 0;
       if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
@@ -189,13 +197,23 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
         term = true;
         break;
       }
+#ifndef CASK_CHASE_TWOLOADS
+      const uint32_t ksz = h.z >> 16, vsz = h.w;
+      const u32x4 row = u32x4{fun(h.x, h.y, 2), fun(h.y, h.z, 2), vsz, ksz};
+#else
       const uint32_t ksz = h.w & 0xFFFFu;
-      const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
       const u32x4 row = u32x4{h.y, h.z, vsz, ksz};
+#endif
+      const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
       const uint64_t pn = p + rl;
+#ifndef CASK_CHASE_TWOLOADS
+      const uint64_t pl = pn + 18 <= W.S.len ? pn + 2 : 0ull;  // (pn < p: rl wrapped, impossible)
+      h = gld16g((const g_u8*)(W.S.data + pl));
+#else
       const uint64_t pl = pn + 18 <= W.S.len ? pn : 0ull;  // (pn < p: rl wrapped, impossible)
       h = gld16g((const g_u8*)(W.S.data + pl));
       vsz = gld4g((const g_u8*)(W.S.data + pl + 14));
+#endif
       const uint32_t r = open_record(a, W, p, csh, true, &j);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
       *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
@@ -639,8 +657,13 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
-  const uint32_t grid = (uint32_t)((nruns + 255) / 256);
-  hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(256), 0, (hipStream_t)stream, a, a.files);
+  // CASK_CHASE_WG (tuning knob): threads per workgroup (a lane per run). One-wave workgroups spread
+  // the chase over every CU (configs[2]: 128 four-wave groups left half of the CUs idle; with
+  // one-wave groups the chase takes 0.35 instead of 0.46 ms)
+  static const uint32_t wg = getenv("CASK_CHASE_WG") ? (uint32_t)atoi(getenv("CASK_CHASE_WG")) : 64u;
+  const uint32_t tpb = wg == 64 || wg == 128 ? wg : 256u;
+  const uint32_t grid = (uint32_t)((nruns + tpb - 1) / tpb);
+  hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(tpb), 0, (hipStream_t)stream, a, a.files);
 }
 
 template <uint32_t D>

@@ -23,9 +23,11 @@ def child(path, steps, files, zipf_gib):
     if path != "product":
         cask_amd._lib.use_library(path)
     ctx = cask_amd.ScanContext(0)
+    want = None
     if zipf_gib > 0:  # configs[2]-shaped
         from cask_amd.workloads import zipf_files
-        fs, _, n, _ = zipf_files(ctx, zipf_gib, 2 ** 31)
+        fs, vsz_all, n, _ = zipf_files(ctx, zipf_gib, 2 ** 31)
+        want = (n, vsz_all[:n].clone())
         fs = [f for f, _ in fs]
     else:
         from cask_amd.workloads import cfg2_files
@@ -46,6 +48,15 @@ def child(path, steps, files, zipf_gib):
         k.append(ctx.last_timings()["chunk_scan_ms"])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if want is not None and not seg:  # the last call's rows against the generator (a variant that
+        res = call()                   # is fast and wrong fails here)
+        torch.cuda.synchronize()
+        wn, wv = want
+        assert res.error is None and res.count == wn, (res.error, res.count, wn)
+        assert int((rows["status"][:wn] != 0).sum().item()) == 0
+        assert torch.equal(rows["vsz"][:wn].to(torch.int64), wv.to(torch.int64))
+        assert torch.equal(rows["seq"][:wn].to(torch.int64), torch.arange(1, wn + 1, device=wv.device))
+        assert int((rows["ksz"][:wn] != 16).sum().item()) == 0
     print(json.dumps({"gibps": nbytes * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps,
                       "k_scan_ms": sum(k) / len(k), "timings": ctx.last_timings(),
                       "geometry": ctx.last_counters()["geometry"]}))

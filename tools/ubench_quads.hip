@@ -159,7 +159,7 @@ static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_
   return best;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int cus = 0;
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const uint64_t bytes = 16ull << 30;
@@ -168,7 +168,20 @@ int main() {
   CK(hipMemset(buf, 0x5A, bytes + 4096));
   uint32_t* sink;
   CK(hipMalloc(&sink, 64));
+  const bool sweep = argc > 1 && argv[1][0] == 's';  // depth / occupancy / mixing sweep (round 3)
   for (uint32_t S : {8192u, 65536u}) {
+    if (sweep) {
+      run<16, true>(buf, bytes, S, 8, 1, cus, sink);
+      run<16, false>(buf, bytes, S, 8, 1, cus, sink);
+      run<16, false>(buf, bytes, S, 12, 1, cus, sink);
+      run<8, true>(buf, bytes, S, 8, 1, cus, sink);
+      run<8, true>(buf, bytes, S, 16, 1, cus, sink);
+      run<8, false>(buf, bytes, S, 16, 1, cus, sink);
+      run<32, false>(buf, bytes, S, 4, 1, cus, sink);
+      run<32, false>(buf, bytes, S, 8, 1, cus, sink);
+      run_lanes<16, true>(buf, bytes, S, 8, 1, cus, sink);
+      continue;
+    }
     run<16, true>(buf, bytes, S, 8, 1, cus, sink, 0, 0);
     run<16, true>(buf, bytes, S, 8, 1, cus, sink, 1, 0);
     run<16, true>(buf, bytes, S, 8, 1, cus, sink, 2, 0);
