@@ -41,6 +41,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E peak, MI355X_MICROARCH.md (8.0 TB/s spec)
 CFG2_GIB, CFG2_MAX_FILE = 32.0, 2 ** 31
 CFG4_FILES_PER_RANK, CFG4_FILE = 32, 2 ** 30
+CFG2_MAX_RECORD = 18 + 16 + 16 * 4096  # the longest configs[2] record (16-B key, value of 16 x 4,096 B)
 SEQ_STRIDE = 1 << 40  # a rank's first sequence / key id (ranks' ranges disjoint and in rank order)
 
 
@@ -238,9 +239,12 @@ def main():
     else:  # one rank's shard of configs[4]: 32 x 1 GiB, file ids rank*32+1.., sequences after rank-1's
         cfg = "configs[4]"
         first_seq, first_key, first_fid = 1 + rank * SEQ_STRIDE, rank * SEQ_STRIDE, 1 + rank * CFG4_FILES_PER_RANK
-        files, vsz, n, rl = zipf_files(ctx, CFG4_FILES_PER_RANK * CFG4_FILE / 2 ** 30, CFG4_FILE,
+        # (each file fills to within one record of CFG4_FILE, so a shard of 32 x (CFG4_FILE - the
+        # longest record) bytes is exactly 32 files: a 33rd would take the next rank's first file id)
+        files, vsz, n, rl = zipf_files(ctx, CFG4_FILES_PER_RANK * (CFG4_FILE - CFG2_MAX_RECORD) / 2 ** 30, CFG4_FILE,
                                        seed=0x5A1F + rank, first_file_id=first_fid, first_seq=first_seq,
                                        first_key=first_key)
+        assert len(files) == CFG4_FILES_PER_RANK, (len(files), CFG4_FILES_PER_RANK)
     torch.cuda.synchronize(dev)
     views = [(f.file_id, f.data) for f, _ in files]
     bytes_per_step = sum(f.data.numel() for f, _ in files)
@@ -267,7 +271,12 @@ def main():
     # step's phase times (HIP events inside the library) are copied out of the context after it
     elapsed, tt = time_loop(torch, dev, run, timings, args.steps, barrier, dist, args.dist_backend)
     ms_per_step = elapsed * 1e3 / args.steps
-    value = bytes_per_step * world * args.steps / elapsed / 2 ** 30
+    bytes_all = bytes_per_step * world
+    if dist is not None:  # every rank's bytes (the shards differ by less than a record each)
+        tb_ = torch.tensor([bytes_per_step], dtype=torch.int64, device=dev if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(tb_)
+        bytes_all = int(tb_.item())
+    value = bytes_all * args.steps / elapsed / 2 ** 30
 
     walk = bool(counters.get("walk_mode"))
     kname = "k_run_hash" if walk else "k_scan_chunks"
@@ -287,6 +296,10 @@ def main():
     if dist is not None and not args.no_gather:
         try:
             from cask_amd.keydir import shard_keydir
+            # every rank's record count (ranks' Zipf draws differ): all of them are live keys
+            tn = torch.tensor([n], dtype=torch.int64, device=dev if args.dist_backend == "nccl" else "cpu")
+            dist.all_reduce(tn)
+            n_all = int(tn.item())
             res = ctx.scan_device(views, rows)
             barrier()
             tb = time.perf_counter()
@@ -325,7 +338,8 @@ def main():
                 extra["keydir_gathered_bytes"] = int(got)
                 extra["keydir_live_keys"] = len(db)
                 # unique keys: every record of every rank is live
-                extra["keydir_ok"] = len(db) == n * world and db.current_sequence == int(mx) + 1
+                extra["keydir_records_all_ranks"] = n_all
+                extra["keydir_ok"] = len(db) == n_all and db.current_sequence == int(mx) + 1
                 db.close()
             del blk
         except Exception as e:  # noqa: BLE001 - reported in the line

@@ -689,7 +689,9 @@ void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
   hipStream_t s = (hipStream_t)stream;
-  if (depth == 16)
+  if (depth == 32)
+    run_hash_at<32>(a, nruns, s);
+  else if (depth == 16)
     run_hash_at<16>(a, nruns, s);
   else if (depth == 4)
     run_hash_at<4>(a, nruns, s);

@@ -12,5 +12,5 @@ timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
   bench.py --gpus 2 --steps 3 --warmup 1 --dist-backend gloo --same-device --no-cpu-baseline > gpurun_out/bench_n2.log 2>&1
 rc=$?; grep '^{' gpurun_out/bench_n2.log | cut -c1-300; grep -o '"keydir[^,]*,' gpurun_out/bench_n2.log; echo "bench n2 rc=$rc"
 fi
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-segmented > gpurun_out/bench.log 2>&1
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/bench.log 2>&1
 rc=$?; tail -1 gpurun_out/bench.log | cut -c1-400; echo "bench rc=$rc"
