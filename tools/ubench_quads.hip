@@ -123,7 +123,8 @@ static float run_lanes(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t 
     CK(hipEventElapsedTime(&ms, a, b));
     best = ms < best ? ms : best;
   }
-  const double rd = (double)nseg * (double)((S - 64) / 16 * 16);
+  const uint64_t nstr = (S - 64) / 16, rds = nstr >= D ? nstr / D * D : D;
+  const double rd = (double)nseg * (double)(rds * 16);
   printf("lanes D=%2u %s S=%6u waves/CU=%2u %s: %.3f ms %.0f GB/s\n", D, HASH ? "hash" : "xor ", S, waves_per_cu,
          scatter ? "scattered" : "adjacent ", best, rd / best / 1e6);
   fflush(stdout);
@@ -151,9 +152,11 @@ static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_
     CK(hipEventElapsedTime(&ms, a, b));
     best = ms < best ? ms : best;
   }
-  // useful bytes: nblk full blocks of each segment the non-idle quads read
-  const double rd = (double)nseg * (double)((S - 64) / 64 * 64) * (4 - idle) / 4.0;
-  printf("D=%2u %s S=%6u waves/CU=%2u %s idle=%u/4 extra=%u: %.3f ms %.0f GB/s useful\n", D, HASH ? "hash" : "xor ", S,
+  // bytes read: the rounds of D blocks that fit a segment's nblk full blocks (D * floor(nblk / D)),
+  // by the non-idle quads (round 3: counting all nblk blocks overstated short segments by up to 2x)
+  const uint64_t nblk = (S - 64) / 64, rdb = nblk >= D ? nblk / D * D : D;
+  const double rd = (double)nseg * (double)(rdb * 64) * (4 - idle) / 4.0;
+  printf("D=%2u %s S=%6u waves/CU=%2u %s idle=%u/4 extra=%u: %.3f ms %.0f GB/s read\n", D, HASH ? "hash" : "xor ", S,
          waves_per_cu, scatter ? "scattered" : "adjacent ", idle, extra, best, rd / best / 1e6);
   fflush(stdout);
   return best;
@@ -169,6 +172,11 @@ int main(int argc, char** argv) {
   uint32_t* sink;
   CK(hipMalloc(&sink, 64));
   const bool sweep = argc > 1 && argv[1][0] == 's';  // depth / occupancy / mixing sweep (round 3)
+  if (argc > 1 && argv[1][0] == 'a') {  // adjacent (a wave's quads on consecutive segments) vs scattered
+    for (uint32_t S : {2048u, 4096u, 8192u, 16384u, 65536u})
+      for (uint32_t sc : {0u, 1u}) run<16, true>(buf, bytes, S, 8, sc, cus, sink);
+    return 0;
+  }
   for (uint32_t S : {8192u, 65536u}) {
     if (sweep) {
       run<16, true>(buf, bytes, S, 8, 1, cus, sink);
