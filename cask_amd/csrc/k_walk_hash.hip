@@ -173,20 +173,11 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
     // stores would cost each hop a store round trip as well. Headers past the file's end are not
     // read (an address inside the file is loaded instead).
     const bool has = p != kNone && p < W.S.b1;
-#ifndef CASK_CHASE_TWOLOADS
     // one 16-B load per hop, of header bytes 2..17 (seq, key size, value size; the checksum's first
     // two bytes are not needed)
     const uint64_t p0 = has && p + 18 <= W.S.len ? p + 2 : 0ull;
     u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
     asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
-#else
-    const uint64_t p0 = has && p + 18 <= W.S.len ? p : 0ull;
-    u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
-    uint32_t vsz = gld4g((const g_u8*)(W.S.data + p0 + 14));
-    // (waited for here, so that the loop's own wait counts the hop's load behind its stores: with
-    // this path arriving at the loop with loads outstanding, it would wait for everything)
-    asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w), "v"(vsz));
-#endif
     while (p != kNone && p < W.S.b1) {
       uint32_t j = 0;
       if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
@@ -197,23 +188,12 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
         term = true;
         break;
       }
-#ifndef CASK_CHASE_TWOLOADS
       const uint32_t ksz = h.z >> 16, vsz = h.w;
       const u32x4 row = u32x4{fun(h.x, h.y, 2), fun(h.y, h.z, 2), vsz, ksz};
-#else
-      const uint32_t ksz = h.w & 0xFFFFu;
-      const u32x4 row = u32x4{h.y, h.z, vsz, ksz};
-#endif
       const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
       const uint64_t pn = p + rl;
-#ifndef CASK_CHASE_TWOLOADS
       const uint64_t pl = pn + 18 <= W.S.len ? pn + 2 : 0ull;  // (pn < p: rl wrapped, impossible)
       h = gld16g((const g_u8*)(W.S.data + pl));
-#else
-      const uint64_t pl = pn + 18 <= W.S.len ? pn : 0ull;  // (pn < p: rl wrapped, impossible)
-      h = gld16g((const g_u8*)(W.S.data + pl));
-      vsz = gld4g((const g_u8*)(W.S.data + pl + 14));
-#endif
       const uint32_t r = open_record(a, W, p, csh, true, &j);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
       *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
@@ -248,24 +228,6 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
   }
 }
 
-// A single-wave claim of the next item of a work counter (every lane takes part in the atomic, lane 0
-// adding 1; no lane-0 branch, which the compiler could thread into the claiming loop's back edge).
-__device__ __forceinline__ uint32_t wave_claim_next(unsigned int* ctr) {
-  const uint32_t old = atomicAdd(ctr, (threadIdx.x & 63) == 0 ? 1u : 0u);
-  return __builtin_amdgcn_readfirstlane(old);
-}
-
-// Fused chase (k_run_hash with a.chase_flag): the chasing wave has written the slot rows, chunk table
-// and cdesc of its 64 runs up to `stage` (1: the first a.hash_h0 chunks of each, 2: all of them).
-// Every store of the wave drained, the XCD's L2 written back (agent release), then the item's flag,
-// tagged with the call's epoch (no clearing between calls). Every lane stores the same word.
-__device__ __forceinline__ void chase_publish(const ScanArgs& a, uint32_t it, uint32_t stage) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __hip_atomic_store(&a.chase_flag[it], (a.epoch << 8) | stage, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // ---------------------------------------------------------------------------------------------
 // Split path, pass 2 — k_run_hash: Entry::from_read's checksum (data.rs:185-198) of every record the
 // chase found. A wave claims runs and hands their records, in order, to its 16 quads: a quad hashes
@@ -293,14 +255,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   const bool qlead = q == 0;
   const uint64_t R = a.run;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
-  // Hash units: with 0 < a.hash_h0 < R, unit u < nruns is the first hash_h0 chunks of run u and unit
-  // nruns + k the rest of run k (the first parts of every run are handed out first: with the chase
-  // fused in, they are the parts chased first); else unit k is run k.
-  const uint64_t H0 = a.hash_h0;
-  const bool split = H0 != 0 && H0 < R;
-  const uint64_t nunits = split ? 2 * nruns : nruns;
-  const uint64_t nitems = (nruns + 63) / 64;  // fused chase: items of 64 runs, a lane each
-  bool chased = a.chase_flag == nullptr;      // every chase item is known done (and visible)
   const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
   const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
   g_u32* slots = (g_u32*)a.slots;
@@ -323,41 +277,13 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t cur = 0;
   bool runs_left = true;
   auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
-  // Fused chase: wait until chase item `item` has published `stage`, then an agent acquire (this CU's
-  // L1 invalidated) so the rows, chunk table and cdesc it wrote are read fresh. Once every item has
-  // finished (chase_done), one acquire covers the rest of the wave's units. A poll that never
-  // matches gives up after ~0.2 s, once per wave (a protocol fault then shows as wrong rows, not as
-  // a hung GPU).
-  auto wait_chase = [&](uint64_t item, uint32_t stage) __attribute__((always_inline)) {
-    const uint32_t done = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&a.ctr->chase_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (done >= nitems) {
-      chased = true;
-    } else {
-      uint32_t polls = 0;
-      for (; polls < (1u << 22); ++polls) {
-        const uint32_t f = __builtin_amdgcn_readfirstlane(
-            __hip_atomic_load(&a.chase_flag[item], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if ((f >> 8) == a.epoch && (f & 0xFFu) >= stage) break;
-        __builtin_amdgcn_s_sleep(2);
-      }
-      if (polls == (1u << 22)) chased = true;  // (gave up: never wait again, so the grid drains)
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  };
-  // unit u's chunk-row prefix into LDS and its bounds into A or B; false if there is no unit u (the
+  // run k's chunk-row prefix into LDS and its bounds into A or B; false if there is no run k (the
   // flags are set by the callers: a store to one of two flags chosen at run time is what the
   // compiler merges into a store through a selected pointer, which keeps both in scratch memory)
-  auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
-    if (u >= nunits) return false;
-    const bool rest = split && u >= nruns;
-    const uint64_t k = rest ? u - nruns : u;
-    if (!chased) wait_chase(k / 64, rest || !split ? 2u : 1u);
-    const uint64_t tr = run_start(k);
-    const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
-    const uint64_t t0 = rest ? tr + H0 : tr;
-    const uint32_t nch = (uint32_t)(!split ? nk : rest ? (nk > H0 ? nk - H0 : 0ull) : (nk < H0 ? nk : H0));
+  auto load_run = [&](bool intoA, uint64_t k) __attribute__((always_inline)) -> bool {
+    if (k >= nruns) return false;
+    const uint64_t t0 = run_start(k);
+    const uint32_t nch = (uint32_t)(a.total_chunks - t0 < R ? a.total_chunks - t0 : R);
     uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
@@ -383,36 +309,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     }
     return true;
   };
-  // Fused chase (a.chase_flag): the first waves to start each take items of 64 runs and chase them
-  // (a lane per run) before they hash: first parts, publish, the rest from where the first part
-  // left the chain, publish. Waiting hashing waves only ever wait for items already claimed by a
-  // running wave (every wave claims chase items before it hashes), so the grid cannot deadlock,
-  // whatever the residency.
-#ifdef CASK_STAMPS
-  const uint64_t wid = blockIdx.x * 4ull + wv;
-  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-  if (a.chase_flag) {
-    for (;;) {
-      const uint32_t it = wave_claim_next(&a.ctr->chase_next);
-      if (it >= nitems) break;
-      const uint64_t i = (uint64_t)it * 64 + lane;
-      uint64_t t0 = 0, t1 = 0;
-      if (i < nruns) walk_run_chunks(a, i, &t0, &t1);
-      const uint64_t tm = split && t0 + H0 < t1 ? t0 + H0 : t1;
-      uint64_t p = i < nruns ? a.tin[t0] : kNone;
-      for (uint32_t st = split ? 1u : 2u; st <= 2u; ++st) {
-        const uint64_t tb = st == 1u ? t0 : tm, te = st == 1u ? tm : t1;
-        if (i < nruns && tb < te) p = chase_range(a, a.files, tb, te, p);
-        chase_publish(a, it, st);
-#ifdef CASK_STAMPS  // (every lane stores the same time: no lane-0 branch in the claiming loop)
-        if (a.stamps && it < kStampChase) a.stamps[16 + 2 * kStampWaves + 2 * it + st - 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-      }
-      atomicAdd(&a.ctr->chase_done, lane == 0 ? 1u : 0u);
-    }
-  }
-  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first unit, by its index
+  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first run, by its index
 
   // a quad's current record (cv) and the round of it in hand: blocks [rlb, rlb + rnl) of its full
   // 64-B blocks, rfin if the record ends in this round (its partial block in T), head if it is the
@@ -437,6 +334,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)hst;
   HST(h_all)
+#ifdef CASK_STAMPS
+  const uint64_t wid = blockIdx.x * 4ull + wv;
+  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
+#endif
   // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi): D full blocks
   // in X, a record's partial last block in T, its stored checksum in x. False: done.
   auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
@@ -680,7 +581,7 @@ static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
     if (per_cu <= 0) per_cu = 8;
   }
   uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
-  if (waves > nruns) waves = nruns;  // (nruns <= the units: every wave's first unit exists)
+  if (waves > nruns) waves = nruns;
   hipLaunchKernelGGL((k_run_hash<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
 }
 
@@ -689,9 +590,7 @@ void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
   hipStream_t s = (hipStream_t)stream;
-  if (depth == 32)
-    run_hash_at<32>(a, nruns, s);
-  else if (depth == 16)
+  if (depth == 16)
     run_hash_at<16>(a, nruns, s);
   else if (depth == 4)
     run_hash_at<4>(a, nruns, s);

@@ -51,8 +51,6 @@ struct Counters {
   unsigned int walk_next[8];     // k_walk_runs: next run of each walk group to hand out (kWalkGroups)
   unsigned int search_next[8];   // k_walk_search: the same, for the searches
   unsigned int hash_next;        // k_walk_hash: next run to hand out (after the first by index)
-  unsigned int chase_next;       // k_run_hash with the chase fused in: next item of 64 runs to chase
-  unsigned int chase_done;       // ... and the items chased to their end
 };
 
 // Layout of the call block: Counters, then row_off[nfiles + 1] (each file's first dense row,
@@ -164,12 +162,7 @@ struct ScanArgs {
   // k_walk_search: candidates of at most this many bytes are verified by their checksum, longer
   // ones are listed for the hop back (kSearchShort; CASK_SEARCH_SHORT tuning knob)
   uint32_t search_short;
-  // k_run_hash: chunks of each walk run in its first hash unit (0: a unit per run). The first units
-  // of every run are handed out before the rest.
-  uint32_t hash_h0;
-  // k_run_hash with the chase fused in (null: k_walk_chase ran before it): per item of 64 walk runs,
-  // the stage its chase has published, tagged with the call's epoch ((epoch << 8) | stage)
-  uint32_t* chase_flag;
+  uint32_t pad_ss;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -261,7 +254,6 @@ void launch_run_hash(const ScanArgs& a, int depth, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
 constexpr uint32_t kProbeRegions = 8;
 constexpr uint32_t kStampWaves = 8192;  // diagnostic builds: waves with start/end stamps
-constexpr uint32_t kStampChase = 2048;  // ... and fused-chase items with their two publish times
 void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

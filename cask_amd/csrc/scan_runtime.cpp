@@ -98,8 +98,6 @@ struct cask_ctx {
   DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
   DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
   DevBuf cdesc;      // walk mode, split path: per chunk its address and its file's end (2 x u64)
-  DevBuf cflag;      // walk mode, chase fused into k_run_hash: per item of 64 runs its published
-                     // stage, tagged with `epoch` (cleared with tstate)
   DevBuf probe;      // k_probe_regions: 3 u64 per region of each file
   DevBuf mruns;      // mixed call: walk-mode run indices | chunk-mode [first, end) stretches
   uint32_t epoch = 0;
@@ -313,8 +311,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   bool fresh = false;  // k_finish look-back granules, 8 per tile
   // (then the group aggregates of the two-level prefix)
   if (!c->tstate.ensure(64ull * (fin_tiles + 1) + 64ull * (fin_tiles / kFinGroup + 2), &fresh)) return CASK_E_NOMEM;
-  bool cflag_fresh = false;  // (at most one item per 64 runs of one chunk)
-  if (!c->cflag.ensure(4ull * (total_chunks / 64 + 2), &cflag_fresh)) return CASK_E_NOMEM;
 
   uint8_t* fbase = c->filebuf.as<uint8_t>();
   FileDesc* d_files = (FileDesc*)fbase;
@@ -436,14 +432,13 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.dense = 0;  // k_long fixes dense rows only once they are validated
 
   // look-back granules carry the call's epoch: no memset between calls, one when the tag wraps
-  if (fresh || cflag_fresh || c->epoch >= 255) {
+  if (fresh || c->epoch >= 255) {
     if (hipMemsetAsync(a.tstate, 0, c->tstate.cap, st) != hipSuccess) return CASK_E_DEVICE;
-    if (hipMemsetAsync(c->cflag.p, 0, c->cflag.cap, st) != hipSuccess) return CASK_E_DEVICE;
     c->epoch = 0;
   }
   a.epoch = ++c->epoch;
 #ifdef CASK_STAMPS
-  if (c->stamps.ensure(8ull * (16 + 2 * kStampWaves + 2 * kStampChase))) a.stamps = c->stamps.as<unsigned long long>();
+  if (c->stamps.ensure(8ull * (16 + 2 * kStampWaves))) a.stamps = c->stamps.as<unsigned long long>();
 #endif
 
   bool ok = true;
@@ -606,15 +601,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   bool long_pre = false;
   // CASK_HASH_D (tuning knob): 64-B blocks in flight per quad of the hashing kernel
   static const int hash_depth = getenv("CASK_HASH_D") ? atoi(getenv("CASK_HASH_D")) : 16;  // (16: 5 % faster than 8)
-  // CASK_FUSE_CHASE=1 (tuning knob): the chase fused into k_run_hash — the first waves chase the
-  // runs while the others hash the parts already chased — instead of k_walk_chase before it.
-  // CASK_HASH_H0 (tuning knob): chunks of each run in its first hash unit, the part chased (and
-  // published) first. Not the default: on configs[2] the chase under the hash's load takes its wave
-  // slots for longer than it saves (first parts of 8 chunks: 7.95 vs 7.51 ms per step; 16: 7.50;
-  // 4: 8.9 — the hash then waits for the runs' second parts).
-  static const bool fuse_chase = getenv("CASK_FUSE_CHASE") && atoi(getenv("CASK_FUSE_CHASE")) == 1;
-  static const uint32_t hash_h0 = getenv("CASK_HASH_H0") ? (uint32_t)atoi(getenv("CASK_HASH_H0")) : (fuse_chase ? 16u : 0u);
-  a.hash_h0 = hash_h0;
   bool fused = false;
   if (mixed) {  // the walk-mode runs (split path), then the chunk-mode runs, then k_finish for all
     fused = true;
@@ -627,12 +613,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     aw.walk_pre = 1;
     if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
     aw.cdesc = c->cdesc.as<uint64_t>();
-    if (fuse_chase) {
-      aw.chase_flag = c->cflag.as<uint32_t>();
-    } else {
-      launch_walk_chase(aw, st);
-      L("k_walk_chase");
-    }
+    launch_walk_chase(aw, st);
+    L("k_walk_chase");
     H(hipEventRecord(c->ev[7], st));
     launch_run_hash(aw, hash_depth, st);
     L("k_run_hash");
@@ -655,17 +637,12 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.walk_pre = 1;
     if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
     a.cdesc = c->cdesc.as<uint64_t>();
-    if (fuse_chase) {
-      a.chase_flag = c->cflag.as<uint32_t>();
-    } else {
-      launch_walk_chase(a, st);
-      L("k_walk_chase");
-    }
+    launch_walk_chase(a, st);
+    L("k_walk_chase");
     H(hipEventRecord(c->ev[7], st));
     launch_run_hash(a, hash_depth, st);
     L("k_run_hash");
     a.walk_pre = 0;
-    a.chase_flag = nullptr;
     long_pre = true;
     if (!ok) return CASK_E_DEVICE;
   } else if (walk) {  // hint bodies: the walk searches its own starts (cheaply: hint records are small)
@@ -761,7 +738,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
     H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
     H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
-    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 8ull * (16 + 2 * kStampWaves + 2 * kStampChase), st));
+    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 8ull * (16 + 2 * kStampWaves), st));
   };
   uint64_t nlong_total = 0;  // records hashed by k_long over all passes (each pass queues only chunks it scanned)
   // validation, long records and summary after a scan of the chunks (events 2..4 when timed)
@@ -1274,7 +1251,7 @@ extern "C" int cask_debug_stamps(cask_ctx* c, uint64_t* out16) {
 }
 // Diagnostic build only: k_run_hash's per-wave start/end real times (2 per wave, kStampWaves waves).
 extern "C" int cask_debug_wave_stamps(cask_ctx* c, uint64_t* out, uint64_t n) {
-  if (!c || !c->stamps.p || n > 2ull * (kStampWaves + kStampChase)) return CASK_E_INVALID_ARG;
+  if (!c || !c->stamps.p || n > 2ull * kStampWaves) return CASK_E_INVALID_ARG;
   if (hipMemcpy(out, (uint8_t*)c->stamps.p + 16 * 8, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return CASK_E_DEVICE;
   return CASK_OK;
 }

@@ -134,13 +134,20 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
         with CaskOptions().max_file_size(1 << 30).open(path) as db:
             assert len(db) == live_want
             maps = [np.memmap(os.path.join(path, f"{i:010}.cask.data"), np.uint8, "r") for i in ids]
-            for i, m in zip(ids, maps):
+
+            def check_hint(i, m):  # (the oracle's C calls drop the GIL: files checked on threads)
                 hb = np.fromfile(os.path.join(path, f"{i:010}.cask.hint"), np.uint8)
                 body = O.hint_body(m)
-                assert hb[:-4].tobytes() == body.tobytes(), i
-                assert int.from_bytes(hb[-4:].tobytes(), "little") == O.xxh32(body.tobytes()), i
-                if i % 16 == 0:
-                    _say(f"cfg3: hint file {i} checked")
+                ok = hb[:-4].tobytes() == body.tobytes() and \
+                    int.from_bytes(hb[-4:].tobytes(), "little") == O.xxh32(body.tobytes())
+                return i, ok
+
+            from concurrent.futures import ThreadPoolExecutor
+            with ThreadPoolExecutor(8) as ex:
+                for i, ok in ex.map(lambda im: check_hint(*im), zip(ids, maps)):
+                    assert ok, i
+                    if i % 16 == 0:
+                        _say(f"cfg3: hint file {i} checked")
             _say("cfg3: hint files checked; oracle replay")
             # the oracle's keydir (threaded replay) and its compaction of the same files, first
             pix = _beat("cfg3 oracle replay", O.PIndex, maps, ids, THREADS)

@@ -40,22 +40,13 @@ def main():
           f"wait {h[5] / tot:.3f}; per iteration {h[0] / max(h[6], 1):.0f} cycles; iterations {h[6]}")
     print("timings", ctx.last_timings(), "rows", res.count)
     # per-wave start/end (100 MHz real-time clock) of the last call's k_run_hash
-    nw, nc = 8192, 2048
+    nw = 8192
     L.cask_debug_wave_stamps.restype = C.c_int
     L.cask_debug_wave_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64]
-    ws = (C.c_uint64 * (2 * nw + 2 * nc))()
-    L.cask_debug_wave_stamps(ctx._h, ws, 2 * nw + 2 * nc)
+    ws = (C.c_uint64 * (2 * nw))()
+    L.cask_debug_wave_stamps(ctx._h, ws, 2 * nw)
     import numpy as np
-    allw = np.frombuffer(ws, np.uint64).astype(np.int64)
-    a = allw[:2 * nw].reshape(nw, 2)
-    ch = allw[2 * nw:].reshape(nc, 2)
-    ch = ch[ch[:, 1] > 0]
-    if ch.size and (a[:, 0] > 0).any():
-        t0c = a[a[:, 0] > 0, 0].min()
-        for k, name in ((0, "stage 1 (first parts)"), (1, "stage 2 (whole runs)")):
-            q = np.percentile((ch[:, k] - t0c) / 100.0, [0, 10, 50, 90, 100])
-            print(f"fused chase, {len(ch)} items, {name} published at 0/10/50/90/100 % = "
-                  f"{' / '.join(f'{x:.1f}' for x in q)} us after the kernel's first wave")
+    a = np.frombuffer(ws, np.uint64).reshape(nw, 2).astype(np.int64)
     a = a[a[:, 1] > 0]
     if a.size:
         t0 = a[:, 0].min()
