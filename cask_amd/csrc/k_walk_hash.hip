@@ -280,10 +280,25 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   // run k's chunk-row prefix into LDS and its bounds into A or B; false if there is no run k (the
   // flags are set by the callers: a store to one of two flags chosen at run time is what the
   // compiler merges into a store through a selected pointer, which keeps both in scratch memory)
-  auto load_run = [&](bool intoA, uint64_t k) __attribute__((always_inline)) -> bool {
-    if (k >= nruns) return false;
-    const uint64_t t0 = run_start(k);
-    const uint32_t nch = (uint32_t)(a.total_chunks - t0 < R ? a.total_chunks - t0 : R);
+  // Units of work: the runs in order, except that the last grid's worth of runs (one per wave) is
+  // handed out in quarters, so that the waves run dry within about a quarter of a run of each other
+  // instead of a whole one (configs[2]: a run is ~0.4 ms of one wave's hashing).
+#ifdef CASK_HASH_NOTAIL  // (A/B variant: whole runs to the end)
+  const uint64_t ntail = 0;
+#else
+  const uint64_t ntail = nruns < (uint64_t)gridDim.x * 4 ? nruns : (uint64_t)gridDim.x * 4;
+#endif
+  const uint64_t nhead = nruns - ntail, nunits = nhead + 4 * ntail;
+  auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
+    if (u >= nunits) return false;
+    const bool tl = u >= nhead;
+    const uint64_t k = tl ? nhead + ((u - nhead) >> 2) : u;
+    const uint64_t tr = run_start(k);
+    const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
+    const uint64_t qr = (R + 3) >> 2, c0 = tl ? ((u - nhead) & 3) * qr : 0ull;
+    const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
+    const uint64_t t0 = tr + c0;
+    const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
     uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
