@@ -66,8 +66,9 @@ def cfg3(ctx, torch, steps, total_gib, max_file):
             "counters": counters, "parity": "rows == generator (count, pos, seq, ksz, vsz, status)"}
 
 
-def compact(ctx, torch, nfiles, workdir):
-    from cask_amd import CaskOptions
+def write_cfg3(ctx, torch, nfiles, path):
+    """configs[3]-shaped data files 1..nfiles in `path`: 290-B records, a key space of a fifth of
+    the records, 10 % of keys ending in a tombstone. Returns (bytes, live keys, records, seconds)."""
     from cask_amd.workloads import CFG2_RECORDS_PER_FILE, variable_file
     dev = torch.device("cuda", ctx.device)
     rpf = CFG2_RECORDS_PER_FILE
@@ -83,8 +84,6 @@ def compact(ctx, torch, nfiles, workdir):
     vsz = torch.full((n,), 256, dtype=torch.int32, device=dev)
     vsz[last[tomb_key]] = -1  # 10 % of keys end in a tombstone
     live_want = int((present & ~tomb_key).sum().item())
-    path = os.path.join(workdir, "db")
-    os.makedirs(path)
     t0 = time.perf_counter()
     nbytes = 0
     for i in range(nfiles):
@@ -102,6 +101,16 @@ def compact(ctx, torch, nfiles, workdir):
     write_s = time.perf_counter() - t0
     del kid, last, present, tomb_key, vsz
     torch.cuda.empty_cache()
+    return nbytes, live_want, n, write_s
+
+
+def compact(ctx, torch, nfiles, workdir):
+    from cask_amd import CaskOptions
+    from cask_amd.workloads import CFG2_RECORDS_PER_FILE
+    rpf = CFG2_RECORDS_PER_FILE
+    path = os.path.join(workdir, "db")
+    os.makedirs(path)
+    nbytes, live_want, n, write_s = write_cfg3(ctx, torch, nfiles, path)
     out = {"config": f"configs[3] shape scaled to {nfiles} files x {rpf} records (290 B, 80 % overwritten/"
                      f"deleted, 10 % of keys end in a tombstone), on disk, 1 GPU",
            "files": nfiles, "records": n, "bytes": nbytes, "write_files_s": write_s}
