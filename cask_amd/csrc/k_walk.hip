@@ -764,7 +764,16 @@ void launch_walk_runs(const ScanArgs& a, void* stream) {
 void launch_walk_search(const ScanArgs& a, void* stream) {
   const uint64_t nruns = launch_runs(a);
   if (!a.total_chunks || !nruns) return;
-  uint64_t grid = (uint64_t)device_cus() * 20u;  // 5 waves per SIMD (95 VGPRs)
+  // A persistent grid of exactly the resident workgroups (LDS-bound: ~12 per CU): a workgroup
+  // beyond them would start only as the first ones finish, holding its first run (by block index)
+  // until the end of the kernel.
+  static int per_cu = 0;
+  if (!per_cu) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk_search, 64, 0) == hipSuccess && nb > 0) per_cu = nb;
+    else per_cu = 12;
+  }
+  uint64_t grid = (uint64_t)device_cus() * (uint64_t)per_cu;
   if (grid > nruns) grid = nruns;
   hipLaunchKernelGGL(k_walk_search, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
 }
