@@ -569,6 +569,40 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
 #endif
 }
 
+// ---------------------------------------------------------------------------------------------
+// Walk mode with k_finish running beside k_run_hash (it needs only the chase's output, so it runs
+// in the slots the hash's last waves leave): the checksum verdicts k_finish may have read before
+// the hash wrote them. Every chunk with a failing row has cerr set (the chase's EOF rows, the
+// hash's atomicMin for every checksum failure), so only those chunks are walked again: a row whose
+// slot has the bad bit and is not an EOF row gets kRowChecksum (k_finish's rule), and the file's
+// first failing row takes the chunk's final cerr. Usually no chunk is flagged: one thread per chunk
+// reads cerr and exits.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_hash_fix(ScanArgs a) {
+  const uint64_t c = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  if (c >= a.total_chunks) return;
+  const uint32_t ce = a.cerr[c];
+  if (ce == 0xFFFFFFFFu) return;
+  const uint32_t fi = find_file(a.files, a.nfiles, c);
+  const FileDesc fd = a.files[fi];
+  const uint64_t base = a.gbase[c], c0 = (c - fd.first_chunk) * (uint64_t)a.chunk;
+  const uint32_t n = a.count[c] & kCountMask;
+  for (uint32_t r = 0; r < n; ++r) {
+    const u32x4 w = *(const u32x4*)(a.slots + (c * (uint64_t)a.slot_cap + r) * 4);
+    const uint32_t ksz = w.w & 0xFFFFu;
+    const uint64_t p = c0 + ((w.w >> 16) & 0x7FFFu);
+    const uint64_t end = p + 18ull + ksz + (w.z == 0xFFFFFFFFu ? 0ull : (uint64_t)w.z);
+    const bool eof = p + 18 > fd.len || end > fd.len;
+    if (!eof && (w.w & kSlotBad) && base + r < a.row_cap) a.status[base + r] = kRowChecksum;
+  }
+  atomicMax(&a.err_inv[fi], ~(unsigned long long)(base + ce));
+}
+
+void launch_hash_fix(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  hipLaunchKernelGGL(k_hash_fix, dim3((uint32_t)((a.total_chunks + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);
+}
+
 void launch_walk_chase(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;

@@ -251,6 +251,8 @@ void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each w
 // every record hashed from HBM; depth = 64-B blocks per quad in flight)
 void launch_walk_chase(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, int depth, void* stream);
+// after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
+void launch_hash_fix(const ScanArgs& a, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
 constexpr uint32_t kProbeRegions = 8;
 constexpr uint32_t kStampWaves = 8192;  // diagnostic builds: waves with start/end stamps

@@ -85,6 +85,7 @@ inline uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 struct cask_ctx {
   int device = 0;
   hipStream_t own = nullptr;
+  hipStream_t side = nullptr;  // walk mode: k_finish beside k_run_hash
   hipStream_t stream = nullptr;
   // Members are destroyed in reverse order: every buffer is freed before the context goes.
   DevBuf chunk;      // spec | exit | base | tin (u64 x4) | count (u32) | tiles | long_r | desc | gbase
@@ -116,6 +117,7 @@ struct cask_ctx {
   int geo = -1;      // k_scan_chunks geometry: -1 picks one per call (CASK_SCAN_GEOMETRY forces one)
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
+  hipEvent_t evf = nullptr;  // walk mode: k_finish done on the side stream
   void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
   float last_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
@@ -144,11 +146,14 @@ struct cask_ctx {
   ~cask_ctx() {
     (void)hipSetDevice(device);
     if (stream) (void)hipStreamSynchronize(stream);
+    if (side) (void)hipStreamSynchronize(side);
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
     if (evw) (void)hipEventDestroy(evw);
     if (kd) kd_scratch_destroy(kd);
     if (own) (void)hipStreamDestroy(own);
+    if (side) (void)hipStreamDestroy(side);
+    if (evf) (void)hipEventDestroy(evf);
   }
 };
 
@@ -180,6 +185,8 @@ cask_ctx* cask_ctx_create(int device, int* status) {
   if (const char* g = getenv("CASK_SCAN_GEOMETRY")) c->geo = atoi(g);
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   (void)hipEventCreateWithFlags(&c->evw, hipEventDisableTiming);
+  (void)hipEventCreateWithFlags(&c->evf, hipEventDisableTiming);
+  (void)hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (!c->err2.ensure(64)) {
     cask_ctx_destroy(c);
     if (status) *status = CASK_E_NOMEM;
@@ -602,6 +609,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // CASK_HASH_D (tuning knob): 64-B blocks in flight per quad of the hashing kernel
   static const int hash_depth = getenv("CASK_HASH_D") ? atoi(getenv("CASK_HASH_D")) : 16;  // (16: 5 % faster than 8)
   bool fused = false;
+  bool fin_done = false;  // k_finish already launched (beside the hash)
   if (mixed) {  // the walk-mode runs (split path), then the chunk-mode runs, then k_finish for all
     fused = true;
     ScanArgs aw = a;
@@ -642,6 +650,21 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipEventRecord(c->ev[7], st));
     launch_run_hash(a, hash_depth, st);
     L("k_run_hash");
+    // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
+    // starts): on a side stream it runs in the slots the hash's last waves leave, and k_hash_fix
+    // then adds the checksum statuses it may have missed. CASK_FIN_OVERLAP=0 (tuning knob): after.
+    static const bool fin_overlap = !(getenv("CASK_FIN_OVERLAP") && atoi(getenv("CASK_FIN_OVERLAP")) == 0);
+    if (dense && fin_overlap && c->side && c->evf) {
+      H(hipEventRecord(c->ev[2], st));  // (the hash's end, for the timings)
+      H(hipStreamWaitEvent(c->side, c->ev[7], 0));
+      launch_finish(a, c->side);
+      L("k_finish (beside the hash)");
+      H(hipEventRecord(c->evf, c->side));
+      H(hipStreamWaitEvent(st, c->evf, 0));
+      launch_hash_fix(a, st);
+      L("k_hash_fix");
+      fin_done = true;
+    }
     a.walk_pre = 0;
     long_pre = true;
     if (!ok) return CASK_E_DEVICE;
@@ -652,13 +675,15 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_scan_chunks(a, geo, st);
     L("k_scan_chunks");
   }
-  H(hipEventRecord(c->ev[2], st));
+  if (!fin_done) H(hipEventRecord(c->ev[2], st));
   // (walk mode has hashed its long records already. Queueing them from the walk itself instead of
   // k_long_enqueue measured 1 ms slower: the queue counters' atomics.)
   const bool long_now = long_pre;
   if (dense) {
-    launch_finish(a, st);
-    L("k_finish");
+    if (!fin_done) {
+      launch_finish(a, st);
+      L("k_finish");
+    }
     H(hipEventRecord(c->ev[3], st));
     read_call();
     if (!ok) return CASK_E_DEVICE;
