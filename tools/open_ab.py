@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--files", type=int, default=64)
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--child", nargs=3)
+    ap.add_argument("--precat", action="store_true", help="read every data file once before the rounds")
     ap.add_argument("libs", nargs="*")
     a = ap.parse_args()
     if a.child:
@@ -59,6 +60,13 @@ ctx = ScanContext(0); print(json.dumps(B.write_cfg3(ctx, torch, {a.files}, {path
             sys.exit(1)
         nbytes, live, n, ws = json.loads(p.stdout.strip().splitlines()[-1])
         print(f"{a.files} files, {nbytes} bytes, {n} records, {live} live keys, written in {ws:.1f} s", flush=True)
+        if a.precat:  # (is the first open's slower read the open's, or the freshly written pages'?)
+            t0 = time.perf_counter()
+            for f in sorted(glob.glob(os.path.join(path, "*.cask.data"))):
+                with open(f, "rb") as fh:
+                    while fh.read(64 << 20):
+                        pass
+            print(f"files read once in {time.perf_counter() - t0:.1f} s", flush=True)
         for r in range(a.rounds):
             for spec in a.libs:
                 name, lib = spec.split("=", 1)
