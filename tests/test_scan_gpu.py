@@ -331,6 +331,28 @@ def test_zipf_sizes_corrupt(gpu_ctx):
     check_against_oracle(gpu_ctx, [bytes(buf)], device=True)
 
 
+def test_zipf_many_failures_on_a_caller_stream(gpu_ctx):
+    """Walk mode with k_finish beside the hash: many checksum failures spread over many chunks (the
+    statuses k_hash_fix sets after both), one record cut short at the end, the scan on a stream the
+    caller owns (the side stream must order itself after it and the caller's stream after the
+    side stream) — rows and the first error against the oracle, twice, the second call reusing the
+    device buffers."""
+    import torch
+    rng = random.Random(53)
+    buf = bytearray(make_records(rng, 6000, lambda r: 16, _zipf_vsz(rng), tomb_p=0.02))
+    for _ in range(150):
+        buf[rng.randrange(len(buf))] ^= 1 << rng.randrange(8)
+    short = bytes(buf[: len(buf) - 7])  # the last record cut short: an UnexpectedEof row
+    s = torch.cuda.Stream()
+    old = gpu_ctx.stream_ptr
+    gpu_ctx.set_stream(s.cuda_stream)
+    try:
+        for _ in range(2):
+            check_against_oracle(gpu_ctx, [bytes(buf), short], device=True)
+    finally:
+        gpu_ctx.set_stream(old)
+
+
 def test_long_record_hash_every_length_residue(gpu_ctx):
     """Records past ScanArgs::big (2 KiB) are hashed from HBM by quads of lanes (k_long_hash): every
     hashed length mod 64 (full 4-stripe blocks, 1-3 trailing stripes, 0-15 tail bytes), with value
