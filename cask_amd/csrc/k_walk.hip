@@ -249,9 +249,6 @@ struct SearchLdsSw {
   uint32_t pad[3];
   uint64_t lx[kLongList], le[kLongList];
 };
-__device__ __forceinline__ uint32_t zero_bytes(uint32_t w) {  // 0x80 in each byte of w that is 0
-  return ~(((w & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | w) & 0x80808080u;
-}
 __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t* data, uint64_t len, uint64_t b0,
                                                    uint64_t b1, uint64_t* wst, uint32_t sshort) {
   const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
@@ -296,7 +293,11 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
         const uint32_t w = wv[j][e];
         const uint32_t wp = e ? wv[j][e - 1] : (pc ? wv[(j + 7) & 7][3] : dprev);
         const uint32_t kszhi_small = ~(((wp & 0x7F7F7F7Fu) + 0x6F6F6F6Fu) | wp) & 0x80808080u;  // byte < 0x11
-        uint32_t m = (zero_bytes(w) | zero_bytes(~w)) & kszhi_small;
+        // bytes 0x00 or 0xFF: all eight bits equal, i.e. no bit differs from the one above it
+        // (the shift's bit 7 comes from the next byte and is masked off); y <= 0x7F per byte, so
+        // the add sets bit 7 exactly where y is not 0 and carries into no other byte
+        const uint32_t y = (w ^ (w >> 1)) & 0x7F7F7F7Fu;
+        uint32_t m = ~(y + 0x7F7F7F7Fu) & 0x80808080u & kszhi_small;
         const uint32_t k = 4 * pc + e;
         while (m) {
           const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
