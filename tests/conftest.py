@@ -29,9 +29,13 @@ def oracle_lib():
 
 @pytest.fixture(scope="session")
 def native():
-    """The product library. Built in-tree if absent (hipcc cross-compiles without a GPU)."""
+    """The product library. Built in-tree if absent (hipcc cross-compiles without a GPU).
+    CASK_TEST_LIB (tools only: checking an A/B variant build before it becomes the product) runs
+    the suite on another build of the library."""
     import cask_amd
-    if not os.path.exists(cask_amd.LIB_PATH):
+    if os.environ.get("CASK_TEST_LIB"):
+        cask_amd._lib.use_library(os.environ["CASK_TEST_LIB"])
+    elif not os.path.exists(cask_amd.LIB_PATH):
         _make(os.path.join(ROOT, "cask_amd"))
     return cask_amd.lib()
 
