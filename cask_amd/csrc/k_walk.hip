@@ -247,7 +247,9 @@ struct SearchLdsSw {
   uint32_t cand[16];
   uint32_t nl;
   uint32_t pad[3];
-  uint64_t lx[kLongList], le[kLongList];
+  // long candidates as offsets from the run's first byte (x - b0 and x + rl - b0: both within the
+  // run and kSearchPast past it, far below 2^32), 2 KiB instead of 4: more searching waves per CU
+  uint32_t lx[kLongList], le[kLongList];
 };
 __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t* data, uint64_t len, uint64_t b0,
                                                    uint64_t b1, uint64_t* wst, uint32_t sshort) {
@@ -311,8 +313,8 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
           } else if (x + rl <= lim) {
             const uint32_t r = atomicAdd(&L.nl, 1u);
             if (r < kLongList) {
-              L.lx[r] = x;
-              L.le[r] = x + rl;
+              L.lx[r] = (uint32_t)(x - b0);
+              L.le[r] = (uint32_t)(x + rl - b0);
             } else {
               over = true;
             }
@@ -376,7 +378,7 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
     if (!over) {
       for (uint32_t i0 = 0; i0 < nlist; i0 += 64) {
         const uint32_t i = i0 + lane;
-        uint64_t x = (i < nlist && L.lx[i] < target && L.le[i] == target) ? L.lx[i] : kNone;
+        uint64_t x = (i < nlist && b0 + L.lx[i] < target && b0 + L.le[i] == target) ? b0 + L.lx[i] : kNone;
         for (int s = 32; s; s >>= 1) {
           const uint64_t y = __shfl_xor(x, s, 64);
           x = y < x ? y : x;
@@ -653,7 +655,9 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
 // Each walk run's speculative first start (walk_search), ahead of the chase: a run whose first chunk
 // starts a file needs none, and only the first segment of a run can. Kept out of k_walk_runs: the
 // search's registers would lower how many chasing waves fit on a CU.
-__global__ __launch_bounds__(64) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
+// (At most 168 VGPRs, so that 3 searching waves fit a SIMD instead of 2 at the 193 the compiler
+// takes unbounded — 12 bytes per lane of spill: search 0.54-0.59 -> 0.47-0.48 ms on configs[2].)
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
   __shared__ SearchLdsSw L;
   uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   (void)wst;
