@@ -656,7 +656,8 @@ __global__ __launch_bounds__(64) void k_walk_runs(ScanArgs a, const FileDesc* __
 // starts a file needs none, and only the first segment of a run can. Kept out of k_walk_runs: the
 // search's registers would lower how many chasing waves fit on a CU.
 // (At most 168 VGPRs, so that 3 searching waves fit a SIMD instead of 2 at the 193 the compiler
-// takes unbounded — 12 bytes per lane of spill: search 0.54-0.59 -> 0.47-0.48 ms on configs[2].)
+// takes unbounded — 12 bytes per lane of spill: search 0.54-0.59 -> 0.47-0.48 ms on configs[2];
+// at 128 VGPRs, 4 per SIMD, the spills cost more than the waves bring: 0.56-0.58 ms.)
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_walk_search(ScanArgs a, const FileDesc* __restrict__ files) {
   __shared__ SearchLdsSw L;
   uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
