@@ -56,7 +56,9 @@ void cask_ctx_destroy(cask_ctx* ctx);
 /* Use a caller stream (hipStream_t passed as void*) instead of the context's own; NULL resets.
  * The context's own stream is non-blocking: it does not wait for work queued on other streams,
  * so device inputs still being produced elsewhere must be complete (or produced on the stream
- * set here) before a call reads them. */
+ * set here) before a call reads them. (A walk-mode scan also runs one kernel on a second stream
+ * the context owns, ordered after the work queued on this stream and joined back into it before
+ * the call returns: work queued on this stream afterwards sees the call complete.) */
 int cask_ctx_set_stream(cask_ctx* ctx, void* hip_stream);
 void* cask_ctx_stream(cask_ctx* ctx);
 /* Make the context's stream wait, on the device and without blocking the host, for the work queued
