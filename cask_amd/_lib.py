@@ -153,6 +153,14 @@ SIGNATURES = [
                                           c_u64p, c_u64p]),
     ("cask_hints_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                     C.c_void_p, C.c_uint64, c_u64p]),
+    ("cask_keydir_exchange_rccl", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                            c_u64p, c_u64p]),
+    ("cask_keydir_owner", C.c_uint32, [C.c_void_p, C.c_uint64, C.c_uint32]),
+    ("cask_keydir_partition", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p),
+                                        c_u64p]),
+    ("cask_keydir_partition_host", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64, c_u64p]),
+    ("cask_keydir_terms", C.c_int64, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_keydir_finish_terms", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     ("cask_keydir_new", C.c_void_p, []),
     ("cask_keydir_merge", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     ("cask_keydir_finish", C.c_int, [C.c_void_p]),

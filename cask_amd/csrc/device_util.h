@@ -317,6 +317,40 @@ __device__ __forceinline__ uint32_t gbl_xxh32(const uint8_t* p, uint64_t len) {
 
 // 4x4 transpose across a quad: lane q enters with stripe q of a 4-stripe block (words 0..3) and
 // leaves with word q of stripes 0..3, in order (two butterfly stages of quad DPP moves).
+#ifdef CASK_TRANSPOSE_DPP  // (A/B variant) each stage as four v_cndmask_b32_dpp: word = lane's bit
+                           // set ? own word : the partner's (the DPP operand), 8 VALU instead of 16
+__device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
+  (void)q;
+  uint32_t x1, y1, z1, w1, x2, y2, z2, w2;
+  // stage 1, partner q ^ 2 (vcc: lanes with q & 2): off-diagonal 2x2 blocks swapped
+  asm volatile(
+      "s_nop 1\n"
+      "s_mov_b32 vcc_lo, 0xcccccccc\n"
+      "s_mov_b32 vcc_hi, 0xcccccccc\n"
+      "v_cndmask_b32_dpp %2, %4, %6, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_cndmask_b32_dpp %3, %5, %7, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "s_not_b64 vcc, vcc\n"
+      "v_cndmask_b32_dpp %0, %6, %4, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      "v_cndmask_b32_dpp %1, %7, %5, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
+      : "=&v"(x1), "=&v"(y1), "=&v"(z1), "=&v"(w1)
+      : "v"(v.x), "v"(v.y), "v"(v.z), "v"(v.w)
+      : "vcc");
+  // stage 2, partner q ^ 1 (vcc: lanes with q & 1): the 2x2 blocks transposed
+  asm volatile(
+      "s_nop 1\n"
+      "s_mov_b32 vcc_lo, 0xaaaaaaaa\n"
+      "s_mov_b32 vcc_hi, 0xaaaaaaaa\n"
+      "v_cndmask_b32_dpp %1, %4, %5, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_cndmask_b32_dpp %3, %6, %7, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "s_not_b64 vcc, vcc\n"
+      "v_cndmask_b32_dpp %0, %5, %4, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      "v_cndmask_b32_dpp %2, %7, %6, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
+      : "=&v"(x2), "=&v"(y2), "=&v"(z2), "=&v"(w2)
+      : "v"(x1), "v"(y1), "v"(z1), "v"(w1)
+      : "vcc");
+  v = u32x4{x2, y2, z2, w2};
+}
+#else
 __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
   const bool b1 = q & 2, b0 = q & 1;
   uint32_t r0 = quad_xor2(b1 ? v.x : v.z), r1 = quad_xor2(b1 ? v.y : v.w);  // swap off-diagonal 2x2 blocks
@@ -325,6 +359,7 @@ __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
   r1 = quad_xor1(b0 ? v.z : v.w);
   if (b0) { v.x = r0; v.z = r1; } else { v.y = r0; v.w = r1; }
 }
+#endif
 
 // XXH32 (seed 0) of global bytes [p, p+len) by a quad of lanes (q = lane & 3), lane q keeping stripe
 // accumulator v_{q+1}. Lane q loads stripe q of each 64-B block (one 16-B load: the quad reads 64

@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <map>
 #include <mutex>
 #include <new>
 #include <regex>
@@ -354,7 +355,12 @@ bool read_file(const std::string& p, std::vector<uint8_t>& out) {
     close(fd);
     return false;
   }
-  out.resize((size_t)st.st_size);
+  try {  // (std::bad_alloc for a file larger than the memory left: the fd is not leaked on the way out)
+    out.resize((size_t)st.st_size);
+  } catch (...) {
+    close(fd);
+    throw;
+  }
   size_t got = 0;
   while (got < out.size()) {
     ssize_t r = read(fd, out.data() + got, out.size() - got);
@@ -852,6 +858,35 @@ static void set_err(cask_open_error* err, int status, uint32_t fid = 0, uint64_t
   err->found = f;
 }
 
+// No C++ exception crosses the C ABI (cask_scan.h): the entry points that allocate or start threads
+// run their bodies under these guards — std::bad_alloc (host memory pressure: a huge hint file, a
+// keydir at cfg5 scale) is CASK_E_NOMEM, anything else (std::system_error from a thread or a mutex)
+// CASK_E_IO. parallel_for (host_ring.h) carries a worker's exception back to its caller, and the open
+// pipeline's threads turn theirs into a batch status, so every exception ends up here.
+extern "C++" {  // (templates; this part of the file is inside the extern "C" block)
+template <class F>
+static auto abi_status(F&& f) noexcept -> decltype(f()) {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    return CASK_E_NOMEM;
+  } catch (...) {
+    return CASK_E_IO;
+  }
+}
+template <class F>
+static cask_db* abi_db(cask_open_error* err, F&& f) noexcept {
+  try {
+    return f();
+  } catch (const std::bad_alloc&) {
+    set_err(err, CASK_E_NOMEM);
+  } catch (...) {
+    set_err(err, CASK_E_IO);
+  }
+  return nullptr;
+}
+}  // extern "C++"
+
 // Log::open (log.rs:36-85): path checks, the lock file, the data files in id order. Returns the
 // handle (no keydir yet) or NULL with *err set.
 static cask_db* open_log(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
@@ -907,9 +942,15 @@ static cask_db* open_log(const char* path_c, const cask_options* opts_in, cask_o
   return db;
 }
 
+static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, cask_open_error* err);
 cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
+  return abi_db(err, [&] { return db_open_impl(path_c, opts_in, err); });
+}
+
+static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, cask_open_error* err) {
   auto t0 = std::chrono::steady_clock::now();
-  cask_db* db = open_log(path_c, opts_in, err);
+  std::unique_ptr<cask_db> own(open_log(path_c, opts_in, err));  // (deleted on every failure: the lock goes)
+  cask_db* db = own.get();
   if (!db) return nullptr;
   const cask_options opts = db->opts;
   const std::string path = db->path;
@@ -994,7 +1035,6 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   if (!views.empty()) {
     ed = engine_dev(opts.device);
     if (!ed) {
-      delete db;
       set_err(err, CASK_E_DEVICE);
       return nullptr;
     }
@@ -1014,21 +1054,26 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     }
     bcv.notify_all();
   };
+  // (the two pipeline threads catch their own exceptions: a batch that throws gets a status, and
+  // every batch is still marked, so nobody waits forever and the threads can be joined)
   auto reader = [&]() {
     const auto tr = std::chrono::steady_clock::now();
     for (size_t b = 0; b < nbat; ++b) {
       int st = dst;
       if (st == CASK_OK && !stop.load() && vcut[b + 1] > vcut[b]) {
-        std::vector<std::string> paths;
-        std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
-        for (size_t v = vcut[b]; v < vcut[b + 1]; ++v) paths.push_back(data_path(path, db->files[view_file[v]]));
-        std::vector<char> ok(vb.size(), 1);
-        st = ed->read_to_device(paths, vb, ok);
-        for (size_t k = 0; k < vb.size(); ++k)
-          if (!ok[k]) {  // the file could not be read whole: Log::entries' Io error when its turn comes
-            data_ok[view_file[vcut[b] + k]] = 0;
-            views[vcut[b] + k].len = 0;
-          }
+        st = abi_status([&] {
+          std::vector<std::string> paths;
+          std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
+          for (size_t v = vcut[b]; v < vcut[b + 1]; ++v) paths.push_back(data_path(path, db->files[view_file[v]]));
+          std::vector<char> ok(vb.size(), 1);
+          const int rs = ed->read_to_device(paths, vb, ok);
+          for (size_t k = 0; k < vb.size(); ++k)
+            if (!ok[k]) {  // the file could not be read whole: Log::entries' Io error when its turn comes
+              data_ok[view_file[vcut[b] + k]] = 0;
+              views[vcut[b] + k].len = 0;
+            }
+          return rs;
+        });
       }
       mark(b, st, false);
     }
@@ -1043,10 +1088,13 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
       const auto td = std::chrono::steady_clock::now();
       int st = bat[b].st;
       if (st == CASK_OK && !stop.load() && vcut[b + 1] > vcut[b]) {
-        std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
-        std::vector<uint64_t> ro(vb.size() + 1);
-        st = ed->scan(vb, ro, bat[b].se);
-        if (st == CASK_OK) st = ed->hints(vb, ro, bat[b].hb, bat[b].fo);
+        st = abi_status([&] {
+          std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
+          std::vector<uint64_t> ro(vb.size() + 1);
+          int ds = ed->scan(vb, ro, bat[b].se);
+          if (ds == CASK_OK) ds = ed->hints(vb, ro, bat[b].hb, bat[b].fo);
+          return ds;
+        });
       }
       t_dev += ms_since(td);
       mark(b, st, true);
@@ -1080,6 +1128,12 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
     if (th_read.joinable()) th_read.join();
     if (th_dev.joinable()) th_dev.join();
   };
+  // an exception in the replay below (std::bad_alloc in the fold) unwinds through here: the pipeline
+  // threads are stopped and joined before anything they use goes away
+  struct JoinOnExit {
+    decltype(join_all)& f;
+    ~JoinOnExit() { f(); }
+  } join_on_exit{join_all};
   db->timings[0] = ms_since(t0);  // (until the replay starts; the reads' own span is added below)
 
   // Replay in ascending file order (cask.rs:348-369), batch after batch; the first Err aborts open().
@@ -1227,11 +1281,10 @@ cask_db* cask_db_open(const char* path_c, const cask_options* opts_in, cask_open
   db->timings[3] = t_fold;
   db->timings[4] = ms_since(t0);
   if (fail != CASK_OK) {
-    delete db;
     set_err(err, fail, fail_fid, fail_pos, fail_e, fail_f);
     return nullptr;
   }
-  return db;
+  return own.release();
 }
 
 void cask_compact_options_default(cask_compact_options* o) {  // cask.rs:229-234
@@ -1248,8 +1301,17 @@ void cask_compact_options_default(cask_compact_options* o) {  // cask.rs:229-234
 // of their files (Log::read_entry -> Entry::from_read, log.rs:150-166) and their bytes are copied
 // into the new data files by the device gather. LogWriter rollover (log.rs:282-306) and the
 // EntryWriter/HintWriter output (log.rs:317-395) are restated on the host.
+static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
+                              cask_open_error* err);
 int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
                           cask_open_error* err) {
+  const int st = abi_status([&] { return compact_files_impl(db, files_in, nfiles, res, err); });
+  if (st != CASK_OK && err && err->status == CASK_OK) set_err(err, st);  // (an exception's status)
+  return st;
+}
+
+static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
+                              cask_open_error* err) {
   set_err(err, CASK_OK);
   if (!db || (nfiles && !files_in)) return CASK_E_INVALID_ARG;
   cask_compact_result R{};
@@ -1472,16 +1534,30 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
     cur += size;
     return outs.size() - 1;
   };
-  auto abort_with = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
+  auto remove_outs = [&]() {
     for (OutFile& o : outs) {  // every file this call created, with any hint file already written
       if (o.fd >= 0) close(o.fd);
+      o.fd = -1;
       (void)unlink(data_path(path, o.fid).c_str());
       (void)unlink(hint_path(path, o.fid).c_str());
     }
     db->file_seq -= (uint32_t)outs.size();
+    outs.clear();
+  };
+  auto abort_with = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
+    remove_outs();
     set_err(err, st, fid, pos, e, f);
     return st;
   };
+  // an exception before the new files are complete (std::bad_alloc while gathering or placing)
+  // removes them too, on its way to cask_db_compact_files' handler
+  struct RemoveOnThrow {
+    decltype(remove_outs)& f;
+    bool armed = true;
+    ~RemoveOnThrow() {
+      if (armed && std::uncaught_exceptions()) f();
+    }
+  } remove_on_throw{remove_outs};
   // one record's bytes into its file, and its hint (Hint::new(entry, entry_pos), data.rs:218-226)
   auto append = [&](size_t oi, const uint8_t* rec, uint64_t n) -> bool {
     OutFile& o = outs[oi];
@@ -1673,6 +1749,7 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
 
   // 6. compact_files (cask.rs:528-550): index the new files from their hints, drop the compacted
   // files' stats, swap the file sets
+  remove_on_throw.armed = false;
   auto t4 = std::chrono::steady_clock::now();
   {
     std::vector<FoldSrc> srcs;
@@ -1729,8 +1806,17 @@ int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles
 
 // Cask::compact (cask.rs:563-642): pick the files by the stats and their sizes; compact them if
 // a trigger fired. Returns the number of files compacted (0: no trigger), or a negative status.
+static int64_t compact_impl(cask_db* db, const cask_compact_options* opts_in, cask_compact_result* res,
+                            cask_open_error* err);
 int64_t cask_db_compact(cask_db* db, const cask_compact_options* opts_in, cask_compact_result* res,
                         cask_open_error* err) {
+  const int64_t st = abi_status([&] { return compact_impl(db, opts_in, res, err); });
+  if (st < 0 && err && err->status == CASK_OK) set_err(err, (int)st);
+  return st;
+}
+
+static int64_t compact_impl(cask_db* db, const cask_compact_options* opts_in, cask_compact_result* res,
+                            cask_open_error* err) {
   set_err(err, CASK_OK);
   if (!db) return CASK_E_INVALID_ARG;
   cask_compact_options o;
@@ -1919,6 +2005,160 @@ int cask_keydir_finish(cask_db* db) {
   return CASK_OK;
 }
 
+// ------------------------------------------------------------------------------------------
+// Key-hash partition of the sharded replay (keydir_format.h, SURVEY.md §8e's huge-keyspace case):
+// every rank splits its block by key owner, owner o folds the parts it receives in rank order (the
+// fold above: each key's records arrive in replay order, all in one part), and the owners' per-file
+// terms summed are the Stats of one fold of every block.
+// ------------------------------------------------------------------------------------------
+uint32_t cask_keydir_owner(const uint8_t* key, uint64_t ksz, uint32_t nparts) {
+  if (nparts < 1 || ksz > 0xFFFFu || (ksz && !key)) return 0;
+  return cask_kd::key_owner(cask_kd::key_hash(key, (uint32_t)ksz), nparts);
+}
+
+static int partition_host_impl(const uint8_t* blk, uint64_t bytes, uint32_t nparts, uint8_t* out, uint64_t cap,
+                               uint64_t* part_off) {
+  using namespace cask_kd;
+  if (!blk || !part_off || nparts < 1 || nparts > kMaxParts || bytes < sizeof(ShardHeader)) return CASK_E_INVALID_ARG;
+  ShardHeader hd;
+  memcpy(&hd, blk, sizeof(hd));
+  if (hd.magic != kMagic || hd.version != kVersion || hd.bytes > bytes ||
+      hd.nrec > (bytes - sizeof(ShardHeader)) / sizeof(ShardRec) ||
+      (uint64_t)hd.nfiles > (bytes - sizeof(ShardHeader)) / sizeof(ShardFileStat))
+    return CASK_E_INVALID_ARG;
+  const uint64_t n = hd.nrec, fst_at = sizeof(ShardHeader) + sizeof(ShardRec) * n,
+                 key_at = fst_at + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
+  if (key_at + hd.key_bytes > hd.bytes) return CASK_E_INVALID_ARG;
+  const ShardRec* rec = (const ShardRec*)(blk + sizeof(ShardHeader));
+  const uint8_t* keys = blk + key_at;
+  std::vector<uint64_t> ko(n + 1, 0);
+  for (uint64_t i = 0; i < n; ++i) ko[i + 1] = ko[i] + rec[i].ksz;
+  if (ko[n] != hd.key_bytes) return CASK_E_INVALID_ARG;
+  std::vector<uint32_t> own(n);
+  std::vector<uint64_t> cnt(nparts, 0), kb(nparts, 0);
+  for (uint64_t i = 0; i < n; ++i) {
+    own[i] = key_owner(key_hash(keys + ko[i], rec[i].ksz), nparts);
+    ++cnt[own[i]];
+    kb[own[i]] += rec[i].ksz;
+  }
+  part_off[0] = 0;
+  for (uint32_t o = 0; o < nparts; ++o) part_off[o + 1] = part_off[o] + part_bytes(cnt[o], kb[o], hd.nfiles);
+  if (!out || cap < part_off[nparts]) return CASK_E_CAPACITY;
+  memset(out, 0, part_off[nparts]);
+  std::vector<uint64_t> r(nparts, 0), k(nparts, 0);
+  const ShardFileStat* fst = (const ShardFileStat*)(blk + fst_at);
+  for (uint32_t o = 0; o < nparts; ++o) {
+    uint8_t* base = out + part_off[o];
+    ShardHeader h{};
+    h.magic = kMagic;
+    h.version = kVersion;
+    h.nrec = cnt[o];
+    h.key_bytes = kb[o];
+    h.nfiles = hd.nfiles;
+    h.max_seq_p1 = hd.max_seq_p1;
+    h.rows_in = o == 0 ? hd.rows_in : 0;
+    h.bytes = part_off[o + 1] - part_off[o];
+    memcpy(base, &h, sizeof(h));
+    ShardFileStat* fo = (ShardFileStat*)(base + sizeof(ShardHeader) + sizeof(ShardRec) * cnt[o]);
+    for (uint32_t f = 0; f < hd.nfiles; ++f) {
+      ShardFileStat st = fst[f];
+      if (o) st.puts = st.put_bytes = st.stale = st.stale_bytes = 0;
+      st.pad = 0;
+      memcpy(fo + f, &st, sizeof(st));
+    }
+  }
+  for (uint64_t i = 0; i < n; ++i) {  // records and keys in block order within each part
+    const uint32_t o = own[i];
+    uint8_t* base = out + part_off[o];
+    memcpy(base + sizeof(ShardHeader) + sizeof(ShardRec) * r[o]++, rec + i, sizeof(ShardRec));
+    const uint64_t ka = sizeof(ShardHeader) + sizeof(ShardRec) * cnt[o] + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
+    memcpy(base + ka + k[o], keys + ko[i], rec[i].ksz);
+    k[o] += rec[i].ksz;
+  }
+  return CASK_OK;
+}
+
+int cask_keydir_partition_host(const uint8_t* block, uint64_t bytes, uint32_t nparts, uint8_t* out, uint64_t cap,
+                               uint64_t* part_off) {
+  return abi_status([&] { return partition_host_impl(block, bytes, nparts, out, cap, part_off); });
+}
+
+// This owner's terms: per file the part-0 sums and stale tombstones folded here, and its live keys.
+static int64_t keydir_terms_impl(const cask_db* db, uint8_t* out, uint64_t cap) {
+  using namespace cask_kd;
+  if (!db || !db->merging) return CASK_E_INVALID_ARG;
+  std::map<uint32_t, KeydirTerm> t;
+  for (const auto& kv : db->terms) {
+    KeydirTerm& x = t[kv.first];
+    x.file_id = kv.first;
+    x.puts += kv.second.puts;
+    x.put_bytes += kv.second.put_bytes;
+    x.stale += kv.second.stale;
+    x.stale_bytes += kv.second.stale_bytes;
+  }
+  for (uint32_t f : db->files) t[f].file_id = f;  // (files with no terms still travel)
+  db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& sl) {
+    KeydirTerm& x = t[sl.e.file_id];
+    x.file_id = sl.e.file_id;
+    x.live += 1;
+    x.live_bytes += sl.e.entry_size;
+  });
+  const uint64_t need = sizeof(KeydirTerm) * t.size();
+  if (out && cap >= need) {
+    uint64_t o = 0;
+    for (const auto& kv : t) {
+      memcpy(out + o, &kv.second, sizeof(KeydirTerm));
+      o += sizeof(KeydirTerm);
+    }
+  }
+  return (int64_t)need;
+}
+
+int64_t cask_keydir_terms(const cask_db* db, uint8_t* out, uint64_t cap) {
+  return abi_status([&] { return keydir_terms_impl(db, out, cap); });
+}
+
+// Stats from every owner's terms (this one's included), as cask_keydir_finish computes them from one
+// whole fold: entries = puts + stale, dead = puts - live + stale, dead_bytes likewise.
+static int keydir_finish_terms_impl(cask_db* db, const uint8_t* terms, uint64_t bytes) {
+  using namespace cask_kd;
+  if (!db || !db->merging || (bytes && !terms) || bytes % sizeof(KeydirTerm)) return CASK_E_INVALID_ARG;
+  std::map<uint32_t, KeydirTerm> sum;
+  for (uint64_t o = 0; o < bytes; o += sizeof(KeydirTerm)) {
+    KeydirTerm t;
+    memcpy(&t, terms + o, sizeof(t));
+    KeydirTerm& x = sum[t.file_id];
+    x.file_id = t.file_id;
+    x.puts += t.puts;
+    x.put_bytes += t.put_bytes;
+    x.stale += t.stale;
+    x.stale_bytes += t.stale_bytes;
+    x.live += t.live;
+    x.live_bytes += t.live_bytes;
+  }
+  for (const auto& kv : sum)
+    if (kv.second.live > kv.second.puts || kv.second.live_bytes > kv.second.put_bytes) return CASK_E_INVALID_ARG;
+  db->index.stats.clear();
+  for (const auto& kv : sum) {
+    const KeydirTerm& t = kv.second;
+    db->files.push_back(kv.first);
+    if (!t.puts && !t.stale) continue;  // no Stats::add_entry for this file
+    StatsEntry& e = db->index.stats[kv.first];
+    e.entries = t.puts + t.stale;
+    e.dead_entries = t.puts - t.live + t.stale;
+    e.dead_bytes = t.put_bytes - t.live_bytes + t.stale_bytes;
+  }
+  std::sort(db->files.begin(), db->files.end());
+  db->files.erase(std::unique(db->files.begin(), db->files.end()), db->files.end());
+  db->file_seq = db->files.empty() ? 0u : db->files.back();
+  db->merging = false;
+  return CASK_OK;
+}
+
+int cask_keydir_finish_terms(cask_db* db, const uint8_t* terms, uint64_t bytes) {
+  return abi_status([&] { return keydir_finish_terms_impl(db, terms, bytes); });
+}
+
 // Cask::open over several GPUs of this process: contiguous file-id ranges, one per devices[] entry;
 // each range is reduced to keydir blocks on its device (one host thread per distinct device, its
 // ranges one after another), and the blocks are folded here in range order. Within a range, files
@@ -1926,15 +2166,30 @@ int cask_keydir_finish(cask_db* db) {
 // (cask_parse_hints_device) and reduced (cask_shard_keydir_hints); the others are scanned
 // (cask_scan_device, cask_shard_keydir) and, with write_hints, get their hint files from the device
 // (cask_hints_device). Each maximal stretch of files of one kind gives one block.
+// The ranges run in parallel, but the reference's replay stops at the first Err (cask.rs:357-368)
+// and never reaches a later file: so every hint file is first written under a temporary name
+// (`.part`), and only once all ranges are done are the ones up to the first failure (in replay order)
+// renamed into place — the failing range's own, which end at its failing file, included — and the
+// later ranges' removed.
+static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in, const int* devices, int ndev,
+                                cask_open_error* err);
 cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, const int* devices, int ndev,
                             cask_open_error* err) {
+  return abi_db(err, [&] { return open_multi_impl(path_c, opts_in, devices, ndev, err); });
+}
+
+static std::string part_path(const std::string& hp) { return hp + ".part"; }
+
+static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in, const int* devices, int ndev,
+                                cask_open_error* err) {
   set_err(err, CASK_OK);
   if (!devices || ndev < 1) {
     set_err(err, CASK_E_INVALID_ARG);
     return nullptr;
   }
   auto t0 = std::chrono::steady_clock::now();
-  cask_db* db = open_log(path_c, opts_in, err);
+  std::unique_ptr<cask_db> own(open_log(path_c, opts_in, err));
+  cask_db* db = own.get();
   if (!db) return nullptr;
   const std::string path = db->path;
   const size_t nf = db->files.size();
@@ -1957,6 +2212,7 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
   struct Shard {
     size_t lo = 0, hi = 0;
     std::vector<std::vector<uint8_t>> blocks;
+    std::vector<uint32_t> parts;  // hint files written under their temporary names, in order
     cask_open_error e{};
     double ms_read = 0, ms_scan = 0;
   };
@@ -2038,7 +2294,8 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
       if (st != CASK_OK) return fail(st);
       // files up to the first failing one (that one included: the drain on drop, log.rs:466-470)
       for (size_t i = 0; i < n; ++i) {
-        if (!write_file_raw2(hint_path(path, db->files[lo + i]), hb.data() + fo[i], fo[i + 1] - fo[i],
+        s.parts.push_back(db->files[lo + i]);
+        if (!write_file_raw2(part_path(hint_path(path, db->files[lo + i])), hb.data() + fo[i], fo[i + 1] - fo[i],
                              cask_xxh::xxh32(hb.data() + fo[i], fo[i + 1] - fo[i], 0)))
           return fail(CASK_E_IO, db->files[lo + i]);
         if (se.kind && se.file_id == db->files[lo + i]) break;
@@ -2070,7 +2327,12 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
     for (size_t i = s.lo; i < s.hi;) {  // maximal stretches of one kind, in order
       size_t j = i + 1;
       while (j < s.hi && use_hint[j] == use_hint[i]) ++j;
-      if (!run_stretch(s, devices[r], ctx, i, j, use_hint[i] != 0)) break;
+      // (an exception in a stretch is its failure, so the context is still destroyed below)
+      const int st = abi_status([&] { return run_stretch(s, devices[r], ctx, i, j, use_hint[i] != 0) ? CASK_OK : 1; });
+      if (st != CASK_OK) {
+        if (st != 1) s.e = cask_open_error{st, 0, 0, 0, 0};
+        break;
+      }
       i = j;
     }
     cask_ctx_destroy(ctx);
@@ -2083,12 +2345,33 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
     for (int r = 0; r < ndev; ++r)
       if (devices[r] == devs[t]) run_shard(r);
   });
-  for (int r = 0; r < ndev; ++r)  // the first failure in replay order
-    if (sh[r].e.status != CASK_OK) {
-      if (err) *err = sh[r].e;
-      delete db;
-      return nullptr;
+  int rf = ndev;  // the first range that failed, in replay order
+  for (int r = 0; r < ndev && rf == ndev; ++r)
+    if (sh[r].e.status != CASK_OK) rf = r;
+  // hint files: into place up to the first failure, removed after it
+  uint32_t ren_fail = 0;
+  bool ren_ok = true;
+  for (int r = 0; r < ndev; ++r)
+    for (uint32_t fid : sh[r].parts) {
+      const std::string hp = hint_path(path, fid);
+      if (r <= rf) {
+        if (ren_ok && rename(part_path(hp).c_str(), hp.c_str()) != 0) {
+          ren_ok = false;
+          ren_fail = fid;
+        }
+        if (!ren_ok) (void)unlink(part_path(hp).c_str());
+      } else {
+        (void)unlink(part_path(hp).c_str());
+      }
     }
+  if (rf < ndev) {
+    if (err) *err = sh[rf].e;
+    return nullptr;
+  }
+  if (!ren_ok) {
+    set_err(err, CASK_E_IO, ren_fail);
+    return nullptr;
+  }
   double rd = 0, sc = 0;
   for (const Shard& s : sh) {
     rd = std::max(rd, s.ms_read);
@@ -2102,7 +2385,6 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
       const int st = cask_keydir_merge(db, b.data(), b.size());
       if (st != CASK_OK) {
         set_err(err, st);
-        delete db;
         return nullptr;
       }
     }
@@ -2112,7 +2394,7 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
   db->timings[2] = 0;
   db->timings[3] = ms_since(tf);
   db->timings[4] = ms_since(t0);
-  return db;
+  return own.release();
 }
 
 // LogWriter::write (log.rs:282-306) for a batch of entries written through one writer that is then
@@ -2121,10 +2403,24 @@ cask_db* cask_db_open_multi(const char* path_c, const cask_options* opts_in, con
 // data.rs:242-256) and its trailer on Drop (log.rs:367-395) are built per file on host threads.
 // Rollover: a new file when there is no writer or pos + size > max_file_size (a record larger than
 // the limit gets a file of its own). File ids are first_file_id, first_file_id + 1, ...
+static int64_t log_write_impl(const char* dir_c, uint32_t first_file_id, uint64_t max_file_size, int write_hints,
+                              int device, uint64_t n, const uint64_t* seq, const uint16_t* ksz, const uint32_t* vsz_raw,
+                              const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
+                              uint32_t* file_ids, uint64_t cap);
 int64_t cask_log_write(const char* dir_c, uint32_t first_file_id, uint64_t max_file_size, int write_hints, int device,
                        uint64_t n, const uint64_t* seq, const uint16_t* ksz, const uint32_t* vsz_raw,
                        const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
                        uint32_t* file_ids, uint64_t cap) {
+  return abi_status([&]() -> int64_t {
+    return log_write_impl(dir_c, first_file_id, max_file_size, write_hints, device, n, seq, ksz, vsz_raw, keys,
+                          key_off, vals, val_off, file_ids, cap);
+  });
+}
+
+static int64_t log_write_impl(const char* dir_c, uint32_t first_file_id, uint64_t max_file_size, int write_hints,
+                              int device, uint64_t n, const uint64_t* seq, const uint16_t* ksz, const uint32_t* vsz_raw,
+                              const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
+                              uint32_t* file_ids, uint64_t cap) {
   if (!dir_c || (n && (!seq || !ksz || !vsz_raw || !key_off || !val_off))) return CASK_E_INVALID_ARG;
   const std::string dir = dir_c;
   if (!n) return 0;  // the writer is created by the first write (log.rs:282-290)

@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <thread>
 #include <vector>
 
@@ -33,22 +34,40 @@ inline unsigned host_threads() {
 }
 
 // fn(t) for t in [0, nt): t = 1.. on threads of their own, t = 0 on the caller. A thread that cannot
-// be created (std::system_error) has its share run on the calling thread: no exception leaves the
-// C ABI, and the result does not depend on how many threads actually ran.
+// be created (std::system_error) has its share run on the calling thread, so the result does not
+// depend on how many threads actually ran. An exception thrown by any share (std::bad_alloc under
+// memory pressure) is caught on its thread and the first one is rethrown here once every thread
+// has been joined: it reaches the entry point's own handler (engine.cpp: abi_status / abi_db) instead of
+// std::terminate, and no thread is left running over the caller's state.
 template <class F>
 void parallel_for(unsigned nt, F fn) {
+  if (!nt) nt = 1;
+  // (everything that allocates happens before the first thread starts: an exception from here on
+  // would unwind past running threads)
+  std::vector<std::exception_ptr> ex(nt);
+  std::vector<char> spawned(nt, 0);
   std::vector<std::thread> th;
-  std::vector<unsigned> here;
+  th.reserve(nt);
+  auto run = [&](unsigned t) {
+    try {
+      fn(t);
+    } catch (...) {
+      ex[t] = std::current_exception();
+    }
+  };
   for (unsigned t = 1; t < nt; ++t) {
     try {
-      th.emplace_back(fn, t);
+      th.emplace_back(run, t);
+      spawned[t] = 1;
     } catch (...) {
-      here.push_back(t);
     }
   }
-  fn(0u);
-  for (unsigned t : here) fn(t);
+  run(0u);
+  for (unsigned t = 1; t < nt; ++t)
+    if (!spawned[t]) run(t);
   for (auto& x : th) x.join();
+  for (auto& e : ex)
+    if (e) std::rethrow_exception(e);
 }
 
 // Page-locked host memory the device can DMA to and from: an anonymous mapping populated when it is

@@ -58,25 +58,7 @@ struct KdArgs {
   const uint64_t* key_at_row;  // per row: offset of its key in its file's bytes (null: pos + 18)
 };
 
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  return z ^ (z >> 31);
-}
-
-// 64-bit hash of a key (any bytes, any length up to 65535); only speed depends on its quality.
-__device__ __forceinline__ uint64_t key_hash(const uint8_t* k, uint32_t n) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ ((uint64_t)n * 0xD6E8FEB86659FD93ull);
-  uint32_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t w;
-    __builtin_memcpy(&w, k + i, 8);
-    h = mix64(h ^ w);
-  }
-  uint64_t t = 0;
-  for (uint32_t j = 0; i + j < n; ++j) t |= (uint64_t)k[i + j] << (8 * j);
-  return mix64(h ^ t ^ 0xA0761D6478BD642Full);
-}
+// key_hash: keydir_format.h (shared with the host's partition and owner lookups)
 
 __device__ __forceinline__ uint32_t row_file(const KdArgs& a, uint64_t d) {
   uint32_t lo = 0, hi = a.nfiles;  // last f with row_off[f] <= d
@@ -293,9 +275,21 @@ struct KdScratch {
   size_t cap = 0;
   void* out = nullptr;
   size_t out_cap = 0;
+  void* part = nullptr;  // kd_partition's output (the block it splits may be `out`)
+  size_t part_cap = 0;
   ~KdScratch() {
     if (p) (void)hipFree(p);
     if (out) (void)hipFree(out);
+    if (part) (void)hipFree(part);
+  }
+  bool ensure_part(size_t b) {
+    if (b <= part_cap) return true;
+    if (part) (void)hipFree(part);
+    part = nullptr;
+    part_cap = 0;
+    if (hipMalloc(&part, b + b / 8 + 256) != hipSuccess) return false;
+    part_cap = b + b / 8 + 256;
+    return true;
   }
   bool ensure(size_t b) {
     if (b <= cap) return true;
@@ -421,6 +415,205 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   if (!ok) return -11;
   *out = S_.out;
   *bytes = total;
+  return 0;
+}
+
+// ------------------------------------------------------------------------------------------
+// Key-hash partition of a keydir block (keydir_format.h): what each rank sends each owner in the
+// all-to-all of the huge-keyspace replay. Owner per record from its key hash, a
+// stable radix sort of (owner, record) — block order within each part — then the parts written
+// whole: records and keys gathered, headers and stats tables. Byte for byte the host's
+// cask_keydir_partition_host.
+// ------------------------------------------------------------------------------------------
+struct PtArgs {
+  const ShardRec* rec;
+  const uint8_t* keys;
+  const ShardFileStat* fst;
+  uint64_t n;
+  uint32_t nparts, nfiles;
+  uint64_t max_seq_p1, rows_in;
+  uint64_t* kl;       // n + 1: key length (input order), then its exclusive sum ko
+  uint64_t* ko;
+  uint16_t* own;      // owner (input order)
+  uint16_t* own_s;    // sorted
+  uint32_t* idx;
+  uint32_t* idx_s;
+  uint64_t* kl2;      // n + 1: key length in sorted order, then its exclusive sum ko2
+  uint64_t* ko2;
+  uint64_t* start;    // nparts + 1: each part's first sorted position, then ko2 there (pkey)
+  uint64_t* pkey;
+  const uint64_t* poff;  // nparts + 1: each part's offset in out
+  uint8_t* out;
+};
+
+__global__ __launch_bounds__(256) void k_pt_len(PtArgs a) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i <= a.n; i += (uint64_t)gridDim.x * 256ull)
+    a.kl[i] = i < a.n ? a.rec[i].ksz : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_pt_own(PtArgs a) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256ull) {
+    a.own[i] = (uint16_t)key_owner(key_hash(a.keys + a.ko[i], a.rec[i].ksz), a.nparts);
+    a.idx[i] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_pt_len2(PtArgs a) {
+  for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j <= a.n; j += (uint64_t)gridDim.x * 256ull)
+    a.kl2[j] = j < a.n ? a.rec[a.idx_s[j]].ksz : 0ull;
+}
+
+__global__ __launch_bounds__(256) void k_pt_bounds(PtArgs a) {
+  for (uint32_t o = blockIdx.x * 256u + threadIdx.x; o <= a.nparts; o += gridDim.x * 256u) {
+    uint64_t lo = 0, hi = a.n;  // the first sorted position with owner >= o
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) >> 1;
+      if (a.own_s[mid] < o) lo = mid + 1; else hi = mid;
+    }
+    a.start[o] = lo;
+    a.pkey[o] = a.ko2[lo];
+  }
+}
+
+__device__ __forceinline__ uint64_t pt_key_at(const PtArgs& a, uint32_t o) {
+  return sizeof(ShardHeader) + sizeof(ShardRec) * (a.start[o + 1] - a.start[o]) + sizeof(ShardFileStat) * (uint64_t)a.nfiles;
+}
+
+__global__ __launch_bounds__(256) void k_pt_write(PtArgs a) {
+  for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < a.n; j += (uint64_t)gridDim.x * 256ull) {
+    const uint32_t o = a.own_s[j];
+    const uint64_t i = a.idx_s[j], r = j - a.start[o];
+    uint8_t* base = a.out + a.poff[o];
+    ((ShardRec*)(base + sizeof(ShardHeader)))[r] = a.rec[i];
+    uint8_t* kd = base + pt_key_at(a, o) + (a.ko2[j] - a.pkey[o]);
+    const uint8_t* ks = a.keys + a.ko[i];
+    for (uint32_t b = 0, k = a.rec[i].ksz; b < k; ++b) kd[b] = ks[b];
+  }
+}
+
+// Headers, stats tables (part 0: the block's; the others: its file ids with zero counts) and the
+// zero padding of each part.
+__global__ __launch_bounds__(256) void k_pt_head(PtArgs a) {
+  const uint64_t tot = (uint64_t)(a.nparts) * (a.nfiles + 1);
+  for (uint64_t x = blockIdx.x * 256ull + threadIdx.x; x < tot; x += (uint64_t)gridDim.x * 256ull) {
+    const uint32_t o = (uint32_t)(x / (a.nfiles + 1)), f = (uint32_t)(x % (a.nfiles + 1));
+    uint8_t* base = a.out + a.poff[o];
+    const uint64_t nr = a.start[o + 1] - a.start[o], kb = a.pkey[o + 1] - a.pkey[o];
+    if (f == a.nfiles) {
+      ShardHeader hd{};
+      hd.magic = kMagic;
+      hd.version = kVersion;
+      hd.nrec = nr;
+      hd.key_bytes = kb;
+      hd.nfiles = a.nfiles;
+      hd.max_seq_p1 = a.max_seq_p1;
+      hd.rows_in = o == 0 ? a.rows_in : 0ull;
+      hd.bytes = a.poff[o + 1] - a.poff[o];
+      *(ShardHeader*)base = hd;
+      for (uint64_t e = pt_key_at(a, o) + kb; e < hd.bytes; ++e) base[e] = 0;
+      continue;
+    }
+    ShardFileStat st = a.fst[f];
+    if (o) st.puts = st.put_bytes = st.stale = st.stale_bytes = 0;
+    st.pad = 0;
+    ((ShardFileStat*)(base + sizeof(ShardHeader) + sizeof(ShardRec) * nr))[f] = st;
+  }
+}
+
+// Returns 0 or a negative cask_status; *out: the parts (device memory owned by the scratch, valid
+// until its next partition), part_off (host, nparts + 1): part o is out[part_off[o], part_off[o + 1]).
+int kd_partition(void* scratch, const void* block, uint64_t bytes, uint32_t nparts, void* stream, void** out,
+                 uint64_t* part_off) {
+  KdScratch& S_ = *(KdScratch*)scratch;
+  hipStream_t st = S(stream);
+  if (!block || nparts < 1 || nparts > kMaxParts || bytes < sizeof(ShardHeader)) return -10;
+  ShardHeader hd;
+  if (hipMemcpyAsync(&hd, block, sizeof(hd), hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
+    return -11;
+  // the same checks as the fold (cask_keydir_merge): counts bounded by the block's size first
+  if (hd.magic != kMagic || hd.version != kVersion || hd.bytes > bytes ||
+      hd.nrec > (bytes - sizeof(ShardHeader)) / sizeof(ShardRec) ||
+      (uint64_t)hd.nfiles > (bytes - sizeof(ShardHeader)) / sizeof(ShardFileStat))
+    return -10;
+  const uint64_t n = hd.nrec, fst_at = sizeof(ShardHeader) + sizeof(ShardRec) * n,
+                 key_at = fst_at + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
+  if (key_at + hd.key_bytes > hd.bytes) return -10;
+  if (n > (uint64_t)INT32_MAX) return -12;  // (hipCUB's int counts)
+  int bits = 1;
+  while ((1u << bits) < nparts) ++bits;
+  size_t t_sort = 0, t_scan = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, (uint16_t*)nullptr, (uint16_t*)nullptr, (uint32_t*)nullptr,
+                                          (uint32_t*)nullptr, (int)std::max<uint64_t>(n, 1), 0, bits, st) != hipSuccess ||
+      hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, (uint64_t*)nullptr, (uint64_t*)nullptr, (int)(n + 1), st) != hipSuccess)
+    return -11;
+  uint64_t o = 0;
+  auto take = [&](uint64_t b) { const uint64_t r = o; o = al(o + b); return r; };
+  const uint64_t n1 = n + 1;
+  const uint64_t o_kl = take(8 * n1), o_ko = take(8 * n1), o_own = take(2 * n1), o_owns = take(2 * n1),
+                 o_idx = take(4 * n1), o_idxs = take(4 * n1), o_kl2 = take(8 * n1), o_ko2 = take(8 * n1),
+                 o_start = take(8ull * (nparts + 1)), o_pkey = take(8ull * (nparts + 1)), o_poff = take(8ull * (nparts + 1)),
+                 o_tmp = take(std::max(t_sort, t_scan));
+  if (!S_.ensure(o)) return -13;
+  uint8_t* b = (uint8_t*)S_.p;
+  PtArgs a{};
+  a.rec = (const ShardRec*)((const uint8_t*)block + sizeof(ShardHeader));
+  a.fst = (const ShardFileStat*)((const uint8_t*)block + fst_at);
+  a.keys = (const uint8_t*)block + key_at;
+  a.n = n;
+  a.nparts = nparts;
+  a.nfiles = hd.nfiles;
+  a.max_seq_p1 = hd.max_seq_p1;
+  a.rows_in = hd.rows_in;
+  a.kl = (uint64_t*)(b + o_kl);
+  a.ko = (uint64_t*)(b + o_ko);
+  a.own = (uint16_t*)(b + o_own);
+  a.own_s = (uint16_t*)(b + o_owns);
+  a.idx = (uint32_t*)(b + o_idx);
+  a.idx_s = (uint32_t*)(b + o_idxs);
+  a.kl2 = (uint64_t*)(b + o_kl2);
+  a.ko2 = (uint64_t*)(b + o_ko2);
+  a.start = (uint64_t*)(b + o_start);
+  a.pkey = (uint64_t*)(b + o_pkey);
+  a.poff = (const uint64_t*)(b + o_poff);
+  void* tmpp = b + o_tmp;
+  bool ok = true;
+  auto H = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+  const uint32_t grid = (uint32_t)std::min<uint64_t>((n + 256) / 256, (uint64_t)device_cus() * 16);
+  hipLaunchKernelGGL(k_pt_len, dim3(grid), dim3(256), 0, st, a);
+  size_t tb = std::max(t_sort, t_scan);
+  H(hipcub::DeviceScan::ExclusiveSum(tmpp, tb, a.kl, a.ko, (int)(n + 1), st));
+  uint64_t kt = 0;  // the keys the records claim must be the block's key bytes
+  H(hipMemcpyAsync(&kt, a.ko + n, 8, hipMemcpyDeviceToHost, st));
+  H(hipStreamSynchronize(st));
+  if (!ok) return -11;
+  if (kt != hd.key_bytes) return -10;
+  if (n) {
+    hipLaunchKernelGGL(k_pt_own, dim3(grid), dim3(256), 0, st, a);
+    tb = std::max(t_sort, t_scan);
+    H(hipcub::DeviceRadixSort::SortPairs(tmpp, tb, a.own, a.own_s, a.idx, a.idx_s, (int)n, 0, bits, st));
+  }
+  hipLaunchKernelGGL(k_pt_len2, dim3(grid), dim3(256), 0, st, a);
+  tb = std::max(t_sort, t_scan);
+  H(hipcub::DeviceScan::ExclusiveSum(tmpp, tb, a.kl2, a.ko2, (int)(n + 1), st));
+  hipLaunchKernelGGL(k_pt_bounds, dim3((nparts + 256) / 256), dim3(256), 0, st, a);
+  std::vector<uint64_t> hs(2ull * (nparts + 1));
+  H(hipMemcpyAsync(hs.data(), a.start, 8ull * (nparts + 1), hipMemcpyDeviceToHost, st));
+  H(hipMemcpyAsync(hs.data() + nparts + 1, a.pkey, 8ull * (nparts + 1), hipMemcpyDeviceToHost, st));
+  H(hipStreamSynchronize(st));
+  if (!ok) return -11;
+  part_off[0] = 0;
+  for (uint32_t p = 0; p < nparts; ++p)
+    part_off[p + 1] = part_off[p] + part_bytes(hs[p + 1] - hs[p], hs[nparts + 1 + p + 1] - hs[nparts + 1 + p], hd.nfiles);
+  if (!S_.ensure_part(part_off[nparts])) return -13;
+  a.out = (uint8_t*)S_.part;
+  H(hipMemcpyAsync((void*)a.poff, part_off, 8ull * (nparts + 1), hipMemcpyHostToDevice, st));
+  if (n) hipLaunchKernelGGL(k_pt_write, dim3(grid), dim3(256), 0, st, a);
+  const uint64_t th = (uint64_t)nparts * (hd.nfiles + 1);
+  hipLaunchKernelGGL(k_pt_head, dim3((uint32_t)std::min<uint64_t>((th + 255) / 256, 4096)), dim3(256), 0, st, a);
+  H(hipStreamSynchronize(st));
+  H(hipGetLastError());
+  if (!ok) return -11;
+  *out = S_.part;
   return 0;
 }
 

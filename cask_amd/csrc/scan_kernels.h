@@ -238,6 +238,8 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
              const uint64_t* row_off_host, const uint64_t* pos, const uint64_t* seq, const uint32_t* vsz,
              const uint16_t* ksz, uint64_t n, void* stream, void** out, uint64_t* bytes,
              const uint64_t* key_at = nullptr);
+int kd_partition(void* scratch, const void* block, uint64_t bytes, uint32_t nparts, void* stream, void** out,
+                 uint64_t* part_off);
 int hint_entries(void* scratch, const FileDesc* files_host, uint32_t nfiles, const uint64_t* row_off_host,
                  uint64_t n, uint64_t* pos, uint64_t* key_at, void* stream);
 int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const uint64_t* row_off_host,

@@ -14,6 +14,7 @@
 
 #include "../../include/cask_scan.h"
 #include "host_ring.h"
+#include "keydir_format.h"
 #include "scan_kernels.h"
 #include "xxh32.h"
 
@@ -1179,6 +1180,23 @@ extern "C" int cask_shard_keydir(cask_ctx* c, const cask_file_view* files, uint3
   }
   *block = out;
   *bytes = nb;
+  return CASK_OK;
+}
+
+extern "C" int cask_keydir_partition(cask_ctx* c, const void* block, uint64_t bytes, uint32_t nparts, const void** parts,
+                                     uint64_t* part_off) {
+  if (!c || !block || !parts || !part_off || nparts < 1 || nparts > cask_kd::kMaxParts) return CASK_E_INVALID_ARG;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (set_dev(c)) return CASK_E_DEVICE;
+  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+  void* out = nullptr;
+  const int rc = kd_partition(c->kd, block, bytes, nparts, c->stream, &out, part_off);
+  if (rc) {
+    snprintf(c->last_error, sizeof(c->last_error), "cask_keydir_partition: %s",
+             rc == CASK_E_NOMEM ? "out of memory" : rc == CASK_E_INVALID_ARG ? "not a keydir block" : "device");
+    return rc;
+  }
+  *parts = out;
   return CASK_OK;
 }
 

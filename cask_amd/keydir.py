@@ -54,9 +54,56 @@ def _shard(ctx, fn, name, files, rows, count, file_row_offset):
     return out
 
 
+def _u8(block):
+    """bytes / numpy uint8 / CPU uint8 tensor -> contiguous numpy uint8."""
+    if hasattr(block, "numpy"):
+        block = block.numpy()
+    return np.ascontiguousarray(np.frombuffer(block, np.uint8) if isinstance(block, (bytes, bytearray)) else block,
+                                dtype=np.uint8)
+
+
+def key_owner(key: bytes, nparts: int) -> int:
+    """cask_keydir_owner: the rank that holds `key` after a partitioned replay."""
+    return int(L.lib().cask_keydir_owner(key, len(key), nparts))
+
+
+def partition_host(block, nparts: int) -> list[np.ndarray]:
+    """cask_keydir_partition_host: the block (host bytes) split by key owner into nparts blocks."""
+    lib = L.lib()
+    a = _u8(block)
+    off = (C.c_uint64 * (nparts + 1))()
+    rc = lib.cask_keydir_partition_host(a.ctypes.data, a.size, nparts, None, 0, off)
+    if rc != L.E_CAPACITY:
+        raise_status(rc, what="cask_keydir_partition_host")
+    out = np.zeros(int(off[nparts]), np.uint8)
+    raise_status(lib.cask_keydir_partition_host(a.ctypes.data, a.size, nparts, out.ctypes.data, out.size, off),
+                 what="cask_keydir_partition_host")
+    return [out[int(off[o]):int(off[o + 1])] for o in range(nparts)]
+
+
+def partition_device(ctx, block, nparts: int):
+    """cask_keydir_partition: a device block (uint8 CUDA tensor) split on its GPU; returns the parts
+    as uint8 CUDA tensors (copies: the context's buffer is reused by its next call)."""
+    import torch
+    off = (C.c_uint64 * (nparts + 1))()
+    parts = C.c_void_p()
+    ctx._inputs_ready()
+    rc = ctx.lib.cask_keydir_partition(ctx._h, C.c_void_p(block.data_ptr()), block.numel(), nparts, C.byref(parts), off)
+    raise_status(rc, what=f"cask_keydir_partition: {ctx.last_error()}")
+    out = torch.empty(int(off[nparts]), dtype=torch.uint8, device=block.device)
+    ctx._inputs_ready()
+    if out.numel():
+        raise_status(ctx.lib.cask_copy(ctx._h, C.c_void_p(out.data_ptr()), parts, out.numel()), what="cask_copy")
+    return [out[int(off[o]):int(off[o + 1])] for o in range(nparts)]
+
+
 class KeydirFold:
     """Rank 0's fold (cask_keydir_new / _merge / _finish): merge the blocks in rank order, then
-    finish() returns a Cask handle with the keydir, stats and sequence of the whole replay."""
+    finish() returns a Cask handle with the keydir, stats and sequence of the whole replay.
+
+    In a partitioned replay each owner merges the parts it was sent (rank order), exchanges terms()
+    with the other owners and calls finish_terms(all owners' terms): its handle then holds its own
+    keys and the whole replay's Stats, files and sequence."""
 
     def __init__(self):
         self.lib = L.lib()
@@ -66,14 +113,30 @@ class KeydirFold:
 
     def merge(self, block):
         """block: bytes, a numpy uint8 array or a CPU uint8 tensor."""
-        if hasattr(block, "numpy"):
-            block = block.numpy()
-        a = np.ascontiguousarray(np.frombuffer(block, np.uint8) if isinstance(block, (bytes, bytearray)) else block,
-                                 dtype=np.uint8)
+        a = _u8(block)
         raise_status(self.lib.cask_keydir_merge(self._h, a.ctypes.data, a.size), what="cask_keydir_merge")
 
     def finish(self) -> Cask:
         raise_status(self.lib.cask_keydir_finish(self._h), what="cask_keydir_finish")
+        h, self._h = self._h, None
+        return Cask(h, "")
+
+    def terms(self) -> np.ndarray:
+        """This owner's per-file terms (KeydirTerm records, 56 B each) after its merges."""
+        n = self.lib.cask_keydir_terms(self._h, None, 0)
+        if n < 0:
+            raise_status(int(n), what="cask_keydir_terms")
+        out = np.zeros(int(n), np.uint8)
+        got = self.lib.cask_keydir_terms(self._h, out.ctypes.data if n else None, out.size)
+        if got != n:
+            raise_status(int(got) if got < 0 else L.E_INVALID_ARG, what="cask_keydir_terms")
+        return out
+
+    def finish_terms(self, all_terms) -> Cask:
+        """Finish with every owner's terms concatenated (this one's included)."""
+        a = _u8(all_terms)
+        raise_status(self.lib.cask_keydir_finish_terms(self._h, a.ctypes.data if a.size else None, a.size),
+                     what="cask_keydir_finish_terms")
         h, self._h = self._h, None
         return Cask(h, "")
 

@@ -372,30 +372,63 @@ cask_db* cask_keydir_new(void);
 int cask_keydir_merge(cask_db* db, const uint8_t* block, uint64_t bytes);
 int cask_keydir_finish(cask_db* db);
 
-/* RCCL over xGMI (no torch needed): a communicator per rank from a unique id that one rank makes
- * and the caller distributes (any side channel: MPI, a file, a TCP socket), then the rooted gather of
- * the ranks' keydir blocks. Every rank calls cask_keydir_gather_rccl with its block (device memory,
- * from cask_shard_keydir); the sizes go round by ncclAllGather, the blocks to `root` by grouped
- * ncclSend/ncclRecv (one message per rank, each over its own xGMI link), the maximum sequence by
- * ncclAllReduce(max) (*max_seq, on every rank, may be NULL). On `root`, `db` (cask_keydir_new) gets
- * the blocks merged in rank order — rank order must be replay order (contiguous file-id ranges) —
- * and the caller then calls cask_keydir_finish. *gathered: the bytes the root received (its own
- * block's size elsewhere). Replaces rank 0's side of the replay loop (cask.rs:346-382) for a sharded
- * open. */
+/* Key-hash partition, for a keyspace too large to gather on one host: a block splits
+ * into nparts blocks of the same format (keydir_format.h), part o holding, in block order, the
+ * records of the keys whose owner is o (cask_keydir_owner) with their keys, and the per-file stats
+ * table (its counts in part 0 only). Owner o merges the parts it is sent in rank order
+ * (cask_keydir_merge into a cask_keydir_new handle), reports its per-file terms
+ * (cask_keydir_terms: 56-B KeydirTerm records), and every owner finishes with the terms of all
+ * owners (cask_keydir_finish_terms): each then holds its own keys and the Stats, file list and
+ * sequence of the whole replay — together exactly what cask_keydir_finish gives after one fold of
+ * every block. */
+uint32_t cask_keydir_owner(const uint8_t* key, uint64_t ksz, uint32_t nparts);
+/* On the device (block in device memory, e.g. from cask_shard_keydir): *parts points to device
+ * memory owned by the context, valid until its next partition; part_off (host, nparts + 1). */
+int cask_keydir_partition(cask_ctx* ctx, const void* block, uint64_t bytes, uint32_t nparts, const void** parts,
+                          uint64_t* part_off);
+/* On the host, byte for byte the same parts: CASK_E_CAPACITY (part_off filled in) when cap <
+ * part_off[nparts]; out may be NULL to ask for the size. */
+int cask_keydir_partition_host(const uint8_t* block, uint64_t bytes, uint32_t nparts, uint8_t* out, uint64_t cap,
+                               uint64_t* part_off);
+/* Bytes of this owner's terms (written to out when cap allows), or a negative status. */
+int64_t cask_keydir_terms(const cask_db* db, uint8_t* out, uint64_t cap);
+int cask_keydir_finish_terms(cask_db* db, const uint8_t* terms, uint64_t bytes);
+
+/* RCCL over xGMI (no torch needed; librccl is loaded on first use, CASK_E_DEVICE without it): a
+ * communicator per rank from a unique id that one rank makes and the caller distributes (any side
+ * channel: MPI, a file, a TCP socket). Every rank of the communicator makes the same calls; a failure
+ * on any rank is agreed on (ncclAllReduce(min) of the ranks' statuses) before data moves, so every
+ * rank returns the same status rather than waiting on a peer that stopped.
+ *  - cask_keydir_gather_rccl: the rooted gather. Every rank passes its block (device memory, from
+ *    cask_shard_keydir); the sizes and maximum sequences go round by ncclAllGather (*max_seq, on
+ *    every rank, may be NULL), the blocks to `root` by grouped ncclSend/ncclRecv (one message per
+ *    rank, each over its own xGMI link). On `root`, `db` (cask_keydir_new) gets the blocks merged in
+ *    rank order — rank order must be replay order (contiguous file-id ranges) — and the caller then
+ *    calls cask_keydir_finish. *gathered: the bytes the root received (its own block's size
+ *    elsewhere). Replaces rank 0's side of the replay loop (cask.rs:346-382) for a sharded open.
+ *  - cask_keydir_exchange_rccl: the key-hash all-to-all. Every rank's block is partitioned on its
+ *    device into one part per rank, part o goes to rank o (grouped ncclSend/ncclRecv), each rank
+ *    merges the parts it owns in rank order into its `db` (cask_keydir_new) and, after an
+ *    ncclAllGather of the owners' terms, finishes it (cask_keydir_finish_terms). No rank holds more
+ *    than its share of the keys. *sent / *received: this rank's bytes out to and in from the others
+ *    (its own part included in *received). */
 #define CASK_RCCL_ID_BYTES 128
 int cask_rccl_unique_id(uint8_t* id /* CASK_RCCL_ID_BYTES */);
 int cask_rccl_comm_init(const uint8_t* id, int nranks, int rank, int device, void** comm);
 int cask_rccl_comm_destroy(void* comm);
 int cask_keydir_gather_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, int root, cask_db* db,
                             uint64_t* gathered, uint64_t* max_seq);
+int cask_keydir_exchange_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, cask_db* db,
+                              uint64_t* sent, uint64_t* received);
 
 /* Cask::open over several GPUs of this process (replaces cask.rs:346-382 like cask_db_open): the
  * data files are split into contiguous ranges, one per entry of `devices` (a device may appear more
  * than once: its shards run one after another); within a range, files with a valid hint file are
  * replayed from it (the body parsed on the device, cask_parse_hints_device), the others scanned
  * (and given their hint files when opts->write_hints); each stretch of files of one kind becomes a
- * keydir block on its device, and the blocks are folded on the host in order. On a failure, hint
- * files of ranges after the failing file may have been written too (the ranges run in parallel). */
+ * keydir block on its device, and the blocks are folded on the host in order. The ranges run in
+ * parallel, but on a failure the hint files on disk are the reference's: those of the files up to
+ * the failing one (it included, with its Ok records), none after it (cask.rs:357-368). */
 cask_db* cask_db_open_multi(const char* path, const cask_options* opts, const int* devices, int ndevices,
                             cask_open_error* err);
 

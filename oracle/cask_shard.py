@@ -176,3 +176,39 @@ def fold_blocks(blocks: list[bytes]):
             le, lb = live.get(fid, (0, 0))
             stats[fid] = (puts + st, puts - le + st, pb - lb + sb)
     return kd, stats, maxs
+
+
+def key_owner(k: bytes, nparts: int) -> int:
+    """keydir_format.h key_owner: the high 32 bits of the key hash scaled to [0, nparts)."""
+    return ((key_hash(k) >> 32) * nparts) >> 32
+
+
+def partition_block(b: bytes, nparts: int) -> list[bytes]:
+    """Restatement of the key-hash partition (keydir_format.h; k_keydir.hip kd_partition, engine.cpp
+    cask_keydir_partition_host): part o = the records whose key's owner is o, in block order, their
+    keys, and the stats table (counts in part 0 only)."""
+    (magic, ver, nrec, kb, nfiles, _, maxp1, rows_in, total, _) = HDR.unpack_from(b, 0)
+    assert magic == MAGIC and ver == VERSION
+    fat = HDR.size + REC.size * nrec
+    kat = fat + FST.size * nfiles
+    fst = [FST.unpack_from(b, fat + FST.size * i) for i in range(nfiles)]
+    recs = [[] for _ in range(nparts)]
+    keys = [[] for _ in range(nparts)]
+    ko = kat
+    for i in range(nrec):
+        raw = b[HDR.size + REC.size * i:HDR.size + REC.size * (i + 1)]
+        ksz = REC.unpack(raw)[4]
+        k = bytes(b[ko:ko + ksz])
+        ko += ksz
+        o = key_owner(k, nparts)
+        recs[o].append(bytes(raw))
+        keys[o].append(k)
+    out = []
+    for o in range(nparts):
+        fb = b"".join(FST.pack(f, 0, *((p, pb, s, sb) if o == 0 else (0, 0, 0, 0))) for (f, _, p, pb, s, sb) in fst)
+        kbytes = b"".join(keys[o])
+        body = b"".join(recs[o]) + fb + kbytes
+        size = (HDR.size + len(body) + 7) & ~7
+        hdr = HDR.pack(MAGIC, VERSION, len(recs[o]), len(kbytes), nfiles, 0, maxp1, rows_in if o == 0 else 0, size, 0)
+        out.append((hdr + body).ljust(size, b"\0"))
+    return out

@@ -173,3 +173,47 @@ def test_engine_file_discovery(native, tmp_path):
     with CaskOptions().open(str(path)) as db:
         assert db.files() == want
         assert len(db) == 0
+
+
+_LIMIT_CHILD = r"""
+import ctypes as C, resource, sys
+sys.path.insert(0, sys.argv[3])
+import cask_amd._lib as L
+lib = L.lib()
+vm = int([l for l in open("/proc/self/status") if l.startswith("VmSize")][0].split()[1]) * 1024
+lim = vm + (int(sys.argv[2]) << 20)
+resource.setrlimit(resource.RLIMIT_AS, (lim, lim))
+err = L.OpenError()
+h = lib.cask_db_open(sys.argv[1].encode(), None, C.byref(err))
+print("RESULT", 1 if h else 0, err.status, flush=True)
+"""
+
+
+def test_open_out_of_memory_returns_status(native, tmp_path):
+    """No C++ exception crosses the C ABI (cask_scan.h): open() of a database whose hint file is
+    larger than the memory the process has left (RLIMIT_AS in a child process) returns
+    CASK_E_NOMEM — the std::bad_alloc of the hint read, on a worker thread, reaches the entry
+    point's handler — instead of terminating the process."""
+    import subprocess
+    import sys
+    import numpy as np
+    path = str(tmp_path / "db")
+    os.makedirs(path)
+    open(R.data_file_path(path, 1), "wb").close()
+    n = 3 << 20  # 3 Mi hint records of 38 B: a 114-MB hint file
+    rec = np.zeros((n, 38), np.uint8)
+    rec[:, 0:8] = np.arange(1, n + 1, dtype="<u8").view(np.uint8).reshape(n, 8)
+    rec[:, 8] = 16  # ksz
+    rec[:, 22:30] = np.arange(n, dtype="<u8").view(np.uint8).reshape(n, 8)  # keys
+    body = rec.tobytes()
+    with open(R.hint_file_path(path, 1), "wb") as f:
+        f.write(body + R.xxhash32(body).to_bytes(4, "little"))
+    out = subprocess.run([sys.executable, "-c", _LIMIT_CHILD, path, "64", ROOT], capture_output=True, text=True,
+                         timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    res = [l for l in out.stdout.splitlines() if l.startswith("RESULT")]
+    assert res == ["RESULT 0 -13"], (out.stdout, out.stderr[-2000:])
+    # and with the memory it needs, the same database opens
+    out = subprocess.run([sys.executable, "-c", _LIMIT_CHILD, path, "4096", ROOT], capture_output=True, text=True,
+                         timeout=300)
+    assert [l for l in out.stdout.splitlines() if l.startswith("RESULT")] == ["RESULT 1 0"], out.stderr[-2000:]

@@ -89,6 +89,68 @@ def _worker(rank, world, port, path, out):
         dist.destroy_process_group()
 
 
+def _pworker(rank, world, port, path, out):
+    """The key-hash partitioned replay (huge keyspace): each rank scans its files (oracle
+    rows), builds its block, splits it by key owner with the native partitioner, sends part o to rank
+    o, folds the parts it owns in rank order and exchanges per-file terms. Each rank reports its keys
+    and its (whole-replay) stats."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import cask_shard as S
+    import oracle_ffi as O
+    from cask_amd.distributed import partitioned_fold, shard_files as shard
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        mine = shard(R.find_data_files(path), world, rank)
+        rows = []
+        for fid in mine:
+            with open(R.data_file_path(path, fid), "rb") as f:
+                buf = f.read()
+            for r in O.scan(buf):
+                p, k = int(r["pos"]), int(r["ksz"])
+                rows.append((fid, R.Row(pos=p, seq=int(r["seq"]), ksz=k, vsz_raw=int(r["vsz_raw"]),
+                                        key=buf[p + 18:p + 18 + k])))
+        db = partitioned_fold(S.shard_block(mine, rows))
+        res = {"current_sequence": db.current_sequence,
+               "keydir": sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence]
+                                for k, e in db.index().items()),
+               "stats": sorted([f, *s] for f, s in db.stats().items()),
+               "files": db.files()}
+        db.close()
+        with open(out + f".{rank}", "w") as f:
+            json.dump(res, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_partitioned_fold_matches_single_process(tmp_path, world):
+    """No rank holds more than its keys, yet together they hold exactly the single-process keydir,
+    each key on its owner, and every rank has the whole replay's Stats, files and sequence —
+    including stale tombstones whose shard and owner differ."""
+    from cask_amd.keydir import key_owner
+    path = str(tmp_path / "db")
+    os.makedirs(path)
+    _make_db(path)
+    want = R.replay(path, write_hints=False)
+    assert want.error is None
+    out = str(tmp_path / "rank")
+    mp.start_processes(_pworker, args=(world, _free_port(), path, out), nprocs=world, join=True, start_method="spawn")
+    got = []
+    for r in range(world):
+        with open(out + f".{r}") as f:
+            got.append(json.load(f))
+    union = sorted(x for g in got for x in g["keydir"])
+    assert union == sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence]
+                           for k, e in want.index.map.items())
+    for r, g in enumerate(got):
+        assert all(key_owner(bytes.fromhex(x[0]), world) == r for x in g["keydir"])
+        assert g["stats"] == sorted([f, *s] for f, s in want.index.stats.map.items())
+        assert g["current_sequence"] == want.current_sequence
+        assert g["files"] == sorted(R.find_data_files(path))
+    assert all(g["keydir"] for g in got)  # (40 keys: every owner holds some)
+
+
 def test_shard_files_contiguous_balanced():
     for n in range(0, 40):
         ids = random.Random(n).sample(range(1, 1000), n)

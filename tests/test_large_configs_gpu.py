@@ -210,12 +210,17 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
 
 @pytest.mark.timeout(1800)
 def test_cfg4_two_rank_shards_fold_against_oracle(gpu_ctx):
+    """Two full configs[4] rank shards (cfg5's 290-B record shape), folded in rank order on one
+    host — and routed through the key-hash partition (SURVEY §8e's huge-keyspace path): each block
+    split on the device into two owners' parts, each owner folding its parts in rank order, Stats
+    from the owners' terms — both against the oracle's replay digest."""
     import torch
-    from cask_amd.keydir import KeydirFold, shard_keydir
+    from cask_amd.keydir import KeydirFold, partition_device, shard_keydir
     from cask_amd.workloads import CFG2_KSZ, CFG2_VSZ, fixed_file
     ctx = gpu_ctx
     per_rank = 32
     fold = KeydirFold()
+    owners = [KeydirFold(), KeydirFold()]
     hosts, ids = [], []
     for rank in range(2):  # ranks 0 and 1 of configs[4]: files 1..32 and 33..64
         files = []
@@ -231,6 +236,10 @@ def test_cfg4_two_rank_shards_fold_against_oracle(gpu_ctx):
         assert int((rows["status"][:res.count] != 0).sum().item()) == 0
         blk = shard_keydir(ctx, views, rows, res.count, res.file_row_offset)
         fold.merge(blk.cpu())
+        parts = partition_device(ctx, blk, 2)
+        for o in range(2):
+            owners[o].merge(parts[o].cpu())
+        del parts
         for f in files:
             hosts.append(f.data.cpu().numpy())
             ids.append(f.file_id)
@@ -252,3 +261,14 @@ def test_cfg4_two_rank_shards_fold_against_oracle(gpu_ctx):
         assert dg == want.digest
     finally:
         db.close()
+    _say("cfg4: partitioned owners")
+    terms = b"".join(f.terms().tobytes() for f in owners)
+    dsum, nsum = 0, 0
+    for f in owners:
+        with _beat("cfg4 owner finish", f.finish_terms, terms) as odb:
+            assert odb.current_sequence == want.max_seq + 1
+            assert _stats_rows(odb) == want_stats
+            dg, n = _beat("cfg4 owner digest", _digest_of_export, odb)
+            assert n > 0
+            dsum, nsum = (dsum + dg) % (1 << 64), nsum + n
+    assert nsum == want.live and dsum == want.digest  # (the digest is a sum over entries)

@@ -184,10 +184,21 @@ def test_open_multi_reports_first_failure(native, tmp_path):
         b = bytearray(open(p, "rb").read())
         b[int(len(b) * at)] ^= 0x40
         open(p, "wb").write(bytes(b))
-    want = R.replay(str(path), write_hints=False).error
+    ref = str(tmp_path / "ref")
+    shutil.copytree(path, ref)
+    want = R.replay(ref, write_hints=True).error  # (writes the reference's hint files into ref/)
     with pytest.raises((errors.InvalidChecksum, errors.UnexpectedEof)) as ei:
         open_multi(path, [0, 0])
     assert (ei.value.file_id, ei.value.pos) == (want.file_id, want.pos)
+    # the replay stops at the first Err (cask.rs:357-368): hint files of the files up to the failing
+    # one (it included, with its Ok records), none after it — though the second range ran in parallel
+    assert want.file_id == 2
+    for fid in R.find_data_files(path):
+        hp, hr = R.hint_file_path(path, fid), R.hint_file_path(ref, fid)
+        assert os.path.exists(hp) == os.path.exists(hr) == (fid <= 2), fid
+        if fid <= 2:
+            assert open(hp, "rb").read() == open(hr, "rb").read(), fid
+    assert not [f for f in os.listdir(path) if f.endswith(".part")]
 
 
 def test_sharded_keydir_unique_keys_large(gpu_ctx):
@@ -244,5 +255,56 @@ def test_rccl_c_abi_gather_single_rank(gpu_ctx, tmp_path):
         db2, got2, _ = gather_fold_rccl(gpu_ctx, comm, torch.empty(0, dtype=torch.uint8, device=blk.device))
         with db2:
             assert len(db2) == 0 and got2 == 0
+    finally:
+        comm.close()
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_device_partition_equals_host(gpu_ctx, tmp_path, seed):
+    """cask_keydir_partition (on the device) byte for byte cask_keydir_partition_host and the
+    restatement, for blocks with overwrites, tombstones and stale records, into 1, 2, 3, 8 and 64
+    owners; and the owners' fold of the parts equals the replay."""
+    import torch
+    from cask_amd.keydir import KeydirFold, partition_device, partition_host
+    path = str(tmp_path / "db")
+    _make_db(path, 30 + seed, nfiles=4, nrec=2500, nkeys=300 if seed == 1 else 5000)
+    files = _files(path)
+    want = _want(path)
+    blocks = [_device_block(gpu_ctx, part) for part in (files[:1], files[1:3], files[3:])]
+    for nparts in (1, 2, 3, 8, 64):
+        owners = [KeydirFold() for _ in range(nparts)]
+        for b in blocks:
+            dev = torch.from_numpy(np.frombuffer(b, np.uint8).copy()).cuda()
+            got = [p.cpu().numpy().tobytes() for p in partition_device(gpu_ctx, dev, nparts)]
+            assert got == [p.tobytes() for p in partition_host(b, nparts)] == S.partition_block(b, nparts)
+            for o in range(nparts):
+                owners[o].merge(got[o])
+        terms = b"".join(f.terms().tobytes() for f in owners)
+        kd = []
+        for f in owners:
+            with f.finish_terms(terms) as db:
+                k, st, cs = _got(db)
+                kd += k
+                assert (st, cs) == (want[1], want[2])
+        assert sorted(kd) == want[0]
+
+
+def test_rccl_c_abi_exchange_single_rank(gpu_ctx, tmp_path):
+    """cask_keydir_exchange_rccl on a one-rank communicator: the block is partitioned on the device
+    (one part), sent to itself, folded and finished from its own terms — the replay's keydir, stats
+    and sequence. (More ranks need as many GPUs: bench.py --gpus N runs it on the driver's node.)"""
+    import torch
+    from cask_amd.distributed import RcclComm, exchange_fold_rccl, rccl_unique_id
+    path = str(tmp_path / "db")
+    _make_db(path, 10, nfiles=3)
+    files = _files(path)
+    want = _want(path)
+    blk = torch.from_numpy(np.frombuffer(_device_block(gpu_ctx, files), np.uint8).copy()).cuda()
+    comm = RcclComm(rccl_unique_id(), 1, 0, gpu_ctx.device)
+    try:
+        db, sent, got = exchange_fold_rccl(gpu_ctx, comm, blk)
+        with db:
+            assert _got(db) == want
+        assert sent == 0 and got == blk.numel()
     finally:
         comm.close()

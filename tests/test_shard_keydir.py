@@ -109,3 +109,78 @@ def test_native_fold_rejects_bad_blocks(native):
     bad = (C.c_uint8 * 64)()
     assert native.cask_keydir_merge(h, bad, 64) == -10
     native.cask_db_close(h)
+
+
+# ---- the key-hash partition (huge keyspace): every rank splits its block by key owner,
+# owner o folds the parts it gets in rank order, and the owners' terms give the Stats ----
+
+def _partitioned_native_fold(blocks, nparts):
+    """Owner by owner: merge part o of every block in order, exchange terms, finish. Returns the
+    union of the owners' keydirs, each owner's stats and sequence, and which owner held each key."""
+    from cask_amd.keydir import KeydirFold, partition_host
+    parts = [partition_host(b, nparts) for b in blocks]
+    folds = [KeydirFold() for _ in range(nparts)]
+    for o in range(nparts):
+        for p in parts:
+            folds[o].merge(p[o])
+    terms = b"".join(f.terms().tobytes() for f in folds)
+    kd, stats, seqs, where = {}, [], [], {}
+    for o, f in enumerate(folds):
+        db = f.finish_terms(terms)
+        for k, e in db.index().items():
+            assert k not in kd
+            kd[k] = (e.file_id, e.entry_pos, e.entry_size, e.sequence)
+            where[k] = o
+        stats.append(db.stats())
+        seqs.append(db.current_sequence - 1)
+        db.close()
+    return kd, stats, seqs, where
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.integers(0, 2 ** 32), st.integers(1, 6), st.integers(1, 4), st.integers(1, 7))
+def test_partition_native_matches_restatement(native, seed, nfiles, nshards, nparts):
+    """cask_keydir_partition_host byte for byte the restatement (oracle/cask_shard.py partition_block)."""
+    rng = random.Random(seed)
+    files = _random_files(rng, nfiles, 25, rng.choice([1, 3, 30]), 0.3, 0.3)
+    nshards = min(nshards, nfiles)
+    cuts = sorted(set([0, nfiles] + rng.sample(range(1, nfiles), nshards - 1) if nfiles > 1 else [0, nfiles]))
+    from cask_amd.keydir import key_owner, partition_host
+    for b in _blocks(files, cuts):
+        got = [bytes(p) for p in partition_host(b, nparts)]
+        assert got == S.partition_block(b, nparts)
+        for o, p in enumerate(got):  # every record of part o is owned by o
+            for rec in S.parse_block(p)[0]:
+                assert key_owner(rec[6], nparts) == o == S.key_owner(rec[6], nparts)
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 8])
+@pytest.mark.parametrize("seed", range(10))
+def test_partitioned_fold_equals_in_order_fold(native, seed, nparts):
+    """The owners together hold exactly the single-process keydir, each key on its owner, and every
+    owner has the whole replay's Stats and sequence — stale tombstones across shards included."""
+    from cask_amd.keydir import key_owner
+    rng = random.Random(500 + seed)
+    files = _random_files(rng, 7, 60, rng.choice([2, 10, 50, 400]), rng.choice([0.1, 0.3]), 0.25)
+    want = _full_fold(files)
+    for cuts in ([0, 7], [0, 3, 7], [0, 1, 2, 4, 7]):
+        kd, stats, seqs, where = _partitioned_native_fold(_blocks(files, cuts), nparts)
+        assert kd == want[0]
+        assert all(s == want[1] for s in stats)
+        assert all(q == max(want[2], 0) for q in seqs)
+        assert all(key_owner(k, nparts) == o for k, o in where.items())
+
+
+def test_partition_rejects_bad_blocks(native):
+    import ctypes as C
+    off = (C.c_uint64 * 3)()
+    bad = (C.c_uint8 * 64)()
+    assert native.cask_keydir_partition_host(bad, 64, 2, None, 0, off) == -10
+    blk = S.shard_block([1], [(1, R.Row(pos=0, seq=1, ksz=3, vsz_raw=5, key=b"abc"))])
+    buf = (C.c_uint8 * len(blk)).from_buffer_copy(blk)
+    assert native.cask_keydir_partition_host(buf, len(blk), 0, None, 0, off) == -10
+    assert native.cask_keydir_partition_host(buf, len(blk), 2, None, 0, off) == -12  # size asked
+    assert off[2] == sum(len(p) for p in S.partition_block(blk, 2))
+    h = native.cask_keydir_new()
+    assert native.cask_keydir_finish_terms(h, None, 3) == -10  # not a whole number of terms
+    native.cask_db_close(h)

@@ -17,7 +17,7 @@ using namespace cask_dev;
 
 // nseg segments of S bytes at base + perm(seg) * S + 4 (the body of a record: 4 B past its start);
 // quad k of the grid takes segments k, k + Q, k + 2Q, ... (Q = quads in the grid).
-template <uint32_t D, bool HASH>
+template <uint32_t D, bool HASH, uint32_t OFF = 4>
 __global__ __launch_bounds__(256) void k_quads(const uint8_t* __restrict__ base, uint64_t nseg, uint32_t S,
                                                uint32_t scatter, uint32_t* __restrict__ sink, uint32_t idle = 0,
                                                uint32_t extra = 0) {
@@ -28,7 +28,7 @@ __global__ __launch_bounds__(256) void k_quads(const uint8_t* __restrict__ base,
   const uint32_t nblk = (S - 64) / 64;  // full blocks of a segment's body
   for (uint64_t k = qid; k < nseg; k += Q) {
     const uint64_t seg = scatter ? (k * 0x9E3779B97F4A7C15ull) % nseg : k;  // (nseg odd: a permutation)
-    const g_u8* lp = idleq ? (const g_u8*)(base + 16 * q) - 64 * 0 : (const g_u8*)(base + seg * S + 4 + 16 * q);
+    const g_u8* lp = idleq ? (const g_u8*)(base + 16 * q) - 64 * 0 : (const g_u8*)(base + seg * S + OFF + 16 * q);
     const int64_t step = idleq ? 0 : 64;
     u32x4 A[D], B[D];
 #pragma unroll
@@ -131,7 +131,7 @@ static float run_lanes(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t 
   return best;
 }
 
-template <uint32_t D, bool HASH>
+template <uint32_t D, bool HASH, uint32_t OFF = 4>
 static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_per_cu, uint32_t scatter, int cus,
                  uint32_t* sink, uint32_t idle = 0, uint32_t extra = 0) {
   uint64_t nseg = bytes / S;
@@ -140,12 +140,12 @@ static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
-  hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink, idle, extra);
+  hipLaunchKernelGGL((k_quads<D, HASH, OFF>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink, idle, extra);
   CK(hipDeviceSynchronize());
   float best = 1e30f;
   for (int it = 0; it < 3; ++it) {
     CK(hipEventRecord(a));
-    hipLaunchKernelGGL((k_quads<D, HASH>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink, idle, extra);
+    hipLaunchKernelGGL((k_quads<D, HASH, OFF>), dim3(grid), dim3(256), 0, 0, buf, nseg, S, scatter, sink, idle, extra);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -156,8 +156,9 @@ static float run(const uint8_t* buf, uint64_t bytes, uint32_t S, uint32_t waves_
   // by the non-idle quads (round 3: counting all nblk blocks overstated short segments by up to 2x)
   const uint64_t nblk = (S - 64) / 64, rdb = nblk >= D ? nblk / D * D : D;
   const double rd = (double)nseg * (double)(rdb * 64) * (4 - idle) / 4.0;
-  printf("D=%2u %s S=%6u waves/CU=%2u %s idle=%u/4 extra=%u: %.3f ms %.0f GB/s read\n", D, HASH ? "hash" : "xor ", S,
-         waves_per_cu, scatter ? "scattered" : "adjacent ", idle, extra, best, rd / best / 1e6);
+  printf("D=%2u %s S=%6u off=%u waves/CU=%2u %s idle=%u/4 extra=%u: %.3f ms %.0f GB/s read (%.3f GB per launch)\n", D,
+         HASH ? "hash" : "xor ", S, OFF, waves_per_cu, scatter ? "scattered" : "adjacent ", idle, extra, best,
+         rd / best / 1e6, rd / 1e9);
   fflush(stdout);
   return best;
 }
@@ -172,6 +173,14 @@ int main(int argc, char** argv) {
   uint32_t* sink;
   CK(hipMalloc(&sink, 64));
   const bool sweep = argc > 1 && argv[1][0] == 's';  // depth / occupancy / mixing sweep (round 3)
+  if (argc > 1 && argv[1][0] == 'o') {  // round 4: record bodies at +4 (rounds share a line) vs 128-B aligned rounds
+    for (uint32_t S : {8192u, 65536u}) {
+      run<16, true, 4>(buf, bytes, S, 8, 1, cus, sink);
+      run<16, true, 0>(buf, bytes, S, 8, 1, cus, sink);
+      run<16, true, 64>(buf, bytes, S, 8, 1, cus, sink);
+    }
+    return 0;
+  }  // depth / occupancy / mixing sweep (round 3)
   if (argc > 1 && argv[1][0] == 'a') {  // adjacent (a wave's quads on consecutive segments) vs scattered
     for (uint32_t S : {2048u, 4096u, 8192u, 16384u, 65536u})
       for (uint32_t sc : {0u, 1u}) run<16, true>(buf, bytes, S, 8, sc, cus, sink);
