@@ -37,6 +37,7 @@
 #include "host_ring.h"
 #include "keydir_format.h"
 #include "xxh32.h"
+#include "knobs.h"
 
 namespace {
 
@@ -548,7 +549,7 @@ struct EngineDev {
     for (uint32_t f = 0; f < v.size(); ++f)
       for (uint64_t o = 0; o < v[f].len; o += kSlotBytes) pieces.push_back(Piece{f, o, std::min<uint64_t>(kSlotBytes, v[f].len - o)});
     // CASK_OPEN_READERS (tuning knob): reader threads, at most kReaders (default: the host threads)
-    static const unsigned readers = getenv("CASK_OPEN_READERS") ? (unsigned)atoi(getenv("CASK_OPEN_READERS")) : 0u;
+    static const unsigned readers = cask_knobs::tune("CASK_OPEN_READERS") ? (unsigned)atoi(cask_knobs::tune("CASK_OPEN_READERS")) : 0u;
     const unsigned want = readers ? std::min<unsigned>(readers, (unsigned)kReaders) : (unsigned)kReaders;
     const unsigned nt = std::max(1u, std::min<unsigned>(want, std::min<unsigned>(host_threads(), (unsigned)pieces.size())));
     std::vector<int> status(nt, CASK_OK);
@@ -601,7 +602,7 @@ struct EngineDev {
   // the other (a copy to pageable memory straight from the device runs at ~10 GB/s). Small copies
   // take cask_copy. The device work that produced `src` (on the context's stream) is waited for first.
   int to_host(uint8_t* dst, const uint8_t* src, uint64_t n, cask_host::PinnedRing* rg = nullptr) {
-    const char* mv = getenv("CASK_STAGE_MIN");  // test knob: smallest copy staged (default 64 MiB)
+    const char* mv = cask_knobs::hook("CASK_STAGE_MIN");  // test knob: smallest copy staged (default 64 MiB)
     if (n < (mv ? strtoull(mv, nullptr, 10) : (64ull << 20)) || !n) return cask_copy(ctx, dst, src, n);
     if (hipSetDevice(device) != hipSuccess || hipStreamSynchronize((hipStream_t)cask_ctx_stream(ctx)) != hipSuccess)
       return CASK_E_DEVICE;
@@ -702,7 +703,7 @@ struct FoldScratch {
 void parallel_fold(const std::vector<FoldSrc>& src, Index& out, FoldScratch* keep = nullptr) {
   uint64_t n = 0;
   for (const FoldSrc& f : src) n += f.cnt;
-  const char* mv = getenv("CASK_PAR_FOLD_MIN");  // tuning/test knob: smallest replay folded in parallel
+  const char* mv = cask_knobs::hook("CASK_PAR_FOLD_MIN");  // tuning/test knob: smallest replay folded in parallel
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
   const unsigned nt = std::min(host_threads(), Index::kSub);
   if (n < min_par || nt == 1) {
@@ -1005,7 +1006,7 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
     uint64_t all = 0, acc = 0;
     for (const auto& v : views) all += v.len;
     // CASK_OPEN_BATCH (test and tuning knob): bytes per batch (1: every file a batch of its own)
-    const uint64_t bb_env = getenv("CASK_OPEN_BATCH") ? strtoull(getenv("CASK_OPEN_BATCH"), nullptr, 10) : 0ull;
+    const uint64_t bb_env = cask_knobs::hook("CASK_OPEN_BATCH") ? strtoull(cask_knobs::hook("CASK_OPEN_BATCH"), nullptr, 10) : 0ull;
     const uint64_t bb = bb_env ? bb_env : std::max<uint64_t>(1ull << 30, all / 8);
     for (size_t v = 0; v < views.size(); ++v) {
       acc += views[v].len;
@@ -1383,7 +1384,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       used.push_back(i);
     }
     unsigned nt = host_threads();
-    const char* mv = getenv("CASK_PAR_FOLD_MIN");  // the same knob as parallel_fold
+    const char* mv = cask_knobs::hook("CASK_PAR_FOLD_MIN");  // the same knob as parallel_fold
     if (nrec < (mv ? strtoull(mv, nullptr, 10) : (1ull << 16))) nt = 1;
     // keydir lookups over all the records, split evenly over threads
     parallel_for(nt, [&](unsigned t) {
@@ -1908,7 +1909,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   // The fold of a block depends on each key's records alone, in order: on threads by keydir table
   // (parallel_fold's split), each table taking its records in block order — first the thresholds
   // against the keydir entering the shard, then the updates. Stale terms are per-file sums.
-  const char* mv = getenv("CASK_PAR_FOLD_MIN");
+  const char* mv = cask_knobs::hook("CASK_PAR_FOLD_MIN");
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
   const unsigned nt = n < min_par ? 1u : std::min(host_threads(), Index::kSub);
   constexpr unsigned S = Index::kSub;

@@ -14,6 +14,7 @@
 #include <exception>
 #include <thread>
 #include <vector>
+#include "knobs.h"
 
 namespace cask_host {
 
@@ -21,7 +22,7 @@ namespace cask_host {
 // 16. CASK_HOST_THREADS (test and tuning knob) sets the count, e.g. to force the threaded paths on a
 // one-CPU machine.
 inline unsigned host_threads() {
-  if (const char* e = getenv("CASK_HOST_THREADS")) {
+  if (const char* e = cask_knobs::hook("CASK_HOST_THREADS")) {
     const int v = atoi(e);
     if (v > 0) return (unsigned)std::min(v, 64);
   }

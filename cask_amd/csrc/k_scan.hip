@@ -21,6 +21,7 @@
 #include "device_util.h"
 
 #include <stdlib.h>
+#include "knobs.h"
 
 namespace cask_dev {
 
@@ -719,13 +720,13 @@ template <class G>
 static void launch_geo(const ScanArgs& a, void* stream) {
   const int cus = device_cus();
   // CASK_WG_PER_CU (diagnostic): fewer resident workgroups per CU than the LDS allows
-  static const uint32_t per_cu = getenv("CASK_WG_PER_CU") ? (uint32_t)atoi(getenv("CASK_WG_PER_CU")) : G::kPerCU;
+  static const uint32_t per_cu = cask_knobs::tune("CASK_WG_PER_CU") ? (uint32_t)atoi(cask_knobs::tune("CASK_WG_PER_CU")) : G::kPerCU;
   uint64_t grid = (uint64_t)cus * per_cu;
   grid = (grid + 7) & ~7ull;
   const uint64_t need = (a.total_chunks + 7) & ~7ull;  // never more workgroups than chunks
   if (need < grid) grid = need;
   // CASK_LDS_PAD (diagnostic): extra dynamic LDS per workgroup, to lower workgroups per CU
-  static const uint32_t pad = getenv("CASK_LDS_PAD") ? (uint32_t)atoi(getenv("CASK_LDS_PAD")) : 0u;
+  static const uint32_t pad = cask_knobs::tune("CASK_LDS_PAD") ? (uint32_t)atoi(cask_knobs::tune("CASK_LDS_PAD")) : 0u;
   // a.ctr->run_next is zero: every launch follows a fresh call block or the repair path's reset
   if (a.exact)
     hipLaunchKernelGGL((k_scan_chunks<G, true>), dim3((uint32_t)grid), dim3(G::kNT), pad, S(stream), a, a.files);

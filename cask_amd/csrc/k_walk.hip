@@ -22,6 +22,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include "knobs.h"
 
 namespace cask_dev {
 
@@ -761,7 +762,7 @@ void launch_walk_runs(const ScanArgs& a, void* stream) {
   if (!a.total_chunks || !nruns) return;
   // CASK_WALK_WAVES (tuning knob): waves per CU of the persistent grid
   // (7 waves per SIMD fit: 66 VGPRs, 2.9 KB of LDS)
-  static const uint32_t per_cu = getenv("CASK_WALK_WAVES") ? (uint32_t)atoi(getenv("CASK_WALK_WAVES")) : 28u;
+  static const uint32_t per_cu = cask_knobs::tune("CASK_WALK_WAVES") ? (uint32_t)atoi(cask_knobs::tune("CASK_WALK_WAVES")) : 28u;
   uint64_t grid = (uint64_t)device_cus() * per_cu;
   if (grid > nruns) grid = nruns;
   hipLaunchKernelGGL(k_walk_runs, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);

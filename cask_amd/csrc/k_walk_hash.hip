@@ -19,6 +19,7 @@
 #include "device_util.h"
 
 #include <stdlib.h>
+#include "knobs.h"
 
 namespace cask_dev {
 
@@ -954,7 +955,7 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
   // CASK_CHASE_WG (tuning knob): threads per workgroup (a lane per run). One-wave workgroups spread
   // the chase over every CU (configs[2]: 128 four-wave groups left half of the CUs idle; with
   // one-wave groups the chase takes 0.35 instead of 0.46 ms)
-  static const uint32_t wg = getenv("CASK_CHASE_WG") ? (uint32_t)atoi(getenv("CASK_CHASE_WG")) : 64u;
+  static const uint32_t wg = cask_knobs::tune("CASK_CHASE_WG") ? (uint32_t)atoi(cask_knobs::tune("CASK_CHASE_WG")) : 64u;
   const uint32_t tpb = wg == 64 || wg == 128 ? wg : 256u;
   const uint32_t grid = (uint32_t)((nruns + tpb - 1) / tpb);
   hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(tpb), 0, (hipStream_t)stream, a, a.files);
@@ -973,7 +974,7 @@ static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (getenv("CASK_HASH_WAVES")) per_cu = atoi(getenv("CASK_HASH_WAVES"));
+    if (cask_knobs::tune("CASK_HASH_WAVES")) per_cu = atoi(cask_knobs::tune("CASK_HASH_WAVES"));
     else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KRH<D>, 256, 0) == hipSuccess && nb > 0)
       per_cu = 4 * nb;
     if (per_cu <= 0) per_cu = 8;

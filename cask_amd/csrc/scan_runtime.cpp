@@ -17,6 +17,7 @@
 #include "keydir_format.h"
 #include "scan_kernels.h"
 #include "xxh32.h"
+#include "knobs.h"
 
 using namespace cask_dev;
 
@@ -183,7 +184,7 @@ cask_ctx* cask_ctx_create(int device, int* status) {
   }
   c->stream = c->own;
   c->geo = -1;
-  if (const char* g = getenv("CASK_SCAN_GEOMETRY")) c->geo = atoi(g);
+  if (const char* g = cask_knobs::tune("CASK_SCAN_GEOMETRY")) c->geo = atoi(g);
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   (void)hipEventCreateWithFlags(&c->evw, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->evf, hipEventDisableTiming);
@@ -401,7 +402,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // longer runs search less often, which is what variable-length logs pay for (a search that lands
     // inside a record longer than the window scans the whole chunk); the balance at the end comes
     // from the quarter-length tail runs below (configs[1]: 32-chunk runs, 1.2 % faster than 16).
-    static const uint32_t run = getenv("CASK_RUN_CHUNKS") ? (uint32_t)atoi(getenv("CASK_RUN_CHUNKS")) : 0u;
+    static const uint32_t run = cask_knobs::tune("CASK_RUN_CHUNKS") ? (uint32_t)atoi(cask_knobs::tune("CASK_RUN_CHUNKS")) : 0u;
     if (run) {
       a.run = run;
     } else {
@@ -411,12 +412,12 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     }
     // The last grid's worth of runs in runs of a quarter of the length (CASK_RUN_TAIL=0: tuning
     // knob, no short runs): the workgroups then run dry within a short run of each other.
-    static const bool tail_on = !(getenv("CASK_RUN_TAIL") && atoi(getenv("CASK_RUN_TAIL")) == 0);
+    static const bool tail_on = !(cask_knobs::tune("CASK_RUN_TAIL") && atoi(cask_knobs::tune("CASK_RUN_TAIL")) == 0);
     const uint64_t grid_runs = (uint64_t)device_cus() * 4u;  // resident k_scan_chunks workgroups
     // CASK_RUN_SMALL / CASK_RUN_TAIL_X (tuning knobs): the short runs' length; the tail's length in
     // resident workgroups x run, in quarters
-    static const uint32_t rs_env = getenv("CASK_RUN_SMALL") ? (uint32_t)atoi(getenv("CASK_RUN_SMALL")) : 0u;
-    static const uint64_t tx = getenv("CASK_RUN_TAIL_X") ? (uint64_t)atoi(getenv("CASK_RUN_TAIL_X")) : 4u;
+    static const uint32_t rs_env = cask_knobs::tune("CASK_RUN_SMALL") ? (uint32_t)atoi(cask_knobs::tune("CASK_RUN_SMALL")) : 0u;
+    static const uint64_t tx = cask_knobs::tune("CASK_RUN_TAIL_X") ? (uint64_t)atoi(cask_knobs::tune("CASK_RUN_TAIL_X")) : 4u;
     a.run_small = rs_env ? std::min(rs_env, a.run) : std::max<uint32_t>(2u, a.run / 4);
     a.run_tail = ~0ull;
     const uint64_t tail = grid_runs * a.run * tx / 4;
@@ -427,15 +428,15 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.regular_ok = rows ? 1u : 0u;
   a.respec = 1u;
   // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
-  static const uint32_t big_env = getenv("CASK_BIG_REC") ? (uint32_t)atoi(getenv("CASK_BIG_REC")) : kBigRec;
+  static const uint32_t big_env = cask_knobs::tune("CASK_BIG_REC") ? (uint32_t)atoi(cask_knobs::tune("CASK_BIG_REC")) : kBigRec;
   a.big = big_env;
   if (a.big < kMinBigRec) a.big = kMinBigRec;  // the long-record queue's smallest length class
   a.win = chunk + geometry_halo(geo);
   // CASK_SEARCH_SHORT (tuning knob): k_walk_search verifies candidates up to this long by checksum
-  static const uint32_t ss_env = getenv("CASK_SEARCH_SHORT") ? (uint32_t)atoi(getenv("CASK_SEARCH_SHORT")) : 2048u;
+  static const uint32_t ss_env = cask_knobs::tune("CASK_SEARCH_SHORT") ? (uint32_t)atoi(cask_knobs::tune("CASK_SEARCH_SHORT")) : 2048u;
   a.search_short = ss_env < 64 ? 64 : ss_env > 2048 ? 2048 : ss_env;
   // the dense path: CASK_DENSE=0 (tuning knob) sends every call through the repair path's k_compact
-  static const bool dense_on = !(getenv("CASK_DENSE") && atoi(getenv("CASK_DENSE")) == 0);
+  static const bool dense_on = !(cask_knobs::tune("CASK_DENSE") && atoi(cask_knobs::tune("CASK_DENSE")) == 0);
   const bool dense = rows != nullptr && dense_on && total_chunks > 0;
   a.dense = 0;  // k_long fixes dense rows only once they are validated
 
@@ -457,7 +458,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     }
   };
   // CASK_SYNC_EACH=1 (diagnostic): synchronise after every launch so a fault names its kernel
-  static const bool sync_each = getenv("CASK_SYNC_EACH") != nullptr;
+  static const bool sync_each = cask_knobs::tune("CASK_SYNC_EACH") != nullptr;
   auto L = [&](const char* what) {
     H(hipGetLastError(), what);
     if (sync_each) {  // (names the kernel a hang or fault is in, on stderr)
@@ -491,7 +492,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   if (hint) {
     walk = true;  // hint bodies are always walked (k_walk_runs' hint mode)
   } else {
-    const char* mode = getenv("CASK_SCAN_MODE");
+    const char* mode = cask_knobs::hook("CASK_SCAN_MODE");
     if (mode && !strcmp(mode, "walk")) {
       walk = true;
     } else if (mode && !strcmp(mode, "chunk")) {
@@ -549,7 +550,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // Each run of kWalkRun chunks in the mode of the region its first chunk lies in: the walk-mode
     // runs by index, the chunk-mode runs as [first, end) stretches for k_scan_chunks (a.runs). Built
     // and copied to the device once per set of files.
-    const char* wr = getenv("CASK_WALK_RUN");
+    const char* wr = cask_knobs::tune("CASK_WALK_RUN");
     a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : kWalkRun;
     a.run_tail = ~0ull;
     const uint64_t R = a.run, nr = (total_chunks + R - 1) / R;
@@ -595,7 +596,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   c->last_geo = walk && !mixed ? -1 : geo;
   if (walk && !hint && !mixed) a.big = kWalkHashMax;  // the walker hashes what fits its window, k_long the rest
   if (walk && !mixed) {  // CASK_WALK_RUN (tuning knob): chunks per walk run, at most kMaxRun
-    const char* wr = getenv("CASK_WALK_RUN");
+    const char* wr = cask_knobs::tune("CASK_WALK_RUN");
     a.run = wr ? (uint32_t)std::min<int>(std::max(1, atoi(wr)), (int)kMaxRun) : hint ? kHintRun : kWalkRun;
     a.run_tail = ~0ull;  // (the chunk scan's short tail runs were sized for its own run length)
   }
@@ -608,7 +609,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // check (slot bad bit, cerr), so k_finish sees them.
   bool long_pre = false;
   // CASK_HASH_D (tuning knob): 64-B blocks in flight per quad of the hashing kernel
-  static const int hash_depth = getenv("CASK_HASH_D") ? atoi(getenv("CASK_HASH_D")) : 16;  // (16: 5 % faster than 8)
+  static const int hash_depth = cask_knobs::tune("CASK_HASH_D") ? atoi(cask_knobs::tune("CASK_HASH_D")) : 16;  // (16: 5 % faster than 8)
   bool fused = false;
   bool fin_done = false;  // k_finish already launched (beside the hash)
   if (mixed) {  // the walk-mode runs (split path), then the chunk-mode runs, then k_finish for all
@@ -654,7 +655,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
     // starts): on a side stream it runs in the slots the hash's last waves leave, and k_hash_fix
     // then adds the checksum statuses it may have missed. CASK_FIN_OVERLAP=0 (tuning knob): after.
-    static const bool fin_overlap = !(getenv("CASK_FIN_OVERLAP") && atoi(getenv("CASK_FIN_OVERLAP")) == 0);
+    static const bool fin_overlap = !(cask_knobs::tune("CASK_FIN_OVERLAP") && atoi(cask_knobs::tune("CASK_FIN_OVERLAP")) == 0);
     if (dense && fin_overlap && c->side && c->evf) {
       H(hipEventRecord(c->ev[2], st));  // (the hash's end, for the timings)
       H(hipStreamWaitEvent(c->side, c->ev[7], 0));
@@ -806,7 +807,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   float repair_ms = 0.f;
   uint64_t invalid_chunks = 0;
 #ifdef CASK_STAMPS
-  if (getenv("CASK_NO_REPAIR")) {  // diagnostic: keep the speculative pass for inspection
+  if (cask_knobs::hook("CASK_NO_REPAIR")) {  // diagnostic: keep the speculative pass for inspection
     c->dbg_spec = a.spec;
     c->dbg_exit = a.exit;
     c->dbg_count = a.count;
@@ -834,8 +835,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     // consecutive flagged chunks walked with a carry; files that were valid keep their chunk
     // table, rows and per-chunk errors (cerr), and k_long queues only chunks scanned since it last ran.
     a.exact = 1;
-    static const bool sparse = getenv("CASK_FULL_REPAIR") == nullptr;  // diagnostic: re-scan everything
-    const int max_local = getenv("CASK_LOCAL_REPAIRS") ? atoi(getenv("CASK_LOCAL_REPAIRS")) : 3;
+    static const bool sparse = cask_knobs::tune("CASK_FULL_REPAIR") == nullptr;  // diagnostic: re-scan everything
+    const int max_local = cask_knobs::hook("CASK_LOCAL_REPAIRS") ? atoi(cask_knobs::hook("CASK_LOCAL_REPAIRS")) : 3;
     if (sparse) redo.resize(total_chunks);
     for (int it = 0; it < max_local && head->any_invalid; ++it) {
       if (sparse) {
@@ -1011,7 +1012,7 @@ extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t
   uint8_t* d = c->stage_data.as<uint8_t>();
   // Large inputs go through the pinned ring on host threads (CASK_STAGE_MIN: the smallest staged
   // input, default 64 MiB; 0 stages everything — the tests' knob)
-  const char* mv = getenv("CASK_STAGE_MIN");
+  const char* mv = cask_knobs::hook("CASK_STAGE_MIN");
   const bool staged = total && total >= (mv ? strtoull(mv, nullptr, 10) : (64ull << 20));
   if (staged) {
     if (!c->ring) c->ring.reset(new (std::nothrow) cask_host::PinnedRing());

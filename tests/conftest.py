@@ -4,6 +4,10 @@ import sys
 
 import pytest
 
+# The library reads its test hooks (CASK_SCAN_MODE, CASK_HOST_THREADS, ... : cask_amd/csrc/knobs.h)
+# only under this switch, fixed when it is first used; child processes of the tests inherit it.
+os.environ.setdefault("CASK_TEST_HOOKS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 sys.path.insert(0, ROOT)

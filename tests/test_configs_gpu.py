@@ -71,8 +71,9 @@ def cfg2(gpu_ctx):
 @pytest.mark.timeout(600)
 @pytest.mark.parametrize("mode", ["chunk", "narrow", "walk"])
 def test_cfg2_full_size_against_generator(gpu_ctx, cfg2, mode, monkeypatch):
-    """Both speculative passes: k_scan_chunks (forced, with either halo) and k_walk_runs (what the
-    library picks for these records), every row against the generator."""
+    """Both speculative passes: k_scan_chunks (forced, with either halo) and the walk mode (what the
+    library picks for these records: k_walk_search, k_walk_chase, k_run_hash), every row against
+    the generator."""
     import torch
     monkeypatch.setenv("CASK_SCAN_MODE", mode)
     files, vsz, n, rl = cfg2
