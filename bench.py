@@ -56,6 +56,8 @@ def parse():
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (H2D+D2H) measurement")
     ap.add_argument("--no-cfg1", action="store_true", help="skip the secondary configs[1] measurement")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the keydir gather + fold after the loop")
+    ap.add_argument("--no-cfg5", action="store_true",
+                    help="N>1: skip the cfg5 shard (290-B records) scan + key-hash partitioned keydir")
     ap.add_argument("--dist-backend", default="nccl",
                     help="rehearsal only: gloo (blocks gathered through host memory)")
     ap.add_argument("--same-device", action="store_true",
@@ -98,13 +100,23 @@ def cpu_baseline(files, nfiles: int, cfg: str):
             assert r.err_kind == 0, r.err_kind
             recs += r.records
         dt = time.perf_counter() - t0
-        # fast restatement (context only): mmap-style tight loop over the first file, 1 core
+        # fast restatement (context only, BASELINE.md's "fast CPU scan" row): a tight in-memory loop
+        # over the first file on 1 core, and the oracle's threaded replay (scan + XXH32 on threads by
+        # file piece, keydir folded on threads by key partition) over the same sample on the host
+        # cores this process may use (at most 16: the box's CPU share per GPU)
         buf = np.fromfile(paths[0][1], dtype=np.uint8)
         ix2 = O.Index()
         t1 = time.perf_counter()
         O.replay_fast(buf, paths[0][0], ix2)
         dt_fast = time.perf_counter() - t1
         del ix, ix2, buf
+        hosts = [np.fromfile(p, dtype=np.uint8) for _, p in paths]
+        ncores = max(1, min(16, len(os.sched_getaffinity(0))))
+        t2 = time.perf_counter()
+        pr, _ = O.replay_parallel(hosts, [fid for fid, _ in paths], ncores)
+        dt_par = time.perf_counter() - t2
+        assert pr.err_kind == 0 and pr.records == recs, (pr.err_kind, pr.records, recs)
+        del hosts
     finally:
         for name in os.listdir(tmp):
             os.remove(os.path.join(tmp, name))
@@ -125,6 +137,7 @@ def cpu_baseline(files, nfiles: int, cfg: str):
                   f"path without hint files (3 read(2) + 5 write(2) + fold per record)",
         "seconds": dt, "host_cpu": cpu, "nproc": os.cpu_count(),
         "fast_restatement_gibps_1core": files[0].data.numel() / dt_fast / 2 ** 30,
+        "fast_restatement_gibps_Ncores": total / dt_par / 2 ** 30, "fast_restatement_cores": ncores,
     }
 
 
@@ -195,6 +208,104 @@ def cfg1_secondary(ctx, torch, dev, steps):
     out = {"gibps": nb * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps, "kernel": "k_scan_chunks",
            "kernel_ms_avg": k, "kernel_frac_of_8TBps": nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS, "bytes": nb}
     del fs, views, rows
+    torch.cuda.empty_cache()
+    return out
+
+
+def cfg5_shard_secondary(ctx, torch, dev, rank, world, dist, backend, same_device, steps, barrier):
+    """N > 1, reported beside the metric: this rank's shard of SURVEY §8d's cfg5 — 32 data files of
+    3,702,558 fixed 290-B records (16-B unique keys, 256-B values; 1,073,741,820 B each), file ids
+    rank*32+1.., 118.5 M records per rank — scanned device-resident (its own GiB/s), then the keydir
+    of the whole job built by the key-hash partition (SURVEY §8e's huge-keyspace path, no rank holds
+    more than its owners' share): each rank's block on its GPU, split on the device by key owner,
+    part o to rank o (cask_keydir_exchange_rccl over RCCL; a gloo rehearsal through torch.distributed),
+    each rank's fold of the keys it owns and the Stats from every owner's terms. Checked: the owners'
+    live keys add up to every record of every rank, each rank's Stats are {file: (records, 0, 0)} for
+    all 32 x N files, and the sequence is the job's. Also the end-to-end rate of the first 2 files
+    of the shard from pageable host memory (H2D, scan, rows D2H)."""
+    from cask_amd.keydir import KeydirFold, partition_device, shard_keydir
+    from cask_amd.workloads import CFG2_KSZ, CFG2_RECORDS_PER_FILE as RPF, CFG2_VSZ, fixed_file
+    out = {"workload": "cfg5 shard: 32 x 1,073,741,820 B of 290-B records per rank (SURVEY 8d cfg5 / configs[4])"}
+    nf = CFG4_FILES_PER_RANK
+    files = []
+    for i in range(nf):
+        fid = rank * nf + i + 1
+        seq0 = 1 + (fid - 1) * RPF
+        files.append(fixed_file(ctx, fid, RPF, CFG2_KSZ, CFG2_VSZ, seq0, seq0, 0xC0FFEE + fid))
+    torch.cuda.synchronize(dev)
+    views = [(f.file_id, f.data) for f in files]
+    n = nf * RPF
+    nbytes = sum(f.data.numel() for f in files)
+    rows = ctx.alloc_rows(n + 16)
+    res = ctx.scan_device(views, rows)
+    assert res.error is None and res.count == n
+    assert int((rows["status"][:n] != 0).sum().item()) == 0
+    run, timings = ctx.prepare_scan(views, rows)
+    run()
+    el, _ = time_loop(torch, dev, run, timings, steps, barrier, dist, backend)
+    out["scan_gibps_all_ranks"] = nbytes * world * steps / el / 2 ** 30
+    out["scan_ms_per_step"] = el * 1e3 / steps
+    res = ctx.scan_device(views, rows)
+    barrier()
+    t0 = time.perf_counter()
+    blk = shard_keydir(ctx, views, rows, res.count, res.file_row_offset)
+    barrier()
+    t1 = time.perf_counter()
+    out["block_ms"] = (t1 - t0) * 1e3
+    out["block_bytes_per_rank"] = int(blk.numel())
+    del rows, res
+    if backend == "nccl" and not same_device:
+        from cask_amd.distributed import exchange_fold_rccl, rccl_comm_from_dist
+        comm = rccl_comm_from_dist(dev.index)
+        barrier()
+        t1 = time.perf_counter()
+        db, sent, got = exchange_fold_rccl(ctx, comm, blk)
+        barrier()
+        t2 = time.perf_counter()
+        comm.close()
+        out["exchange"] = "cask_keydir_exchange_rccl (device partition, grouped send/recv over xGMI, owner folds, terms all-gather)"
+    else:  # rehearsal: the same parts through torch.distributed point-to-point
+        from cask_amd.distributed import all_gather_bytes, exchange_parts
+        barrier()
+        t1 = time.perf_counter()
+        parts = [p.cpu() for p in partition_device(ctx, blk, world)]
+        sent = sum(int(p.numel()) for i, p in enumerate(parts) if i != rank)
+        recv = exchange_parts(parts)
+        got = sum(int(p.numel()) for p in recv)
+        fold = KeydirFold()
+        for p in recv:
+            fold.merge(p)
+        terms = all_gather_bytes(torch.from_numpy(fold.terms()))
+        db = fold.finish_terms(b"".join(t.numpy().tobytes() for t in terms))
+        del parts, recv
+        barrier()
+        t2 = time.perf_counter()
+        out["exchange"] = f"torch.distributed {backend} rehearsal (device partition, parts through host memory)"
+    out["exchange_fold_ms"] = (t2 - t1) * 1e3
+    out["sent_bytes_per_rank"] = int(sent)
+    out["received_bytes_per_rank"] = int(got)
+    mine = len(db)
+    tn = torch.tensor([mine], dtype=torch.int64, device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(tn)
+    stats_ok = db.stats() == {f: (RPF, 0, 0) for f in range(1, nf * world + 1)}
+    ok = torch.tensor([1 if stats_ok and db.current_sequence == nf * world * RPF + 1 else 0], dtype=torch.int64,
+                      device=dev if backend == "nccl" else "cpu")
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    out["live_keys_this_rank"] = mine
+    out["live_keys_all_ranks"] = int(tn.item())
+    out["keydir_ok"] = int(tn.item()) == nf * world * RPF and int(ok.item()) == 1
+    db.close()
+    del blk
+    if rank == 0:  # end to end: the first 2 files from pageable host memory
+        host = [(f.file_id, f.data.cpu().numpy()) for f in files[:2]]
+        ctx.scan_host(host[:1])
+        te = time.perf_counter()
+        hr = ctx.scan_host(host)
+        e2e = time.perf_counter() - te
+        assert hr.count == 2 * RPF and hr.error is None
+        out["e2e_host_scan_gibps"] = sum(b.size for _, b in host) / e2e / 2 ** 30
+        del host, hr
+    del files, views
     torch.cuda.empty_cache()
     return out
 
@@ -344,6 +455,21 @@ def main():
             del blk
         except Exception as e:  # noqa: BLE001 - reported in the line
             extra["keydir_gather_error"] = f"{type(e).__name__}: {e}"[:300]
+
+    # N>1: SURVEY's cfg5 shard per rank and the key-hash partitioned keydir (reported beside the metric)
+    if dist is not None and not args.no_cfg5:
+        try:
+            del res
+            zf = (files, vsz, rl)
+            files = vsz = rl = None
+            rows = None
+            torch.cuda.empty_cache()
+            extra["cfg5_shard"] = cfg5_shard_secondary(ctx, torch, dev, rank, world, dist, args.dist_backend,
+                                                       args.same_device, max(3, min(args.steps, 10)), barrier)
+            files, vsz, rl = zf
+            res = ctx.scan_device(views, ctx.alloc_rows(n + 16))
+        except Exception as e:  # noqa: BLE001 - reported in the line
+            extra["cfg5_shard_error"] = f"{type(e).__name__}: {e}"[:300]
 
     # end-to-end: host-resident files -> H2D -> scan -> rows D2H (cask_scan_host), first 2 files
     if rank == 0 and not args.no_e2e:

@@ -39,11 +39,6 @@ class ScanError(C.Structure):
                 ("found", C.c_uint32), ("row", C.c_uint64)]
 
 
-class Segments(C.Structure):
-    _fields_ = [("nchunks", C.c_uint64), ("chunk_bytes", C.c_uint32), ("slot_cap", C.c_uint32),
-                ("slots", C.c_void_p), ("count", C.c_void_p), ("base", C.c_void_p), ("total_rows", C.c_uint64)]
-
-
 class Options(C.Structure):
     _fields_ = [("create", C.c_int32), ("write_hints", C.c_int32), ("max_file_size", C.c_uint64),
                 ("device", C.c_int32), ("reserved", C.c_int32)]
@@ -103,8 +98,6 @@ SIGNATURES = [
                                    C.POINTER(ScanError)]),
     ("cask_scan_device", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                    C.POINTER(ScanError)]),
-    ("cask_scan_device_segmented", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Segments),
-                                             c_u64p, C.POINTER(ScanError)]),
     ("cask_scan_host", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                  C.POINTER(ScanError)]),
     ("cask_last_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_float)]),

@@ -228,19 +228,13 @@ struct Meta {
 };
 
 // Slot rows [0, n) of a chunk from LDS row buffer `par` to its slots, one 16-B store per row.
-// nt: the rows are the call's output (the segmented output: nothing on the device reads them back),
-// stored nontemporal so that they do not sit dirty in the Infinity Cache for the next scan.
 template <class G>
-__device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t n, bool nt) {
+__device__ __forceinline__ void flush_rows(ScanLdsT<G>& L, uint32_t par, uint32_t* slots, uint32_t n) {
   u32x4* srow = (u32x4*)slots;
   if (G::kStoreWave && threadIdx.x < G::kLoadT) return;  // the store wave's job
   const uint32_t first = G::kStoreWave ? threadIdx.x - G::kLoadT : threadIdx.x;
   const uint32_t step = G::kStoreWave ? 64u : G::kNT;
-  if (nt) {
-    for (uint32_t r = first; r < n; r += step) __builtin_nontemporal_store(L.rows[par][r], &srow[r]);
-  } else {
-    for (uint32_t r = first; r < n; r += step) srow[r] = L.rows[par][r];
-  }
+  for (uint32_t r = first; r < n; r += step) srow[r] = L.rows[par][r];
 }
 
 template <class G, bool EXACT>
@@ -413,7 +407,7 @@ __device__ __forceinline__ void process_chunk(ScanLdsT<G>& L, const ScanArgs& a,
   if (slow) {
     // starts[] overlays both row buffers: flush this chunk's buffered rows now (the previous chunk's
     // were read before this chunk's barrier... and its flush loop runs before process_chunk)
-    flush_rows<G>(L, par, pf_slots, pf_n, !a.regular_ok);
+    flush_rows<G>(L, par, pf_slots, pf_n);
     pf_n = 0;
     BAR();
     if (wave == 0) {
@@ -631,7 +625,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
 #endif
     // the previous chunk's buffered rows go out ahead of the prefetch: no vector-memory instruction
     // is issued while the chunk is processed, and none waits behind the prefetch's loads
-    flush_rows<G>(L, par ^ 1, pf_slots, pf_n, !a.regular_ok);
+    flush_rows<G>(L, par ^ 1, pf_slots, pf_n);
     pf_n = 0;
     ChunkPos nxt = cur;
     if (more) {
@@ -682,7 +676,7 @@ __global__ __launch_bounds__(G::kNT, G::kWavesPerSimd) void k_scan_chunks(ScanAr
     run_end = next_end;
     cur = nxt;
   }
-  flush_rows<G>(L, par ^ 1, pf_slots, pf_n, !a.regular_ok);  // the last chunk's rows (visible: the loop ended on a barrier)
+  flush_rows<G>(L, par ^ 1, pf_slots, pf_n);  // the last chunk's rows (visible: the loop ended on a barrier)
 #ifdef CASK_STAMPS
   dg.st[7] = __builtin_amdgcn_s_memtime() - dg.st[7];
   if (a.stamps && threadIdx.x == 0) {

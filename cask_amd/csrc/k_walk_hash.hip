@@ -573,7 +573,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
 
 // The same pass with every round on whole 128-B lines (see k_run_hash_al's state comment).
 template <uint32_t D>
-__global__ __launch_bounds__(256) void k_run_hash_al(ScanArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 16 ? 1 : D == 8 ? 3 : 4)))
+void k_run_hash_al(ScanArgs a) {
+  constexpr uint32_t RW = 16 * D, RSH = D == 16 ? 8 : D == 8 ? 7 : 6;  // dwords per round (64 D bytes)
+  static_assert(RW == 1u << RSH, "D is 4, 8 or 16");
   constexpr uint32_t RT = kMaxRun + 1;
   __shared__ uint32_t s_pf[4][2][RT];  // per wave, two runs: the exclusive prefix of their chunks' rows
   __shared__ uint64_t s_cd[4][2][2 * kMaxRun];  // and their chunks' first-byte and file-end addresses
@@ -713,9 +716,9 @@ __global__ __launch_bounds__(256) void k_run_hash_al(ScanArgs a) {
     const uint32_t M2 = cont ? cM : (uint32_t)((b2 - la2) >> 2), sb2 = cont ? csb : (uint32_t)(b2 & 3);
     const uint32_t ns2 = hl2 >> 4;  // full stripes
     const uint32_t tl2 = cont ? ctl : M2 + 4 * ns2;
-    const uint32_t nrd2 = cont ? cnrd : (ns2 ? (tl2 >> 8) + 1 : 1u);
+    const uint32_t nrd2 = cont ? cnrd : (ns2 ? (tl2 >> RSH) + 1 : 1u);
     const uint32_t ri2 = cont ? cri + 1 : 0u;
-    const uint32_t nl2 = round2 && ns2 ? ((tl2 - 256 * ri2) >> 4) + 1 < D ? ((tl2 - 256 * ri2) >> 4) + 1 : D : 0u;
+    const uint32_t nl2 = round2 && ns2 ? ((tl2 - RW * ri2) >> 4) + 1 < D ? ((tl2 - RW * ri2) >> 4) + 1 : D : 0u;
     const bool fin2 = round2 && ri2 + 1 == nrd2;
     const uint64_t pt = nt;
     const uint32_t pr = nr, pw3 = w3n;
@@ -783,7 +786,7 @@ __global__ __launch_bounds__(256) void k_run_hash_al(ScanArgs a) {
     // the iteration's loads is in a register before the first load issues: an address built after
     // a load may be built in that load's destination, a write that waits for every load in flight.
     const uint64_t end16 = (end2 + 15) & ~15ull;
-    const uint64_t bpa = la2 + 1024ull * ri2 + 16ull * q;
+    const uint64_t bpa = la2 + 64ull * D * ri2 + 16ull * q;
     uint64_t ya[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 && bpa + 64ull * d < end16 ? bpa + 64ull * d : safe;
@@ -810,10 +813,12 @@ __global__ __launch_bounds__(256) void k_run_hash_al(ScanArgs a) {
       // the elements of this round the record's full stripes use: dword t = 256 cri + 16 d + 4 k + q
       // of its lines (lane q, block d, word k after the transpose) for t in [cM + 1, ctl], i.e.
       // e = 4 d + k in [e_lo, e_lo + span]
-      const int32_t A = (int32_t)(cM + 1 - q) - (int32_t)(256 * cri), B = (int32_t)(ctl - q) - (int32_t)(256 * cri);
+      // (e_lo <= 8: only the first elements of a record's first round can come before its first
+      // stripe, so the others test the upper bound alone)
+      const int32_t A = (int32_t)(cM + 1 - q) - (int32_t)(RW * cri), B = (int32_t)(ctl - q) - (int32_t)(RW * cri);
       int32_t e_lo = A <= 0 ? 0 : (A + 3) >> 2;
-      const int32_t e_hi = B < 0 ? -1 : (B >> 2 < 63 ? B >> 2 : 63);
-      e_lo = e_hi < e_lo ? 64 : e_lo;
+      const int32_t e_hi = B < 0 ? -1 : (B >> 2 < (int32_t)(4 * D - 1) ? B >> 2 : (int32_t)(4 * D - 1));
+      e_lo = e_hi < e_lo ? (int32_t)(4 * D) : e_lo;
       const uint32_t span = (uint32_t)(e_hi - e_lo);
 #pragma unroll
       for (uint32_t d = 0; d < D; ++d) {
@@ -828,7 +833,7 @@ __global__ __launch_bounds__(256) void k_run_hash_al(ScanArgs a) {
         quad_transpose(x, q);
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
-          const bool ok = (uint32_t)((int32_t)(4 * d + k) - e_lo) <= span;
+          const bool ok = 4 * d + k < 8 ? (uint32_t)((int32_t)(4 * d + k) - e_lo) <= span : (int32_t)(4 * d + k) <= e_hi;
           // (computed whatever ok says, then selected: left to itself the compiler masks exec around
           // the round, a VALU -> SALU -> VALU round trip per word)
           uint32_t w = xround(v, x[k]);

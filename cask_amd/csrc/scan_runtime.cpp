@@ -258,17 +258,15 @@ int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
 
 }  // extern "C"
 
-// Core pipeline on device-resident files. rows == nullptr: segmented output only (slots + chunk
-// table, owned by the context); otherwise dense SoA rows in the caller's arrays.
+// Core pipeline on device-resident files: dense SoA rows in the caller's arrays.
 //
 // Dense path (the common case): k_scan_chunks, then k_finish validates every speculated chunk
 // start and writes the dense rows; one copy of the call block tells the host whether every start
 // held and whether records longer than the window wait for k_long. Two kernels when the log has
 // no long records. If some start was wrong the repair path takes over (validate, exact re-scans,
-// k_compact), as does the segmented output.
+// k_compact).
 static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
-                            cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err,
-                            bool hint = false) {
+                            uint64_t* file_row_offset, cask_scan_error* err, bool hint = false) {
   if (nfiles && !files) return CASK_E_INVALID_ARG;
   if (rows && rows->capacity && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status))
     return CASK_E_INVALID_ARG;
@@ -423,9 +421,8 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     const uint64_t tail = grid_runs * a.run * tx / 4;
     if (tail_on && total_chunks >= 4 * tail) a.run_tail = (total_chunks - tail) / a.run * a.run;
   }
-  // regular chunks keep only their first slot row when the rows go to the dense output (k_finish
-  // and k_compact expand them); the segmented output hands the slots to the caller
-  a.regular_ok = rows ? 1u : 0u;
+  // regular chunks keep only their first slot row (k_finish and k_compact expand them)
+  a.regular_ok = 1u;
   a.respec = 1u;
   // CASK_BIG_REC (tuning knob): records longer than this go to k_long even when they fit the window
   static const uint32_t big_env = cask_knobs::tune("CASK_BIG_REC") ? (uint32_t)atoi(cask_knobs::tune("CASK_BIG_REC")) : kBigRec;
@@ -760,7 +757,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     return CASK_OK;
   }
 
-  // ---- repair path (and the segmented output) --------------------------------------------------
+  // ---- repair path ------------------------------------------------------------------------------
   auto reset = [&]() {
     H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
     H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
@@ -929,15 +926,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   const uint64_t* ferr_row = row_off + nfiles + 1 + 2ull * nfiles;
   const uint64_t* ferr_slot = ferr_row + nfiles;
   if (file_row_offset) memcpy(file_row_offset, row_off, 8ull * (nfiles + 1));
-  if (seg) {
-    seg->nchunks = total_chunks;
-    seg->chunk_bytes = chunk;
-    seg->slot_cap = slot_cap;
-    seg->slots = a.slots;
-    seg->count = a.count;
-    seg->base = a.base;
-    seg->total_rows = head->total_rows;
-  }
   if (rows) {
     rows->count = head->total_rows;
     if (head->total_rows > rows->capacity) return CASK_E_CAPACITY;
@@ -970,7 +958,7 @@ extern "C" int cask_parse_hints_device(cask_ctx* c, const cask_file_view* files,
   for (uint32_t i = 0; i < nfiles; ++i)
     if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  return scan_device_impl(c, files, nfiles, rows, nullptr, file_row_offset, err, true);
+  return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, true);
 }
 
 extern "C" int cask_scan_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
@@ -979,16 +967,7 @@ extern "C" int cask_scan_device(cask_ctx* c, const cask_file_view* files, uint32
   for (uint32_t i = 0; i < nfiles; ++i)
     if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
   std::lock_guard<std::mutex> g(c->mu);
-  return scan_device_impl(c, files, nfiles, rows, nullptr, file_row_offset, err);
-}
-
-extern "C" int cask_scan_device_segmented(cask_ctx* c, const cask_file_view* files, uint32_t nfiles,
-                                          cask_segments* seg, uint64_t* file_row_offset, cask_scan_error* err) {
-  if (!c || !seg) return CASK_E_INVALID_ARG;
-  for (uint32_t i = 0; i < nfiles; ++i)
-    if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  return scan_device_impl(c, files, nfiles, nullptr, seg, file_row_offset, err);
+  return scan_device_impl(c, files, nfiles, rows, file_row_offset, err);
 }
 
 extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
@@ -1040,7 +1019,7 @@ extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t
   dr.vsz = (uint32_t*)(rb + 2 * align_up(rcap * 8, 256));
   dr.ksz = (uint16_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256));
   dr.status = (uint8_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256) + align_up(rcap * 2, 256));
-  int rc = scan_device_impl(c, dv.data(), nfiles, &dr, nullptr, file_row_offset, err);
+  int rc = scan_device_impl(c, dv.data(), nfiles, &dr, file_row_offset, err);
   rows->count = dr.count;
   if (rc != CASK_OK) return rc;
   if (dr.count > rows->capacity) return CASK_E_CAPACITY;

@@ -180,25 +180,6 @@ class ScanContext:
         return ScanResult(int(r.count), rows["pos"], rows["seq"], rows["vsz"], rows["ksz"], rows["status"],
                           list(off), _err(e))
 
-    def scan_device_segmented(self, files):
-        """Segmented output (cask_scan_device_segmented): per-chunk slot rows owned by the context,
-        valid until the next call. Returns (Segments, file_row_offset, ScanFailure|None)."""
-        n = len(files)
-        views = (L.FileView * max(n, 1))()
-        for i, (fid, t) in enumerate(files):
-            assert t.is_cuda and t.dtype.itemsize == 1 and t.is_contiguous()
-            views[i].file_id = int(fid)
-            views[i].flags = L.VIEW_DEVICE
-            views[i].data = t.data_ptr() if t.numel() else None
-            views[i].len = t.numel()
-        seg = L.Segments()
-        off = (C.c_uint64 * (n + 1))()
-        e = L.ScanError()
-        self._inputs_ready()
-        rc = self.lib.cask_scan_device_segmented(self._h, views, n, C.byref(seg), off, C.byref(e))
-        raise_status(rc, what=f"cask_scan_device_segmented: {self.last_error()}")
-        return seg, list(off), _err(e)
-
     # -- host-resident ------------------------------------------------------------------------
     def scan_host(self, files) -> ScanResult:
         """files: list of (file_id, bytes | np.ndarray[uint8]). Rows come back as numpy arrays."""

@@ -118,27 +118,6 @@ uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles);
 int cask_scan_device(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
                      cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);
 
-/* Segmented device output (no dense compaction): the scan's own per-chunk slot rows. Chunk c of
- * the call holds count[c] rows at slots[(c * slot_cap + r) * 4 .. +4] (r < count[c]) as four u32:
- * seq low, seq high, value_size raw, ksz | (pos - chunk_start) << 16 | checksum_failed << 31,
- * where chunk_start = (c - first chunk of its file) * chunk_bytes; a row whose record runs past
- * the file end is the UnexpectedEof row. Row r of chunk c is row file_row_offset[f] + base[c] + r
- * of the dense order. All pointers are device memory owned by the context, valid until its next
- * call. Files map to consecutive chunk ranges of ceil(len / chunk_bytes) chunks each. */
-typedef struct cask_segments {
-  uint64_t nchunks;
-  uint32_t chunk_bytes;
-  uint32_t slot_cap;
-  const uint32_t* slots;
-  const uint32_t* count;
-  const uint64_t* base;
-  uint64_t total_rows;
-} cask_segments;
-
-int cask_scan_device_segmented(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
-                               cask_segments* out, uint64_t* file_row_offset,
-                               cask_scan_error* err);
-
 /* Same, for host-resident files and host row arrays: stages H2D, scans, copies rows D2H. */
 int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
                    cask_rows* rows, uint64_t* file_row_offset, cask_scan_error* err);

@@ -36,8 +36,8 @@ def child(path, steps, files, zipf_gib):
     views = [(f.file_id, f.data) for f in fs]
     rows = ctx.alloc_rows(n + 16)
     nbytes = sum(f.data.numel() for f in fs)
-    seg = os.environ.get("AB_SEGMENTED") == "1"  # time the segmented output instead
-    call = (lambda: ctx.scan_device_segmented(views)) if seg else (lambda: ctx.scan_device(views, rows))
+    seg = False
+    call = (lambda: ctx.scan_device(views, rows))
     for _ in range(3):
         call()
     torch.cuda.synchronize()
