@@ -777,8 +777,9 @@ void launch_walk_search(const ScanArgs& a, void* stream) {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk_search, 64, 0) == hipSuccess && nb > 0) per_cu = nb;
-    else per_cu = 12;
+    if (cask_knobs::tune("CASK_SEARCH_WAVES")) per_cu = atoi(cask_knobs::tune("CASK_SEARCH_WAVES"));  // (tuning)
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk_search, 64, 0) == hipSuccess && nb > 0) per_cu = nb;
+    if (per_cu <= 0) per_cu = 12;
   }
   uint64_t grid = (uint64_t)device_cus() * (uint64_t)per_cu;
   if (grid > nruns) grid = nruns;

@@ -145,11 +145,42 @@ __device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* fil
 // it leaves the range at (kTerm once an EOF row ended it, kNone if it never had a start). Chasing a
 // run as [t0, tm) and then [tm, t1) from the first range's exit writes exactly what one range
 // [t0, t1) writes: the chain is one walk either way.
+#ifdef CASK_CHASE_BATCH  // (A/B variant) slot rows staged in LDS, 8 (one 128-B line) per store burst
+// A lane's pending slot rows: consecutive rows of one chunk from `at` on, in LDS (the lane's 8 slots);
+// written out as one burst of up to 8 16-B stores when the line is full, the chunk changes or the
+// range ends, so that each 128-B line of rows reaches the L2 whole instead of a row per hop.
+struct RowBatch {
+  u32x4* buf;  // this lane's 8 LDS slots
+  g_u32x4* at = nullptr;
+  uint32_t n = 0;
+  __device__ __forceinline__ void flush() {
+    for (uint32_t k = 0; k < 8; ++k)
+      if (k < n) at[k] = buf[k];
+    n = 0;
+  }
+  __device__ __forceinline__ void put(g_u32x4* p, const u32x4& row) {
+    if (n && (n == 8 || p != at + n)) flush();
+    if (!n) at = p;
+    buf[n++] = row;
+  }
+};
+#endif
+
 __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t tb, uint64_t te,
                                 uint64_t p_in) {
   const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   g_u32* slots = (g_u32*)a.slots;
   g_u64* cd = (g_u64*)a.cdesc;
+#ifdef CASK_CHASE_BATCH
+  __shared__ u32x4 s_rows[256 * 8];
+  RowBatch rb;
+  rb.buf = s_rows + 8 * threadIdx.x;
+#define CHASE_ROW(addr, val) rb.put((g_u32x4*)(addr), (val))
+#define CHASE_FLUSH() rb.flush()
+#else
+#define CHASE_ROW(addr, val) (*(g_u32x4*)(addr) = (val))
+#define CHASE_FLUSH()
+#endif
   Walk W;
   W.cn = 0;
   W.ccerr = 0xFFFFFFFFu;
@@ -184,7 +215,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
         const uint32_t r = open_record(a, W, p, csh, true, &j);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
+        CHASE_ROW(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4, (u32x4{0u, 0u, 0u, off << 16}));
         if (r < W.ccerr) W.ccerr = r;
         term = true;
         break;
@@ -197,7 +228,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       h = gld16g((const g_u8*)(W.S.data + pl));
       const uint32_t r = open_record(a, W, p, csh, true, &j);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-      *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
+      CHASE_ROW(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4, (u32x4{row.x, row.y, row.z, row.w | (off << 16)}));
       if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
         if (r < W.ccerr) W.ccerr = r;
         term = true;
@@ -208,8 +239,11 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
     close_segment(a, W, term ? kTerm : p, true);
     if (term) p = kTerm;
   }
+  CHASE_FLUSH();
   return p;
 }
+#undef CHASE_ROW
+#undef CHASE_FLUSH
 
 // The chunk range of walk run i (an index into a.wruns, or the run itself): [t0, t1).
 __device__ __forceinline__ void walk_run_chunks(const ScanArgs& a, uint64_t i, uint64_t* t0, uint64_t* t1) {
