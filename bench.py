@@ -389,8 +389,9 @@ def main():
         bytes_all = int(tb_.item())
     value = bytes_all * args.steps / elapsed / 2 ** 30
 
-    walk = bool(counters.get("walk_mode"))
-    kname = "k_run_hash" if walk else "k_scan_chunks"
+    walk = int(counters.get("walk_mode") or 0)
+    # (a call that ran both modes times k_run_hash and k_scan_chunks as one span: cask_scan.h)
+    kname = {0: "k_scan_chunks", 1: "k_run_hash"}.get(walk, "k_run_hash+k_scan_chunks")
     k_avg = sum(t[1] for t in tt) / len(tt)
     achieved = bytes_per_step / (k_avg * 1e-3) / 1e9  # algorithmic GB/s of the dominant kernel
     traffic, traffic_src = load_traffic(kname)

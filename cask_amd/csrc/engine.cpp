@@ -523,7 +523,12 @@ struct EngineDev {
   } data, rows, hint;
   // pinned staging: reads of data files to the device, copies of results back to the host
   cask_host::PinnedRing ring;
-  cask_host::PinnedRing ring_out;  // open(): hint bodies back to the host while `ring` reads files in
+  // open(): hint bodies back to the host while `ring` reads files in. Hint bodies are ~1/8 of the data
+  // at most (22 + key bytes per record), so 4 threads' slots (256 MiB) are made, and only when the
+  // first hint copy is large enough to be staged; if they cannot be made, cask_copy carries it.
+  cask_host::PinnedRing ring_out;
+  bool ring_out_tried = false, ring_out_ok = false;
+  static constexpr int kOutThreads = 4;
   static constexpr int kReaders = cask_host::PinnedRing::kThreads;
   static constexpr size_t kSlotBytes = cask_host::PinnedRing::kBytes;
   cask_rows r{};
@@ -535,7 +540,7 @@ struct EngineDev {
       ctx = cask_ctx_create(device, &st);
       if (!ctx) return st;
     }
-    return ring.init(device) && ring_out.init(device) ? CASK_OK : CASK_E_NOMEM;
+    return ring.init(device) ? CASK_OK : CASK_E_NOMEM;
   }
 
   // Reader thread t takes every kReaders-th 32-MiB piece of the files, alternating between its two
@@ -601,9 +606,12 @@ struct EngineDev {
   // piece (CASK_STAGE_MIN=0 stages every copy: the tests run the small cases through it), the DMA of one piece into a slot overlapping the host copy of the previous piece out of
   // the other (a copy to pageable memory straight from the device runs at ~10 GB/s). Small copies
   // take cask_copy. The device work that produced `src` (on the context's stream) is waited for first.
-  int to_host(uint8_t* dst, const uint8_t* src, uint64_t n, cask_host::PinnedRing* rg = nullptr) {
+  static bool staged(uint64_t n) {
     const char* mv = cask_knobs::hook("CASK_STAGE_MIN");  // test knob: smallest copy staged (default 64 MiB)
-    if (n < (mv ? strtoull(mv, nullptr, 10) : (64ull << 20)) || !n) return cask_copy(ctx, dst, src, n);
+    return n && n >= (mv ? strtoull(mv, nullptr, 10) : (64ull << 20));
+  }
+  int to_host(uint8_t* dst, const uint8_t* src, uint64_t n, cask_host::PinnedRing* rg = nullptr) {
+    if (!staged(n)) return cask_copy(ctx, dst, src, n);
     if (hipSetDevice(device) != hipSuccess || hipStreamSynchronize((hipStream_t)cask_ctx_stream(ctx)) != hipSuccess)
       return CASK_E_DEVICE;
     std::vector<cask_host::PinnedRing::Piece> ps;
@@ -645,8 +653,14 @@ struct EngineDev {
     st = cask_hints_device(ctx, v.data(), (uint32_t)v.size(), &r, row_off.data(), hint.p, hint.cap, fo.data());
     if (st != CASK_OK) return st;
     if (!hbuf.resize(fo[v.size()])) return CASK_E_NOMEM;
-    if (!hbuf.empty() && to_host(hbuf.data(), hint.p, hbuf.size(), &ring_out) != CASK_OK) return CASK_E_DEVICE;
-    return CASK_OK;
+    if (hbuf.empty()) return CASK_OK;
+    if (staged(hbuf.size()) && !ring_out_tried) {
+      ring_out_tried = true;
+      ring_out_ok = ring_out.init(device, kOutThreads);
+      if (!ring_out_ok) ring_out.release();
+    }
+    if (staged(hbuf.size()) && !ring_out_ok) return cask_copy(ctx, hbuf.data(), hint.p, hbuf.size());
+    return to_host(hbuf.data(), hint.p, hbuf.size(), &ring_out) != CASK_OK ? CASK_E_DEVICE : CASK_OK;
   }
 };
 

@@ -98,6 +98,7 @@ struct PinnedRing {
   static constexpr int kThreads = 16, kSlots = 2;
   static constexpr size_t kBytes = 32ull << 20;
   int device = -1;
+  int nthr = kThreads;  // threads (and slot pairs) this ring was made with
   void* pin[kThreads][kSlots] = {};
   hipStream_t rs[kThreads] = {};
   hipEvent_t ev[kThreads][kSlots] = {};
@@ -116,11 +117,13 @@ struct PinnedRing {
   PinnedRing& operator=(const PinnedRing&) = delete;
   ~PinnedRing() { release(); }
 
-  // Allocates what is missing (on `dev`); false on failure (what was made stays for release()).
-  bool init(int dev) {
+  // Allocates what is missing (on `dev`) for `threads` threads; false on failure (what was made stays
+  // for release()).
+  bool init(int dev, int threads = kThreads) {
     device = dev;
+    nthr = std::max(1, std::min(threads, kThreads));
     if (hipSetDevice(dev) != hipSuccess) return false;
-    for (int t = 0; t < kThreads; ++t) {
+    for (int t = 0; t < nthr; ++t) {
       if (!rs[t] && hipStreamCreateWithFlags(&rs[t], hipStreamNonBlocking) != hipSuccess) return false;
       for (int k = 0; k < kSlots; ++k) {
         if (!pin[t][k] && !(pin[t][k] = pinned_alloc(kBytes))) return false;
@@ -207,8 +210,8 @@ struct PinnedRing {
   }
 
  private:
-  static unsigned threads_for(size_t pieces) {
-    return std::max(1u, std::min<unsigned>((unsigned)kThreads, std::min<unsigned>(host_threads(), (unsigned)pieces)));
+  unsigned threads_for(size_t pieces) const {
+    return std::max(1u, std::min<unsigned>((unsigned)nthr, std::min<unsigned>(host_threads(), (unsigned)pieces)));
   }
 };
 

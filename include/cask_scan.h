@@ -127,7 +127,8 @@ int cask_scan_host(cask_ctx* ctx, const cask_file_view* files, uint32_t nfiles,
  * [3] validation kernels, [4] repair (0 when speculation held), [5] compaction. */
 int cask_last_timings(const cask_ctx* ctx, float* ms6);
 /* The same six, then, in walk mode, [6] the run searches (k_walk_search) and [7] the header chase
- * (k_walk_chase); [1] is then the hashing kernel alone. */
+ * (k_walk_chase); [1] is then the hashing kernel alone (cask_last_walk() == 1), or the hashing
+ * kernel and k_scan_chunks together when one call ran both modes (cask_last_walk() == 2). */
 int cask_last_timings8(const cask_ctx* ctx, float* ms8);
 /* Counters of the last call: [0] chunks, [1] long records, [2] chunks from each file's first
  * invalid one on (0: speculation held), [3] local exact re-scans, [4] 1 if the serial boundary
