@@ -1537,6 +1537,17 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     std::vector<uint8_t> hints;
   };
   std::vector<OutFile> outs;
+  // (reserved: the writer thread below holds references into `outs` while placement appends to it.
+  // Two consecutive files hold more than max_file_size together — the second was opened because
+  // the first could not take its first record — so there are at most 2 x bytes / max + 1 of them.)
+  {
+    uint64_t in_bytes = del_key_bytes.size() + 18ull * del_seq.size();
+    for (uint32_t f : srcs) {
+      struct stat stt;
+      if (stat(data_path(path, f).c_str(), &stt) == 0) in_bytes += (uint64_t)stt.st_size;
+    }
+    outs.reserve(2 * (in_bytes / std::max<uint64_t>(db->opts.max_file_size, 1)) + 4);
+  }
   std::vector<uint32_t> new_files, tomb_files;
   uint64_t cur = 0;
   auto place = [&](uint64_t size, bool live) -> size_t {  // LogWriter::write's rollover
@@ -1565,7 +1576,8 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     return st;
   };
   // an exception before the new files are complete (std::bad_alloc while gathering or placing)
-  // removes them too, on its way to cask_db_compact_files' handler
+  // removes them too, on its way to cask_db_compact_files' handler (the writer thread, declared
+  // after this guard, is joined first)
   struct RemoveOnThrow {
     decltype(remove_outs)& f;
     bool armed = true;
@@ -1588,15 +1600,129 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     o.len += n;
     return true;
   };
-  auto write_all = [&](int fd, const uint8_t* b, uint64_t n) -> bool {
+  auto pwrite_all = [](int fd, const uint8_t* b, uint64_t n, uint64_t at) -> bool {
     while (n) {
-      const ssize_t w = write(fd, b, n);
+      const ssize_t w = pwrite(fd, b, n, (off_t)at);
       if (w < 0 && errno == EINTR) continue;
       if (w <= 0) return false;
       b += w;
+      at += (uint64_t)w;
       n -= (uint64_t)w;
     }
     return true;
+  };
+  // The live records' writes, one batch behind the device: a writer thread takes each batch's
+  // gathered bytes (in write order) while this thread reads, verifies and gathers the next batch
+  // on the device. Within a batch, the runs of records bound for one file (placement only moves
+  // forward: one run per file per batch) get their hints appended on a thread each, and their bytes
+  // written with pwrite in pieces of at most 64 MiB at their offsets in the file, all on threads.
+  struct WBatch {
+    std::unique_ptr<uint8_t[]> host;
+    std::vector<uint64_t> dst, len, foff;  // per record: offset in host, length, offset in its file
+    std::vector<size_t> oi;                // per record: its output file
+  };
+  struct Writer {
+    std::thread th;
+    std::mutex m;
+    std::condition_variable cv;
+    std::unique_ptr<WBatch> pending;
+    bool busy = false, quit = false;
+    uint32_t fail_fid = 0;
+    int status = CASK_OK;
+    double ms = 0;
+    void wait_idle() {
+      std::unique_lock<std::mutex> lk(m);
+      cv.wait(lk, [&] { return !busy && !pending; });
+    }
+    void stop() {
+      if (!th.joinable()) return;
+      {
+        std::lock_guard<std::mutex> g(m);
+        quit = true;
+      }
+      cv.notify_all();
+      th.join();
+    }
+    ~Writer() { stop(); }
+  } writer;
+  auto write_batch = [&](WBatch& B) -> int {  // (on the writer thread)
+    const uint64_t n = B.oi.size();
+    std::vector<std::pair<uint64_t, uint64_t>> runs;
+    for (uint64_t k = 0; k < n;) {
+      uint64_t e = k;
+      while (e < n && B.oi[e] == B.oi[k]) ++e;
+      runs.emplace_back(k, e);
+      k = e;
+    }
+    for (const auto& r : runs) {  // (fds opened here, on one thread)
+      OutFile& o = outs[B.oi[r.first]];
+      if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) {
+        writer.fail_fid = o.fid;
+        return CASK_E_IO;
+      }
+    }
+    struct Piece {
+      size_t run;
+      uint64_t at, n;  // host offset, bytes
+      uint64_t foff;
+    };
+    std::vector<Piece> pieces;
+    constexpr uint64_t kWPiece = 64ull << 20;
+    for (size_t r = 0; r < runs.size(); ++r) {
+      const uint64_t k = runs[r].first, e = runs[r].second;
+      const uint64_t a = B.dst[k], b = B.dst[e - 1] + B.len[e - 1];
+      for (uint64_t x = a; x < b; x += kWPiece) pieces.push_back(Piece{r, x, std::min(kWPiece, b - x), B.foff[k] + (x - a)});
+    }
+    std::vector<char> ok(runs.size(), 1);
+    const size_t ntask = runs.size() + pieces.size();  // tasks [0, runs): hints; then the pieces
+    const unsigned ntw = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)ntask));
+    parallel_for(ntw, [&](unsigned t) {
+      for (size_t x = t; x < ntask; x += ntw) {
+        if (x < runs.size()) {
+          for (uint64_t j = runs[x].first; j < runs[x].second; ++j) append(B.oi[j], B.host.get() + B.dst[j], B.len[j]);
+        } else {
+          const Piece& pc = pieces[x - runs.size()];
+          if (!pwrite_all(outs[B.oi[runs[pc.run].first]].fd, B.host.get() + pc.at, pc.n, pc.foff)) ok[pc.run] = 0;
+        }
+      }
+    });
+    for (size_t r = 0; r < runs.size(); ++r)
+      if (!ok[r]) {
+        writer.fail_fid = outs[B.oi[runs[r].first]].fid;
+        return CASK_E_IO;
+      }
+    return CASK_OK;
+  };
+  // an error while the writer may hold a batch: it finishes (or skips) that batch and stops before
+  // the files are removed
+  auto abort_w = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
+    writer.stop();
+    return abort_with(st, fid, pos, e, f);
+  };
+  auto start_writer = [&]() {
+    writer.th = std::thread([&] {
+      for (;;) {
+        std::unique_ptr<WBatch> B;
+        {
+          std::unique_lock<std::mutex> lk(writer.m);
+          writer.cv.wait(lk, [&] { return writer.quit || writer.pending; });
+          if (!writer.pending) return;  // quit
+          B = std::move(writer.pending);
+          writer.busy = true;
+        }
+        const auto tw0 = std::chrono::steady_clock::now();
+        const int st = writer.status == CASK_OK ? abi_status([&] { return write_batch(*B); }) : writer.status;
+        const double dt = ms_since(tw0);
+        B.reset();  // (the batch's host bytes go before the next one is taken)
+        {
+          std::lock_guard<std::mutex> g(writer.m);
+          if (writer.status == CASK_OK) writer.status = st;
+          writer.ms += dt;
+          writer.busy = false;
+        }
+        writer.cv.notify_all();
+      }
+    });
   };
   double t_verify = 0, t_gather = 0, t_write = 0;
   std::vector<uint64_t> slen(ns, 0);
@@ -1606,10 +1732,10 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   }
   if (!ins.empty()) {
     EngineDev* ed = engine_dev(db->opts.device);
-    if (!ed) return abort_with(CASK_E_DEVICE);
+    if (!ed) return abort_w(CASK_E_DEVICE);
     std::lock_guard<std::mutex> g(ed->mu);
     int st = ed->prepare();
-    if (st != CASK_OK) return abort_with(st);
+    if (st != CASK_OK) return abort_w(st);
     constexpr uint64_t kBatch = 16ull << 30;
     size_t k0 = 0;
     for (size_t b0 = 0; b0 < ns;) {
@@ -1617,7 +1743,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       size_t b1 = b0 + 1;
       uint64_t bytes = (slen[b0] + 255) & ~255ull;
       while (b1 < ns && bytes + ((slen[b1] + 255) & ~255ull) <= kBatch) bytes += (slen[b1++] + 255) & ~255ull;
-      if (!ed->data.ensure(bytes + 256)) return abort_with(CASK_E_NOMEM);
+      if (!ed->data.ensure(bytes + 256)) return abort_w(CASK_E_NOMEM);
       std::vector<std::string> paths;
       std::vector<cask_file_view> views;
       std::vector<const uint8_t*> dsrc;
@@ -1629,9 +1755,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         off += (slen[i] + 255) & ~255ull;
       }
       std::vector<char> okr(views.size(), 1);
-      if ((st = ed->read_to_device(paths, views, okr)) != CASK_OK) return abort_with(st);
+      if ((st = ed->read_to_device(paths, views, okr)) != CASK_OK) return abort_w(st);
       for (size_t i = 0; i < okr.size(); ++i)  // File::open / read failed: Io (log.rs:150-166)
-        if (!okr[i]) return abort_with(CASK_E_IO, srcs[b0 + i]);
+        if (!okr[i]) return abort_w(CASK_E_IO, srcs[b0 + i]);
       R.bytes_in += off;
       size_t k1 = k0;
       while (k1 < ins.size() && ins[k1].src < b1) ++k1;
@@ -1647,16 +1773,20 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       std::vector<uint64_t> blen(slen.begin() + b0, slen.begin() + b1);
       st = cask_read_entries_device(ed->ctx, dsrc.data(), blen.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), n,
                                     len.data(), stv.data(), ex.data(), fd.data());
-      if (st != CASK_OK) return abort_with(st);
+      if (st != CASK_OK) return abort_w(st);
       for (uint64_t k = 0; k < n; ++k)  // in write order: the first failure is the reference's
         if (stv[k] != CASK_ROW_OK)
-          return stv[k] == CASK_ROW_EOF ? abort_with(CASK_E_EOF, srcs[ins[k0 + k].src], pos[k])
-                                        : abort_with(CASK_E_CHECKSUM, srcs[ins[k0 + k].src], pos[k], ex[k], fd[k]);
+          return stv[k] == CASK_ROW_EOF ? abort_w(CASK_E_EOF, srcs[ins[k0 + k].src], pos[k])
+                                        : abort_w(CASK_E_CHECKSUM, srcs[ins[k0 + k].src], pos[k], ex[k], fd[k]);
       t_verify += ms_since(tv);
       // placement and the batch's bytes, gathered on the device in write order
       auto tg = std::chrono::steady_clock::now();
-      std::vector<uint64_t> dst(n);
-      std::vector<size_t> oi(n);
+      std::unique_ptr<WBatch> WB(new WBatch());
+      std::vector<uint64_t>& dst = WB->dst;
+      std::vector<size_t>& oi = WB->oi;
+      dst.resize(n);
+      oi.resize(n);
+      WB->foff.resize(n);
       // the gather's pieces: a record longer than kPiece (value sizes reach 0xFFFFFFFE B, data.rs:13)
       // goes as several consecutive pieces of at most kPiece bytes
       constexpr uint64_t kPiece = 1ull << 31;
@@ -1669,6 +1799,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       uint64_t total = 0;
       for (uint64_t k = 0; k < n; ++k) {
         oi[k] = place(len[k], true);
+        WB->foff[k] = cur - len[k];  // (its offset in its file: placement just added it)
         dst[k] = total;
         for (uint64_t o = 0; o < len[k]; o += kPiece) {
           gsrc.push_back(src[k]);
@@ -1678,42 +1809,38 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         }
         total += len[k];
       }
-      std::unique_ptr<uint8_t[]> host(new (std::nothrow) uint8_t[std::max<uint64_t>(total, 1)]);
-      if (!host) return abort_with(CASK_E_NOMEM);
+      // (the previous batch's writes are still going on: its host bytes and this one's both live)
+      WB->host.reset(new (std::nothrow) uint8_t[std::max<uint64_t>(total, 1)]);
+      if (!WB->host) return abort_w(CASK_E_NOMEM);
       if (total) {
-        if (!ed->hint.ensure(total + 256)) return abort_with(CASK_E_NOMEM);
+        if (!ed->hint.ensure(total + 256)) return abort_w(CASK_E_NOMEM);
         st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), gsrc.data(), gpos.data(), gdst.data(),
                                 glen.data(), (uint64_t)glen.size(), ed->hint.p);
-        if (st == CASK_OK) st = ed->to_host(host.get(), ed->hint.p, total);
-        if (st != CASK_OK) return abort_with(st);
+        if (st == CASK_OK) st = ed->to_host(WB->host.get(), ed->hint.p, total);
+        if (st != CASK_OK) return abort_w(st);
       }
+      WB->len.assign(len.begin(), len.end());
       t_gather += ms_since(tg);
+      // hand the batch to the writer once it has taken the previous one
       auto tw = std::chrono::steady_clock::now();
-      // runs of records bound for one file (placement only moves forward): each run's hints and its
-      // one write, runs on threads (distinct files)
-      std::vector<std::pair<uint64_t, uint64_t>> runs;
-      for (uint64_t k = 0; k < n;) {
-        uint64_t e = k;
-        while (e < n && oi[e] == oi[k]) ++e;
-        runs.emplace_back(k, e);
-        k = e;
+      if (!writer.th.joinable()) start_writer();
+      writer.wait_idle();
+      if (writer.status != CASK_OK) return abort_w(writer.status, writer.fail_fid);
+      {
+        std::lock_guard<std::mutex> g(writer.m);
+        writer.pending = std::move(WB);
       }
-      std::vector<char> wok(runs.size(), 1);
-      const unsigned ntw = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)runs.size()));
-      parallel_for(ntw, [&](unsigned t) {
-        for (size_t r = t; r < runs.size(); r += ntw) {
-          const uint64_t k = runs[r].first, e = runs[r].second;
-          for (uint64_t j = k; j < e && wok[r]; ++j) wok[r] = append(oi[j], host.get() + dst[j], len[j]);
-          if (wok[r]) wok[r] = write_all(outs[oi[k]].fd, host.get() + dst[k], dst[e - 1] + len[e - 1] - dst[k]);
-        }
-      });
-      for (size_t r = 0; r < runs.size(); ++r)
-        if (!wok[r]) return abort_with(CASK_E_IO, outs[oi[runs[r].first]].fid);
-      t_write += ms_since(tw);
+      writer.cv.notify_all();
+      t_write += ms_since(tw);  // (the time this thread waited for the writer)
       k0 = k1;
       b0 = b1;
     }
   }
+  // the last batch's writes; the writer's own time is in R.ms[3]
+  writer.wait_idle();
+  writer.stop();
+  t_write += writer.ms;
+  if (writer.status != CASK_OK) return abort_with(writer.status, writer.fail_fid);
   R.ms[1] = t_verify;
   R.ms[2] = t_gather;
   // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen
@@ -1722,9 +1849,10 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   {
     std::vector<uint8_t> run;
     size_t run_file = SIZE_MAX;
+    uint64_t run_at = 0;  // the run's offset in its file (the live records went in with pwrite)
     auto flush = [&]() -> bool {
       if (run.empty()) return true;
-      const bool ok = write_all(outs[run_file].fd, run.data(), run.size());
+      const bool ok = pwrite_all(outs[run_file].fd, run.data(), run.size(), run_at);
       run.clear();
       return ok;
     };
@@ -1738,6 +1866,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       if (o != run_file) {
         if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
         run_file = o;
+        run_at = outs[o].len;
       }
       const size_t at = run.size();
       run.insert(run.end(), rec_h, rec_h + 18);
