@@ -48,6 +48,8 @@ def child(path, steps, files, zipf_gib):
         k.append(ctx.last_timings()["chunk_scan_ms"])
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if os.environ.get("AB_NOCHECK") == "1":  # timing diagnostics whose rows are known wrong
+        want = None
     if want is not None and not seg:  # the last call's rows against the generator (a variant that
         res = call()                   # is fast and wrong fails here)
         torch.cuda.synchronize()
