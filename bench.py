@@ -141,6 +141,34 @@ def cpu_baseline(files, nfiles: int, cfg: str):
     }
 
 
+def stream_ceiling(torch, dev, views, passes: int = 5):
+    """The measured read-only stream ceiling over the same resident files:
+    cask_amd/libcask_stream.so reads every byte once per pass (plain and nontemporal loads, the
+    better of the two), HIP events around `passes` launches. None when the utility is not built."""
+    p = os.path.join(ROOT, "cask_amd", "libcask_stream.so")
+    if not os.path.exists(p):
+        return None
+    lib = C.CDLL(p)
+    fn = lib.cask_stream_read
+    fn.restype = C.c_int
+    fn.argtypes = [C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_uint32, C.c_uint32, C.c_int, C.c_int,
+                   C.POINTER(C.c_double), C.POINTER(C.c_double)]
+    n = len(views)
+    bufs = (C.c_void_p * n)(*[t.data_ptr() for _, t in views])
+    lens = (C.c_uint64 * n)(*[t.numel() for _, t in views])
+    torch.cuda.synchronize(dev)
+    out = {}
+    for nt in (0, 1):
+        g, ms = C.c_double(), C.c_double()
+        rc = fn(bufs, lens, n, passes, nt, dev.index, C.byref(g), C.byref(ms))
+        if rc != 0:
+            return {"error": f"cask_stream_read: HIP error {rc}"}
+        out["nontemporal" if nt else "plain"] = {"gbps": g.value, "ms_per_pass": ms.value}
+    best = max(v["gbps"] for v in out.values())
+    return {"gbps": best, "frac_of_8TBps": best / HBM_PEAK_GBPS, "bytes_per_pass": int(sum(lens)),
+            "passes": passes, "kernel": "k_stream_read (cask_amd/csrc/stream_ceiling.hip)", **out}
+
+
 def load_traffic(kernel: str):
     """Per-launch HBM bytes of `kernel` from the committed rocprofv3 PMC passes
     (profiles/pmc_traffic.json, written by tools/pmc_summary.py); null when absent."""
@@ -395,6 +423,8 @@ def main():
     k_avg = sum(t[1] for t in tt) / len(tt)
     achieved = bytes_per_step / (k_avg * 1e-3) / 1e9  # algorithmic GB/s of the dominant kernel
     traffic, traffic_src = load_traffic(kname)
+    # the read-only stream ceiling over the same bytes, beside the roofline (not in `value`)
+    ceiling = stream_ceiling(torch, dev, views) if rank == 0 else None
     names = ["pipeline_ms", "hash_or_chunk_scan_ms", "long_ms", "validate_ms", "repair_ms", "compact_ms",
              "search_ms", "chase_ms"]
     breakdown = {nm: sum(t[i] for t in tt) / len(tt) for i, nm in enumerate(names)}
@@ -537,6 +567,8 @@ def main():
                 "traffic_source": traffic_src,
                 "kernel_ms_avg": k_avg,
                 "algorithmic_bytes_per_launch": bytes_per_step,
+                "stream_ceiling": ceiling,
+                "frac_of_stream_ceiling": (achieved / ceiling["gbps"]) if ceiling and "gbps" in ceiling else None,
             },
             "cpu_baseline": cpu,
             "counters": counters,

@@ -363,9 +363,9 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
 
   // a quad's current record (cv) and the round of it in hand: blocks [rlb, rlb + rnl) of its full
   // 64-B blocks, rfin if the record ends in this round (its partial block in T), head if it is the
-  // record's first (its stored checksum in xst); tclamp: the partial stripe is near the file end
-  bool cv = false, rfin = false, head = false, tclamp = false;
-  uint64_t cbase = 0, crl = 0, cend = 0, ct_t = 0;
+  // record's first (its stored checksum in xst)
+  bool cv = false, rfin = false, head = false;
+  uint64_t cbase = 0, crl = 0, ct_t = 0;
   uint32_t cnblk = 0, crem = 0, rlb = 0, rnl = 0, v = 0, cstored = 0, ct_r = 0, cw3 = 0;
   // its next record: ns = 0 none, 1 slot row + chunk address loading (issued last iteration), 2 ready
   uint32_t ns = 0;
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     // (an UnexpectedEof row, cut by the file's end, has failed already: nothing to hash)
     const bool round2 = cont || (promote && bn + rln <= en);
     const uint32_t lb2 = cont ? rlb + D : 0u;
-    const uint64_t base2 = cont ? cbase : bn, rl2 = cont ? crl : rln, end2 = cont ? cend : en;
+    const uint64_t base2 = cont ? cbase : bn, rl2 = cont ? crl : rln;
     const uint32_t nblk2 = cont ? cnblk : (uint32_t)((rln - 4) >> 6);
     const uint32_t rb2 = cont ? crem : (uint32_t)((rln - 4) & 63);
     const uint32_t left = nblk2 - lb2;
@@ -486,12 +486,14 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     uint64_t ya[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;
-    const bool tail2 = round2 && fin2 && rb2 != 0;  // the record's partial last block, into T
-    const uint64_t end16 = (end2 + 15) & ~15ull;
+    // the record's partial last block, into T: the lanes of its full stripes load them, the lane of
+    // its partial stripe the record's last 16 bytes (ending where the record ends: no load reaches
+    // past the record into a line that the next record's quad reads at another time, nor past the
+    // file's end), the others the safe line
+    const bool tail2 = round2 && fin2 && rb2 != 0;
+    const uint32_t rq2 = rb2 >> 4;
     const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
-    const uint64_t tpart = base2 + 4 + 64ull * nblk2 + 16ull * (rb2 >> 4);
-    const bool tclamp2 = tail2 && (rb2 & 15) != 0 && tpart + 16 > end16;
-    uint64_t ta = tail2 ? (tq + 16 <= end16 ? tq : end16 - 16) : safe;
+    uint64_t ta = tail2 && q < rq2 ? tq : tail2 && q == rq2 && (rb2 & 15) != 0 ? base2 + rl2 - 16 : safe;
     uint64_t sa = round2 && !cont ? base2 : safe;
     asm volatile("" : "+v"(arow), "+v"(sa), "+v"(ta));
 #pragma unroll
@@ -537,11 +539,8 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         tw.y = (uint32_t)__shfl((int)T.y, src, 64);
         tw.z = (uint32_t)__shfl((int)T.z, src, 64);
         tw.w = (uint32_t)__shfl((int)T.w, src, 64);
-        // the file ends within the partial stripe's 16 bytes: its lane loaded the file's last
-        // granule instead, which holds the stripe from byte xs - (e16 - 16) on
-        const uint64_t xs = cbase + 4 + 64ull * cnblk + 16ull * rem;
-        const uint64_t e16 = (cend + 15) & ~15ull;
-        tw = shr_bytes(tw, tclamp ? (uint32_t)(xs - (e16 - 16)) : 0u);
+        // the partial stripe's lane loaded the record's last 16 bytes: the stripe from byte 16 - tb on
+        tw = shr_bytes(tw, tb ? 16u - tb : 0u);
         const uint32_t n4 = tb >> 2, n1 = tb & 3;
         h = n4 > 0 ? tail4(h, tw.x) : h;
         h = n4 > 1 ? tail4(h, tw.y) : h;
@@ -564,19 +563,16 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       rlb = lb2;
       rnl = nl2;
       rfin = fin2;
-      tclamp = tclamp2;
       head = false;
     } else {
       cv = promote && round2;
       cbase = base2;
       crl = rl2;
-      cend = end2;
       cnblk = nblk2;
       crem = rb2;
       rlb = 0;
       rnl = nl2;
       rfin = fin2;
-      tclamp = tclamp2;
       head = true;
       v = vinit;
       ct_t = pt;

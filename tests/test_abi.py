@@ -32,6 +32,23 @@ def test_exports_every_declared_symbol(native):
         assert hasattr(native, name), name
 
 
+def test_stream_ceiling_utility_loads():
+    """bench.py's read-only stream ceiling (cask_amd/libcask_stream.so, built by build()): it loads,
+    exports its one entry point and rejects bad arguments before touching a device."""
+    import ctypes as C
+    p = os.path.join(ROOT, "cask_amd", "libcask_stream.so")
+    if not os.path.exists(p):
+        pytest.skip("libcask_stream.so not built")
+    lib = C.CDLL(p)
+    fn = lib.cask_stream_read
+    fn.restype = C.c_int
+    g = C.c_double()
+    assert fn(None, None, 0, 1, 0, 0, C.byref(g), None) != 0
+    bufs, lens = (C.c_void_p * 1)(), (C.c_uint64 * 1)(16)
+    assert fn(bufs, lens, 65, 1, 0, 0, C.byref(g), None) != 0  # more buffers than it takes
+    assert fn(bufs, lens, 1, 0, 0, 0, C.byref(g), None) != 0   # no passes
+
+
 def test_host_xxh32_kat(native):
     import cask_amd
     with open(os.path.join(GOLDEN, "kat.json")) as f:

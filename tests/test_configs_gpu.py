@@ -145,3 +145,17 @@ def test_cfg2_full_size_corrupted_against_oracle(gpu_ctx, cfg2):
             _assert_rows_equal(_dev_rows(res, res.file_rows(i)), w, f"{mode}: file {fd.file_id}")
         e = res.error
         assert (e.kind, e.file_id, e.pos, e.expected, e.found) == first, mode
+
+
+def test_stream_ceiling_measures_resident_bytes():
+    """bench.py's stream ceiling on a few resident buffers: a positive rate in both load policies,
+    below the 8 TB/s peak (it reads what it says it reads: 3 buffers, 16-B-rounded lengths)."""
+    import torch
+    import bench
+    dev = torch.device("cuda", 0)
+    bufs = [torch.ones(n, dtype=torch.uint8, device=dev) for n in (1 << 30, (512 << 20) + 7, 256 << 20)]
+    c = bench.stream_ceiling(torch, dev, [(i + 1, b) for i, b in enumerate(bufs)], passes=3)
+    assert c is not None and "error" not in c, c
+    assert c["bytes_per_pass"] == sum(b.numel() for b in bufs)
+    for k in ("plain", "nontemporal"):
+        assert 100.0 < c[k]["gbps"] < bench.HBM_PEAK_GBPS, c
