@@ -482,7 +482,11 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     // of the iteration's loads is in a register before the first load issues: an address built
     // after a load may be built in that load's destination, a write that waits for every load in
     // flight.
+#ifdef CASK_HASH_ALIGNDIAG  // (timing diagnostic only, wrong checksums: each round from its 128-B line)
+    const uint64_t bpa = ((base2 + 4 + 64ull * lb2) & ~127ull) + 16ull * q;
+#else
     const uint64_t bpa = base2 + 4 + 64ull * lb2 + 16ull * q;
+#endif
     uint64_t ya[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;

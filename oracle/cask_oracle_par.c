@@ -7,8 +7,12 @@
  * occupant's own add, or the add just before a stale record's remove), so the fold splits exactly
  * by key: each partition of the key space folds its keys in replay order (file, pos) into its own
  * index (orc_index_update, the restatement of cask.rs:60-90), and the per-file counters of the
- * partitions add up. The scan per file is Entries::next + Entry::from_read (log.rs:403-429,
- * data.rs:161-206); the first failure in replay order ends the replay (cask.rs:360,365).
+ * partitions add up. The scan is Entries::next + Entry::from_read (log.rs:403-429,
+ * data.rs:161-206) in two passes: each file's chain of record lengths from the headers (files on
+ * threads), then every record's checksum with the records split over the threads by byte range (so
+ * a sample of a few large files still uses every thread); a file's first failure is its first
+ * failing checksum before the chain's cut-short record, else that record, and the first failure in
+ * replay order ends the replay (cask.rs:360,365).
  */
 #include <pthread.h>
 #include <stdlib.h>
@@ -66,9 +70,12 @@ typedef struct {
   const uint8_t* const* bufs;
   const uint64_t* lens;
   const uint32_t* fids;
-  uint32_t nfiles, nparts;
+  uint32_t nfiles, nparts, nthreads;
+  uint64_t** offs;  /* per file: the record chain's offsets, up to its first cut-short record */
   prow** rows;      /* per file: its Ok rows before its first failure */
   uint64_t* nrows;
+  uint64_t* fbad;   /* per file: the index of its first record whose checksum fails (UINT64_MAX none) */
+  uint64_t* fbyte;  /* prefix of the file lengths: the byte ranges the verify threads split */
   int32_t* ferr;    /* per file: the first failure's kind (0 none), pos, expected, found */
   uint64_t* fpos;
   uint32_t *fexp, *ffound;
@@ -76,7 +83,7 @@ typedef struct {
   orc_index** ix;   /* per partition */
   uint64_t* pmax;   /* per partition: max sequence */
   uint64_t* pdig;   /* per partition: digest */
-  uint32_t next;    /* work counter of the scan */
+  uint32_t next;    /* work counter of the chain walk */
   pthread_mutex_t mu;
 } pjob;
 
@@ -87,46 +94,85 @@ static uint32_t take(pjob* j) {
   return v;
 }
 
-static void* scan_worker(void* arg) {
+/* 1. Entries::next per file (log.rs:403-429): the chain of record lengths from the headers alone,
+ * to the first record cut short by the file's end (Io(UnexpectedEof), data.rs:163,172,181: a
+ * record's reads fail before its checksum is computed). Files on threads. */
+static void* walk_worker(void* arg) {
   pjob* j = (pjob*)arg;
   for (uint32_t f; (f = take(j)) < j->nfiles;) {
     const uint8_t* b = j->bufs[f];
     const uint64_t len = j->lens[f];
-    prow* r = (prow*)malloc((len / 18 + 1) * sizeof(prow));
+    uint64_t* o = (uint64_t*)malloc((len / 18 + 1) * sizeof(uint64_t));
     uint64_t n = 0, pos = 0;
     while (pos < len) {
-      if (len - pos < 18) { /* header cut short: Io(UnexpectedEof) (data.rs:163) */
+      if (len - pos < 18) { /* header cut short */
         j->ferr[f] = ORC_ROW_EOF;
         j->fpos[f] = pos;
         break;
       }
       const uint8_t* h = b + pos;
-      const uint16_t ksz = rd16(h + 12);
       const uint32_t vsz = rd32(h + 14);
-      const uint64_t rl = 18 + (uint64_t)ksz + (vsz == ORC_ENTRY_TOMBSTONE ? 0 : vsz);
-      if (len - pos < rl) { /* key or value cut short (data.rs:172,181) */
+      const uint64_t rl = 18 + (uint64_t)rd16(h + 12) + (vsz == ORC_ENTRY_TOMBSTONE ? 0 : vsz);
+      if (len - pos < rl) { /* key or value cut short */
         j->ferr[f] = ORC_ROW_EOF;
         j->fpos[f] = pos;
         break;
       }
-      const uint32_t found = orc_xxh32(h + 4, rl - 4, 0);
-      if (found != rd32(h)) { /* InvalidChecksum (data.rs:193-198) */
-        j->ferr[f] = ORC_ROW_CHECKSUM;
-        j->fpos[f] = pos;
-        j->fexp[f] = rd32(h);
-        j->ffound[f] = found;
-        break;
+      o[n++] = pos;
+      pos += rl;
+    }
+    j->offs[f] = o;
+    j->nrows[f] = n;
+    j->rows[f] = (prow*)malloc((n + 1) * sizeof(prow));
+  }
+  return NULL;
+}
+
+typedef struct {
+  pjob* j;
+  uint32_t t;
+} pverify;
+
+/* 2. Entry::from_read's checksum (data.rs:185-198) of every walked record, the records split over
+ * threads by byte range (a record belongs to the thread whose range holds its first byte); each
+ * file's first failing index is kept (an atomic minimum). */
+static void* verify_worker(void* arg) {
+  const pverify* a = (const pverify*)arg;
+  pjob* j = a->j;
+  const uint64_t total = j->fbyte[j->nfiles];
+  const uint64_t b0 = (uint64_t)(((unsigned __int128)total * a->t) / j->nthreads);
+  const uint64_t b1 = (uint64_t)(((unsigned __int128)total * (a->t + 1)) / j->nthreads);
+  for (uint32_t f = 0; f < j->nfiles; ++f) {
+    const uint64_t fs = j->fbyte[f], fe = j->fbyte[f + 1];
+    if (fe <= b0 || fs >= b1 || !j->nrows[f]) continue;
+    const uint64_t* o = j->offs[f];
+    const uint64_t n = j->nrows[f];
+    const uint64_t s = b0 > fs ? b0 - fs : 0, e = b1 - fs; /* offsets in [s, e) of this file */
+    uint64_t i = 0, hi = n; /* the first record at or after s */
+    while (i < hi) {
+      const uint64_t m = (i + hi) / 2;
+      if (o[m] < s) i = m + 1; else hi = m;
+    }
+    const uint8_t* b = j->bufs[f];
+    prow* r = j->rows[f];
+    for (; i < n && o[i] < e; ++i) {
+      const uint8_t* h = b + o[i];
+      const uint16_t ksz = rd16(h + 12);
+      const uint32_t vsz = rd32(h + 14);
+      const uint64_t rl = 18 + (uint64_t)ksz + (vsz == ORC_ENTRY_TOMBSTONE ? 0 : vsz);
+      if (orc_xxh32(h + 4, rl - 4, 0) != rd32(h)) {
+        uint64_t cur = __atomic_load_n(&j->fbad[f], __ATOMIC_RELAXED);
+        while (i < cur && !__atomic_compare_exchange_n(&j->fbad[f], &cur, i, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {
+        }
+        continue;
       }
-      prow* x = &r[n++];
-      x->pos = pos;
+      prow* x = &r[i];
+      x->pos = o[i];
       x->seq = rd64(h + 4);
       x->vsz = vsz;
       x->ksz = ksz;
       x->part = (uint8_t)(part_hash(h + 18, ksz) % j->nparts);
-      pos += rl;
     }
-    j->rows[f] = r;
-    j->nrows[f] = n;
   }
   return NULL;
 }
@@ -192,16 +238,42 @@ orc_pindex* orc_pindex_build(const uint8_t* const* bufs, const uint64_t* lens, c
   j.fids = file_ids;
   j.nfiles = nfiles;
   j.nparts = nthreads;
+  j.nthreads = nthreads;
+  j.offs = (uint64_t**)calloc(nfiles + 1, sizeof(uint64_t*));
   j.rows = (prow**)calloc(nfiles + 1, sizeof(prow*));
   j.nrows = (uint64_t*)calloc(nfiles + 1, 8);
+  j.fbad = (uint64_t*)malloc((nfiles + 1) * 8);
+  j.fbyte = (uint64_t*)calloc(nfiles + 1, 8);
   j.ferr = (int32_t*)calloc(nfiles + 1, 4);
   j.fpos = (uint64_t*)calloc(nfiles + 1, 8);
   j.fexp = (uint32_t*)calloc(nfiles + 1, 4);
   j.ffound = (uint32_t*)calloc(nfiles + 1, 4);
+  for (uint32_t f = 0; f < nfiles; ++f) {
+    j.fbad[f] = UINT64_MAX;
+    j.fbyte[f + 1] = j.fbyte[f] + lens[f];
+  }
   pthread_mutex_init(&j.mu, NULL);
   pthread_t th[64];
-  for (uint32_t t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, scan_worker, &j);
+  for (uint32_t t = 0; t < nthreads; ++t) pthread_create(&th[t], NULL, walk_worker, &j);
   for (uint32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  pverify va[64];
+  for (uint32_t t = 0; t < nthreads; ++t) {
+    va[t].j = &j;
+    va[t].t = t;
+    pthread_create(&th[t], NULL, verify_worker, &va[t]);
+  }
+  for (uint32_t t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  /* each file's first failure: a checksum failure before the walk's cut-short record, else that */
+  for (uint32_t f = 0; f < nfiles; ++f) {
+    if (j.fbad[f] == UINT64_MAX) continue;
+    const uint8_t* h = bufs[f] + j.offs[f][j.fbad[f]];
+    const uint64_t rl = 18 + (uint64_t)rd16(h + 12) + (rd32(h + 14) == ORC_ENTRY_TOMBSTONE ? 0 : rd32(h + 14));
+    j.ferr[f] = ORC_ROW_CHECKSUM;
+    j.fpos[f] = j.offs[f][j.fbad[f]];
+    j.fexp[f] = rd32(h);
+    j.ffound[f] = orc_xxh32(h + 4, rl - 4, 0);
+    j.nrows[f] = j.fbad[f];
+  }
   j.stop = nfiles;
   for (uint32_t f = 0; f < nfiles; ++f)
     if (j.ferr[f]) {
@@ -260,7 +332,13 @@ orc_pindex* orc_pindex_build(const uint8_t* const* bufs, const uint64_t* lens, c
   orc_pindex* out = (orc_pindex*)malloc(sizeof(orc_pindex));
   out->ix = j.ix;
   out->nparts = j.nparts;
-  for (uint32_t f = 0; f < nfiles; ++f) free(j.rows[f]);
+  for (uint32_t f = 0; f < nfiles; ++f) {
+    free(j.rows[f]);
+    free(j.offs[f]);
+  }
+  free(j.offs);
+  free(j.fbad);
+  free(j.fbyte);
   free(j.pmax);
   free(j.pdig);
   free(j.rows);

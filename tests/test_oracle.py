@@ -317,6 +317,32 @@ def test_parallel_replay_matches_serial(oracle_lib, threads):
     assert (r2.err_kind, r2.err_file_id, r2.err_pos) == (int(first["status"]), fids[3], int(first["pos"]))
 
 
+@pytest.mark.parametrize("threads", [2, 8])
+def test_parallel_replay_splits_one_file_over_threads(oracle_lib, threads):
+    """A sample of one large file uses every thread (the checksums split by byte range) and still
+    folds in order; a corrupted value size (a record cut short: UnexpectedEof) and a checksum
+    failure before it end the replay where the serial scan's first failure is."""
+    rng = random.Random(7 + threads)
+    ents = _log_entries(rng, 5000, nkeys=700, p_del=0.1)
+    buf = b"".join(e.write_bytes() for e in ents)
+    ix = O.Index()
+    rr = O.replay_fast(np.frombuffer(buf, np.uint8), 9, ix)
+    r, stats = O.replay_parallel([buf], [9], threads)
+    assert r.err_kind == 0 and r.records == len(ents) == rr.records
+    assert (r.live, r.max_seq, r.digest) == (len(ix), rr.max_seq, ix.digest())
+    assert stats == ix.stats()
+    offs = np.cumsum([0] + [len(e.write_bytes()) for e in ents])
+    for cut, flip in ((3000, None), (3000, 1200), (4999, 10)):
+        bad = bytearray(buf)
+        bad[offs[cut] + 17] = 0x7F  # value size's high byte: the record runs past the file's end
+        if flip is not None:
+            bad[offs[flip] + 20] ^= 0x40  # a key byte of an earlier record: its checksum fails
+        want = O.scan(bytes(bad))
+        k = int(np.flatnonzero(want["status"] != 0)[0])  # the replay keeps the rows before it
+        r2, _ = O.replay_parallel([bytes(bad)], [9], threads)
+        assert (r2.err_kind, r2.err_pos, r2.records) == (int(want["status"][k]), int(want["pos"][k]), k), (cut, flip)
+
+
 def test_keydir_digest_numpy_equals_c(oracle_lib):
     """The vectorised digest the GPU tests apply to a product export equals the C oracle's."""
     rng = np.random.default_rng(3)
