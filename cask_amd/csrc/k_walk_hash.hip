@@ -259,7 +259,18 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nruns; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t t0, t1;
     walk_run_chunks(a, i, &t0, &t1);
+#ifdef CASK_SEARCH_CHASE_OVERLAP
+    // the chase runs beside k_walk_search: each lane waits for its run's start to be published
+    // (tin[t0] leaves kPending with a release store; the lanes of a wave hold consecutive runs,
+    // which the search claims in order)
+    uint64_t s = kNone;
+    if (a.walk_pre)
+      while ((s = __hip_atomic_load(&a.tin[t0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == kPending)
+        __builtin_amdgcn_s_sleep(16);
+    (void)chase_range(a, files, t0, t1, s);
+#else
     (void)chase_range(a, files, t0, t1, a.walk_pre ? a.tin[t0] : kNone);
+#endif
   }
 }
 
