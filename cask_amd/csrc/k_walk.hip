@@ -243,13 +243,8 @@ __device__ __forceinline__ uint64_t walk_search(SearchLds& L, const uint8_t* dat
 constexpr uint32_t kSwNL = 8, kSwWin = kSwNL * 1024, kSwUse = kSwWin - 16, kSwStep = kSwUse - 18;
 constexpr uint32_t kSwDw = 32;  // dwords of candidate bytes per lane per window (64 x 32 x 4 >= kSwStep)
 static_assert(64 * kSwDw * 4 >= kSwStep, "every candidate byte of a window is scanned");
-#ifdef CASK_SEARCH_DMA  // (A/B variant) the next window is loaded into a second buffer by LDS-DMA
-constexpr uint32_t kSwBufs = 2;
-#else
-constexpr uint32_t kSwBufs = 1;
-#endif
 struct SearchLdsSw {
-  uint32_t wins[kSwBufs][kSwWin / 4 + 16];
+  uint32_t wins[1][kSwWin / 4 + 16];
   uint32_t cand[16];
   uint32_t nl;
   uint32_t pad[3];
@@ -257,25 +252,6 @@ struct SearchLdsSw {
   // run and kSearchPast past it, far below 2^32), 2 KiB instead of 4: more searching waves per CU
   uint32_t lx[kLongList], le[kLongList];
 };
-#ifdef CASK_SEARCH_DMA
-// Issue the LDS-DMA loads of the window whose first usable byte is file byte wb into W (the same
-// granules walk_stage loads; completion is waited for at the next barrier). Returns wb's LDS byte.
-template <uint32_t NL>
-__device__ __forceinline__ uint32_t walk_stage_dma(uint32_t* W, const uint8_t* data, uint64_t len, uint64_t wb) {
-  constexpr uint32_t use = NL * 1024 - 16;
-  const uintptr_t g = (uintptr_t)(data + wb), a0 = g & ~(uintptr_t)15;
-  const uint64_t we = (wb + use < len) ? wb + use : len;
-  const uintptr_t aend = ((uintptr_t)(data + we) + 15) & ~(uintptr_t)15;
-  const uint32_t n16 = (uint32_t)((aend - a0) >> 4);
-  typedef __attribute__((address_space(3))) void lds_void;
-#pragma unroll
-  for (uint32_t k = 0; k < NL; ++k) {
-    const uint32_t i = threadIdx.x + 64 * k;
-    __builtin_amdgcn_global_load_lds((const void*)(a0 + 16ull * (i < n16 ? i : n16 - 1)), (lds_void*)(W + 256 * k), 16, 0, 0);
-  }
-  return (uint32_t)(g - a0);
-}
-#endif
 
 __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t* data, uint64_t len, uint64_t b0,
                                                    uint64_t b1, uint64_t* wst, uint32_t sshort) {
@@ -286,25 +262,12 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
   uint64_t kA = kNone;
   if (lane == 0) L.nl = 0;
   bool over = false;
-#ifdef CASK_SEARCH_DMA
-  uint32_t xn = walk_stage_dma<kSwNL>(L.wins[0], data, len, b0);
-  __syncthreads();  // (waits for the DMA: a barrier drains vmcnt)
-  uint32_t it = 0;
-#endif
   // (staging the next window into registers while this one is searched measured no faster: 207
   // VGPRs, 2 waves per SIMD instead of 3)
   for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kSwStep) {
     WST(tw0)
-#ifdef CASK_SEARCH_DMA
-    uint32_t* W = L.wins[it & 1];
-    const uint32_t x0 = xn;
-    // the next window's DMA, in flight while this one is searched (phase 2's first barrier waits)
-    if (wb + kSwStep < lim) xn = walk_stage_dma<kSwNL>(L.wins[(it + 1) & 1], data, len, wb + kSwStep);
-    ++it;
-#else
     uint32_t* W = L.wins[0];
     const uint32_t x0 = walk_stage<kSwNL>(W, data, len, wb);  // (its barriers also publish L.nl)
-#endif
     WADD(1, tw0)
     WCNT(5)
     WST(tw1)
@@ -406,9 +369,6 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
       if (mo) break;
     }
     WADD(3, tw2)
-#ifdef CASK_SEARCH_DMA
-    __syncthreads();  // the prefetched window has landed (the barrier drains vmcnt) and L.nl is published
-#endif
   }
   over = __any(over) || L.nl > kLongList;
   WST(th0)

@@ -264,9 +264,18 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
     // (tin[t0] leaves kPending with a release store; the lanes of a wave hold consecutive runs,
     // which the search claims in order)
     uint64_t s = kNone;
-    if (a.walk_pre)
+    if (a.walk_pre) {
+      // one lane polls (the wave's last run, claimed last), slowly: a poll by every lane is 64 lines
+      // per instruction, which starved the search of L2 requests
+      const uint64_t il = __builtin_amdgcn_readfirstlane((uint32_t)(i | 63u)) < nruns ? (i | 63u) : nruns - 1;
+      uint64_t tl, tl1;
+      walk_run_chunks(a, il, &tl, &tl1);
+      while (__hip_atomic_load(&a.tin[__builtin_amdgcn_readfirstlane((uint32_t)tl)], __ATOMIC_ACQUIRE,
+                               __HIP_MEMORY_SCOPE_AGENT) == kPending)
+        __builtin_amdgcn_s_sleep(127);
       while ((s = __hip_atomic_load(&a.tin[t0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == kPending)
-        __builtin_amdgcn_s_sleep(16);
+        __builtin_amdgcn_s_sleep(32);
+    }
     (void)chase_range(a, files, t0, t1, s);
 #else
     (void)chase_range(a, files, t0, t1, a.walk_pre ? a.tin[t0] : kNone);
@@ -565,6 +574,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
         h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
         h = avalanche(h);
+#if defined(CASK_HASH_ALIGNDIAG) || defined(CASK_HASH_NOVALID)  // (timing diagnostics: checksums wrong by design)
+        asm volatile("" ::"v"(h));
+        h = cstored;
+#endif
         if (h != cstored && qlead) {  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
           slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
           atomicMin(&a.cerr[ct_t], ct_r);
@@ -910,6 +923,10 @@ void k_run_hash_al(ScanArgs a) {
         h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
         h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
         h = avalanche(h);
+#if defined(CASK_HASH_ALIGNDIAG) || defined(CASK_HASH_NOVALID)  // (timing diagnostics: checksums wrong by design)
+        asm volatile("" ::"v"(h));
+        h = cstored;
+#endif
         if (h != cstored && qlead) {  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
           slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
           atomicMin(&a.cerr[ct_t], ct_r);
