@@ -679,11 +679,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     const uint64_t b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint64_t b1 = ((se - fd.first_chunk) * (uint64_t)a.chunk < fd.len) ? (se - fd.first_chunk) * (uint64_t)a.chunk : fd.len;
     const uint64_t s0 = b0 == 0 ? 0 : walk_search_sw(L, fd.data, fd.len, b0, b1, wst, a.search_short);
-#ifdef CASK_SEARCH_CHASE_OVERLAP  // (the chase of this run may be waiting for it: publish with release)
-    if (threadIdx.x == 0) __hip_atomic_store(&a.tin[t], s0, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-#else
     if (threadIdx.x == 0) a.tin[t] = s0;
-#endif
   }
 #ifdef CASK_STAMPS
   if (a.stamps && threadIdx.x == 0)

@@ -38,6 +38,11 @@ namespace {
 typedef __attribute__((address_space(1))) uint32_t g_u32;
 typedef __attribute__((address_space(1))) uint64_t g_u64;
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+#ifdef CASK_HASH_NTX  // (A/B variant: the rounds' block loads nontemporal; their addresses are 16-B aligned)
+__device__ __forceinline__ u32x4 gld16x(const g_u8* p) { return __builtin_nontemporal_load((const g_u32x4*)p); }
+#else
+__device__ __forceinline__ u32x4 gld16x(const g_u8* p) { return gld16g(p); }
+#endif
 
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
 
@@ -259,27 +264,7 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
   for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nruns; i += (uint64_t)gridDim.x * blockDim.x) {
     uint64_t t0, t1;
     walk_run_chunks(a, i, &t0, &t1);
-#ifdef CASK_SEARCH_CHASE_OVERLAP
-    // the chase runs beside k_walk_search: each lane waits for its run's start to be published
-    // (tin[t0] leaves kPending with a release store; the lanes of a wave hold consecutive runs,
-    // which the search claims in order)
-    uint64_t s = kNone;
-    if (a.walk_pre) {
-      // one lane polls (the wave's last run, claimed last), slowly: a poll by every lane is 64 lines
-      // per instruction, which starved the search of L2 requests
-      const uint64_t il = __builtin_amdgcn_readfirstlane((uint32_t)(i | 63u)) < nruns ? (i | 63u) : nruns - 1;
-      uint64_t tl, tl1;
-      walk_run_chunks(a, il, &tl, &tl1);
-      while (__hip_atomic_load(&a.tin[__builtin_amdgcn_readfirstlane((uint32_t)tl)], __ATOMIC_ACQUIRE,
-                               __HIP_MEMORY_SCOPE_AGENT) == kPending)
-        __builtin_amdgcn_s_sleep(127);
-      while ((s = __hip_atomic_load(&a.tin[t0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) == kPending)
-        __builtin_amdgcn_s_sleep(32);
-    }
-    (void)chase_range(a, files, t0, t1, s);
-#else
     (void)chase_range(a, files, t0, t1, a.walk_pre ? a.tin[t0] : kNone);
-#endif
   }
 }
 
@@ -524,7 +509,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
     nrow = *(const g_u32x4*)(uintptr_t)arow;
 #pragma unroll
-    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16g((const g_u8*)(uintptr_t)ya[d]);
+    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16x((const g_u8*)(uintptr_t)ya[d]);
     Ti = gld16g((const g_u8*)(uintptr_t)ta);
     xi = gld4g((const g_u8*)(uintptr_t)sa);
     // the round in hand's last block and checksum are used from here on: nothing that reads them
@@ -858,7 +843,7 @@ void k_run_hash_al(ScanArgs a) {
     for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
     nrow = *(const g_u32x4*)(uintptr_t)arow;
 #pragma unroll
-    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16g((const g_u8*)(uintptr_t)ya[d]);
+    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16x((const g_u8*)(uintptr_t)ya[d]);
     Ti = gld16g((const g_u8*)(uintptr_t)ta);
     xi = gld4g((const g_u8*)(uintptr_t)sa);
     // the round in hand's last block and checksum are used from here on: nothing that reads them

@@ -9,7 +9,6 @@ namespace cask_dev {
 constexpr int kDefaultGeometry = 0;           // index into the k_scan_chunks instantiations
 constexpr uint64_t kNone = ~0ull;             // "no record starts in this chunk" / no error
 constexpr uint64_t kTerm = ~0ull;             // chain ended by an UnexpectedEof record
-constexpr uint64_t kPending = 0xFEFEFEFEFEFEFEFEull;  // a run start not searched yet (tin filled with 0xFE bytes)
 
 enum : uint8_t { kRowOk = 0, kRowChecksum = 1, kRowEof = 2 };
 

@@ -639,33 +639,14 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     as.run_lo = 0;
     as.run_hi = nruns;
     if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
-#ifdef CASK_SEARCH_CHASE_OVERLAP  // (A/B variant) the chase on the side stream beside the search
-    if (c->side && c->evf) {
-      H(hipMemsetAsync(a.tin, 0xFE, 8ull * total_chunks, st));  // every start kPending
-      H(hipEventRecord(c->evf, st));
-      H(hipStreamWaitEvent(c->side, c->evf, 0));
-      launch_walk_search(as, st);
-      L("k_walk_search");
-      H(hipEventRecord(c->ev[6], st));
-      a.walk_pre = 1;
-      a.cdesc = c->cdesc.as<uint64_t>();
-      launch_walk_chase(a, c->side);
-      L("k_walk_chase (beside the search)");
-      H(hipEventRecord(c->evf, c->side));
-      H(hipStreamWaitEvent(st, c->evf, 0));
-      H(hipEventRecord(c->ev[7], st));
-    } else
-#endif
-    {
-      launch_walk_search(as, st);
-      L("k_walk_search");
-      H(hipEventRecord(c->ev[6], st));
-      a.walk_pre = 1;
-      a.cdesc = c->cdesc.as<uint64_t>();
-      launch_walk_chase(a, st);
-      L("k_walk_chase");
-      H(hipEventRecord(c->ev[7], st));
-    }
+    launch_walk_search(as, st);
+    L("k_walk_search");
+    H(hipEventRecord(c->ev[6], st));
+    a.walk_pre = 1;
+    a.cdesc = c->cdesc.as<uint64_t>();
+    launch_walk_chase(a, st);
+    L("k_walk_chase");
+    H(hipEventRecord(c->ev[7], st));
     launch_run_hash(a, hash_depth, st);
     L("k_run_hash");
     // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
