@@ -1316,6 +1316,32 @@ void cask_compact_options_default(cask_compact_options* o) {  // cask.rs:229-234
 // of their files (Log::read_entry -> Entry::from_read, log.rs:150-166) and their bytes are copied
 // into the new data files by the device gather. LogWriter rollover (log.rs:282-306) and the
 // EntryWriter/HintWriter output (log.rs:317-395) are restated on the host.
+// A host buffer of anonymous memory advised to huge pages (2 MiB faults instead of 4-KiB ones when a
+// multi-GiB batch is first written), unmapped when dropped.
+struct HostBuf {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { reset(); }
+  void reset() {
+    if (p) munmap(p, n);
+    p = nullptr;
+    n = 0;
+  }
+  bool alloc(size_t bytes) {
+    reset();
+    void* q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) return false;
+    (void)madvise(q, bytes, MADV_HUGEPAGE);
+    p = (uint8_t*)q;
+    n = bytes;
+    return true;
+  }
+  uint8_t* get() const { return p; }
+};
+
 static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
                               cask_open_error* err);
 int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
@@ -1359,6 +1385,14 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   std::vector<Ins> ins;
   std::vector<uint8_t> del_key_bytes;     // the tombstone tail, in first-seen order
   std::vector<uint64_t> del_key_off, del_seq;
+  // (test hook CASK_COMPACT_TRACE: the hint pass's sub-phases to stderr)
+  const bool tracing = cask_knobs::hook("CASK_COMPACT_TRACE") != nullptr;
+  auto tp = std::chrono::steady_clock::now();
+  auto trace = [&](const char* what) {
+    if (!tracing) return;
+    fprintf(stderr, "compact hint pass: %s %.1f ms\n", what, ms_since(tp));
+    tp = std::chrono::steady_clock::now();
+  };
   {
     const size_t nh = files.size();
     std::vector<HintFile> hf(nh);
@@ -1384,6 +1418,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         }
       }
     });
+    trace("read+parse");
     uint64_t nrec = 0;
     std::vector<size_t> used;  // indices into hf of the compacted files, in order
     for (size_t i = 0; i < nh; ++i) {
@@ -1433,6 +1468,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         ++u;
       }
     });
+    trace("lookups");
     const unsigned ntu = std::max(1u, std::min<unsigned>(nt, (unsigned)std::max<size_t>(used.size(), 1)));
     parallel_for(ntu, [&](unsigned t) {
       for (size_t j = t; j < used.size(); j += ntu) {
@@ -1480,6 +1516,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         }
       }
     });
+    trace("lists");
     // the tail: each absent key once, at its first tombstone, with its highest sequence; keys
     // deduplicated by hash-split tables on threads
     constexpr unsigned S = Index::kSub;
@@ -1512,6 +1549,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         }
       }
     });
+    trace("tail-dedup");
     for (const Tomb& T : tombs) {
       if (!T.first) continue;
       del_key_off.push_back(del_key_bytes.size());
@@ -1520,6 +1558,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     }
     del_key_off.push_back(del_key_bytes.size());
   }
+  trace("tail");
   R.ms[0] = ms_since(t0);
 
   // 2-5. The live records, source file batch by batch (at most ~kBatch bytes of sources on the
@@ -1617,7 +1656,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   // forward: one run per file per batch) get their hints appended on a thread each, and their bytes
   // written with pwrite in pieces of at most 64 MiB at their offsets in the file, all on threads.
   struct WBatch {
-    std::unique_ptr<uint8_t[]> host;
+    HostBuf host;  // (huge pages: the D2H copy into it does not fault 4-KiB pages one by one)
     std::vector<uint64_t> dst, len, foff;  // per record: offset in host, length, offset in its file
     std::vector<size_t> oi;                // per record: its output file
   };
@@ -1724,7 +1763,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       }
     });
   };
-  double t_verify = 0, t_gather = 0, t_write = 0;
+  double t_verify = 0, t_gather = 0, t_write = 0, tr_read = 0, tr_d2h = 0;
   std::vector<uint64_t> slen(ns, 0);
   for (size_t i = 0; i < ns; ++i) {
     struct stat stt;
@@ -1755,7 +1794,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         off += (slen[i] + 255) & ~255ull;
       }
       std::vector<char> okr(views.size(), 1);
+      auto ts = std::chrono::steady_clock::now();
       if ((st = ed->read_to_device(paths, views, okr)) != CASK_OK) return abort_w(st);
+      tr_read += ms_since(ts);
       for (size_t i = 0; i < okr.size(); ++i)  // File::open / read failed: Io (log.rs:150-166)
         if (!okr[i]) return abort_w(CASK_E_IO, srcs[b0 + i]);
       R.bytes_in += off;
@@ -1810,13 +1851,14 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         total += len[k];
       }
       // (the previous batch's writes are still going on: its host bytes and this one's both live)
-      WB->host.reset(new (std::nothrow) uint8_t[std::max<uint64_t>(total, 1)]);
-      if (!WB->host) return abort_w(CASK_E_NOMEM);
+      if (!WB->host.alloc(std::max<uint64_t>(total, 1))) return abort_w(CASK_E_NOMEM);
       if (total) {
         if (!ed->hint.ensure(total + 256)) return abort_w(CASK_E_NOMEM);
         st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), gsrc.data(), gpos.data(), gdst.data(),
                                 glen.data(), (uint64_t)glen.size(), ed->hint.p);
+        ts = std::chrono::steady_clock::now();
         if (st == CASK_OK) st = ed->to_host(WB->host.get(), ed->hint.p, total);
+        tr_d2h += ms_since(ts);
         if (st != CASK_OK) return abort_w(st);
       }
       WB->len.assign(len.begin(), len.end());
@@ -1843,6 +1885,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   if (writer.status != CASK_OK) return abort_with(writer.status, writer.fail_fid);
   R.ms[1] = t_verify;
   R.ms[2] = t_gather;
+  if (tracing)
+    fprintf(stderr, "compact batches: sources to device %.1f ms (of verify), D2H %.1f ms (of gather), writer busy %.1f ms\n",
+            tr_read, tr_d2h, writer.ms);
   // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen
   // order; one write per run of records bound for one file
   auto tw = std::chrono::steady_clock::now();
