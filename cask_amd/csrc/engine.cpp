@@ -497,6 +497,62 @@ struct RawBytes {
   bool empty() const { return n == 0; }
 };
 
+// A host buffer of anonymous memory advised to huge pages (2 MiB faults instead of 4-KiB ones when a
+// multi-GiB batch is first written), unmapped when dropped.
+struct HostBuf {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  HostBuf() = default;
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  ~HostBuf() { reset(); }
+  void reset() {
+    if (p) munmap(p, n);
+    p = nullptr;
+    n = 0;
+  }
+  bool alloc(size_t bytes) {
+    reset();
+    void* q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (q == MAP_FAILED) return false;
+    (void)madvise(q, bytes, MADV_HUGEPAGE);
+    p = (uint8_t*)q;
+    n = bytes;
+    return true;
+  }
+  uint8_t* get() const { return p; }
+};
+
+// A whole file into a HostBuf (no zero fill before the read, huge pages); false on an I/O error.
+bool read_file_buf(const std::string& p, HostBuf& out, uint64_t& len) {
+  len = 0;
+  const int fd = open(p.c_str(), O_RDONLY);
+  if (fd < 0) return false;
+  struct stat st;
+  if (fstat(fd, &st) != 0) {
+    close(fd);
+    return false;
+  }
+  if (!out.alloc(std::max<size_t>((size_t)st.st_size, 1))) {
+    close(fd);
+    throw std::bad_alloc();  // (mapping refused: the entry point's handler reports CASK_E_NOMEM)
+  }
+  uint64_t got = 0;
+  while (got < (uint64_t)st.st_size) {
+    const ssize_t r = read(fd, out.get() + got, (size_t)st.st_size - got);
+    if (r < 0) {
+      if (errno == EINTR) continue;
+      close(fd);
+      return false;
+    }
+    if (r == 0) break;
+    got += (uint64_t)r;
+  }
+  close(fd);
+  len = got;
+  return true;
+}
+
 // The scan side of Cask::open on one GPU, kept per device for the life of the process (a context,
 // its buffers and a ring of pinned staging buffers are created once, not per open): data files
 // read by host threads into pinned buffers and copied to the device as they arrive, the device
@@ -1316,32 +1372,6 @@ void cask_compact_options_default(cask_compact_options* o) {  // cask.rs:229-234
 // of their files (Log::read_entry -> Entry::from_read, log.rs:150-166) and their bytes are copied
 // into the new data files by the device gather. LogWriter rollover (log.rs:282-306) and the
 // EntryWriter/HintWriter output (log.rs:317-395) are restated on the host.
-// A host buffer of anonymous memory advised to huge pages (2 MiB faults instead of 4-KiB ones when a
-// multi-GiB batch is first written), unmapped when dropped.
-struct HostBuf {
-  uint8_t* p = nullptr;
-  size_t n = 0;
-  HostBuf() = default;
-  HostBuf(const HostBuf&) = delete;
-  HostBuf& operator=(const HostBuf&) = delete;
-  ~HostBuf() { reset(); }
-  void reset() {
-    if (p) munmap(p, n);
-    p = nullptr;
-    n = 0;
-  }
-  bool alloc(size_t bytes) {
-    reset();
-    void* q = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-    if (q == MAP_FAILED) return false;
-    (void)madvise(q, bytes, MADV_HUGEPAGE);
-    p = (uint8_t*)q;
-    n = bytes;
-    return true;
-  }
-  uint8_t* get() const { return p; }
-};
-
 static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
                               cask_open_error* err);
 int cask_db_compact_files(cask_db* db, const uint32_t* files_in, uint64_t nfiles, cask_compact_result* res,
@@ -1375,7 +1405,8 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     uint64_t pos;
   };
   struct HintFile {
-    std::vector<uint8_t> hb;
+    HostBuf hb;
+    uint64_t hn = 0;  // the file's length
     bool ok = false;
     uint64_t bad = UINT64_MAX, base = 0, nlive = 0, ntomb = 0, ins0 = 0, tomb0 = 0;
     std::vector<uint64_t> offs;
@@ -1385,6 +1416,13 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   std::vector<Ins> ins;
   std::vector<uint8_t> del_key_bytes;     // the tombstone tail, in first-seen order
   std::vector<uint64_t> del_key_off, del_seq;
+  std::thread reaper;  // frees the hint pass's buffers beside the batches
+  struct JoinReaper {
+    std::thread& t;
+    ~JoinReaper() {
+      if (t.joinable()) t.join();
+    }
+  } join_reaper{reaper};
   // (test hook CASK_COMPACT_TRACE: the hint pass's sub-phases to stderr)
   const bool tracing = cask_knobs::hook("CASK_COMPACT_TRACE") != nullptr;
   auto tp = std::chrono::steady_clock::now();
@@ -1401,20 +1439,21 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       for (size_t i = t; i < nh; i += ntf) {
         HintFile& H = hf[i];
         const std::string hp = hint_path(path, files[i]);
-        if (!is_file_follow(hp) || !read_file(hp, H.hb) || H.hb.size() < 4 ||
-            cask_xxh::xxh32(H.hb.data(), H.hb.size() - 4, 0) != rd32(H.hb.data() + H.hb.size() - 4)) {
-          std::vector<uint8_t>().swap(H.hb);
+        if (!is_file_follow(hp) || !read_file_buf(hp, H.hb, H.hn) || H.hn < 4 ||
+            cask_xxh::xxh32(H.hb.get(), H.hn - 4, 0) != rd32(H.hb.get() + H.hn - 4)) {
+          H.hb.reset();
+          H.hn = 0;
           continue;
         }
         H.ok = true;
-        const uint64_t body = H.hb.size() - 4;
+        const uint64_t body = H.hn - 4;
         for (uint64_t p = 0; p < body;) {
-          if (body - p < 22 || body - p - 22 < rd16(H.hb.data() + p + 8)) {
+          if (body - p < 22 || body - p - 22 < rd16(H.hb.get() + p + 8)) {
             H.bad = p;
             break;
           }
           H.offs.push_back(p);
-          p += 22ull + rd16(H.hb.data() + p + 8);
+          p += 22ull + rd16(H.hb.get() + p + 8);
         }
       }
     });
@@ -1446,7 +1485,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         constexpr uint64_t D = 16;  // lookups in flight: slots prefetched D records ahead, keys D/2
         uint64_t hr[D];
         auto hash_at = [&](uint64_t i) {
-          const uint8_t* h = H.hb.data() + H.offs[i];
+          const uint8_t* h = H.hb.get() + H.offs[i];
           return hash_key(h + 22, rd16(h + 8));
         };
         const uint64_t i0 = g - H.base, i1 = e - H.base;
@@ -1456,7 +1495,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         }
         for (uint64_t i = i0; i < i1; ++i) {
           if (i + D / 2 < i1) db->index.prefetch_key(hr[(i + D / 2) % D]);
-          const uint8_t* h = H.hb.data() + H.offs[i];
+          const uint8_t* h = H.hb.get() + H.offs[i];
           const cask_index_entry* ie = db->index.get_h(h + 22, rd16(h + 8), hr[i % D]);
           H.kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
           if (i + D < i1) {
@@ -1506,7 +1545,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         uint64_t a = H.ins0, d = H.tomb0;
         for (uint64_t i = 0; i < H.kind.size(); ++i) {
           if (!H.kind[i]) continue;
-          const uint8_t* h = H.hb.data() + H.offs[i];
+          const uint8_t* h = H.hb.get() + H.offs[i];
           if (H.kind[i] == 1) {
             ins[a++] = Ins{si, rd64(h + 14)};
           } else {
@@ -1550,15 +1589,49 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       }
     });
     trace("tail-dedup");
-    for (const Tomb& T : tombs) {
-      if (!T.first) continue;
-      del_key_off.push_back(del_key_bytes.size());
-      del_key_bytes.insert(del_key_bytes.end(), T.key, T.key + T.ksz);
-      del_seq.push_back(T.seq);
+    // the tail's keys and sequences in first-seen order: counted per slice of `tombs` on threads,
+    // then each slice writes its part at its prefix
+    {
+      const unsigned nts = ntomb < 65536 ? 1u : nt;
+      std::vector<uint64_t> cnt(nts + 1, 0), kb(nts + 1, 0);
+      parallel_for(nts, [&](unsigned t) {
+        for (uint64_t i = ntomb * t / nts, e = ntomb * (t + 1) / nts; i < e; ++i)
+          if (tombs[i].first) {
+            ++cnt[t + 1];
+            kb[t + 1] += tombs[i].ksz;
+          }
+      });
+      for (unsigned t = 0; t < nts; ++t) {
+        cnt[t + 1] += cnt[t];
+        kb[t + 1] += kb[t];
+      }
+      del_key_off.resize(cnt[nts] + 1);
+      del_seq.resize(cnt[nts]);
+      del_key_bytes.resize(kb[nts]);
+      parallel_for(nts, [&](unsigned t) {
+        uint64_t j = cnt[t], o = kb[t];
+        for (uint64_t i = ntomb * t / nts, e = ntomb * (t + 1) / nts; i < e; ++i) {
+          const Tomb& T = tombs[i];
+          if (!T.first) continue;
+          del_key_off[j] = o;
+          del_seq[j++] = T.seq;
+          if (T.ksz) memcpy(del_key_bytes.data() + o, T.key, T.ksz);
+          o += T.ksz;
+        }
+      });
+      del_key_off[cnt[nts]] = kb[nts];
     }
-    del_key_off.push_back(del_key_bytes.size());
+    trace("tail");
+    // the hint files' buffers (GiB at configs[3] scale) are unmapped on a thread of their own while
+    // the live records go through the device
+    std::vector<HintFile>* dying = new std::vector<HintFile>(std::move(hf));
+    try {
+      reaper = std::thread([dying] { delete dying; });
+    } catch (...) {  // (no thread: freed here)
+      delete dying;
+    }
   }
-  trace("tail");
+  trace("hint pass end");
   R.ms[0] = ms_since(t0);
 
   // 2-5. The live records, source file batch by batch (at most ~kBatch bytes of sources on the
@@ -1940,6 +2013,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   // files' stats, swap the file sets
   remove_on_throw.armed = false;
   auto t4 = std::chrono::steady_clock::now();
+  tp = t4;
   {
     std::vector<FoldSrc> srcs;
     for (uint32_t fid : new_files) {
@@ -1959,6 +2033,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     }
     parallel_fold(srcs, db->index);
   }
+  trace("(swap) re-index of the new files");
   for (uint32_t fid : compacted) db->index.stats.erase(fid);  // Stats::remove_files (stats.rs:50-54)
   {  // Log::swap_files (log.rs:198-217): the compacted files removed (on threads; the first failure
      // in file order is the error, as the reference's loop would return it)
@@ -1980,6 +2055,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   }
   db->files.insert(db->files.end(), new_files.begin(), new_files.end());
   std::sort(db->files.begin(), db->files.end());
+  trace("(swap) stats + unlink");
   R.ms[4] = ms_since(t4);
 
   R.n_compacted = (uint32_t)compacted.size();
