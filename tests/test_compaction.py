@@ -222,6 +222,10 @@ def test_engine_compact_files_matches_oracle(native, tmp_path, seed, mfs, thread
         _check_same(db, path, rdb, ref)
     with CaskOptions().max_file_size(mfs).open(path) as db:  # the result re-opens
         assert {k: e.sequence for k, e in db.index().items()} == {k: v.sequence for k, v in rdb.index.map.items()}
+    # the compacted files were renamed out of the data-file names at once and unlinked by the db's
+    # reclaim thread, which the close joins: nothing but the database's own files is left
+    left = sorted(f for f in os.listdir(path) if f != "cask.lock")
+    assert left == sorted(os.listdir(ref)), (left, sorted(os.listdir(ref)))
 
 
 @pytest.mark.gpu
