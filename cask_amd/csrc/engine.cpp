@@ -505,6 +505,20 @@ struct HostBuf {
   HostBuf() = default;
   HostBuf(const HostBuf&) = delete;
   HostBuf& operator=(const HostBuf&) = delete;
+  HostBuf(HostBuf&& o) noexcept : p(o.p), n(o.n) {
+    o.p = nullptr;
+    o.n = 0;
+  }
+  HostBuf& operator=(HostBuf&& o) noexcept {
+    if (this != &o) {
+      reset();
+      p = o.p;
+      n = o.n;
+      o.p = nullptr;
+      o.n = 0;
+    }
+    return *this;
+  }
   ~HostBuf() { reset(); }
   void reset() {
     if (p) munmap(p, n);
@@ -1737,9 +1751,10 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   // forward: one run per file per batch) get their hints appended on a thread each, and their bytes
   // written with pwrite in pieces of at most 64 MiB at their offsets in the file, all on threads.
   struct WBatch {
-    HostBuf host;  // (huge pages: the D2H copy into it does not fault 4-KiB pages one by one)
-    std::vector<uint64_t> dst, len, foff;  // per record: offset in host, length, offset in its file
-    std::vector<size_t> oi;                // per record: its output file
+    std::vector<HostBuf> regions;       // per source file of the batch: its live records' bytes, in order
+    std::vector<const uint8_t*> at;     // per record: its bytes (in a region)
+    std::vector<uint64_t> len, foff;    // per record: length, offset in its output file
+    std::vector<size_t> oi;             // per record: its output file
   };
   struct Writer {
     std::thread th;
@@ -1783,15 +1798,20 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     }
     struct Piece {
       size_t run;
-      uint64_t at, n;  // host offset, bytes
-      uint64_t foff;
+      const uint8_t* at;  // host bytes
+      uint64_t n, foff;
     };
     std::vector<Piece> pieces;
     constexpr uint64_t kWPiece = 64ull << 20;
-    for (size_t r = 0; r < runs.size(); ++r) {
-      const uint64_t k = runs[r].first, e = runs[r].second;
-      const uint64_t a = B.dst[k], b = B.dst[e - 1] + B.len[e - 1];
-      for (uint64_t x = a; x < b; x += kWPiece) pieces.push_back(Piece{r, x, std::min(kWPiece, b - x), B.foff[k] + (x - a)});
+    for (size_t r = 0; r < runs.size(); ++r) {  // each run's records contiguous in memory (one source's region)
+      for (uint64_t k = runs[r].first, e = runs[r].second; k < e;) {
+        uint64_t j = k + 1;
+        while (j < e && B.at[j] == B.at[j - 1] + B.len[j - 1]) ++j;
+        const uint8_t* a = B.at[k];
+        const uint64_t nb = (uint64_t)(B.at[j - 1] + B.len[j - 1] - a);
+        for (uint64_t x = 0; x < nb; x += kWPiece) pieces.push_back(Piece{r, a + x, std::min(kWPiece, nb - x), B.foff[k] + x});
+        k = j;
+      }
     }
     std::vector<char> ok(runs.size(), 1);
     const size_t ntask = runs.size() + pieces.size();  // tasks [0, runs): hints; then the pieces
@@ -1799,10 +1819,10 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     parallel_for(ntw, [&](unsigned t) {
       for (size_t x = t; x < ntask; x += ntw) {
         if (x < runs.size()) {
-          for (uint64_t j = runs[x].first; j < runs[x].second; ++j) append(B.oi[j], B.host.get() + B.dst[j], B.len[j]);
+          for (uint64_t j = runs[x].first; j < runs[x].second; ++j) append(B.oi[j], B.at[j], B.len[j]);
         } else {
           const Piece& pc = pieces[x - runs.size()];
-          if (!pwrite_all(outs[B.oi[runs[pc.run].first]].fd, B.host.get() + pc.at, pc.n, pc.foff)) ok[pc.run] = 0;
+          if (!pwrite_all(outs[B.oi[runs[pc.run].first]].fd, pc.at, pc.n, pc.foff)) ok[pc.run] = 0;
         }
       }
     });
@@ -1844,12 +1864,22 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       }
     });
   };
-  double t_verify = 0, t_gather = 0, t_write = 0, tr_read = 0, tr_d2h = 0;
+  double t_verify = 0, t_gather = 0, t_write = 0, tr_read = 0, tr_h2d = 0;
   std::vector<uint64_t> slen(ns, 0);
   for (size_t i = 0; i < ns; ++i) {
     struct stat stt;
     slen[i] = stat(data_path(path, srcs[i]).c_str(), &stt) == 0 ? (uint64_t)stt.st_size : 0;
   }
+  // Per batch of source files (at most ~kBatch bytes of them): pass 1 on host threads, a source
+  // file each — the file mapped, each live record's header read at its hint position and its bytes
+  // copied, in write order, into the file's region of the batch (Log::read_entry's reads,
+  // log.rs:150-166; only the live records' lines are touched, not the dead 80 % of configs[3]); a
+  // record cut short by the file's end is its UnexpectedEof and ends that file's pass. Then the
+  // regions' bytes go to the device through the pinned ring and the device verifies every copied
+  // record (cask_read_entries_device: the header's length again, XXH32 against the stored
+  // checksum, Entry::from_read, data.rs:161-206). The first failure in write order — an EOF from
+  // pass 1 or a checksum from the device — is the reference's error. The batch's bytes are already
+  // in write order on the host: placement, and the batch to the writer thread.
   if (!ins.empty()) {
     EngineDev* ed = engine_dev(db->opts.device);
     if (!ed) return abort_w(CASK_E_DEVICE);
@@ -1861,88 +1891,139 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     for (size_t b0 = 0; b0 < ns;) {
       auto tv = std::chrono::steady_clock::now();
       size_t b1 = b0 + 1;
-      uint64_t bytes = (slen[b0] + 255) & ~255ull;
-      while (b1 < ns && bytes + ((slen[b1] + 255) & ~255ull) <= kBatch) bytes += (slen[b1++] + 255) & ~255ull;
-      if (!ed->data.ensure(bytes + 256)) return abort_w(CASK_E_NOMEM);
-      std::vector<std::string> paths;
-      std::vector<cask_file_view> views;
-      std::vector<const uint8_t*> dsrc;
-      uint64_t off = 0;
-      for (size_t i = b0; i < b1; ++i) {
-        paths.push_back(data_path(path, srcs[i]));
-        views.push_back(cask_file_view{srcs[i], CASK_VIEW_DEVICE, ed->data.p + off, slen[i]});
-        dsrc.push_back(ed->data.p + off);
-        off += (slen[i] + 255) & ~255ull;
-      }
-      std::vector<char> okr(views.size(), 1);
-      auto ts = std::chrono::steady_clock::now();
-      if ((st = ed->read_to_device(paths, views, okr)) != CASK_OK) return abort_w(st);
-      tr_read += ms_since(ts);
-      for (size_t i = 0; i < okr.size(); ++i)  // File::open / read failed: Io (log.rs:150-166)
-        if (!okr[i]) return abort_w(CASK_E_IO, srcs[b0 + i]);
-      R.bytes_in += off;
+      uint64_t bytes = slen[b0];
+      while (b1 < ns && bytes + slen[b1] <= kBatch) bytes += slen[b1++];
+      R.bytes_in += bytes;
+      const size_t nf = b1 - b0;
+      // the batch's records: ins[k0, k1), file f's from fk[f]
+      std::vector<size_t> fk(nf + 1, k0);
       size_t k1 = k0;
-      while (k1 < ins.size() && ins[k1].src < b1) ++k1;
+      for (size_t f = 0; f < nf; ++f) {
+        fk[f] = k1;
+        while (k1 < ins.size() && ins[k1].src == b0 + f) ++k1;
+      }
+      fk[nf] = k1;
       const uint64_t n = k1 - k0;
-      std::vector<uint32_t> src(n);
-      std::vector<uint64_t> pos(n), len(n);
-      std::vector<uint8_t> stv(n);
-      std::vector<uint32_t> ex(n), fd(n);
-      for (uint64_t k = 0; k < n; ++k) {
-        src[k] = ins[k0 + k].src - (uint32_t)b0;
-        pos[k] = ins[k0 + k].pos;
-      }
-      std::vector<uint64_t> blen(slen.begin() + b0, slen.begin() + b1);
-      st = cask_read_entries_device(ed->ctx, dsrc.data(), blen.data(), (uint32_t)dsrc.size(), src.data(), pos.data(), n,
-                                    len.data(), stv.data(), ex.data(), fd.data());
-      if (st != CASK_OK) return abort_w(st);
-      for (uint64_t k = 0; k < n; ++k)  // in write order: the first failure is the reference's
-        if (stv[k] != CASK_ROW_OK)
-          return stv[k] == CASK_ROW_EOF ? abort_w(CASK_E_EOF, srcs[ins[k0 + k].src], pos[k])
-                                        : abort_w(CASK_E_CHECKSUM, srcs[ins[k0 + k].src], pos[k], ex[k], fd[k]);
-      t_verify += ms_since(tv);
-      // placement and the batch's bytes, gathered on the device in write order
-      auto tg = std::chrono::steady_clock::now();
       std::unique_ptr<WBatch> WB(new WBatch());
-      std::vector<uint64_t>& dst = WB->dst;
-      std::vector<size_t>& oi = WB->oi;
-      dst.resize(n);
-      oi.resize(n);
-      WB->foff.resize(n);
-      // the gather's pieces: a record longer than kPiece (value sizes reach 0xFFFFFFFE B, data.rs:13)
-      // goes as several consecutive pieces of at most kPiece bytes
-      constexpr uint64_t kPiece = 1ull << 31;
-      std::vector<uint32_t> gsrc, glen;
-      std::vector<uint64_t> gpos, gdst;
-      gsrc.reserve(n);
-      glen.reserve(n);
-      gpos.reserve(n);
-      gdst.reserve(n);
-      uint64_t total = 0;
-      for (uint64_t k = 0; k < n; ++k) {
-        oi[k] = place(len[k], true);
-        WB->foff[k] = cur - len[k];  // (its offset in its file: placement just added it)
-        dst[k] = total;
-        for (uint64_t o = 0; o < len[k]; o += kPiece) {
-          gsrc.push_back(src[k]);
-          gpos.push_back(pos[k] + o);
-          gdst.push_back(total + o);
-          glen.push_back((uint32_t)std::min<uint64_t>(kPiece, len[k] - o));
+      WB->regions.resize(nf);
+      WB->at.assign(n, nullptr);
+      WB->len.assign(n, 0);
+      std::vector<uint64_t> used(nf, 0);      // bytes copied into each region
+      std::vector<uint64_t> eof(nf, UINT64_MAX);  // per file: its first record cut short (batch index)
+      std::vector<char> io_ok(nf, 1);
+      auto ts = std::chrono::steady_clock::now();
+      const unsigned ntf = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)nf));
+      parallel_for(ntf, [&](unsigned t) {
+        for (size_t f = t; f < nf; f += ntf) {
+          if (fk[f] == fk[f + 1]) continue;
+          const int fdsc = open(data_path(path, srcs[b0 + f]).c_str(), O_RDONLY);  // File::open: Io
+          struct stat stt;
+          if (fdsc < 0 || fstat(fdsc, &stt) != 0) {
+            if (fdsc >= 0) close(fdsc);
+            io_ok[f] = 0;
+            continue;
+          }
+          const uint64_t flen = (uint64_t)stt.st_size;
+          const uint8_t* m = nullptr;
+          if (flen) {
+            void* q = mmap(nullptr, flen, PROT_READ, MAP_PRIVATE, fdsc, 0);
+            if (q == MAP_FAILED) {
+              close(fdsc);
+              io_ok[f] = 0;
+              continue;
+            }
+            m = (const uint8_t*)q;
+          }
+          close(fdsc);
+          HostBuf& rg = WB->regions[f];
+          if (!rg.alloc(std::max<uint64_t>(flen, 1))) {
+            if (m) munmap((void*)m, flen);
+            throw std::bad_alloc();
+          }
+          uint64_t o = 0;
+          for (size_t k = fk[f]; k < fk[f + 1]; ++k) {
+            const uint64_t pos = ins[k].pos;
+            if (pos > flen || flen - pos < 18) {  // header cut short (data.rs:163)
+              eof[f] = k - k0;
+              break;
+            }
+            const uint8_t* h = m + pos;
+            const uint32_t vsz = rd32(h + 14);
+            const uint64_t rl = 18ull + rd16(h + 12) + (vsz == CASK_ENTRY_TOMBSTONE ? 0ull : (uint64_t)vsz);
+            if (flen - pos < rl) {  // key or value cut short (data.rs:172,181)
+              eof[f] = k - k0;
+              break;
+            }
+            memcpy(rg.get() + o, h, rl);
+            WB->at[k - k0] = rg.get() + o;
+            WB->len[k - k0] = rl;
+            o += rl;
+          }
+          used[f] = o;
+          if (m) munmap((void*)m, flen);
         }
-        total += len[k];
+      });
+      tr_read += ms_since(ts);
+      // the first file that could not be opened ends the batch there (its records come first in
+      // write order after the earlier files')
+      size_t nv = n;  // records verified: those before the batch's first failure from pass 1
+      for (size_t f = 0; f < nf; ++f) {
+        if (!io_ok[f] && fk[f] != fk[f + 1]) {
+          nv = std::min<size_t>(nv, fk[f] - k0);
+          break;
+        }
+        if (eof[f] != UINT64_MAX) {
+          nv = std::min<size_t>(nv, eof[f]);
+          break;
+        }
       }
-      // (the previous batch's writes are still going on: its host bytes and this one's both live)
-      if (!WB->host.alloc(std::max<uint64_t>(total, 1))) return abort_w(CASK_E_NOMEM);
-      if (total) {
-        if (!ed->hint.ensure(total + 256)) return abort_w(CASK_E_NOMEM);
-        st = cask_gather_device(ed->ctx, dsrc.data(), (uint32_t)dsrc.size(), gsrc.data(), gpos.data(), gdst.data(),
-                                glen.data(), (uint64_t)glen.size(), ed->hint.p);
+      // the copied bytes to the device, contiguous; the device verifies records [0, nv)
+      uint64_t total = 0;
+      std::vector<uint64_t> doff(nf, 0);
+      for (size_t f = 0; f < nf; ++f) {
+        doff[f] = total;
+        total += used[f];
+      }
+      std::vector<uint64_t> pos(nv), len(nv);
+      std::vector<uint32_t> src(nv, 0u), ex(nv), fd(nv);
+      std::vector<uint8_t> stv(nv);
+      if (nv) {
+        if (!ed->data.ensure(total + 256)) return abort_w(CASK_E_NOMEM);
         ts = std::chrono::steady_clock::now();
-        if (st == CASK_OK) st = ed->to_host(WB->host.get(), ed->hint.p, total);
-        tr_d2h += ms_since(ts);
+        std::vector<cask_host::PinnedRing::Piece> ps;
+        for (size_t f = 0; f < nf; ++f)
+          if (used[f]) cask_host::PinnedRing::split(WB->regions[f].get(), ed->data.p + doff[f], used[f], ps);
+        if (!ed->ring.h2d(ps)) return abort_w(CASK_E_DEVICE);
+        tr_h2d += ms_since(ts);
+        size_t f = 0;
+        for (uint64_t k = 0; k < nv; ++k) {
+          while (k0 + k >= fk[f + 1]) ++f;
+          pos[k] = doff[f] + (uint64_t)(WB->at[k] - WB->regions[f].get());
+        }
+        const uint8_t* dsrc = ed->data.p;
+        st = cask_read_entries_device(ed->ctx, &dsrc, &total, 1, src.data(), pos.data(), nv, len.data(), stv.data(),
+                                      ex.data(), fd.data());
         if (st != CASK_OK) return abort_w(st);
       }
-      WB->len.assign(len.begin(), len.end());
+      for (uint64_t k = 0; k < nv; ++k)  // in write order: the first failure is the reference's
+        if (stv[k] != CASK_ROW_OK || len[k] != WB->len[k])
+          return stv[k] == CASK_ROW_CHECKSUM ? abort_w(CASK_E_CHECKSUM, srcs[ins[k0 + k].src], ins[k0 + k].pos, ex[k], fd[k])
+                                             : abort_w(CASK_E_EOF, srcs[ins[k0 + k].src], ins[k0 + k].pos);
+      if (nv < n) {  // pass 1's failure: File::open / read (Io) or a record cut short (UnexpectedEof)
+        const uint32_t fid = srcs[ins[k0 + nv].src];
+        const size_t f = ins[k0 + nv].src - b0;
+        if (!io_ok[f]) return abort_w(CASK_E_IO, fid);
+        return abort_w(CASK_E_EOF, fid, ins[k0 + nv].pos);
+      }
+      t_verify += ms_since(tv);
+      // placement (LogWriter::write's rollover, log.rs:282-306), in write order
+      auto tg = std::chrono::steady_clock::now();
+      WB->oi.resize(n);
+      WB->foff.resize(n);
+      for (uint64_t k = 0; k < n; ++k) {
+        WB->oi[k] = place(WB->len[k], true);
+        WB->foff[k] = cur - WB->len[k];  // (its offset in its file: placement just added it)
+      }
       t_gather += ms_since(tg);
       // hand the batch to the writer once it has taken the previous one
       auto tw = std::chrono::steady_clock::now();
@@ -1967,8 +2048,8 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   R.ms[1] = t_verify;
   R.ms[2] = t_gather;
   if (tracing)
-    fprintf(stderr, "compact batches: sources to device %.1f ms (of verify), D2H %.1f ms (of gather), writer busy %.1f ms\n",
-            tr_read, tr_d2h, writer.ms);
+    fprintf(stderr, "compact batches: live records copied from the mapped sources %.1f ms, to the device %.1f ms (of verify), writer busy %.1f ms\n",
+            tr_read, tr_h2d, writer.ms);
   // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen
   // order; one write per run of records bound for one file
   auto tw = std::chrono::steady_clock::now();

@@ -277,10 +277,12 @@ typedef struct cask_compact_result {
   uint32_t pad;
   uint64_t live_records;
   uint64_t tombstones;
-  uint64_t bytes_in;      /* data bytes of the compacted files with live records (to the device) */
+  uint64_t bytes_in;      /* data bytes of the compacted files with live records (read from) */
   uint64_t bytes_out;     /* bytes written to new data files */
-  double ms[5];           /* [0] hints + liveness, [1] device verify, [2] device gather,
-                             [3] file writes, [4] keydir update + file swap */
+  double ms[5];           /* [0] hints + liveness, [1] live records copied from the mapped
+                             sources + to the device + device verify, [2] placement,
+                             [3] file writes (the wait for the writer thread and its last
+                             batch), [4] keydir update + file swap */
   double ms_total;
 } cask_compact_result;
 
