@@ -67,7 +67,9 @@ def raise_status(status: int, file_id: int = 0, pos: int = 0, expected: int = 0,
     if status == L.E_LOCKED:
         raise Locked(what)
     if status == L.E_IO:
-        raise Io(what or "io error")
+        e = Io(f"{what or 'io error'} (file {file_id})" if file_id else (what or "io error"))
+        e.file_id = file_id  # (the file the failing call named, when it names one)
+        raise e
     if status in (L.E_DEVICE, L.E_NOMEM):
         raise DeviceError(f"device failure ({status}) {what}")
     raise Error(f"cask status {status} {what}")

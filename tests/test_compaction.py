@@ -292,6 +292,60 @@ def test_engine_compact_truncated_live_record(native, tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("order", ["checksum_first", "eof_first"])
+def test_engine_compact_first_failure_in_write_order(native, tmp_path, order):
+    """A live record whose checksum fails and a live record cut short by its file's end, in two
+    files of one batch: the error is the one met first in write order (file order, then hint
+    order), as the reference's loop meets it — the EOF comes from the host's pass over the mapped
+    source, the checksum from the device."""
+    from cask_amd import CaskOptions, errors
+    rng = random.Random(41)
+    path, ref = _both(tmp_path, _workload(rng, 6000, 3000, del_p=0.0), 64 << 10)
+    rdb = R.replay(ref)
+    files = sorted(rdb.files)
+    assert len(files) >= 4
+    fa, fb = (files[1], files[3]) if order == "checksum_first" else (files[3], files[1])
+    live_a = min((v for v in rdb.index.map.values() if v.file_id == fa), key=lambda v: v.entry_pos)
+    last_b = max((v for v in rdb.index.map.values() if v.file_id == fb), key=lambda v: v.entry_pos)
+    for p in (path, ref):
+        with open(R.data_file_path(p, fa), "r+b") as f:  # a key byte of fa's first live record
+            f.seek(live_a.entry_pos + 18)
+            b = f.read(1)
+            f.seek(live_a.entry_pos + 18)
+            f.write(bytes([b[0] ^ 0x55]))
+        os.truncate(R.data_file_path(p, fb), last_b.entry_pos + 10)  # inside fb's last live record
+    with pytest.raises(R.CaskError) as want:
+        R.compact_files(ref, rdb, files, 64 << 10)
+    assert want.value.kind == ("checksum" if order == "checksum_first" else "eof")
+    with CaskOptions().max_file_size(64 << 10).open(path) as db:  # (valid hints: nothing is scanned)
+        before = set(os.listdir(path))
+        with pytest.raises((errors.InvalidChecksum, errors.UnexpectedEof)) as got:
+            db.compact_files(db.files())
+        assert set(os.listdir(path)) == before  # the files this call created are gone again
+    assert isinstance(got.value, errors.InvalidChecksum if want.value.kind == "checksum" else errors.UnexpectedEof)
+    assert (got.value.file_id, got.value.pos) == (want.value.file_id, want.value.pos)
+    if want.value.kind == "checksum":
+        assert (got.value.expected, got.value.found) == (want.value.expected, want.value.found)
+
+
+@pytest.mark.gpu
+def test_engine_compact_missing_data_file_is_io(native, tmp_path):
+    """A compacted file whose hint file is there but whose data file is not: File::open fails in
+    Log::read_entry (log.rs:150-166), an Io error naming that file; nothing is left behind."""
+    from cask_amd import CaskOptions, errors
+    rng = random.Random(42)
+    path, _ = _both(tmp_path, _workload(rng, 3000, 1500, del_p=0.0), 64 << 10)
+    with CaskOptions().max_file_size(64 << 10).open(path) as db:
+        files = db.files()
+        os.remove(os.path.join(path, "%010d.cask.data" % files[2]))
+        before = set(os.listdir(path))
+        with pytest.raises(errors.Io) as got:
+            db.compact_files(files)
+        assert set(os.listdir(path)) == before
+    assert got.value.file_id == files[2]
+
+
+@pytest.mark.gpu
 def test_engine_compact_trigger(native, tmp_path):
     from cask_amd import CaskOptions
     ents = [R.entry_new(i + 1, b"a%d" % (i % 10), b"x" * 10) for i in range(100)]
