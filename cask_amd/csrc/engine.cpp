@@ -2040,10 +2040,12 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       b0 = b1;
     }
   }
-  // the last batch's writes; the writer's own time is in R.ms[3]
+  // the last batch's writes (R.ms[3] counts what this thread waited for the writer, not the writer's
+  // time beside the device work)
+  auto twl = std::chrono::steady_clock::now();
   writer.wait_idle();
   writer.stop();
-  t_write += writer.ms;
+  t_write += ms_since(twl);
   if (writer.status != CASK_OK) return abort_with(writer.status, writer.fail_fid);
   R.ms[1] = t_verify;
   R.ms[2] = t_gather;
