@@ -1045,13 +1045,8 @@ void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
   hipStream_t s = (hipStream_t)stream;
-#ifdef CASK_HASH_DX  // (A/B variant: another product depth, e.g. 18 or 20 blocks per round)
-  if (depth == 16)
-    run_hash_at<CASK_HASH_DX>(a, nruns, s);
-#else
-  if (depth == 16)
+  if (depth == 16)  // (18 blocks, the most that keep 2 waves per SIMD: no faster, profiles/r04_ab_variants.txt)
     run_hash_at<16>(a, nruns, s);
-#endif
   else if (depth == 4)
     run_hash_at<4>(a, nruns, s);
   else
