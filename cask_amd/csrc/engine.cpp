@@ -2094,17 +2094,30 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     }
     if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
   }
-  // hint files (HintWriter: body + XXH32 trailer), closed data files
-  for (OutFile& o : outs) {
-    if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0)
-      return abort_with(CASK_E_IO, o.fid);
-    close(o.fd);
-    o.fd = -1;
-    if (!write_file_raw2(hint_path(path, o.fid), o.hints.data(), o.hints.size(),
-                         cask_xxh::xxh32(o.hints.data(), o.hints.size(), 0)))
-      return abort_with(CASK_E_IO, o.fid);
+  // hint files (HintWriter: body + XXH32 trailer) and the data files closed, a file per thread (the
+  // first failure in file order is the error)
+  {
+    std::vector<char> okh(outs.size(), 1);
+    const unsigned nth = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)outs.size()));
+    parallel_for(nth, [&](unsigned t) {
+      for (size_t i = t; i < outs.size(); i += nth) {
+        OutFile& o = outs[i];
+        if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) {
+          okh[i] = 0;
+          continue;
+        }
+        close(o.fd);
+        o.fd = -1;
+        okh[i] = write_file_raw2(hint_path(path, o.fid), o.hints.data(), o.hints.size(),
+                                 cask_xxh::xxh32(o.hints.data(), o.hints.size(), 0));
+      }
+    });
+    for (size_t i = 0; i < outs.size(); ++i)
+      if (!okh[i]) return abort_with(CASK_E_IO, outs[i].fid);
   }
   t_write += ms_since(tw);
+  tp = tw;
+  trace("(writes) tombstone tail + hint files");
   R.ms[3] = t_write;
   uint64_t bytes_out = 0;
   for (const OutFile& o : outs) bytes_out += o.len;
