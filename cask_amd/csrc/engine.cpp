@@ -1943,8 +1943,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
           uint64_t o = 0;
           // the records' lines are loaded kAhead records before they are read (positions come from the
           // hints): each is a miss in a GiB mapping otherwise, one at a time
-          constexpr size_t kAhead = 12;
+          static const size_t kAhead = cask_knobs::hook("CASK_COMPACT_AHEAD") ? (size_t)atoi(cask_knobs::hook("CASK_COMPACT_AHEAD")) : 12;
           auto ahead = [&](size_t k) {
+            if (!kAhead) return;
             const uint64_t q = ins[k].pos;
             for (uint64_t b = 0; b < 320 && q + b < flen; b += 64) __builtin_prefetch(m + q + b);
           };
