@@ -1941,17 +1941,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
             throw std::bad_alloc();
           }
           uint64_t o = 0;
-          // the records' lines are loaded kAhead records before they are read (positions come from the
-          // hints): each is a miss in a GiB mapping otherwise, one at a time
-          static const size_t kAhead = cask_knobs::hook("CASK_COMPACT_AHEAD") ? (size_t)atoi(cask_knobs::hook("CASK_COMPACT_AHEAD")) : 12;
-          auto ahead = [&](size_t k) {
-            if (!kAhead) return;
-            const uint64_t q = ins[k].pos;
-            for (uint64_t b = 0; b < 320 && q + b < flen; b += 64) __builtin_prefetch(m + q + b);
-          };
-          for (size_t k = fk[f]; k < std::min(fk[f + 1], fk[f] + kAhead); ++k) ahead(k);
           for (size_t k = fk[f]; k < fk[f + 1]; ++k) {
-            if (k + kAhead < fk[f + 1]) ahead(k + kAhead);
             const uint64_t pos = ins[k].pos;
             if (pos > flen || flen - pos < 18) {  // header cut short (data.rs:163)
               eof[f] = k - k0;
