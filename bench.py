@@ -33,6 +33,7 @@ import json
 import os
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -62,6 +63,9 @@ def parse():
                     help="rehearsal only: gloo (blocks gathered through host memory)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (a one-GPU box)")
+    ap.add_argument("--secondary-timeout", type=float, default=900.0,
+                    help="N>1: seconds the multi-rank secondary measurements may take after the timed loop "
+                         "before rank 0 prints the line without them (a stalled collective cannot hide the metric)")
     ap.add_argument("--allow-tuning", action="store_true",
                     help="run with CASK_* tuning variables set (diagnostics; the line says so)")
     return ap.parse_args()
@@ -433,6 +437,82 @@ def main():
              # (HIP events), per GPU; `value` above is the wall clock, host gap included
              "device_gibps_per_gpu": bytes_per_step / (breakdown["pipeline_ms"] * 1e-3) / 2 ** 30}
 
+    # the line, built now: the secondary measurements below only add keys to `extra`, and a watchdog on
+    # rank 0 prints it without them if they stall (a collective that never returns)
+    line = None
+    if rank == 0:
+        if world == 1:
+            workload = ("configs[2]: 32 GiB, 16-B keys, Zipf(1.1) value sizes 16 B-64 KiB, files of <= 2 GiB "
+                        "(LogWriter rollover at the default max_file_size), 1-GPU device-resident scan")
+        else:
+            workload = (f"configs[4]: 32 x 1 GiB data files per GPU ({world} GPUs, {32 * world} files), "
+                        f"configs[2]'s record distribution, unique keys, device-resident scan per rank")
+        line = {
+            "metric": "GiB/s of log bytes CRC-verified+decoded, device-resident, at 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (device-generated records: splitmix64 keys/values, XXH32 seed 0 checksums)",
+            "config": {
+                "workload": workload,
+                "files_per_gpu": nfiles,
+                "records_per_gpu": n,
+                "mean_record_bytes": bytes_per_step / n,
+                "bytes_per_gpu": bytes_per_step,
+                "chunk_bytes": ctx.chunk_bytes(),
+                "checksum": "XXH32 seed 0 (the reference's twox-hash, not CRC32: SURVEY.md §0)",
+                "parallelism": f"file-sharded x{world}",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": kname,
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBPS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
+                "kernel_ms_avg": k_avg,
+                "algorithmic_bytes_per_launch": bytes_per_step,
+                "stream_ceiling": ceiling,
+                "frac_of_stream_ceiling": (achieved / ceiling["gbps"]) if ceiling and "gbps" in ceiling else None,
+            },
+            "cpu_baseline": None,  # (rank 0 at N = 1: filled in below)
+            "counters": counters,
+            "cask_env": env,
+            "library": {"path": os.path.relpath(lib_path, ROOT), "sha256": lib_sha},
+        }
+    printed = threading.Lock()
+    done = []
+
+    def emit(extra_now, note=None):
+        with printed:
+            if done or line is None:
+                return
+            done.append(1)
+            out = dict(line)
+            out.update(extra_now)
+            if note:
+                out["secondary_timeout"] = note
+            print(json.dumps(out), flush=True)
+
+    watchdog = None
+    if rank == 0 and dist is not None:
+        def fire():
+            emit(dict(extra), f"the multi-rank secondary measurements did not finish within {args.secondary_timeout:.0f} s; "
+                              f"the line was printed without the ones still running")
+            os._exit(0)
+        watchdog = threading.Timer(args.secondary_timeout, fire)
+        watchdog.daemon = True
+        watchdog.start()
+
     # N>1: this rank's keydir block and the blocks' gather + rank-0 fold over RCCL through the C ABI
     # (cask_keydir_gather_rccl), reported apart from the metric; a failure is reported, not fatal
     if dist is not None and not args.no_gather:
@@ -518,6 +598,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline([f for f, _ in files], max(1, min(args.cpu_sample_files, len(files))), cfg)
+        line["cpu_baseline"] = cpu
 
     if rank == 0 and world == 1 and not args.no_cfg1:
         del res
@@ -526,57 +607,10 @@ def main():
         torch.cuda.empty_cache()
         extra["configs1_secondary"] = cfg1_secondary(ctx, torch, dev, max(10, args.steps))
 
+    if watchdog is not None:
+        watchdog.cancel()
     if rank == 0:
-        if world == 1:
-            workload = ("configs[2]: 32 GiB, 16-B keys, Zipf(1.1) value sizes 16 B-64 KiB, files of <= 2 GiB "
-                        "(LogWriter rollover at the default max_file_size), 1-GPU device-resident scan")
-        else:
-            workload = (f"configs[4]: 32 x 1 GiB data files per GPU ({world} GPUs, {32 * world} files), "
-                        f"configs[2]'s record distribution, unique keys, device-resident scan per rank")
-        line = {
-            "metric": "GiB/s of log bytes CRC-verified+decoded, device-resident, at 1/2/4/8 GPUs",
-            "value": value,
-            "unit": "GiB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u32",
-            "data": "synthetic (device-generated records: splitmix64 keys/values, XXH32 seed 0 checksums)",
-            "config": {
-                "workload": workload,
-                "files_per_gpu": nfiles,
-                "records_per_gpu": n,
-                "mean_record_bytes": bytes_per_step / n,
-                "bytes_per_gpu": bytes_per_step,
-                "chunk_bytes": ctx.chunk_bytes(),
-                "checksum": "XXH32 seed 0 (the reference's twox-hash, not CRC32: SURVEY.md §0)",
-                "parallelism": f"file-sharded x{world}",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "kernel": kname,
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBPS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBPS,
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel_ms_avg": k_avg,
-                "algorithmic_bytes_per_launch": bytes_per_step,
-                "stream_ceiling": ceiling,
-                "frac_of_stream_ceiling": (achieved / ceiling["gbps"]) if ceiling and "gbps" in ceiling else None,
-            },
-            "cpu_baseline": cpu,
-            "counters": counters,
-            "cask_env": env,
-            "library": {"path": os.path.relpath(lib_path, ROOT), "sha256": lib_sha},
-        }
-        line.update(extra)
-        print(json.dumps(line), flush=True)
+        emit(extra)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
