@@ -63,7 +63,7 @@ def parse():
                     help="rehearsal only: gloo (blocks gathered through host memory)")
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal only: every rank on cuda:0 (a one-GPU box)")
-    ap.add_argument("--secondary-timeout", type=float, default=900.0,
+    ap.add_argument("--secondary-timeout", type=float, default=300.0,
                     help="N>1: seconds the multi-rank secondary measurements may take after the timed loop "
                          "before rank 0 prints the line without them (a stalled collective cannot hide the metric)")
     ap.add_argument("--allow-tuning", action="store_true",
