@@ -240,8 +240,11 @@ __device__ __forceinline__ uint64_t walk_search(SearchLds& L, const uint8_t* dat
 // offsets whose record could neither be short nor end within the horizon, and offsets whose
 // key_size is larger (a run start after such a key is found later and k_finish's check sends the
 // run to the repair: speed only).
-constexpr uint32_t kSwNL = 8, kSwWin = kSwNL * 1024, kSwUse = kSwWin - 16, kSwStep = kSwUse - 18;
-constexpr uint32_t kSwDw = 32;  // dwords of candidate bytes per lane per window (64 x 32 x 4 >= kSwStep)
+#ifndef CASK_SW_NL  // (A/B variant: the window in KiB)
+#define CASK_SW_NL 8
+#endif
+constexpr uint32_t kSwNL = CASK_SW_NL, kSwWin = kSwNL * 1024, kSwUse = kSwWin - 16, kSwStep = kSwUse - 18;
+constexpr uint32_t kSwDw = 4 * kSwNL;  // dwords of candidate bytes per lane per window (64 x 32 x 4 >= kSwStep)
 static_assert(64 * kSwDw * 4 >= kSwStep, "every candidate byte of a window is scanned");
 struct SearchLdsSw {
   uint32_t wins[1][kSwWin / 4 + 16];
@@ -285,18 +288,21 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
     // read j — so that the 8 lanes of each LDS cycle hit 8 different bank quads (in plain order a
     // 128-B lane stride put every lane on 2 of them)
     const uint32_t d0 = (((x0 + 17) >> 2) & ~3u) + kSwDw * lane;
-    uint64_t sm[2] = {0ull, 0ull};
-    u32x4 wv[kSwDw / 4];
+    constexpr uint32_t kP = kSwDw / 4, kG = kSwDw / 16;  // b128 pieces per lane; 64-bit masks of them
+    uint64_t sm[kG];
+#pragma unroll
+    for (uint32_t g = 0; g < kG; ++g) sm[g] = 0ull;
+    u32x4 wv[kP];
     const uint32_t dprev = W[d0 - 1];  // (x0 + 17 >= 17: d0 >= 4)
 #pragma unroll
-    for (uint32_t j = 0; j < kSwDw / 4; ++j) wv[j] = ((const u32x4*)W)[d0 / 4 + ((j + lane) & 7)];
+    for (uint32_t j = 0; j < kP; ++j) wv[j] = ((const u32x4*)W)[d0 / 4 + ((j + lane) & (kP - 1))];
 #pragma unroll
-    for (uint32_t j = 0; j < kSwDw / 4; ++j) {
-      const uint32_t pc = (j + lane) & 7;  // the piece in wv[j]
+    for (uint32_t j = 0; j < kP; ++j) {
+      const uint32_t pc = (j + lane) & (kP - 1);  // the piece in wv[j]
 #pragma unroll
       for (uint32_t e = 0; e < 4; ++e) {
         const uint32_t w = wv[j][e];
-        const uint32_t wp = e ? wv[j][e - 1] : (pc ? wv[(j + 7) & 7][3] : dprev);
+        const uint32_t wp = e ? wv[j][e - 1] : (pc ? wv[(j + kP - 1) & (kP - 1)][3] : dprev);
         const uint32_t kszhi_small = ~(((wp & 0x7F7F7F7Fu) + 0x6F6F6F6Fu) | wp) & 0x80808080u;  // byte < 0x11
         // bytes 0x00 or 0xFF: all eight bits equal, i.e. no bit differs from the one above it
         // (the shift's bit 7 comes from the next byte and is masked off); y <= 0x7F per byte, so
@@ -330,7 +336,9 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
     // phase 2: the short candidates in offset order, 16 per round (one per quad)
     for (;;) {
       WCNT(6)
-      const uint32_t mine = (uint32_t)__builtin_popcountll(sm[0]) + (uint32_t)__builtin_popcountll(sm[1]);
+      uint32_t mine = 0;
+#pragma unroll
+      for (uint32_t g = 0; g < kG; ++g) mine += (uint32_t)__builtin_popcountll(sm[g]);
       // exclusive prefix of the counts over lanes (lane order is offset order)
       uint32_t pre = mine;
       for (int s = 1; s < 64; s <<= 1) {
@@ -343,7 +351,7 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
       // this lane's candidates with global rank < 16 go to cand[rank]
       uint32_t r = pre;
 #pragma unroll
-      for (uint32_t g = 0; g < 2; ++g) {
+      for (uint32_t g = 0; g < kG; ++g) {
         while (sm[g] && r < 16) {
           const uint32_t bit = (uint32_t)__builtin_ctzll(sm[g]);
           sm[g] &= sm[g] - 1;
