@@ -1886,7 +1886,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     std::lock_guard<std::mutex> g(ed->mu);
     int st = ed->prepare();
     if (st != CASK_OK) return abort_w(st);
-    constexpr uint64_t kBatch = 16ull << 30;
+    // (test hook CASK_COMPACT_BATCH: source bytes per batch, so small databases run several batches)
+    const char* bh = cask_knobs::hook("CASK_COMPACT_BATCH");
+    const uint64_t kBatch = bh && strtoull(bh, nullptr, 10) ? strtoull(bh, nullptr, 10) : (16ull << 30);
     size_t k0 = 0;
     for (size_t b0 = 0; b0 < ns;) {
       auto tv = std::chrono::steady_clock::now();

@@ -229,6 +229,57 @@ def test_engine_compact_files_matches_oracle(native, tmp_path, seed, mfs, thread
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 100_000, 300_000])
+def test_engine_compact_many_batches_matches_oracle(native, tmp_path, batch, monkeypatch):
+    """Source batches of ~`batch` bytes (test hook; a batch holds at least one source file), so the
+    writer thread takes several batches while the next ones are copied and verified, and the
+    rollover runs across batch boundaries: files, stats and keydir equal the oracle's."""
+    from cask_amd import CaskOptions
+    monkeypatch.setenv("CASK_COMPACT_BATCH", str(batch))
+    rng = random.Random(51)
+    path, ref = _both(tmp_path, _workload(rng, 8000, 900, vmax=400), 64 << 10)
+    rdb = R.replay(ref)
+    with CaskOptions().max_file_size(64 << 10).open(path) as db:
+        files = db.files()
+        assert len(files) >= 6
+        rep = db.compact_files(files)
+        rc, rn = R.compact_files(ref, rdb, files, 64 << 10)
+        assert rep["compacted"] == len(rc) and rep["new_files"] == len(rn)
+        _check_same(db, path, rdb, ref)
+
+
+@pytest.mark.gpu
+def test_engine_compact_failure_in_a_later_batch(native, tmp_path, monkeypatch):
+    """A checksum failure in the last source file, with one file per batch: the earlier batches
+    were already handed to the writer thread; the error is the reference's and every file the call
+    created is removed again."""
+    from cask_amd import CaskOptions, errors
+    monkeypatch.setenv("CASK_COMPACT_BATCH", "1")
+    rng = random.Random(52)
+    path, ref = _both(tmp_path, _workload(rng, 6000, 3000, del_p=0.0), 64 << 10)
+    rdb = R.replay(ref)
+    files = sorted(rdb.files)
+    fl = files[-1]
+    live = min((v for v in rdb.index.map.values() if v.file_id == fl), key=lambda v: v.entry_pos)
+    for p in (path, ref):
+        with open(R.data_file_path(p, fl), "r+b") as f:
+            f.seek(live.entry_pos + 20)
+            b = f.read(1)
+            f.seek(live.entry_pos + 20)
+            f.write(bytes([b[0] ^ 0x0F]))
+    with pytest.raises(R.CaskError) as want:
+        R.compact_files(ref, rdb, files, 64 << 10)
+    with CaskOptions().max_file_size(64 << 10).open(path) as db:
+        before = set(os.listdir(path))
+        with pytest.raises(errors.InvalidChecksum) as got:
+            db.compact_files(db.files())
+        assert set(os.listdir(path)) == before
+        assert db.files() == files  # (nothing was swapped)
+    assert (got.value.file_id, got.value.pos, got.value.expected, got.value.found) == \
+        (want.value.file_id, want.value.pos, want.value.expected, want.value.found)
+
+
+@pytest.mark.gpu
 def test_engine_compact_subset_and_missing_hints(native, tmp_path):
     from cask_amd import CaskOptions
     rng = random.Random(21)
