@@ -263,9 +263,9 @@ def test_engine_compact_failure_in_a_later_batch(native, tmp_path, monkeypatch):
     live = min((v for v in rdb.index.map.values() if v.file_id == fl), key=lambda v: v.entry_pos)
     for p in (path, ref):
         with open(R.data_file_path(p, fl), "r+b") as f:
-            f.seek(live.entry_pos + 20)
+            f.seek(live.entry_pos + 18)
             b = f.read(1)
-            f.seek(live.entry_pos + 20)
+            f.seek(live.entry_pos + 18)
             f.write(bytes([b[0] ^ 0x0F]))
     with pytest.raises(R.CaskError) as want:
         R.compact_files(ref, rdb, files, 64 << 10)
