@@ -1755,6 +1755,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     std::vector<const uint8_t*> at;     // per record: its bytes (in a region)
     std::vector<uint64_t> len, foff;    // per record: length, offset in its output file
     std::vector<size_t> oi;             // per record: its output file
+    size_t complete = 0;                // outs[0, complete) take no record after this batch
   };
   struct Writer {
     std::thread th;
@@ -1839,6 +1840,34 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     writer.stop();
     return abort_with(st, fid, pos, e, f);
   };
+  // Output files [lo, hi) finished: hint file (HintWriter: body + XXH32 trailer) written and data
+  // file closed, a file per thread (the first failure in file order is the error). The writer thread
+  // finishes each output file once no later batch can add to it; this thread the rest at the end.
+  size_t hints_done = 0;
+  auto finish_outputs = [&](size_t lo, size_t hi, uint32_t* fail) -> int {
+    if (hi <= lo) return CASK_OK;
+    std::vector<char> okh(hi - lo, 1);
+    const unsigned nth = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)(hi - lo)));
+    parallel_for(nth, [&](unsigned t) {
+      for (size_t i = lo + t; i < hi; i += nth) {
+        OutFile& o = outs[i];
+        if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) {
+          okh[i - lo] = 0;
+          continue;
+        }
+        close(o.fd);
+        o.fd = -1;
+        okh[i - lo] = write_file_raw2(hint_path(path, o.fid), o.hints.data(), o.hints.size(),
+                                      cask_xxh::xxh32(o.hints.data(), o.hints.size(), 0));
+      }
+    });
+    for (size_t i = lo; i < hi; ++i)
+      if (!okh[i - lo]) {
+        *fail = outs[i].fid;
+        return CASK_E_IO;
+      }
+    return CASK_OK;
+  };
   auto start_writer = [&]() {
     writer.th = std::thread([&] {
       for (;;) {
@@ -1851,7 +1880,11 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
           writer.busy = true;
         }
         const auto tw0 = std::chrono::steady_clock::now();
-        const int st = writer.status == CASK_OK ? abi_status([&] { return write_batch(*B); }) : writer.status;
+        int st = writer.status == CASK_OK ? abi_status([&] { return write_batch(*B); }) : writer.status;
+        if (st == CASK_OK && B->complete > hints_done) {  // (output files no later batch adds to)
+          st = abi_status([&] { return finish_outputs(hints_done, B->complete, &writer.fail_fid); });
+          if (st == CASK_OK) hints_done = B->complete;
+        }
         const double dt = ms_since(tw0);
         B.reset();  // (the batch's host bytes go before the next one is taken)
         {
@@ -2026,6 +2059,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         WB->oi[k] = place(WB->len[k], true);
         WB->foff[k] = cur - WB->len[k];  // (its offset in its file: placement just added it)
       }
+      WB->complete = outs.empty() ? 0 : outs.size() - 1;  // (the last output file may take more)
       t_gather += ms_since(tg);
       // hand the batch to the writer once it has taken the previous one
       auto tw = std::chrono::steady_clock::now();
@@ -2087,26 +2121,10 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     }
     if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
   }
-  // hint files (HintWriter: body + XXH32 trailer) and the data files closed, a file per thread (the
-  // first failure in file order is the error)
+  // the output files the writer thread has not finished (the last live one, the tombstone tail's)
   {
-    std::vector<char> okh(outs.size(), 1);
-    const unsigned nth = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)outs.size()));
-    parallel_for(nth, [&](unsigned t) {
-      for (size_t i = t; i < outs.size(); i += nth) {
-        OutFile& o = outs[i];
-        if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) {
-          okh[i] = 0;
-          continue;
-        }
-        close(o.fd);
-        o.fd = -1;
-        okh[i] = write_file_raw2(hint_path(path, o.fid), o.hints.data(), o.hints.size(),
-                                 cask_xxh::xxh32(o.hints.data(), o.hints.size(), 0));
-      }
-    });
-    for (size_t i = 0; i < outs.size(); ++i)
-      if (!okh[i]) return abort_with(CASK_E_IO, outs[i].fid);
+    uint32_t ff = 0;
+    if (finish_outputs(hints_done, outs.size(), &ff) != CASK_OK) return abort_with(CASK_E_IO, ff);
   }
   t_write += ms_since(tw);
   tp = tw;
