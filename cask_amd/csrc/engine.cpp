@@ -2089,37 +2089,69 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     fprintf(stderr, "compact batches: live records copied from the mapped sources %.1f ms, to the device %.1f ms (of verify), writer busy %.1f ms\n",
             tr_read, tr_h2d, writer.ms);
   // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen
-  // order; one write per run of records bound for one file
+  // order. The placement (the rollover) runs in order; the records, their checksums and their hints
+  // are then laid out on threads, and each output file's run of them goes out in one pwrite.
   auto tw = std::chrono::steady_clock::now();
-  {
-    std::vector<uint8_t> run;
-    size_t run_file = SIZE_MAX;
-    uint64_t run_at = 0;  // the run's offset in its file (the live records went in with pwrite)
-    auto flush = [&]() -> bool {
-      if (run.empty()) return true;
-      const bool ok = pwrite_all(outs[run_file].fd, run.data(), run.size(), run_at);
-      run.clear();
-      return ok;
-    };
+  if (nt) {
+    std::vector<uint32_t> to(nt);
+    std::vector<uint64_t> at(nt), hat(nt);  // offset in its file; offset in its file's hints
+    std::vector<uint64_t> hl;               // per output: hint bytes as placed
     for (size_t j = 0; j < nt; ++j) {
-      const uint64_t ko = del_key_off[j], kn = del_key_off[j + 1] - ko;
-      uint8_t rec_h[18];
-      wr64(rec_h + 4, del_seq[j]);
-      wr16(rec_h + 12, (uint16_t)kn);
-      wr32(rec_h + 14, CASK_ENTRY_TOMBSTONE);
+      const uint64_t kn = del_key_off[j + 1] - del_key_off[j];
       const size_t o = place(18 + kn, false);
-      if (o != run_file) {
-        if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
-        run_file = o;
-        run_at = outs[o].len;
-      }
-      const size_t at = run.size();
-      run.insert(run.end(), rec_h, rec_h + 18);
-      run.insert(run.end(), del_key_bytes.data() + ko, del_key_bytes.data() + ko + kn);
-      wr32(run.data() + at, cask_xxh::xxh32(run.data() + at + 4, 14 + kn, 0));
-      if (!append(o, run.data() + at, 18 + kn)) return abort_with(CASK_E_IO, outs[o].fid);
+      to[j] = (uint32_t)o;
+      at[j] = cur - (18 + kn);
+      if (hl.size() <= o) hl.resize(o + 1, UINT64_MAX);
+      if (hl[o] == UINT64_MAX) hl[o] = outs[o].hints.size();
+      hat[j] = hl[o];
+      hl[o] += 22 + kn;
     }
-    if (!flush()) return abort_with(CASK_E_IO, outs[run_file].fid);
+    struct TRun {
+      size_t j0, j1;
+      std::vector<uint8_t> bytes;
+    };
+    std::vector<TRun> runs;
+    for (size_t j = 0; j < nt;) {
+      size_t e = j + 1;
+      while (e < nt && to[e] == to[j]) ++e;
+      runs.push_back(TRun{j, e, {}});
+      j = e;
+    }
+    std::vector<uint32_t> run_of(nt);
+    for (size_t r = 0; r < runs.size(); ++r) {
+      const TRun& R = runs[r];
+      const uint64_t kl = del_key_off[R.j1] - del_key_off[R.j1 - 1];
+      runs[r].bytes.resize(at[R.j1 - 1] + 18 + kl - at[R.j0]);
+      OutFile& o = outs[to[R.j0]];
+      o.hints.resize(hl[to[R.j0]]);
+      o.len = at[R.j1 - 1] + 18 + kl;
+      for (size_t j = R.j0; j < R.j1; ++j) run_of[j] = (uint32_t)r;
+    }
+    const unsigned ntt = nt < 65536 ? 1u : host_threads();
+    parallel_for(ntt, [&](unsigned t) {
+      for (size_t j = nt * t / ntt, e = nt * (t + 1) / ntt; j < e; ++j) {
+        const TRun& R = runs[run_of[j]];
+        const uint64_t ko = del_key_off[j], kn = del_key_off[j + 1] - ko;
+        uint8_t* rec = (uint8_t*)R.bytes.data() + (at[j] - at[R.j0]);
+        wr64(rec + 4, del_seq[j]);
+        wr16(rec + 12, (uint16_t)kn);
+        wr32(rec + 14, CASK_ENTRY_TOMBSTONE);
+        if (kn) memcpy(rec + 18, del_key_bytes.data() + ko, kn);
+        wr32(rec, cask_xxh::xxh32(rec + 4, 14 + kn, 0));
+        uint8_t* h = outs[to[j]].hints.data() + hat[j];  // Hint::new(entry, entry_pos) (data.rs:218-226)
+        wr64(h, del_seq[j]);
+        wr16(h + 8, (uint16_t)kn);
+        wr32(h + 10, CASK_ENTRY_TOMBSTONE);
+        wr64(h + 14, at[j]);
+        if (kn) memcpy(h + 22, del_key_bytes.data() + ko, kn);
+      }
+    });
+    for (const TRun& R : runs) {
+      OutFile& o = outs[to[R.j0]];
+      if ((o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) ||
+          !pwrite_all(o.fd, R.bytes.data(), R.bytes.size(), at[R.j0]))
+        return abort_with(CASK_E_IO, o.fid);
+    }
   }
   // the output files the writer thread has not finished (the last live one, the tombstone tail's)
   {
