@@ -1504,25 +1504,31 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       for (uint64_t g = lo; g < hi;) {
         HintFile& H = hf[used[u]];
         const uint64_t e = std::min<uint64_t>(hi, H.base + H.offs.size());
-        constexpr uint64_t D = 16;  // lookups in flight: slots prefetched D records ahead, keys D/2
-        uint64_t hr[D];
+        // lookups in flight: slots prefetched D records ahead, keys D/2 (test hook
+        // CASK_COMPACT_LOOKAHEAD: a power of two up to 64)
+        static const uint64_t D = [] {
+          const char* v = cask_knobs::hook("CASK_COMPACT_LOOKAHEAD");
+          const uint64_t d = v ? strtoull(v, nullptr, 10) : 16;
+          return d >= 2 && d <= 64 && !(d & (d - 1)) ? d : 16ull;
+        }();
+        uint64_t hr[64];
         auto hash_at = [&](uint64_t i) {
           const uint8_t* h = H.hb.get() + H.offs[i];
           return hash_key(h + 22, rd16(h + 8));
         };
         const uint64_t i0 = g - H.base, i1 = e - H.base;
         for (uint64_t i = i0; i < std::min(i1, i0 + D); ++i) {
-          hr[i % D] = hash_at(i);
-          db->index.prefetch(hr[i % D]);
+          hr[i & (D - 1)] = hash_at(i);
+          db->index.prefetch(hr[i & (D - 1)]);
         }
         for (uint64_t i = i0; i < i1; ++i) {
-          if (i + D / 2 < i1) db->index.prefetch_key(hr[(i + D / 2) % D]);
+          if (i + D / 2 < i1) db->index.prefetch_key(hr[(i + D / 2) & (D - 1)]);
           const uint8_t* h = H.hb.get() + H.offs[i];
-          const cask_index_entry* ie = db->index.get_h(h + 22, rd16(h + 8), hr[i % D]);
+          const cask_index_entry* ie = db->index.get_h(h + 22, rd16(h + 8), hr[i & (D - 1)]);
           H.kind[i] = rd32(h + 10) == CASK_ENTRY_TOMBSTONE ? (ie ? 0 : 2) : (ie && ie->sequence == rd64(h)) ? 1 : 0;
           if (i + D < i1) {
-            hr[i % D] = hash_at(i + D);
-            db->index.prefetch(hr[i % D]);
+            hr[i & (D - 1)] = hash_at(i + D);
+            db->index.prefetch(hr[i & (D - 1)]);
           }
         }
         g = e;
