@@ -127,8 +127,6 @@ SIGNATURES = [
     ("cask_db_current_sequence", C.c_uint64, [C.c_void_p]),
     ("cask_db_files", C.c_uint64, [C.c_void_p, c_u32p, C.c_uint64]),
     ("cask_db_open_timings", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
-    ("cask_gather_device", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, c_u32p, c_u64p, c_u64p, c_u32p,
-                                     C.c_uint64, C.c_void_p]),
     ("cask_compact_options_default", None, [C.POINTER(CompactOptions)]),
     ("cask_db_compact_files", C.c_int, [C.c_void_p, c_u32p, C.c_uint64, C.POINTER(CompactResult),
                                         C.POINTER(OpenError)]),
@@ -139,6 +137,7 @@ SIGNATURES = [
     ("cask_shard_keydir", C.c_int, [C.c_void_p, C.POINTER(FileView), C.c_uint32, C.POINTER(Rows), c_u64p,
                                     C.POINTER(C.c_void_p), c_u64p]),
     ("cask_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_debug_inject", C.c_int, [C.c_void_p, C.c_uint32]),
     ("cask_rccl_unique_id", C.c_int, [C.c_void_p]),
     ("cask_rccl_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("cask_rccl_comm_destroy", C.c_int, [C.c_void_p]),

@@ -33,6 +33,7 @@
 
 #include <hip/hip_runtime_api.h>
 
+#include "abi_guard.h"
 #include "../../include/cask_scan.h"
 #include "host_ring.h"
 #include "keydir_format.h"
@@ -958,13 +959,7 @@ static void set_err(cask_open_error* err, int status, uint32_t fid = 0, uint64_t
 extern "C++" {  // (templates; this part of the file is inside the extern "C" block)
 template <class F>
 static auto abi_status(F&& f) noexcept -> decltype(f()) {
-  try {
-    return f();
-  } catch (const std::bad_alloc&) {
-    return CASK_E_NOMEM;
-  } catch (...) {
-    return CASK_E_IO;
-  }
+  return cask_abi::guard(static_cast<F&&>(f));
 }
 template <class F>
 static cask_db* abi_db(cask_open_error* err, F&& f) noexcept {
@@ -2423,29 +2418,31 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
 // Stats after the last shard: per file, entries = puts + stale tombstones, dead = puts that are not
 // the key's final entry + stale tombstones (stats.rs:23-48 summed over Index::update's cases).
 int cask_keydir_finish(cask_db* db) {
-  if (!db || !db->merging) return CASK_E_INVALID_ARG;
-  std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> live;  // file -> (entries, bytes)
-  db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& sl) {
-    auto& l = live[sl.e.file_id];
-    l.first += 1;
-    l.second += sl.e.entry_size;
+  return cask_abi::guard([&]() -> int {
+    if (!db || !db->merging) return CASK_E_INVALID_ARG;
+    std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> live;  // file -> (entries, bytes)
+    db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& sl) {
+      auto& l = live[sl.e.file_id];
+      l.first += 1;
+      l.second += sl.e.entry_size;
+    });
+    db->index.stats.clear();
+    for (const auto& kv : db->terms) {
+      const cask_db::ShardTerms& t = kv.second;
+      if (!t.puts && !t.stale) continue;  // no Stats::add_entry for this file
+      const auto it = live.find(kv.first);
+      const uint64_t le = it == live.end() ? 0 : it->second.first, lb = it == live.end() ? 0 : it->second.second;
+      StatsEntry& e = db->index.stats[kv.first];
+      e.entries = t.puts + t.stale;
+      e.dead_entries = t.puts - le + t.stale;
+      e.dead_bytes = t.put_bytes - lb + t.stale_bytes;
+    }
+    std::sort(db->files.begin(), db->files.end());
+    db->files.erase(std::unique(db->files.begin(), db->files.end()), db->files.end());
+    db->file_seq = db->files.empty() ? 0u : db->files.back();
+    db->merging = false;
+    return CASK_OK;
   });
-  db->index.stats.clear();
-  for (const auto& kv : db->terms) {
-    const cask_db::ShardTerms& t = kv.second;
-    if (!t.puts && !t.stale) continue;  // no Stats::add_entry for this file
-    const auto it = live.find(kv.first);
-    const uint64_t le = it == live.end() ? 0 : it->second.first, lb = it == live.end() ? 0 : it->second.second;
-    StatsEntry& e = db->index.stats[kv.first];
-    e.entries = t.puts + t.stale;
-    e.dead_entries = t.puts - le + t.stale;
-    e.dead_bytes = t.put_bytes - lb + t.stale_bytes;
-  }
-  std::sort(db->files.begin(), db->files.end());
-  db->files.erase(std::unique(db->files.begin(), db->files.end()), db->files.end());
-  db->file_seq = db->files.empty() ? 0u : db->files.back();
-  db->merging = false;
-  return CASK_OK;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2975,109 +2972,113 @@ void cask_db_close(cask_db* db) { delete db; }
 uint64_t cask_db_len(const cask_db* db) { return db ? db->index.live() : 0; }
 
 int cask_db_get_entry(const cask_db* db, const uint8_t* key, uint64_t ksz, cask_index_entry* out) {
-  if (!db || (ksz && !key) || ksz > 0xFFFF) return 0;
-  const cask_index_entry* e = db->index.get(key, (uint32_t)ksz);
-  if (!e) return 0;
-  if (out) *out = *e;
-  return 1;
+  return cask_abi::guard([&]() -> int {
+    if (!db || (ksz && !key) || ksz > 0xFFFF) return 0;
+    const cask_index_entry* e = db->index.get(key, (uint32_t)ksz);
+    if (!e) return 0;
+    if (out) *out = *e;
+    return 1;
+  });
 }
 
 int64_t cask_db_export(const cask_db* db, uint8_t* key_bytes, uint64_t key_cap, uint64_t* key_off,
                        uint64_t* key_len, cask_index_entry* entries, uint64_t nkeys) {
-  if (!db) return CASK_E_INVALID_ARG;
-  if (!key_bytes && !key_off && !key_len && !entries) {  // sizing call: no order needed
-    uint64_t total = 0, n = 0;
-    db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& s) {
-      total += s.ksz;
-      ++n;
+  return cask_abi::guard([&]() -> int64_t {
+    if (!db) return CASK_E_INVALID_ARG;
+    if (!key_bytes && !key_off && !key_len && !entries) {  // sizing call: no order needed
+      uint64_t total = 0, n = 0;
+      db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& s) {
+        total += s.ksz;
+        ++n;
+      });
+      return nkeys < n ? CASK_E_CAPACITY : (int64_t)total;
+    }
+    struct Ref {
+      const uint8_t* key;
+      uint32_t ksz;
+      const cask_index_entry* e;
+    };
+    // Bytewise key order on host threads: refs bucketed by their first two bytes (a missing byte
+    // sorts first: "" < "a" < "a\0"), each bucket sorted with the full comparison, then written out
+    // in parallel pieces. (One std::sort of 237 M refs, configs[4]'s keydir, took minutes.)
+    auto bucket_of = [](const uint8_t* k, uint32_t n) -> uint32_t {
+      const uint32_t b0 = n >= 1 ? k[0] + 1u : 0u, b1 = n >= 2 ? k[1] + 1u : 0u;
+      return b0 * 257u + b1;
+    };
+    constexpr uint32_t kB = 257u * 257u;
+    const auto& sub = db->index.sub;
+    const unsigned nt = std::min<unsigned>(host_threads(), (unsigned)Index::kSub);
+    // pass 1: per-thread bucket counts over the thread's tables
+    std::vector<std::vector<uint64_t>> cnt(nt, std::vector<uint64_t>(kB, 0));
+    parallel_for(nt, [&](unsigned t) {
+      for (size_t q = t; q < Index::kSub; q += nt)
+        for (const KeyDir::Slot& sl : sub[q].slots)
+          if (sl.state == 1) ++cnt[t][bucket_of(sub[q].key_of(sl), sl.ksz)];
     });
-    return nkeys < n ? CASK_E_CAPACITY : (int64_t)total;
-  }
-  struct Ref {
-    const uint8_t* key;
-    uint32_t ksz;
-    const cask_index_entry* e;
-  };
-  // Bytewise key order on host threads: refs bucketed by their first two bytes (a missing byte
-  // sorts first: "" < "a" < "a\0"), each bucket sorted with the full comparison, then written out
-  // in parallel pieces. (One std::sort of 237 M refs, configs[4]'s keydir, took minutes.)
-  auto bucket_of = [](const uint8_t* k, uint32_t n) -> uint32_t {
-    const uint32_t b0 = n >= 1 ? k[0] + 1u : 0u, b1 = n >= 2 ? k[1] + 1u : 0u;
-    return b0 * 257u + b1;
-  };
-  constexpr uint32_t kB = 257u * 257u;
-  const auto& sub = db->index.sub;
-  const unsigned nt = std::min<unsigned>(host_threads(), (unsigned)Index::kSub);
-  // pass 1: per-thread bucket counts over the thread's tables
-  std::vector<std::vector<uint64_t>> cnt(nt, std::vector<uint64_t>(kB, 0));
-  parallel_for(nt, [&](unsigned t) {
-    for (size_t q = t; q < Index::kSub; q += nt)
-      for (const KeyDir::Slot& sl : sub[q].slots)
-        if (sl.state == 1) ++cnt[t][bucket_of(sub[q].key_of(sl), sl.ksz)];
-  });
-  std::vector<uint64_t> bstart(kB + 1, 0);
-  for (uint32_t b = 0; b < kB; ++b) {
-    uint64_t c = 0;
-    for (unsigned t = 0; t < nt; ++t) c += cnt[t][b];
-    bstart[b + 1] = bstart[b] + c;
-  }
-  const uint64_t n = bstart[kB];
-  if (nkeys < n) return CASK_E_CAPACITY;
-  // pass 2: scatter (thread t's refs of bucket b after threads 0..t-1's; the counts become each
-  // thread's write positions first)
-  for (uint32_t b = 0; b < kB; ++b) {
-    uint64_t o = bstart[b];
-    for (unsigned t = 0; t < nt; ++t) {
-      const uint64_t c = cnt[t][b];
-      cnt[t][b] = o;
-      o += c;
+    std::vector<uint64_t> bstart(kB + 1, 0);
+    for (uint32_t b = 0; b < kB; ++b) {
+      uint64_t c = 0;
+      for (unsigned t = 0; t < nt; ++t) c += cnt[t][b];
+      bstart[b + 1] = bstart[b] + c;
     }
-  }
-  std::vector<Ref> idx(n);
-  parallel_for(nt, [&](unsigned t) {
-    std::vector<uint64_t>& at = cnt[t];
-    for (size_t q = t; q < Index::kSub; q += nt)
-      for (const KeyDir::Slot& sl : sub[q].slots)
-        if (sl.state == 1) {
-          const uint8_t* k = sub[q].key_of(sl);
-          idx[at[bucket_of(k, sl.ksz)]++] = Ref{k, sl.ksz, &sl.e};
-        }
-  });
-  // pass 3: buckets sorted on threads (claimed in order)
-  std::atomic<uint32_t> next{0};
-  parallel_for(host_threads(), [&](unsigned) {
-    for (uint32_t b; (b = next.fetch_add(1)) < kB;)
-      if (bstart[b + 1] - bstart[b] > 1)
-        std::sort(idx.begin() + bstart[b], idx.begin() + bstart[b + 1], [](const Ref& A, const Ref& B) {
-          const uint32_t m = std::min(A.ksz, B.ksz);
-          const int c = m ? memcmp(A.key, B.key, m) : 0;
-          if (c) return c < 0;
-          return A.ksz < B.ksz;
-        });
-  });
-  // pass 4: key offsets (prefix over pieces), then the arrays in parallel pieces
-  const unsigned np = host_threads();
-  std::vector<uint64_t> pbytes(np + 1, 0);
-  parallel_for(np, [&](unsigned t) {
-    uint64_t b = 0;
-    for (uint64_t j = n * t / np; j < n * (t + 1) / np; ++j) b += idx[j].ksz;
-    pbytes[t + 1] = b;
-  });
-  for (unsigned t = 0; t < np; ++t) pbytes[t + 1] += pbytes[t];
-  const uint64_t total = pbytes[np];
-  if (key_bytes && key_cap < total) return CASK_E_CAPACITY;
-  parallel_for(np, [&](unsigned t) {
-    uint64_t off = pbytes[t];
-    for (uint64_t j = n * t / np; j < n * (t + 1) / np; ++j) {
-      const Ref& r = idx[j];
-      if (key_bytes && r.ksz) memcpy(key_bytes + off, r.key, r.ksz);
-      if (key_off) key_off[j] = off;
-      if (key_len) key_len[j] = r.ksz;
-      if (entries) entries[j] = *r.e;
-      off += r.ksz;
+    const uint64_t n = bstart[kB];
+    if (nkeys < n) return CASK_E_CAPACITY;
+    // pass 2: scatter (thread t's refs of bucket b after threads 0..t-1's; the counts become each
+    // thread's write positions first)
+    for (uint32_t b = 0; b < kB; ++b) {
+      uint64_t o = bstart[b];
+      for (unsigned t = 0; t < nt; ++t) {
+        const uint64_t c = cnt[t][b];
+        cnt[t][b] = o;
+        o += c;
+      }
     }
+    std::vector<Ref> idx(n);
+    parallel_for(nt, [&](unsigned t) {
+      std::vector<uint64_t>& at = cnt[t];
+      for (size_t q = t; q < Index::kSub; q += nt)
+        for (const KeyDir::Slot& sl : sub[q].slots)
+          if (sl.state == 1) {
+            const uint8_t* k = sub[q].key_of(sl);
+            idx[at[bucket_of(k, sl.ksz)]++] = Ref{k, sl.ksz, &sl.e};
+          }
+    });
+    // pass 3: buckets sorted on threads (claimed in order)
+    std::atomic<uint32_t> next{0};
+    parallel_for(host_threads(), [&](unsigned) {
+      for (uint32_t b; (b = next.fetch_add(1)) < kB;)
+        if (bstart[b + 1] - bstart[b] > 1)
+          std::sort(idx.begin() + bstart[b], idx.begin() + bstart[b + 1], [](const Ref& A, const Ref& B) {
+            const uint32_t m = std::min(A.ksz, B.ksz);
+            const int c = m ? memcmp(A.key, B.key, m) : 0;
+            if (c) return c < 0;
+            return A.ksz < B.ksz;
+          });
+    });
+    // pass 4: key offsets (prefix over pieces), then the arrays in parallel pieces
+    const unsigned np = host_threads();
+    std::vector<uint64_t> pbytes(np + 1, 0);
+    parallel_for(np, [&](unsigned t) {
+      uint64_t b = 0;
+      for (uint64_t j = n * t / np; j < n * (t + 1) / np; ++j) b += idx[j].ksz;
+      pbytes[t + 1] = b;
+    });
+    for (unsigned t = 0; t < np; ++t) pbytes[t + 1] += pbytes[t];
+    const uint64_t total = pbytes[np];
+    if (key_bytes && key_cap < total) return CASK_E_CAPACITY;
+    parallel_for(np, [&](unsigned t) {
+      uint64_t off = pbytes[t];
+      for (uint64_t j = n * t / np; j < n * (t + 1) / np; ++j) {
+        const Ref& r = idx[j];
+        if (key_bytes && r.ksz) memcpy(key_bytes + off, r.key, r.ksz);
+        if (key_off) key_off[j] = off;
+        if (key_len) key_len[j] = r.ksz;
+        if (entries) entries[j] = *r.e;
+        off += r.ksz;
+      }
+    });
+    return (int64_t)total;
   });
-  return (int64_t)total;
 }
 
 uint64_t cask_db_stats(const cask_db* db, uint32_t* file_id, uint64_t* entries, uint64_t* dead_entries,
@@ -3103,9 +3104,11 @@ uint64_t cask_db_files(const cask_db* db, uint32_t* ids, uint64_t cap) {
 }
 
 int cask_db_open_timings(const cask_db* db, double* ms5) {
-  if (!db || !ms5) return CASK_E_INVALID_ARG;
-  memcpy(ms5, db->timings, sizeof(db->timings));
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!db || !ms5) return CASK_E_INVALID_ARG;
+    memcpy(ms5, db->timings, sizeof(db->timings));
+    return CASK_OK;
+  });
 }
 
 }  // extern "C"

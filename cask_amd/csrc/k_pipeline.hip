@@ -769,29 +769,6 @@ void launch_validate(const ScanArgs& a, void* stream) {
 void launch_summary(const ScanArgs& a, uint64_t* summary, void* stream) {
   hipLaunchKernelGGL(k_summary, dim3(1), dim3(256), 0, S(stream), a, summary);
 }
-// ------------------------------------------------------------------------------------------
-// K_gather (compaction rewrite, cask.rs:505-513 + log.rs:282-306): live records copied byte for
-// byte to their place in the new data files (same fields => same bytes and checksum,
-// data.rs:90-121). One wave per record: 16-B loads/stores (unaligned access), bytes at the tail.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gather(const GatherRec* __restrict__ recs, uint64_t n,
-                                                const uint8_t* const* __restrict__ src, uint8_t* __restrict__ dst) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  for (uint64_t r = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += nw) {
-    const GatherRec g = recs[r];
-    const uint8_t* s = src[g.src] + g.pos;
-    uint8_t* d = dst + g.dst;
-    const uint64_t n16 = g.len >> 4;
-    for (uint64_t i = lane; i < n16; i += 64) {
-      const u32x4 v = gld16(s + 16 * i);
-      __builtin_memcpy(d + 16 * i, &v, 16);
-    }
-    const uint32_t tail = (uint32_t)(g.len & 15);
-    if (lane < tail) d[16 * n16 + lane] = s[16 * n16 + lane];
-  }
-}
-
 // K_read_entries (compaction, cask.rs:505-508 -> Log::read_entry, log.rs:150-166 ->
 // Entry::from_read, data.rs:161-206): the live records only, verified where the hints say they
 // are — not a re-scan of their files. One quad of lanes per record (quad_gbl_xxh32).
@@ -834,13 +811,6 @@ void launch_read_entries(const uint64_t* pos, const uint32_t* src, uint64_t n, c
   uint64_t g = (n + 63) / 64;
   if (g > 16384) g = 16384;
   hipLaunchKernelGGL(k_read_entries, dim3((uint32_t)g), dim3(256), 0, S(stream), pos, src, n, srcs, slen, len, st, expct, found);
-}
-
-void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src, uint8_t* dst, void* stream) {
-  if (!n) return;
-  uint64_t g = (n + 3) / 4;
-  if (g > 65536) g = 65536;
-  hipLaunchKernelGGL(k_gather, dim3((uint32_t)g), dim3(256), 0, S(stream), recs, n, src, dst);
 }
 
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream) {

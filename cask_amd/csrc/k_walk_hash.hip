@@ -38,11 +38,6 @@ namespace {
 typedef __attribute__((address_space(1))) uint32_t g_u32;
 typedef __attribute__((address_space(1))) uint64_t g_u64;
 typedef __attribute__((address_space(1))) u32x4 g_u32x4;
-#ifdef CASK_HASH_NTX  // (A/B variant: the rounds' block loads nontemporal; their addresses are 16-B aligned)
-__device__ __forceinline__ u32x4 gld16x(const g_u8* p) { return __builtin_nontemporal_load((const g_u32x4*)p); }
-#else
-__device__ __forceinline__ u32x4 gld16x(const g_u8* p) { return gld16g(p); }
-#endif
 
 constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
 
@@ -150,42 +145,12 @@ __device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* fil
 // it leaves the range at (kTerm once an EOF row ended it, kNone if it never had a start). Chasing a
 // run as [t0, tm) and then [tm, t1) from the first range's exit writes exactly what one range
 // [t0, t1) writes: the chain is one walk either way.
-#ifdef CASK_CHASE_BATCH  // (A/B variant) slot rows staged in LDS, 8 (one 128-B line) per store burst
-// A lane's pending slot rows: consecutive rows of one chunk from `at` on, in LDS (the lane's 8 slots);
-// written out as one burst of up to 8 16-B stores when the line is full, the chunk changes or the
-// range ends, so that each 128-B line of rows reaches the L2 whole instead of a row per hop.
-struct RowBatch {
-  u32x4* buf;  // this lane's 8 LDS slots
-  g_u32x4* at = nullptr;
-  uint32_t n = 0;
-  __device__ __forceinline__ void flush() {
-    for (uint32_t k = 0; k < 8; ++k)
-      if (k < n) at[k] = buf[k];
-    n = 0;
-  }
-  __device__ __forceinline__ void put(g_u32x4* p, const u32x4& row) {
-    if (n && (n == 8 || p != at + n)) flush();
-    if (!n) at = p;
-    buf[n++] = row;
-  }
-};
-#endif
 
 __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t tb, uint64_t te,
                                 uint64_t p_in) {
   const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   g_u32* slots = (g_u32*)a.slots;
   g_u64* cd = (g_u64*)a.cdesc;
-#ifdef CASK_CHASE_BATCH
-  __shared__ u32x4 s_rows[256 * 8];
-  RowBatch rb;
-  rb.buf = s_rows + 8 * threadIdx.x;
-#define CHASE_ROW(addr, val) rb.put((g_u32x4*)(addr), (val))
-#define CHASE_FLUSH() rb.flush()
-#else
-#define CHASE_ROW(addr, val) (*(g_u32x4*)(addr) = (val))
-#define CHASE_FLUSH()
-#endif
   Walk W;
   W.cn = 0;
   W.ccerr = 0xFFFFFFFFu;
@@ -220,7 +185,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
         const uint32_t r = open_record(a, W, p, csh, true, &j);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-        CHASE_ROW(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4, (u32x4{0u, 0u, 0u, off << 16}));
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
         if (r < W.ccerr) W.ccerr = r;
         term = true;
         break;
@@ -233,7 +198,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       h = gld16g((const g_u8*)(W.S.data + pl));
       const uint32_t r = open_record(a, W, p, csh, true, &j);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-      CHASE_ROW(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4, (u32x4{row.x, row.y, row.z, row.w | (off << 16)}));
+      *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
       if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
         if (r < W.ccerr) W.ccerr = r;
         term = true;
@@ -244,11 +209,8 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
     close_segment(a, W, term ? kTerm : p, true);
     if (term) p = kTerm;
   }
-  CHASE_FLUSH();
   return p;
 }
-#undef CHASE_ROW
-#undef CHASE_FLUSH
 
 // The chunk range of walk run i (an index into a.wruns, or the run itself): [t0, t1).
 __device__ __forceinline__ void walk_run_chunks(const ScanArgs& a, uint64_t i, uint64_t* t0, uint64_t* t1) {
@@ -323,11 +285,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   // Units of work: the runs in order, except that the last grid's worth of runs (one per wave) is
   // handed out in quarters, so that the waves run dry within about a quarter of a run of each other
   // instead of a whole one (configs[2]: a run is ~0.4 ms of one wave's hashing).
-#ifdef CASK_HASH_NOTAIL  // (A/B variant: whole runs to the end)
-  const uint64_t ntail = 0;
-#else
   const uint64_t ntail = nruns < (uint64_t)gridDim.x * 4 ? nruns : (uint64_t)gridDim.x * 4;
-#endif
   const uint64_t nhead = nruns - ntail, nunits = nhead + 4 * ntail;
   auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
     if (u >= nunits) return false;
@@ -487,11 +445,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     // of the iteration's loads is in a register before the first load issues: an address built
     // after a load may be built in that load's destination, a write that waits for every load in
     // flight.
-#ifdef CASK_HASH_ALIGNDIAG  // (timing diagnostic only, wrong checksums: each round from its 128-B line)
-    const uint64_t bpa = ((base2 + 4 + 64ull * lb2) & ~127ull) + 16ull * q;
-#else
     const uint64_t bpa = base2 + 4 + 64ull * lb2 + 16ull * q;
-#endif
     uint64_t ya[D];
 #pragma unroll
     for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;
@@ -509,7 +463,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
     nrow = *(const g_u32x4*)(uintptr_t)arow;
 #pragma unroll
-    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16x((const g_u8*)(uintptr_t)ya[d]);
+    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16g((const g_u8*)(uintptr_t)ya[d]);
     Ti = gld16g((const g_u8*)(uintptr_t)ta);
     xi = gld4g((const g_u8*)(uintptr_t)sa);
     // the round in hand's last block and checksum are used from here on: nothing that reads them
@@ -559,10 +513,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
         h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
         h = avalanche(h);
-#if defined(CASK_HASH_ALIGNDIAG) || defined(CASK_HASH_NOVALID)  // (timing diagnostics: checksums wrong by design)
-        asm volatile("" ::"v"(h));
-        h = cstored;
-#endif
         if (h != cstored && qlead) {  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
           slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
           atomicMin(&a.cerr[ct_t], ct_r);
@@ -614,362 +564,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
 }
 
 
-// The same pass with every round on whole 128-B lines (see k_run_hash_al's state comment).
-template <uint32_t D>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(D == 16 ? 1 : D == 8 ? 3 : 4)))
-void k_run_hash_al(ScanArgs a) {
-  constexpr uint32_t RW = 16 * D, RSH = D == 16 ? 8 : D == 8 ? 7 : 6;  // dwords per round (64 D bytes)
-  static_assert(RW == 1u << RSH, "D is 4, 8 or 16");
-  constexpr uint32_t RT = kMaxRun + 1;
-  __shared__ uint32_t s_pf[4][2][RT];  // per wave, two runs: the exclusive prefix of their chunks' rows
-  __shared__ uint64_t s_cd[4][2][2 * kMaxRun];  // and their chunks' first-byte and file-end addresses
-  const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6;
-  const bool qlead = q == 0;
-  const uint64_t R = a.run;
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
-  g_u32* slots = (g_u32*)a.slots;
-  const g_u64* cd = (const g_u64*)a.cdesc;
-  uint32_t* pfA = s_pf[wv][0];  // the run records are handed out from (A) and the one after it (B)
-  uint32_t* pfB = s_pf[wv][1];
-  uint64_t* cdA = s_cd[wv][0];
-  uint64_t* cdB = s_cd[wv][1];
-  const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
-  const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;      // a line every idle load may read
-
-  // The wave's record stream (uniform): two runs, A (records are handed out from it, at cursor
-  // cur) and B (the next one, once loaded: fullB), each as its first chunk, chunk count and row
-  // count. B is refilled from the claim counter as soon as it is free (at the top of an iteration:
-  // the wait for the claim also waits for the round in flight, once a run). (Plain variables, not
-  // arrays indexed by the slot: those go to scratch memory, whose loads wait for every load.)
-  uint64_t rtA = 0, rtB = 0;
-  uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
-  bool fullB = false;
-  uint32_t cur = 0;
-  bool runs_left = true;
-  auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
-  // run k's chunk-row prefix into LDS and its bounds into A or B; false if there is no run k (the
-  // flags are set by the callers: a store to one of two flags chosen at run time is what the
-  // compiler merges into a store through a selected pointer, which keeps both in scratch memory)
-  // Units of work: the runs in order, except that the last grid's worth of runs (one per wave) is
-  // handed out in quarters, so that the waves run dry within about a quarter of a run of each other
-  // instead of a whole one (configs[2]: a run is ~0.4 ms of one wave's hashing).
-#ifdef CASK_HASH_NOTAIL  // (A/B variant: whole runs to the end)
-  const uint64_t ntail = 0;
-#else
-  const uint64_t ntail = nruns < (uint64_t)gridDim.x * 4 ? nruns : (uint64_t)gridDim.x * 4;
-#endif
-  const uint64_t nhead = nruns - ntail, nunits = nhead + 4 * ntail;
-  auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
-    if (u >= nunits) return false;
-    const bool tl = u >= nhead;
-    const uint64_t k = tl ? nhead + ((u - nhead) >> 2) : u;
-    const uint64_t tr = run_start(k);
-    const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
-    const uint64_t qr = (R + 3) >> 2, c0 = tl ? ((u - nhead) & 3) * qr : 0ull;
-    const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
-    const uint64_t t0 = tr + c0;
-    const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
-    uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if ((int)lane >= o) inc += u;
-    }
-    uint32_t* pf = intoA ? pfA : pfB;
-    if (lane < nch) pf[lane + 1] = inc;
-    if (lane == 0) pf[0] = 0;
-    uint64_t* cdt = intoA ? cdA : cdB;
-    if (lane < nch) {
-      cdt[2 * lane] = cd[2 * (t0 + lane)];
-      cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
-    }
-    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
-    if (intoA) {
-      rtA = t0;
-      rchA = nch;
-      rnA = n;
-    } else {
-      rtB = t0;
-      rchB = nch;
-      rnB = n;
-    }
-    return true;
-  };
-  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first run, by its index
-
-  // a quad's current record (cv) and the round of it in hand: round cri of its cnrd rounds, rfin if
-  // it is the last (the record's tail bytes in T), head if it is the first (its stored checksum in
-  // xst). The record's body (data.rs:185-198: everything after the stored checksum) starts at cb,
-  // chl bytes long; its rounds are the 1-KiB stretches of the lines from cb's line on: dword t of
-  // the record's lines (t = 0 at cb & ~127) is body dword w = t - cM - 1's upper neighbour, cM the
-  // dword of cb in its line and csb its byte; ctl = the last dword a full stripe needs. tclamp: the
-  // tail's 16 bytes were loaded from the file's last granule instead (shifted by ctsh).
-  bool cv = false, rfin = false, head = false, tclamp = false;
-  uint64_t cb = 0, cend = 0, ct_t = 0;
-  uint32_t chl = 0, cM = 0, csb = 0, ctl = 0, cnrd = 0, cri = 0, ctsh = 0;
-  uint32_t v = 0, carry = 0, mrot = 1, cstored = 0, ct_r = 0, cw3 = 0;
-  // its next record: ns = 0 none, 1 slot row + chunk address loading (issued last iteration), 2 ready
-  uint32_t ns = 0;
-  uint64_t nt = 0;
-  uint32_t nr = 0;
-  u32x4 nrow = u32x4{0u, 0u, 0u, 0u};
-  uint64_t ncb = 0, nce = 0;  // its chunk's first byte and its file's end (from the run's LDS table)
-  // where the slot row is read from: every iteration reloads it (a quad that has claimed a record it
-  // cannot start yet reads the same slot row again; one with no record reads the safe line)
-  uint64_t carow = safe;
-  u32x4 XA[D], XB[D], TA = u32x4{0u, 0u, 0u, 0u}, TB = u32x4{0u, 0u, 0u, 0u};
-  uint32_t sA = 0, sB = 0;
-#pragma unroll
-  for (uint32_t d = 0; d < D; ++d) XA[d] = XB[d] = u32x4{0u, 0u, 0u, 0u};
-
-  uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  (void)hst;
-  HST(h_all)
-#ifdef CASK_STAMPS
-  const uint64_t wid = blockIdx.x * 4ull + wv;
-  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-  // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi): D full blocks
-  // in X, a record's partial last block in T, its stored checksum in x. False: done.
-  auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
-    HCNT(6)
-    HST(h0)
-    if (ns == 1) ns = 2;
-    if (runs_left && !fullB) {  // (every lane takes part in the atomic, lane 0 adding 1)
-      const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
-      const bool got = load_run(false, (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old));
-      runs_left = got;
-      fullB = got;
-    }
-    // ---- plan this quad's next round: the rest of its record, or the next record from its slot row
-    // and its chunk's address (branch-free: every lane computes both and selects, so the counted
-    // waits see one path)
-    const bool cont = cv && !rfin;
-    const bool promote = !cont && ns == 2;
-    const uint32_t w3n = nrow.w, vszn = nrow.z;
-    const uint64_t bn = ncb + ((w3n >> 16) & 0x7FFFu);
-    const uint64_t en = nce;
-    const uint64_t rln = 18ull + (w3n & 0xFFFFu) + (vszn == 0xFFFFFFFFu ? 0ull : (uint64_t)vszn);
-    // (an UnexpectedEof row, cut by the file's end, has failed already: nothing to hash)
-    const bool round2 = cont || (promote && bn + rln <= en);
-    // the record of the next round: the current one, or the promoted one (body at bn + 4)
-    const uint64_t b2 = cont ? cb : bn + 4, end2 = cont ? cend : en;
-    const uint32_t hl2 = cont ? chl : (uint32_t)(rln - 4);  // (a record is < 2^32 + 2^16 + 18 B; its
-                                                           // body fits u32 as the file ends first)
-    const uint64_t la2 = b2 & ~127ull;
-    const uint32_t M2 = cont ? cM : (uint32_t)((b2 - la2) >> 2), sb2 = cont ? csb : (uint32_t)(b2 & 3);
-    const uint32_t ns2 = hl2 >> 4;  // full stripes
-    const uint32_t tl2 = cont ? ctl : M2 + 4 * ns2;
-    const uint32_t nrd2 = cont ? cnrd : (ns2 ? (tl2 >> RSH) + 1 : 1u);
-    const uint32_t ri2 = cont ? cri + 1 : 0u;
-    const uint32_t nl2 = round2 && ns2 ? ((tl2 - RW * ri2) >> 4) + 1 < D ? ((tl2 - RW * ri2) >> 4) + 1 : D : 0u;
-    const bool fin2 = round2 && ri2 + 1 == nrd2;
-    const uint64_t pt = nt;
-    const uint32_t pr = nr, pw3 = w3n;
-    ns = promote ? 0u : ns;
-    HADD(1, h0)
-    HST(h1)
-    // ---- the stream's next records to the quads that have none (in lane order)
-    const bool want = ns == 0;
-    const unsigned long long wm = __ballot(qlead && want) & qmask;
-    const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
-    // every lane loads a slot row and a chunk address every iteration (the safe line when it takes
-    // no record): a load into a loop-carried register only under a branch is a copy after the
-    // merge, and the copy waits for every load in flight
-    // (branch-free for the lanes: the rank, chunk search and addresses are computed by every lane)
-    const uint32_t l0 = lane & ~3u;
-    const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (l0 ? (~0ull >> (64 - l0)) : 0ull));
-    const uint32_t rem = rnA - cur;
-    const bool up = myrank >= rem;
-    const uint32_t idx = up ? myrank - rem : cur + myrank;
-    const bool claimed = want && (up ? (fullB && idx < rnB) : true);
-    const uint32_t* pf = up ? pfB : pfA;
-    uint32_t lo = 0, hi = up ? rchB : rchA;  // the last chunk j with pf[j] <= idx
-#pragma unroll
-    for (int it = 0; it < 6; ++it) {  // (a run is at most 64 chunks)
-      const uint32_t mid = (lo + hi) >> 1;
-      const bool go = hi - lo > 1;
-      const bool le = go && pf[mid] <= idx;
-      lo = le ? mid : lo;
-      hi = go && !le ? mid : hi;
-    }
-    const uint64_t ntc = (up ? rtB : rtA) + lo;
-    const uint32_t nrc = idx - pf[lo];
-    nt = claimed ? ntc : nt;
-    nr = claimed ? nrc : nr;
-    const uint64_t* cdt = up ? cdB : cdA;
-    const uint64_t cbc = cdt[2 * lo], cec = cdt[2 * lo + 1];
-    ncb = claimed ? cbc : ncb;
-    nce = claimed ? cec : nce;
-    carow = claimed ? (uint64_t)(uintptr_t)(slots + (ntc * (uint64_t)a.slot_cap + nrc) * 4) : promote ? safe : carow;
-    uint64_t arow = carow;
-    if (nw) {
-      const uint32_t avail = rem + (fullB ? rnB : 0u);
-      const uint32_t used = nw < avail ? nw : avail;
-      if (used >= rem && fullB) {  // run A is handed out: the stream moves on to B
-        rtA = rtB;
-        rnA = rnB;
-        rchA = rchB;
-        uint32_t* t = pfA;
-        pfA = pfB;
-        pfB = t;
-        uint64_t* tc = cdA;
-        cdA = cdB;
-        cdB = tc;
-        fullB = false;
-        cur = used - rem;
-      } else {
-        cur += used;
-      }
-    }
-    ns = claimed ? 1u : ns;
-    // ---- issue the round: D 64-B blocks of 128-B-aligned lines (lane q: the 16 B at 64 d + 16 q),
-    // so no line is read by two rounds; the record's tail (its last hl % 16 bytes, into T); the
-    // stored checksum (first round). Every quad issues every load (the ones it does not need read
-    // the safe line, as do lanes whose granule starts past the file's last one). Every address of
-    // the iteration's loads is in a register before the first load issues: an address built after
-    // a load may be built in that load's destination, a write that waits for every load in flight.
-    const uint64_t end16 = (end2 + 15) & ~15ull;
-    const uint64_t bpa = la2 + 64ull * D * ri2 + 16ull * q;
-    uint64_t ya[D];
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 && bpa + 64ull * d < end16 ? bpa + 64ull * d : safe;
-    const bool tail2 = round2 && fin2 && (hl2 & 15) != 0;
-    const uint64_t tp = b2 + 16ull * ns2;
-    const bool tclamp2 = tail2 && tp + 16 > end16;
-    uint64_t ta = tail2 ? (tclamp2 ? end16 - 16 : tp) : safe;
-    uint64_t sa = round2 && !cont ? b2 - 4 : safe;
-    asm volatile("" : "+v"(arow), "+v"(sa), "+v"(ta));
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
-    nrow = *(const g_u32x4*)(uintptr_t)arow;
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16x((const g_u8*)(uintptr_t)ya[d]);
-    Ti = gld16g((const g_u8*)(uintptr_t)ta);
-    xi = gld4g((const g_u8*)(uintptr_t)sa);
-    // the round in hand's last block and checksum are used from here on: nothing that reads them
-    // (nor the wait for them, one counted past this round's loads) is scheduled above the loads
-    asm volatile("" : "+v"(xm)::"memory");
-    HADD(2, h1)
-    HST(h2)
-    // ---- mix the round in hand
-    if (cv) {
-      // the elements of this round the record's full stripes use: dword t = 256 cri + 16 d + 4 k + q
-      // of its lines (lane q, block d, word k after the transpose) for t in [cM + 1, ctl], i.e.
-      // e = 4 d + k in [e_lo, e_lo + span]
-      // (e_lo <= 8: only the first elements of a record's first round can come before its first
-      // stripe, so the others test the upper bound alone)
-      const int32_t A = (int32_t)(cM + 1 - q) - (int32_t)(RW * cri), B = (int32_t)(ctl - q) - (int32_t)(RW * cri);
-      int32_t e_lo = A <= 0 ? 0 : (A + 3) >> 2;
-      const int32_t e_hi = B < 0 ? -1 : (B >> 2 < (int32_t)(4 * D - 1) ? B >> 2 : (int32_t)(4 * D - 1));
-      e_lo = e_hi < e_lo ? (int32_t)(4 * D) : e_lo;
-      const uint32_t span = (uint32_t)(e_hi - e_lo);
-#pragma unroll
-      for (uint32_t d = 0; d < D; ++d) {
-        const u32x4 g = Xm[d];
-        // body dword w = funnel of line dwords t - 1, t at byte csb: three of a lane's four pairs are
-        // its own words; the first takes its lower word from lane q - 1 (lane 0: lane 3's of the
-        // previous block, carried)
-        const uint32_t dv = (uint32_t)__builtin_amdgcn_mov_dpp((int)g.w, 0x93, 0xF, 0xF, false);  // [3,0,1,2]
-        const uint32_t p0 = q == 0 ? carry : dv;
-        carry = dv;
-        u32x4 x = u32x4{fun(p0, g.x, csb), fun(g.x, g.y, csb), fun(g.y, g.z, csb), fun(g.z, g.w, csb)};
-        quad_transpose(x, q);
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-#ifdef CASK_HASH_NOVALID  // (timing diagnostic only: wrong checksums)
-          const bool ok = true;
-#else
-          const bool ok = 4 * d + k < 8 ? (uint32_t)((int32_t)(4 * d + k) - e_lo) <= span : (int32_t)(4 * d + k) <= e_hi;
-#endif
-          // (computed whatever ok says, then selected: left to itself the compiler masks exec around
-          // the round, a VALU -> SALU -> VALU round trip per word)
-          uint32_t w = xround(v, x[k]);
-          asm volatile("" : "+v"(w));
-          v = ok ? w : v;
-        }
-      }
-      if (head) cstored = xm;
-      HST(h3)
-      if (rfin) {  // merge, length, tail, avalanche (data.rs:185-198)
-        const uint32_t tb = chl & 15;
-        uint32_t m = rotl_var(v, mrot);
-        m += quad_xor1(m);
-        m += quad_xor2(m);
-        uint32_t h = (chl >= 16 ? m : P5) + chl;
-        // the file ends within the tail's 16 bytes: the file's last granule was loaded instead,
-        // which holds the tail from byte ctsh on
-        const u32x4 tw = shr_bytes(Tm, tclamp ? ctsh : 0u);
-        const uint32_t n4 = tb >> 2, n1 = tb & 3;
-        h = n4 > 0 ? tail4(h, tw.x) : h;
-        h = n4 > 1 ? tail4(h, tw.y) : h;
-        h = n4 > 2 ? tail4(h, tw.z) : h;
-        const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
-        h = n1 > 0 ? tail1(h, lw & 0xFFu) : h;
-        h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
-        h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
-        h = avalanche(h);
-#if defined(CASK_HASH_ALIGNDIAG) || defined(CASK_HASH_NOVALID)  // (timing diagnostics: checksums wrong by design)
-        asm volatile("" ::"v"(h));
-        h = cstored;
-#endif
-        if (h != cstored && qlead) {  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
-          slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
-          atomicMin(&a.cerr[ct_t], ct_r);
-        }
-      }
-      HADD(4, h3)
-    }
-    HADD(3, h2)
-    // ---- state for the next iteration
-    if (cont) {
-      cri = ri2;
-      rfin = fin2;
-      tclamp = tclamp2;
-      ctsh = (uint32_t)(tp - (end16 - 16));
-      head = false;
-    } else {
-      cv = promote && round2;
-      cb = b2;
-      cend = end2;
-      chl = hl2;
-      cM = M2;
-      csb = sb2;
-      ctl = tl2;
-      cnrd = nrd2;
-      cri = 0;
-      rfin = fin2;
-      tclamp = tclamp2;
-      ctsh = (uint32_t)(tp - (end16 - 16));
-      head = true;
-      // lane q holds the words of stripe accumulator j = w mod 4 = (q - cM - 1) mod 4
-      const uint32_t j = (q - M2 - 1) & 3;
-      v = j == 0 ? P1 + P2 : j == 1 ? P2 : j == 2 ? 0u : 0u - P1;
-      mrot = j == 0 ? 1u : j == 1 ? 7u : j == 2 ? 12u : 18u;
-      ct_t = pt;
-      ct_r = pr;
-      cw3 = pw3;
-    }
-    const bool stream_left = rnA != cur || (fullB && rnB != 0) || runs_left;
-    // (uniform by construction, and made visibly so: a loop exit the compiler must treat as divergent
-    // becomes an exec-mask loop in which the exit after the first step also reaches the loop header,
-    // so the header's waits count the first step's loads as possibly in flight and wait for them)
-    return __builtin_amdgcn_readfirstlane((int)(stream_left || __any(cv || ns != 0))) != 0;
-  };
-  // (one exit, after the second step: a wave that finishes in the first step runs the second as a
-  // no-op — nothing left to claim or load but safe lines — so that no path from the middle of the
-  // body reaches the loop header with the first step's loads in flight)
-  for (;;) {
-    (void)step(XA, TA, sA, XB, TB, sB);
-    if (!step(XB, TB, sB, XA, TA, sA)) break;
-  }
-#ifdef CASK_STAMPS
-  HADD(0, h_all)
-  if (a.stamps && lane == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[8 + i], (unsigned long long)hst[i]);
-  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[17 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-}
-
 // ---------------------------------------------------------------------------------------------
 // Walk mode with k_finish running beside k_run_hash (it needs only the chase's output, so it runs
 // in the slots the hash's last waves leave): the checksum verdicts k_finish may have read before
@@ -1017,11 +611,6 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(tpb), 0, (hipStream_t)stream, a, a.files);
 }
 
-#ifdef CASK_HASH_ALIGNED  // (A/B variant)
-#define KRH k_run_hash_al
-#else
-#define KRH k_run_hash
-#endif
 template <uint32_t D>
 static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
   // A persistent grid of exactly the resident workgroups: a workgroup beyond them would start only
@@ -1031,13 +620,13 @@ static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
   if (!per_cu) {
     int nb = 0;
     if (cask_knobs::tune("CASK_HASH_WAVES")) per_cu = atoi(cask_knobs::tune("CASK_HASH_WAVES"));
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, KRH<D>, 256, 0) == hipSuccess && nb > 0)
+    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash<D>, 256, 0) == hipSuccess && nb > 0)
       per_cu = 4 * nb;
     if (per_cu <= 0) per_cu = 8;
   }
   uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
   if (waves > nruns) waves = nruns;
-  hipLaunchKernelGGL((KRH<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL((k_run_hash<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
 }
 
 void launch_run_hash(const ScanArgs& a, int depth, void* stream) {

@@ -10,31 +10,40 @@
 //    (cask_keydir_partition), part o to rank o by grouped send/recv, each rank folding the parts it
 //    owns in rank order, then Stats from every owner's per-file terms (one more all-gather).
 // RCCL is loaded on first use (dlopen): the library itself needs no librccl to load, and a host
-// without it gets CASK_E_DEVICE from these calls only.
+// without it gets CASK_E_DEVICE from these calls only. (Under CASK_TEST_HOOKS=1, CASK_RCCL_LIB names
+// another library with RCCL's entry points: tests/fake_rccl, ranks as threads of one process.)
 //
-// Every rank issues the same sequence of collectives whatever it passes (a NULL max_seq, an empty
-// block), and a failure on any rank between two collectives (a root that cannot allocate the
-// gathered size) is agreed on by an ncclAllReduce(min) of a status flag before the data moves: all
-// ranks then return the same error instead of some blocking in ncclSend forever.
+// Every rank issues the same sequence of collectives whatever it passes (a bad argument, a NULL
+// max_seq, an empty block) and whatever fails on it between two collectives (an allocation, the
+// partition, the fold): each such status is carried to the next agreement — an ncclAllReduce(min)
+// of the ranks' statuses — before any data moves, so all ranks return the same status and none is
+// left waiting in a send, receive or all-gather that a peer will never issue. Nothing allocates
+// between an agreement and the collective it guards: the small all-gathers use device scratch made
+// with the communicator, the large buffers are allocated before the agreement that covers them.
+// Only a collective that itself fails (a broken communicator) returns without agreeing.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <mutex>
-#include <type_traits>
 #include <new>
+#include <string>
+#include <type_traits>
 #include <vector>
 
 #include "../../include/cask_scan.h"
+#include "abi_guard.h"
 #include "keydir_format.h"
+#include "knobs.h"
 
 static_assert(CASK_RCCL_ID_BYTES == NCCL_UNIQUE_ID_BYTES, "unique id size");
 
 namespace {
 
-// The RCCL entry points this file uses, resolved from librccl at first use.
+// The RCCL entry points this file uses, resolved from a library at first use.
 struct Rccl {
   decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
   decltype(&ncclCommInitRank) CommInitRank = nullptr;
@@ -50,32 +59,57 @@ struct Rccl {
   bool ok = false;
 };
 
+const Rccl* load_rccl(const char* path) {
+  Rccl* r = new (std::nothrow) Rccl();
+  if (!r) return nullptr;
+  void* h = path ? dlopen(path, RTLD_NOW | RTLD_LOCAL) : dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h && !path) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+  if (!h) return r;
+  bool all = true;
+  auto sym = [&](auto& f, const char* name) {
+    f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
+    all = all && f != nullptr;
+  };
+  sym(r->GetUniqueId, "ncclGetUniqueId");
+  sym(r->CommInitRank, "ncclCommInitRank");
+  sym(r->CommDestroy, "ncclCommDestroy");
+  sym(r->CommCount, "ncclCommCount");
+  sym(r->CommUserRank, "ncclCommUserRank");
+  sym(r->AllGather, "ncclAllGather");
+  sym(r->AllReduce, "ncclAllReduce");
+  sym(r->Send, "ncclSend");
+  sym(r->Recv, "ncclRecv");
+  sym(r->GroupStart, "ncclGroupStart");
+  sym(r->GroupEnd, "ncclGroupEnd");
+  r->ok = all;
+  return r;
+}
+
+// librccl, or the test hook's library; each loaded once and kept for the process.
 const Rccl* rccl() {
-  static Rccl r;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
-    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
-    if (!h) return;
-    bool all = true;
-    auto sym = [&](auto& f, const char* name) {
-      f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(h, name));
-      all = all && f != nullptr;
-    };
-    sym(r.GetUniqueId, "ncclGetUniqueId");
-    sym(r.CommInitRank, "ncclCommInitRank");
-    sym(r.CommDestroy, "ncclCommDestroy");
-    sym(r.CommCount, "ncclCommCount");
-    sym(r.CommUserRank, "ncclCommUserRank");
-    sym(r.AllGather, "ncclAllGather");
-    sym(r.AllReduce, "ncclAllReduce");
-    sym(r.Send, "ncclSend");
-    sym(r.Recv, "ncclRecv");
-    sym(r.GroupStart, "ncclGroupStart");
-    sym(r.GroupEnd, "ncclGroupEnd");
-    r.ok = all;
-  });
-  return r.ok ? &r : nullptr;
+  static std::mutex mu;
+  static std::map<std::string, const Rccl*> loaded;
+  const char* alt = cask_knobs::hook("CASK_RCCL_LIB");
+  const std::string key = alt ? alt : "";
+  std::lock_guard<std::mutex> g(mu);
+  auto it = loaded.find(key);
+  const Rccl* r = it != loaded.end() ? it->second : (loaded[key] = load_rccl(alt));
+  return r && r->ok ? r : nullptr;
+}
+
+// What cask_rccl_comm_init hands out: the communicator, the library that made it, and device scratch
+// for the small collectives (statuses, sizes) so that they never allocate between two agreements.
+struct Comm {
+  const Rccl* R = nullptr;
+  ncclComm_t c = nullptr;
+  int nranks = 0, rank = 0, device = 0;
+  void* scratch = nullptr;
+  uint64_t cap = 0;  // bytes of scratch
+};
+
+uint64_t scratch_bytes(int nranks) {  // the N x N size matrix, in and out, and the status words
+  const uint64_t n = (uint64_t)nranks;
+  return 8 * (n * n + 2 * n + 8) + 256;
 }
 
 struct DevMem {  // device memory of one call
@@ -85,109 +119,150 @@ struct DevMem {  // device memory of one call
   }
 };
 
-// Every rank's `n` u64 values, in rank order, on every rank (ncclAllGather through device memory).
-bool allgather_u64(const Rccl& R, ncclComm_t c, hipStream_t st, int nranks, const uint64_t* mine, uint64_t n,
-                   std::vector<uint64_t>& all) {
-  DevMem m;
-  if (hipMalloc(&m.p, 8ull * n * (nranks + 1)) != hipSuccess) return false;
-  uint64_t* dm = (uint64_t*)m.p;
-  all.assign(n * nranks, 0);
-  return hipMemcpyAsync(dm + n * nranks, mine, 8ull * n, hipMemcpyHostToDevice, st) == hipSuccess &&
-         R.AllGather(dm + n * nranks, dm, n, ncclUint64, c, st) == ncclSuccess &&
-         hipMemcpyAsync(all.data(), dm, 8ull * n * nranks, hipMemcpyDeviceToHost, st) == hipSuccess &&
+// Every rank's `n` u64 values, in rank order, on every rank (ncclAllGather through device memory:
+// the communicator's scratch, or `big` when the values do not fit it). A rank that has failed takes
+// part all the same: with `mine` NULL it sends zeros, with `all` empty it keeps nothing. False when
+// a collective or copy fails: the communicator is then unusable and the caller returns
+// CASK_E_DEVICE.
+bool allgather_u64(const Comm& K, hipStream_t st, const uint64_t* mine, uint64_t n, std::vector<uint64_t>& all,
+                   void* big = nullptr) {
+  const uint64_t need = 8ull * n * (K.nranks + 1);
+  uint64_t* dm = (uint64_t*)(need <= K.cap ? K.scratch : big);
+  if (!dm) return false;
+  if (!n) return true;
+  const bool in = mine ? hipMemcpyAsync(dm + n * K.nranks, mine, 8ull * n, hipMemcpyHostToDevice, st) == hipSuccess
+                       : hipMemsetAsync(dm + n * K.nranks, 0, 8ull * n, st) == hipSuccess;
+  return in && K.R->AllGather(dm + n * K.nranks, dm, n, ncclUint64, K.c, st) == ncclSuccess &&
+         (all.size() < n * K.nranks ||
+          hipMemcpyAsync(all.data(), dm, 8ull * n * K.nranks, hipMemcpyDeviceToHost, st) == hipSuccess) &&
          hipStreamSynchronize(st) == hipSuccess;
 }
 
 // The status every rank returns: the lowest (most severe) of the ranks' own statuses (0 = ok), by
-// ncclAllReduce(min). A rank that fails between two collectives still calls this, so no peer is left
-// waiting in a send or receive it will never match.
-int agree(const Rccl& R, ncclComm_t c, hipStream_t st, int mine) {
-  DevMem m;
-  if (hipMalloc(&m.p, 16) != hipSuccess) return CASK_E_NOMEM;  // (16 B: peers would wait here)
-  int32_t* dm = (int32_t*)m.p;
+// ncclAllReduce(min) in the communicator's scratch. A rank that fails between two collectives still
+// calls this, so no peer is left waiting in a collective it will never match.
+int agree(const Comm& K, hipStream_t st, int mine) {
+  int32_t* dm = (int32_t*)K.scratch;
   int32_t v = mine, out = 0;
   if (hipMemcpyAsync(dm, &v, 4, hipMemcpyHostToDevice, st) != hipSuccess ||
-      R.AllReduce(dm, dm + 1, 1, ncclInt32, ncclMin, c, st) != ncclSuccess ||
+      K.R->AllReduce(dm, dm + 1, 1, ncclInt32, ncclMin, K.c, st) != ncclSuccess ||
       hipMemcpyAsync(&out, dm + 1, 4, hipMemcpyDeviceToHost, st) != hipSuccess || hipStreamSynchronize(st) != hipSuccess)
     return CASK_E_DEVICE;
   return out;
 }
 
-int comm_shape(const Rccl& R, ncclComm_t c, int* nranks, int* rank) {
-  return R.CommCount(c, nranks) == ncclSuccess && R.CommUserRank(c, rank) == ncclSuccess ? CASK_OK : CASK_E_DEVICE;
+// A host vector sized without throwing: false (and the vector empty) when the memory is not there.
+template <class T>
+bool host_alloc(std::vector<T>& v, uint64_t n) {
+  try {
+    v.assign(n, T{});
+    return true;
+  } catch (const std::bad_alloc&) {
+    v.clear();
+    return false;
+  }
 }
 
 }  // namespace
 
 extern "C" int cask_rccl_unique_id(uint8_t* id) {
-  if (!id) return CASK_E_INVALID_ARG;
-  const Rccl* R = rccl();
-  if (!R) return CASK_E_DEVICE;
-  ncclUniqueId u;
-  if (R->GetUniqueId(&u) != ncclSuccess) return CASK_E_DEVICE;
-  memcpy(id, &u, sizeof(u));
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!id) return CASK_E_INVALID_ARG;
+    const Rccl* R = rccl();
+    if (!R) return CASK_E_DEVICE;
+    ncclUniqueId u;
+    if (R->GetUniqueId(&u) != ncclSuccess) return CASK_E_DEVICE;
+    memcpy(id, &u, sizeof(u));
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_rccl_comm_init(const uint8_t* id, int nranks, int rank, int device, void** comm) {
-  if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return CASK_E_INVALID_ARG;
-  const Rccl* R = rccl();
-  if (!R) return CASK_E_DEVICE;
-  if (hipSetDevice(device) != hipSuccess) return CASK_E_DEVICE;
-  ncclUniqueId u;
-  memcpy(&u, id, sizeof(u));
-  ncclComm_t c = nullptr;
-  if (R->CommInitRank(&c, nranks, u, rank) != ncclSuccess) return CASK_E_DEVICE;
-  *comm = c;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!id || !comm || nranks < 1 || rank < 0 || rank >= nranks) return CASK_E_INVALID_ARG;
+    const Rccl* R = rccl();
+    if (!R) return CASK_E_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return CASK_E_DEVICE;
+    Comm* K = new (std::nothrow) Comm();
+    if (!K) return CASK_E_NOMEM;
+    K->R = R;
+    K->nranks = nranks;
+    K->rank = rank;
+    K->device = device;
+    K->cap = scratch_bytes(nranks);
+    // (the scratch first: a rank that cannot make it fails before joining, and the others' init
+    // fails on the missing peer, as RCCL's own would)
+    if (hipMalloc(&K->scratch, K->cap) != hipSuccess) {
+      delete K;
+      return CASK_E_NOMEM;
+    }
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof(u));
+    if (R->CommInitRank(&K->c, nranks, u, rank) != ncclSuccess) {
+      (void)hipFree(K->scratch);
+      delete K;
+      return CASK_E_DEVICE;
+    }
+    *comm = K;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_rccl_comm_destroy(void* comm) {
-  if (!comm) return CASK_E_INVALID_ARG;
-  const Rccl* R = rccl();
-  if (!R) return CASK_E_DEVICE;
-  return R->CommDestroy((ncclComm_t)comm) == ncclSuccess ? CASK_OK : CASK_E_DEVICE;
+  return cask_abi::guard([&]() -> int {
+    if (!comm) return CASK_E_INVALID_ARG;
+    Comm* K = (Comm*)comm;
+    const int st = K->R->CommDestroy(K->c) == ncclSuccess ? CASK_OK : CASK_E_DEVICE;
+    (void)hipSetDevice(K->device);
+    (void)hipFree(K->scratch);
+    delete K;
+    return st;
+  });
 }
 
-extern "C" int cask_keydir_gather_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, int root,
-                                       cask_db* db, uint64_t* gathered, uint64_t* max_seq) {
+static int gather_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes, int root, cask_db* db,
+                       uint64_t* gathered, uint64_t* max_seq) {
   using namespace cask_kd;
-  if (!ctx || !comm || (bytes && !block)) return CASK_E_INVALID_ARG;
-  const Rccl* Rp = rccl();
-  if (!Rp) return CASK_E_DEVICE;
-  const Rccl& R = *Rp;
-  ncclComm_t c = (ncclComm_t)comm;
-  int nranks = 0, rank = 0;
-  if (comm_shape(R, c, &nranks, &rank) != CASK_OK) return CASK_E_DEVICE;
-  // (argument errors that differ between ranks are agreed on below, like any other failure)
-  if (root < 0 || root >= nranks) return CASK_E_INVALID_ARG;
+  const int nranks = K.nranks, rank = K.rank;
   if (hipSetDevice(cask_ctx_device(ctx)) != hipSuccess) return CASK_E_DEVICE;
   hipStream_t st = (hipStream_t)cask_ctx_stream(ctx);
+  // argument errors on any rank are agreed on below, like any other failure (a bad root: this rank
+  // goes through the all-gather with root 0 in its place, then every rank stops at the agreement)
+  int status = (bytes && !block) ? CASK_E_INVALID_ARG : CASK_OK;
+  std::vector<uint64_t> all, off;
+  if (!host_alloc(all, 2ull * nranks) || !host_alloc(off, (uint64_t)nranks + 1)) status = CASK_E_NOMEM;
+  if (root < 0 || root >= nranks) {
+    status = CASK_E_INVALID_ARG;
+    root = 0;
+  }
+  if (rank == root && !db) status = CASK_E_INVALID_ARG;
   // this rank's block header (its max sequence) from the device
   ShardHeader hd{};
-  int status = rank == root && !db ? CASK_E_INVALID_ARG : CASK_OK;
-  if (bytes >= sizeof(hd) &&
-      (hipMemcpyAsync(&hd, block, sizeof(hd), hipMemcpyDeviceToHost, st) != hipSuccess ||
-       hipStreamSynchronize(st) != hipSuccess))
+  const bool has_hd = status == CASK_OK && bytes >= sizeof(hd);
+  if (has_hd && (hipMemcpyAsync(&hd, block, sizeof(hd), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                 hipStreamSynchronize(st) != hipSuccess))
     status = CASK_E_DEVICE;
   // every rank's block size and max sequence + 1 (ncclAllGather of two u64 per rank): the global
   // maximum sequence is the largest of them on every rank, with no collective of its own
-  const uint64_t mine[2] = {status == CASK_OK ? bytes : 0, bytes >= sizeof(hd) ? hd.max_seq_p1 : 0};
-  std::vector<uint64_t> all;
-  if (!allgather_u64(R, c, st, nranks, mine, 2, all)) return CASK_E_DEVICE;
-  uint64_t mx = 0;
-  for (int r = 0; r < nranks; ++r) mx = std::max(mx, all[2ull * r + 1]);
-  if (max_seq) *max_seq = mx ? mx - 1 : 0;
-  std::vector<uint64_t> off(nranks + 1, 0);
-  for (int r = 0; r < nranks; ++r) off[r + 1] = off[r] + ((all[2ull * r] + 255) & ~255ull);
-  if (gathered) *gathered = rank == root ? off[nranks] : bytes;
-  // the root's receive buffer, then the agreed status: every rank goes on, or every rank stops
+  const uint64_t mine[2] = {status == CASK_OK ? bytes : 0, has_hd ? hd.max_seq_p1 : 0};
+  if (!allgather_u64(K, st, mine, 2, all)) return CASK_E_DEVICE;
+  if (status == CASK_OK) {
+    uint64_t mx = 0;
+    for (int r = 0; r < nranks; ++r) mx = std::max(mx, all[2ull * r + 1]);
+    if (max_seq) *max_seq = mx ? mx - 1 : 0;
+    for (int r = 0; r < nranks; ++r) off[r + 1] = off[r] + ((all[2ull * r] + 255) & ~255ull);
+    if (gathered) *gathered = rank == root ? off[nranks] : bytes;
+  }
+  // the root's receive and host buffers, then the agreed status: every rank goes on, or every one stops
   DevMem buf;
-  if (status == CASK_OK && rank == root && off[nranks] && hipMalloc(&buf.p, off[nranks]) != hipSuccess)
+  std::vector<uint8_t> host;
+  if (status == CASK_OK && rank == root &&
+      (cask_abi::take_inject(ctx, cask_abi::kInjRootAlloc) || (off[nranks] && hipMalloc(&buf.p, off[nranks]) != hipSuccess) ||
+       !host_alloc(host, off[nranks] ? off[nranks] : 1)))
     status = CASK_E_NOMEM;
-  if ((status = agree(R, c, st, status)) != CASK_OK) return status;
+  if ((status = agree(K, st, status)) != CASK_OK) return status;
   // the blocks to the root: one grouped send per rank, nranks - 1 receives on the root
-  if (R.GroupStart() != ncclSuccess) return CASK_E_DEVICE;
+  if (K.R->GroupStart() != ncclSuccess) return CASK_E_DEVICE;
   bool sent = true;
   if (rank == root) {
     for (int r = 0; r < nranks; ++r) {
@@ -196,111 +271,122 @@ extern "C" int cask_keydir_gather_rccl(cask_ctx* ctx, void* comm, const void* bl
       if (r == root)
         sent = sent && hipMemcpyAsync(dst, block, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess;
       else
-        sent = sent && R.Recv(dst, all[2ull * r], ncclUint8, r, c, st) == ncclSuccess;
+        sent = sent && K.R->Recv(dst, all[2ull * r], ncclUint8, r, K.c, st) == ncclSuccess;
     }
   } else if (bytes) {
-    sent = R.Send(block, bytes, ncclUint8, root, c, st) == ncclSuccess;
+    sent = K.R->Send(block, bytes, ncclUint8, root, K.c, st) == ncclSuccess;
   }
-  if (R.GroupEnd() != ncclSuccess || !sent || hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;
-  if (rank != root) return CASK_OK;
-  // the root's fold, in rank order (= replay order)
-  std::vector<uint8_t> host;
-  try {
-    host.resize(off[nranks] ? off[nranks] : 1);
-  } catch (const std::bad_alloc&) {
-    return CASK_E_NOMEM;
+  if (K.R->GroupEnd() != ncclSuccess || !sent || hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;
+  // the root's fold, in rank order (= replay order); its outcome is every rank's status
+  int fst = CASK_OK;
+  if (rank == root) {
+    if (off[nranks] && hipMemcpy(host.data(), buf.p, off[nranks], hipMemcpyDeviceToHost) != hipSuccess) fst = CASK_E_DEVICE;
+    if (fst == CASK_OK && cask_abi::take_inject(ctx, cask_abi::kInjFold)) fst = CASK_E_NOMEM;
+    for (int r = 0; r < nranks && fst == CASK_OK; ++r)
+      if (all[2ull * r]) fst = cask_keydir_merge(db, host.data() + off[r], all[2ull * r]);
   }
-  if (off[nranks] && hipMemcpy(host.data(), buf.p, off[nranks], hipMemcpyDeviceToHost) != hipSuccess)
-    return CASK_E_DEVICE;
-  for (int r = 0; r < nranks; ++r) {
-    if (!all[2ull * r]) continue;
-    const int rc = cask_keydir_merge(db, host.data() + off[r], all[2ull * r]);
-    if (rc != CASK_OK) return rc;
-  }
-  return CASK_OK;
+  return agree(K, st, fst);
 }
 
-extern "C" int cask_keydir_exchange_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, cask_db* db,
-                                         uint64_t* sent_bytes, uint64_t* recv_bytes) {
+extern "C" int cask_keydir_gather_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, int root,
+                                       cask_db* db, uint64_t* gathered, uint64_t* max_seq) {
+  return cask_abi::guard([&]() -> int {
+    if (!ctx || !comm) return CASK_E_INVALID_ARG;  // (no communicator to agree over)
+    return gather_impl(ctx, *(Comm*)comm, block, bytes, root, db, gathered, max_seq);
+  });
+}
+
+static int exchange_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes, cask_db* db, uint64_t* sent_bytes,
+                         uint64_t* recv_bytes) {
   using namespace cask_kd;
-  if (!ctx || !comm || !db || (bytes && !block)) return CASK_E_INVALID_ARG;
-  const Rccl* Rp = rccl();
-  if (!Rp) return CASK_E_DEVICE;
-  const Rccl& R = *Rp;
-  ncclComm_t c = (ncclComm_t)comm;
-  int nranks = 0, rank = 0;
-  if (comm_shape(R, c, &nranks, &rank) != CASK_OK) return CASK_E_DEVICE;
-  if ((uint32_t)nranks > kMaxParts) return CASK_E_INVALID_ARG;
+  const int nranks = K.nranks, rank = K.rank;
+  const uint64_t N = (uint64_t)nranks;
   if (hipSetDevice(cask_ctx_device(ctx)) != hipSuccess) return CASK_E_DEVICE;
   hipStream_t st = (hipStream_t)cask_ctx_stream(ctx);
+  int status = (!db || (bytes && !block) || N > kMaxParts) ? CASK_E_INVALID_ARG : CASK_OK;
+  std::vector<uint64_t> poff, mine, all, roff, counts;
+  if (!host_alloc(poff, N + 1) || !host_alloc(mine, N) || !host_alloc(all, N * N) || !host_alloc(roff, N + 1) ||
+      !host_alloc(counts, N))
+    status = CASK_E_NOMEM;
   // 1. this rank's block split by key owner, on its device
-  std::vector<uint64_t> poff(nranks + 1, 0);
   const void* parts = nullptr;
-  int status = bytes ? cask_keydir_partition(ctx, block, bytes, (uint32_t)nranks, &parts, poff.data()) : CASK_OK;
+  if (status == CASK_OK && bytes) status = cask_keydir_partition(ctx, block, bytes, (uint32_t)nranks, &parts, poff.data());
   // 2. the nranks x nranks matrix of part sizes (row r: what rank r sends to each owner)
-  std::vector<uint64_t> mine(nranks, 0), all;
   for (int o = 0; o < nranks && status == CASK_OK; ++o) mine[o] = poff[o + 1] - poff[o];
-  if (!allgather_u64(R, c, st, nranks, mine.data(), (uint64_t)nranks, all)) return CASK_E_DEVICE;
-  std::vector<uint64_t> roff(nranks + 1, 0);  // what this rank receives from each rank, in rank order
-  for (int r = 0; r < nranks; ++r) roff[r + 1] = roff[r] + ((all[(uint64_t)r * nranks + rank] + 255) & ~255ull);
+  if (!allgather_u64(K, st, status == CASK_OK ? mine.data() : nullptr, N, all)) return CASK_E_DEVICE;
+  for (int r = 0; r < nranks && status == CASK_OK; ++r) roff[r + 1] = roff[r] + ((all[(uint64_t)r * N + rank] + 255) & ~255ull);
   DevMem buf;
-  if (status == CASK_OK && roff[nranks] && hipMalloc(&buf.p, roff[nranks]) != hipSuccess) status = CASK_E_NOMEM;
-  if ((status = agree(R, c, st, status)) != CASK_OK) return status;
+  std::vector<uint8_t> host;
+  if (status == CASK_OK && roff[nranks] && (hipMalloc(&buf.p, roff[nranks]) != hipSuccess || !host_alloc(host, roff[nranks])))
+    status = CASK_E_NOMEM;
+  if ((status = agree(K, st, status)) != CASK_OK) return status;
   // 3. the all-to-all: part o to rank o, one grouped send/recv per pair
-  if (R.GroupStart() != ncclSuccess) return CASK_E_DEVICE;
+  if (K.R->GroupStart() != ncclSuccess) return CASK_E_DEVICE;
   bool moved = true;
   for (int r = 0; r < nranks; ++r) {
-    const uint64_t in = all[(uint64_t)r * nranks + rank], out = all[(uint64_t)rank * nranks + r];
+    const uint64_t in = all[(uint64_t)r * N + rank], out = all[(uint64_t)rank * N + r];
     if (r == rank) {
       if (in) moved = moved && hipMemcpyAsync((uint8_t*)buf.p + roff[r], (const uint8_t*)parts + poff[r], in,
                                               hipMemcpyDeviceToDevice, st) == hipSuccess;
       continue;
     }
-    if (out) moved = moved && R.Send((const uint8_t*)parts + poff[r], out, ncclUint8, r, c, st) == ncclSuccess;
-    if (in) moved = moved && R.Recv((uint8_t*)buf.p + roff[r], in, ncclUint8, r, c, st) == ncclSuccess;
+    if (out) moved = moved && K.R->Send((const uint8_t*)parts + poff[r], out, ncclUint8, r, K.c, st) == ncclSuccess;
+    if (in) moved = moved && K.R->Recv((uint8_t*)buf.p + roff[r], in, ncclUint8, r, K.c, st) == ncclSuccess;
   }
-  if (R.GroupEnd() != ncclSuccess || !moved || hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;
+  if (K.R->GroupEnd() != ncclSuccess || !moved || hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;
   uint64_t sent = 0, got = 0;
   for (int r = 0; r < nranks; ++r) {
-    if (r != rank) sent += all[(uint64_t)rank * nranks + r];
-    got += all[(uint64_t)r * nranks + rank];
+    if (r != rank) sent += all[(uint64_t)rank * N + r];
+    got += all[(uint64_t)r * N + rank];
   }
   if (sent_bytes) *sent_bytes = sent;
   if (recv_bytes) *recv_bytes = got;
   // 4. this owner's fold of its parts, in rank order (= replay order)
-  std::vector<uint8_t> host;
   int fst = CASK_OK;
-  try {
-    host.resize(roff[nranks] ? roff[nranks] : 1);
-  } catch (const std::bad_alloc&) {
-    fst = CASK_E_NOMEM;
-  }
-  if (fst == CASK_OK && roff[nranks] && hipMemcpy(host.data(), buf.p, roff[nranks], hipMemcpyDeviceToHost) != hipSuccess)
-    fst = CASK_E_DEVICE;
+  if (roff[nranks] && hipMemcpy(host.data(), buf.p, roff[nranks], hipMemcpyDeviceToHost) != hipSuccess) fst = CASK_E_DEVICE;
+  if (fst == CASK_OK && cask_abi::take_inject(ctx, cask_abi::kInjFold)) fst = CASK_E_NOMEM;
   for (int r = 0; r < nranks && fst == CASK_OK; ++r) {
-    const uint64_t in = all[(uint64_t)r * nranks + rank];
+    const uint64_t in = all[(uint64_t)r * N + rank];
     if (in) fst = cask_keydir_merge(db, host.data() + roff[r], in);
   }
-  // 5. Stats: every owner's per-file terms to every rank (sizes, then the padded tables), summed
+  // 5. Stats: every owner's per-file terms to every rank (counts, then the padded tables), summed
   int64_t tb = fst == CASK_OK ? cask_keydir_terms(db, nullptr, 0) : 0;
   if (tb < 0) {
     fst = (int)tb;
     tb = 0;
   }
-  if ((fst = agree(R, c, st, fst)) != CASK_OK) return fst;
+  if ((fst = agree(K, st, fst)) != CASK_OK) return fst;
   const uint64_t nt = (uint64_t)tb / sizeof(KeydirTerm);
-  std::vector<uint64_t> counts;
-  if (!allgather_u64(R, c, st, nranks, &nt, 1, counts)) return CASK_E_DEVICE;
+  if (!allgather_u64(K, st, &nt, 1, counts)) return CASK_E_DEVICE;
   uint64_t mt = 0;
   for (uint64_t x : counts) mt = std::max(mt, x);
   const uint64_t w = mt * sizeof(KeydirTerm) / 8;  // u64 per rank's padded table
-  std::vector<uint64_t> tab(std::max<uint64_t>(w, 1), 0), tall;
-  if (tb && cask_keydir_terms(db, (uint8_t*)tab.data(), (uint64_t)tb) != tb) return CASK_E_INVALID_ARG;
-  if (w && !allgather_u64(R, c, st, nranks, tab.data(), w, tall)) return CASK_E_DEVICE;
-  std::vector<uint8_t> terms;
-  for (int r = 0; r < nranks; ++r) {
-    const uint8_t* p = (const uint8_t*)(tall.data() + (uint64_t)r * w);
-    terms.insert(terms.end(), p, p + counts[r] * sizeof(KeydirTerm));
+  std::vector<uint64_t> tab, tall;
+  DevMem big;  // the all-gather's device buffer when the tables do not fit the scratch
+  int tst = host_alloc(tab, std::max<uint64_t>(w, 1)) && host_alloc(tall, std::max<uint64_t>(w * N, 1)) ? CASK_OK : CASK_E_NOMEM;
+  if (tst == CASK_OK && 8ull * w * (N + 1) > K.cap && hipMalloc(&big.p, 8ull * w * (N + 1)) != hipSuccess) tst = CASK_E_NOMEM;
+  if (tst == CASK_OK && cask_abi::take_inject(ctx, cask_abi::kInjTerms)) tst = CASK_E_INVALID_ARG;
+  if (tst == CASK_OK && tb && cask_keydir_terms(db, (uint8_t*)tab.data(), (uint64_t)tb) != tb) tst = CASK_E_INVALID_ARG;
+  if ((tst = agree(K, st, tst)) != CASK_OK) return tst;
+  if (w && !allgather_u64(K, st, tab.data(), w, tall, big.p)) return CASK_E_DEVICE;
+  int ft = CASK_OK;
+  try {
+    std::vector<uint8_t> terms;
+    for (int r = 0; r < nranks; ++r) {
+      const uint8_t* p = (const uint8_t*)(tall.data() + (uint64_t)r * w);
+      terms.insert(terms.end(), p, p + counts[r] * sizeof(KeydirTerm));
+    }
+    ft = cask_keydir_finish_terms(db, terms.data(), terms.size());
+  } catch (const std::bad_alloc&) {
+    ft = CASK_E_NOMEM;
   }
-  return cask_keydir_finish_terms(db, terms.data(), terms.size());
+  return agree(K, st, ft);
+}
+
+extern "C" int cask_keydir_exchange_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, cask_db* db,
+                                         uint64_t* sent_bytes, uint64_t* recv_bytes) {
+  return cask_abi::guard([&]() -> int {
+    if (!ctx || !comm) return CASK_E_INVALID_ARG;  // (no communicator to agree over)
+    return exchange_impl(ctx, *(Comm*)comm, block, bytes, db, sent_bytes, recv_bytes);
+  });
 }

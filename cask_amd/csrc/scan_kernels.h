@@ -207,14 +207,7 @@ struct SummaryHead {
 };
 // followed by row_off[nfiles+1], then per file: first_bad, bad_T, err_row, err_slot
 
-// One record of a compaction rewrite: len bytes from src file `src` at `pos` to output byte `dst`.
-struct GatherRec {
-  uint64_t pos, dst;
-  uint32_t src, len;
-};
-
 // Host-callable launchers (defined in scan_kernels.hip).
-void launch_gather(const GatherRec* recs, uint64_t n, const uint8_t* const* src, uint8_t* dst, void* stream);
 void launch_read_entries(const uint64_t* pos, const uint32_t* src, uint64_t n, const uint8_t* const* srcs,
                          const uint64_t* slen, uint64_t* len, uint8_t* st, uint32_t* expct, uint32_t* found, void* stream);
 uint32_t geometry_chunk(int geo);

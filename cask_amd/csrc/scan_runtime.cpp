@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "../../include/cask_scan.h"
+#include "abi_guard.h"
 #include "host_ring.h"
 #include "keydir_format.h"
 #include "scan_kernels.h"
@@ -94,7 +95,7 @@ struct cask_ctx {
   DevBuf slots;      // 16-B slot rows, slot_cap per chunk
   DevBuf filebuf;    // FileDesc[] | call block (CallLayout) | file_err[] | first_bad[] | file_total[] | summary
   DevBuf err2;       // error detail words
-  DevBuf gather;     // compaction rewrite: GatherRec[] | source pointers
+  DevBuf gather;     // cask_read_entries_device: positions, sources and outputs of one batch
   DevBuf stamps;     // diagnostic builds (-DCASK_STAMPS) only
   DevBuf repair;     // runs (u64 x 2 per chunk) | cerr (u32) | redo (u8) | long_done (u8)
   DevBuf lq;         // long-record queue (slot indices by length class)
@@ -104,6 +105,7 @@ struct cask_ctx {
   DevBuf probe;      // k_probe_regions: 3 u64 per region of each file
   DevBuf mruns;      // mixed call: walk-mode run indices | chunk-mode [first, end) stretches
   uint32_t epoch = 0;
+  uint32_t inject = 0;  // test hooks: cask_debug_inject (abi_guard.h)
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
   uint64_t* dbg_tin = nullptr;
@@ -163,6 +165,19 @@ static int set_dev(const cask_ctx* c) {
   return hipSetDevice(c->device) == hipSuccess ? CASK_OK : CASK_E_DEVICE;
 }
 
+bool cask_abi::take_inject(cask_ctx* c, uint32_t bit) {
+  if (!c || !(c->inject & bit)) return false;
+  c->inject &= ~bit;
+  return true;
+}
+
+// Test hook: force failures on this context (abi_guard.h); CASK_E_INVALID_ARG outside the tests.
+extern "C" int cask_debug_inject(cask_ctx* c, uint32_t bits) {
+  if (!c || !cask_knobs::test_hooks()) return CASK_E_INVALID_ARG;
+  c->inject = bits;
+  return CASK_OK;
+}
+
 extern "C" {
 
 cask_ctx* cask_ctx_create(int device, int* status) {
@@ -203,20 +218,24 @@ void cask_ctx_destroy(cask_ctx* c) {
 }
 
 int cask_ctx_set_stream(cask_ctx* c, void* s) {
-  if (!c) return CASK_E_INVALID_ARG;
-  c->stream = s ? (hipStream_t)s : c->own;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c) return CASK_E_INVALID_ARG;
+    c->stream = s ? (hipStream_t)s : c->own;
+    return CASK_OK;
+  });
 }
 
 int cask_ctx_wait_stream(cask_ctx* c, void* other) {
-  if (!c) return CASK_E_INVALID_ARG;
-  if ((hipStream_t)other == c->stream) return CASK_OK;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (hipEventRecord(c->evw, (hipStream_t)other) != hipSuccess ||
-      hipStreamWaitEvent(c->stream, c->evw, 0) != hipSuccess)
-    return CASK_E_DEVICE;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c) return CASK_E_INVALID_ARG;
+    if ((hipStream_t)other == c->stream) return CASK_OK;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (hipEventRecord(c->evw, (hipStream_t)other) != hipSuccess ||
+        hipStreamWaitEvent(c->stream, c->evw, 0) != hipSuccess)
+      return CASK_E_DEVICE;
+    return CASK_OK;
+  });
 }
 
 void* cask_ctx_stream(cask_ctx* c) { return c ? (void*)c->stream : nullptr; }
@@ -233,15 +252,19 @@ uint64_t cask_rows_bound(const cask_file_view* files, uint32_t nfiles) {
 uint32_t cask_xxh32(const uint8_t* data, uint64_t len) { return cask_xxh::xxh32(data, len, 0); }
 
 int cask_last_timings(const cask_ctx* c, float* ms6) {
-  if (!c || !ms6) return CASK_E_INVALID_ARG;
-  memcpy(ms6, c->last_ms, 6 * sizeof(float));
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c || !ms6) return CASK_E_INVALID_ARG;
+    memcpy(ms6, c->last_ms, 6 * sizeof(float));
+    return CASK_OK;
+  });
 }
 
 int cask_last_timings8(const cask_ctx* c, float* ms8) {
-  if (!c || !ms8) return CASK_E_INVALID_ARG;
-  memcpy(ms8, c->last_ms, 8 * sizeof(float));
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c || !ms8) return CASK_E_INVALID_ARG;
+    memcpy(ms8, c->last_ms, 8 * sizeof(float));
+    return CASK_OK;
+  });
 }
 
 int cask_last_dense(const cask_ctx* c) { return c ? c->last_dense : 0; }
@@ -251,9 +274,11 @@ int cask_last_walk(const cask_ctx* c) { return c ? c->last_walk : 0; }
 int cask_last_geometry(const cask_ctx* c) { return c ? c->last_geo : -1; }
 
 int cask_last_counters(const cask_ctx* c, uint64_t* c5) {
-  if (!c || !c5) return CASK_E_INVALID_ARG;
-  memcpy(c5, c->last_counters, sizeof(c->last_counters));
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c || !c5) return CASK_E_INVALID_ARG;
+    memcpy(c5, c->last_counters, sizeof(c->last_counters));
+    return CASK_OK;
+  });
 }
 
 }  // extern "C"
@@ -954,315 +979,324 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
 
 extern "C" int cask_parse_hints_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
                                        uint64_t* file_row_offset, cask_scan_error* err) {
-  if (!c || !rows) return CASK_E_INVALID_ARG;
-  for (uint32_t i = 0; i < nfiles; ++i)
-    if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, true);
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !rows) return CASK_E_INVALID_ARG;
+    for (uint32_t i = 0; i < nfiles; ++i)
+      if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, true);
+  });
 }
 
 extern "C" int cask_scan_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
                                 uint64_t* file_row_offset, cask_scan_error* err) {
-  if (!c || !rows) return CASK_E_INVALID_ARG;
-  for (uint32_t i = 0; i < nfiles; ++i)
-    if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  return scan_device_impl(c, files, nfiles, rows, file_row_offset, err);
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !rows) return CASK_E_INVALID_ARG;
+    for (uint32_t i = 0; i < nfiles; ++i)
+      if (files && !(files[i].flags & CASK_VIEW_DEVICE)) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    return scan_device_impl(c, files, nfiles, rows, file_row_offset, err);
+  });
 }
 
 extern "C" int cask_scan_host(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
                               uint64_t* file_row_offset, cask_scan_error* err) {
-  if (!c || !rows || (nfiles && !files)) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  hipStream_t st = c->stream;
-  // stage every file at a 256-B aligned offset of one device buffer
-  std::vector<uint64_t> off(nfiles + 1, 0);
-  uint64_t total = 0;
-  for (uint32_t i = 0; i < nfiles; ++i) {
-    off[i] = total;
-    total = align_up(total + files[i].len, 256);
-  }
-  const uint64_t bound = cask_rows_bound(files, nfiles);
-  const uint64_t rcap = std::min<uint64_t>(bound, rows->capacity ? rows->capacity : bound);
-  if (!c->stage_data.ensure(total + 256)) return CASK_E_NOMEM;
-  if (!c->stage_rows.ensure(rcap * 23 + 5 * 256)) return CASK_E_NOMEM;
-  std::vector<cask_file_view> dv(nfiles);
-  uint8_t* d = c->stage_data.as<uint8_t>();
-  // Large inputs go through the pinned ring on host threads (CASK_STAGE_MIN: the smallest staged
-  // input, default 64 MiB; 0 stages everything — the tests' knob)
-  const char* mv = cask_knobs::hook("CASK_STAGE_MIN");
-  const bool staged = total && total >= (mv ? strtoull(mv, nullptr, 10) : (64ull << 20));
-  if (staged) {
-    if (!c->ring) c->ring.reset(new (std::nothrow) cask_host::PinnedRing());
-    if (!c->ring || !c->ring->init(c->device)) return CASK_E_NOMEM;
-    if (hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;  // stage_data is free
-  }
-  std::vector<cask_host::PinnedRing::Piece> ps;
-  for (uint32_t i = 0; i < nfiles; ++i) {
-    dv[i] = files[i];
-    dv[i].flags = CASK_VIEW_DEVICE;
-    dv[i].data = d + off[i];
-    if (staged) {
-      cask_host::PinnedRing::split((uint8_t*)files[i].data, d + off[i], files[i].len, ps);
-    } else if (files[i].len && hipMemcpyAsync(d + off[i], files[i].data, files[i].len, hipMemcpyHostToDevice, st) != hipSuccess) {
-      return CASK_E_DEVICE;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !rows || (nfiles && !files)) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    hipStream_t st = c->stream;
+    // stage every file at a 256-B aligned offset of one device buffer
+    std::vector<uint64_t> off(nfiles + 1, 0);
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < nfiles; ++i) {
+      off[i] = total;
+      total = align_up(total + files[i].len, 256);
     }
-  }
-  if (staged && !c->ring->h2d(ps)) return CASK_E_DEVICE;
-  (void)set_dev(c);  // (the calling thread's device, for the launches below)
-  uint8_t* rb = c->stage_rows.as<uint8_t>();
-  cask_rows dr{};
-  dr.capacity = rcap;
-  dr.pos = (uint64_t*)rb;
-  dr.seq = (uint64_t*)(rb + align_up(rcap * 8, 256));
-  dr.vsz = (uint32_t*)(rb + 2 * align_up(rcap * 8, 256));
-  dr.ksz = (uint16_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256));
-  dr.status = (uint8_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256) + align_up(rcap * 2, 256));
-  int rc = scan_device_impl(c, dv.data(), nfiles, &dr, file_row_offset, err);
-  rows->count = dr.count;
-  if (rc != CASK_OK) return rc;
-  if (dr.count > rows->capacity) return CASK_E_CAPACITY;
-  const uint64_t n = dr.count;
-  bool ok = true;
-  auto H = [&](hipError_t e) { ok = ok && (e == hipSuccess); };
-  if (n && staged) {  // the five row arrays through the ring too
+    const uint64_t bound = cask_rows_bound(files, nfiles);
+    const uint64_t rcap = std::min<uint64_t>(bound, rows->capacity ? rows->capacity : bound);
+    if (!c->stage_data.ensure(total + 256)) return CASK_E_NOMEM;
+    if (!c->stage_rows.ensure(rcap * 23 + 5 * 256)) return CASK_E_NOMEM;
+    std::vector<cask_file_view> dv(nfiles);
+    uint8_t* d = c->stage_data.as<uint8_t>();
+    // Large inputs go through the pinned ring on host threads (CASK_STAGE_MIN: the smallest staged
+    // input, default 64 MiB; 0 stages everything — the tests' knob)
+    const char* mv = cask_knobs::hook("CASK_STAGE_MIN");
+    const bool staged = total && total >= (mv ? strtoull(mv, nullptr, 10) : (64ull << 20));
+    if (staged) {
+      if (!c->ring) c->ring.reset(new (std::nothrow) cask_host::PinnedRing());
+      if (!c->ring || !c->ring->init(c->device)) return CASK_E_NOMEM;
+      if (hipStreamSynchronize(st) != hipSuccess) return CASK_E_DEVICE;  // stage_data is free
+    }
+    std::vector<cask_host::PinnedRing::Piece> ps;
+    for (uint32_t i = 0; i < nfiles; ++i) {
+      dv[i] = files[i];
+      dv[i].flags = CASK_VIEW_DEVICE;
+      dv[i].data = d + off[i];
+      if (staged) {
+        cask_host::PinnedRing::split((uint8_t*)files[i].data, d + off[i], files[i].len, ps);
+      } else if (files[i].len && hipMemcpyAsync(d + off[i], files[i].data, files[i].len, hipMemcpyHostToDevice, st) != hipSuccess) {
+        return CASK_E_DEVICE;
+      }
+    }
+    if (staged && !c->ring->h2d(ps)) return CASK_E_DEVICE;
+    (void)set_dev(c);  // (the calling thread's device, for the launches below)
+    uint8_t* rb = c->stage_rows.as<uint8_t>();
+    cask_rows dr{};
+    dr.capacity = rcap;
+    dr.pos = (uint64_t*)rb;
+    dr.seq = (uint64_t*)(rb + align_up(rcap * 8, 256));
+    dr.vsz = (uint32_t*)(rb + 2 * align_up(rcap * 8, 256));
+    dr.ksz = (uint16_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256));
+    dr.status = (uint8_t*)(rb + 2 * align_up(rcap * 8, 256) + align_up(rcap * 4, 256) + align_up(rcap * 2, 256));
+    int rc = scan_device_impl(c, dv.data(), nfiles, &dr, file_row_offset, err);
+    rows->count = dr.count;
+    if (rc != CASK_OK) return rc;
+    if (dr.count > rows->capacity) return CASK_E_CAPACITY;
+    const uint64_t n = dr.count;
+    bool ok = true;
+    auto H = [&](hipError_t e) { ok = ok && (e == hipSuccess); };
+    if (n && staged) {  // the five row arrays through the ring too
+      H(hipStreamSynchronize(st));
+      std::vector<cask_host::PinnedRing::Piece> rp;
+      cask_host::PinnedRing::split((uint8_t*)rows->pos, (uint8_t*)dr.pos, n * 8, rp);
+      cask_host::PinnedRing::split((uint8_t*)rows->seq, (uint8_t*)dr.seq, n * 8, rp);
+      cask_host::PinnedRing::split((uint8_t*)rows->vsz, (uint8_t*)dr.vsz, n * 4, rp);
+      cask_host::PinnedRing::split((uint8_t*)rows->ksz, (uint8_t*)dr.ksz, n * 2, rp);
+      cask_host::PinnedRing::split(rows->status, dr.status, n, rp);
+      if (ok && !c->ring->d2h(rp)) ok = false;
+      return ok ? CASK_OK : CASK_E_DEVICE;
+    }
+    if (n) {
+      H(hipMemcpyAsync(rows->pos, dr.pos, n * 8, hipMemcpyDeviceToHost, st));
+      H(hipMemcpyAsync(rows->seq, dr.seq, n * 8, hipMemcpyDeviceToHost, st));
+      H(hipMemcpyAsync(rows->vsz, dr.vsz, n * 4, hipMemcpyDeviceToHost, st));
+      H(hipMemcpyAsync(rows->ksz, dr.ksz, n * 2, hipMemcpyDeviceToHost, st));
+      H(hipMemcpyAsync(rows->status, dr.status, n, hipMemcpyDeviceToHost, st));
+    }
     H(hipStreamSynchronize(st));
-    std::vector<cask_host::PinnedRing::Piece> rp;
-    cask_host::PinnedRing::split((uint8_t*)rows->pos, (uint8_t*)dr.pos, n * 8, rp);
-    cask_host::PinnedRing::split((uint8_t*)rows->seq, (uint8_t*)dr.seq, n * 8, rp);
-    cask_host::PinnedRing::split((uint8_t*)rows->vsz, (uint8_t*)dr.vsz, n * 4, rp);
-    cask_host::PinnedRing::split((uint8_t*)rows->ksz, (uint8_t*)dr.ksz, n * 2, rp);
-    cask_host::PinnedRing::split(rows->status, dr.status, n, rp);
-    if (ok && !c->ring->d2h(rp)) ok = false;
     return ok ? CASK_OK : CASK_E_DEVICE;
-  }
-  if (n) {
-    H(hipMemcpyAsync(rows->pos, dr.pos, n * 8, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(rows->seq, dr.seq, n * 8, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(rows->vsz, dr.vsz, n * 4, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(rows->ksz, dr.ksz, n * 2, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(rows->status, dr.status, n, hipMemcpyDeviceToHost, st));
-  }
-  H(hipStreamSynchronize(st));
-  return ok ? CASK_OK : CASK_E_DEVICE;
+  });
 }
 
 extern "C" int cask_copy(cask_ctx* c, void* dst, const void* src, uint64_t bytes) {
-  if (!c || (bytes && (!dst || !src))) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (bytes && (hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->stream) != hipSuccess ||
-                hipStreamSynchronize(c->stream) != hipSuccess))
-    return CASK_E_DEVICE;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c || (bytes && (!dst || !src))) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (bytes && (hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, c->stream) != hipSuccess ||
+                  hipStreamSynchronize(c->stream) != hipSuccess))
+      return CASK_E_DEVICE;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_hints_device(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
                                  const uint64_t* file_row_offset, uint8_t* out, uint64_t cap, uint64_t* file_hint_offset) {
-  if (!c || !rows || !file_hint_offset || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
-  if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status)) return CASK_E_INVALID_ARG;
-  for (uint32_t i = 0; i < nfiles; ++i)
-    if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
-  if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
-  std::vector<FileDesc> fd(nfiles + 1);
-  for (uint32_t i = 0; i < nfiles; ++i) fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
-  if (rows->count <= (uint64_t)INT32_MAX)
-    return hint_pack(c->kd, fd.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz,
-                     rows->status, rows->count, out, out ? cap : 0, file_hint_offset, c->stream);
-  // more rows than one device scan takes (an int count): groups of whole files, bodies back to back
-  uint64_t at = 0;  // bytes of the bodies so far
-  int rc = CASK_OK;
-  for (uint32_t f0 = 0; f0 < nfiles;) {
-    const uint64_t r0 = file_row_offset[f0];
-    uint32_t f1 = f0 + 1;
-    while (f1 < nfiles && file_row_offset[f1 + 1] - r0 <= (uint64_t)INT32_MAX) ++f1;
-    const uint64_t n = file_row_offset[f1] - r0;
-    if (n > (uint64_t)INT32_MAX) return CASK_E_CAPACITY;  // one file of more than 2^31 records
-    std::vector<uint64_t> ro(f1 - f0 + 1), fs(f1 - f0 + 1);
-    for (uint32_t f = f0; f <= f1; ++f) ro[f - f0] = file_row_offset[f] - r0;
-    const bool room = out && at <= cap;
-    const int st = hint_pack(c->kd, fd.data() + f0, f1 - f0, ro.data(), rows->pos + r0, rows->seq + r0, rows->vsz + r0,
-                             rows->ksz + r0, rows->status + r0, n, room ? out + at : nullptr, room ? cap - at : 0,
-                             fs.data(), c->stream);
-    if (st != CASK_OK && st != CASK_E_CAPACITY) return st;
-    if (st == CASK_E_CAPACITY) rc = CASK_E_CAPACITY;
-    for (uint32_t f = f0; f < f1; ++f) file_hint_offset[f] = at + fs[f - f0];
-    at += fs[f1 - f0];
-    f0 = f1;
-  }
-  file_hint_offset[nfiles] = at;
-  if (out && at > cap) rc = CASK_E_CAPACITY;
-  return rc;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !rows || !file_hint_offset || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
+    if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz || !rows->status)) return CASK_E_INVALID_ARG;
+    for (uint32_t i = 0; i < nfiles; ++i)
+      if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
+    if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+    std::vector<FileDesc> fd(nfiles + 1);
+    for (uint32_t i = 0; i < nfiles; ++i) fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
+    if (rows->count <= (uint64_t)INT32_MAX)
+      return hint_pack(c->kd, fd.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz,
+                       rows->status, rows->count, out, out ? cap : 0, file_hint_offset, c->stream);
+    // more rows than one device scan takes (an int count): groups of whole files, bodies back to back
+    uint64_t at = 0;  // bytes of the bodies so far
+    int rc = CASK_OK;
+    for (uint32_t f0 = 0; f0 < nfiles;) {
+      const uint64_t r0 = file_row_offset[f0];
+      uint32_t f1 = f0 + 1;
+      while (f1 < nfiles && file_row_offset[f1 + 1] - r0 <= (uint64_t)INT32_MAX) ++f1;
+      const uint64_t n = file_row_offset[f1] - r0;
+      if (n > (uint64_t)INT32_MAX) return CASK_E_CAPACITY;  // one file of more than 2^31 records
+      std::vector<uint64_t> ro(f1 - f0 + 1), fs(f1 - f0 + 1);
+      for (uint32_t f = f0; f <= f1; ++f) ro[f - f0] = file_row_offset[f] - r0;
+      const bool room = out && at <= cap;
+      const int st = hint_pack(c->kd, fd.data() + f0, f1 - f0, ro.data(), rows->pos + r0, rows->seq + r0, rows->vsz + r0,
+                               rows->ksz + r0, rows->status + r0, n, room ? out + at : nullptr, room ? cap - at : 0,
+                               fs.data(), c->stream);
+      if (st != CASK_OK && st != CASK_E_CAPACITY) return st;
+      if (st == CASK_E_CAPACITY) rc = CASK_E_CAPACITY;
+      for (uint32_t f = f0; f < f1; ++f) file_hint_offset[f] = at + fs[f - f0];
+      at += fs[f1 - f0];
+      f0 = f1;
+    }
+    file_hint_offset[nfiles] = at;
+    if (out && at > cap) rc = CASK_E_CAPACITY;
+    return rc;
+  });
 }
 
 // The shard block of hint-file bodies (the hint fast path on the multi-GPU replay): rows as
 // cask_parse_hints_device left them; their pos is rewritten to the entry positions.
 extern "C" int cask_shard_keydir_hints(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, cask_rows* rows,
                                        const uint64_t* file_row_offset, const void** block, uint64_t* bytes) {
-  if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
-  if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz)) return CASK_E_INVALID_ARG;
-  for (uint32_t i = 0; i < nfiles; ++i)
-    if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
-  if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
-  if (!c->keyat.ensure(8 * (rows->count + 1))) return CASK_E_NOMEM;
-  std::vector<FileDesc> fd(nfiles + 1);
-  std::vector<uint32_t> ids(nfiles + 1, 0);
-  for (uint32_t i = 0; i < nfiles; ++i) {
-    fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
-    ids[i] = files[i].file_id;
-  }
-  uint64_t* key_at = c->keyat.as<uint64_t>();
-  int rc = hint_entries(c->kd, fd.data(), nfiles, file_row_offset, rows->count, rows->pos, key_at, c->stream);
-  void* out = nullptr;
-  uint64_t nb = 0;
-  if (!rc)
-    rc = kd_build(c->kd, fd.data(), ids.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz,
-                  rows->count, c->stream, &out, &nb, key_at);
-  if (rc) {
-    snprintf(c->last_error, sizeof(c->last_error), "cask_shard_keydir_hints: %s", rc == CASK_E_NOMEM ? "out of memory" : "device");
-    return rc;
-  }
-  *block = out;
-  *bytes = nb;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
+    if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz)) return CASK_E_INVALID_ARG;
+    for (uint32_t i = 0; i < nfiles; ++i)
+      if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
+    if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+    if (!c->keyat.ensure(8 * (rows->count + 1))) return CASK_E_NOMEM;
+    std::vector<FileDesc> fd(nfiles + 1);
+    std::vector<uint32_t> ids(nfiles + 1, 0);
+    for (uint32_t i = 0; i < nfiles; ++i) {
+      fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
+      ids[i] = files[i].file_id;
+    }
+    uint64_t* key_at = c->keyat.as<uint64_t>();
+    int rc = hint_entries(c->kd, fd.data(), nfiles, file_row_offset, rows->count, rows->pos, key_at, c->stream);
+    void* out = nullptr;
+    uint64_t nb = 0;
+    if (!rc)
+      rc = kd_build(c->kd, fd.data(), ids.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz, rows->ksz,
+                    rows->count, c->stream, &out, &nb, key_at);
+    if (rc) {
+      snprintf(c->last_error, sizeof(c->last_error), "cask_shard_keydir_hints: %s", rc == CASK_E_NOMEM ? "out of memory" : "device");
+      return rc;
+    }
+    *block = out;
+    *bytes = nb;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_shard_keydir(cask_ctx* c, const cask_file_view* files, uint32_t nfiles, const cask_rows* rows,
                                  const uint64_t* file_row_offset, const void** block, uint64_t* bytes) {
-  if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
-  if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz)) return CASK_E_INVALID_ARG;
-  for (uint32_t i = 0; i < nfiles; ++i)
-    if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
-  if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
-  std::vector<FileDesc> fd(nfiles + 1);
-  std::vector<uint32_t> ids(nfiles + 1, 0);
-  for (uint32_t i = 0; i < nfiles; ++i) {
-    fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
-    ids[i] = files[i].file_id;
-  }
-  void* out = nullptr;
-  uint64_t nb = 0;
-  const int rc = kd_build(c->kd, fd.data(), ids.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz,
-                          rows->ksz, rows->count, c->stream, &out, &nb);
-  if (rc) {
-    snprintf(c->last_error, sizeof(c->last_error), "cask_shard_keydir: %s", rc == CASK_E_NOMEM ? "out of memory" : "device");
-    return rc;
-  }
-  *block = out;
-  *bytes = nb;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !rows || !block || !bytes || (nfiles && (!files || !file_row_offset))) return CASK_E_INVALID_ARG;
+    if (rows->count && (!rows->pos || !rows->seq || !rows->vsz || !rows->ksz)) return CASK_E_INVALID_ARG;
+    for (uint32_t i = 0; i < nfiles; ++i)
+      if (!(files[i].flags & CASK_VIEW_DEVICE) || (files[i].len && !files[i].data)) return CASK_E_INVALID_ARG;
+    if (file_row_offset[nfiles] != rows->count) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+    std::vector<FileDesc> fd(nfiles + 1);
+    std::vector<uint32_t> ids(nfiles + 1, 0);
+    for (uint32_t i = 0; i < nfiles; ++i) {
+      fd[i] = FileDesc{files[i].data, files[i].len, 0, 0, 0, 0};
+      ids[i] = files[i].file_id;
+    }
+    void* out = nullptr;
+    uint64_t nb = 0;
+    const int rc = kd_build(c->kd, fd.data(), ids.data(), nfiles, file_row_offset, rows->pos, rows->seq, rows->vsz,
+                            rows->ksz, rows->count, c->stream, &out, &nb);
+    if (rc) {
+      snprintf(c->last_error, sizeof(c->last_error), "cask_shard_keydir: %s", rc == CASK_E_NOMEM ? "out of memory" : "device");
+      return rc;
+    }
+    *block = out;
+    *bytes = nb;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_keydir_partition(cask_ctx* c, const void* block, uint64_t bytes, uint32_t nparts, const void** parts,
                                      uint64_t* part_off) {
-  if (!c || !block || !parts || !part_off || nparts < 1 || nparts > cask_kd::kMaxParts) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
-  void* out = nullptr;
-  const int rc = kd_partition(c->kd, block, bytes, nparts, c->stream, &out, part_off);
-  if (rc) {
-    snprintf(c->last_error, sizeof(c->last_error), "cask_keydir_partition: %s",
-             rc == CASK_E_NOMEM ? "out of memory" : rc == CASK_E_INVALID_ARG ? "not a keydir block" : "device");
-    return rc;
-  }
-  *parts = out;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || !block || !parts || !part_off || nparts < 1 || nparts > cask_kd::kMaxParts) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (!c->kd && !(c->kd = kd_scratch_create())) return CASK_E_NOMEM;
+    if (cask_abi::take_inject(c, cask_abi::kInjPartition)) return CASK_E_NOMEM;
+    void* out = nullptr;
+    const int rc = kd_partition(c->kd, block, bytes, nparts, c->stream, &out, part_off);
+    if (rc) {
+      snprintf(c->last_error, sizeof(c->last_error), "cask_keydir_partition: %s",
+               rc == CASK_E_NOMEM ? "out of memory" : rc == CASK_E_INVALID_ARG ? "not a keydir block" : "device");
+      return rc;
+    }
+    *parts = out;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_encode_synthetic_device(cask_ctx* c, uint64_t nrec, const uint64_t* off, const uint64_t* seq,
                                             const uint16_t* ksz, const uint32_t* vsz_raw, const uint64_t* key_id,
                                             uint64_t value_seed, uint8_t* out) {
-  if (!c || (nrec && (!off || !seq || !ksz || !vsz_raw || !key_id || !out))) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  launch_encode_synth(nrec, off, seq, ksz, vsz_raw, key_id, value_seed, out, c->stream);
-  launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
-  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    if (!c || (nrec && (!off || !seq || !ksz || !vsz_raw || !key_id || !out))) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    launch_encode_synth(nrec, off, seq, ksz, vsz_raw, key_id, value_seed, out, c->stream);
+    launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_encode_device(cask_ctx* c, uint64_t nrec, const uint64_t* off, const uint64_t* seq,
                                   const uint16_t* ksz, const uint32_t* vsz_raw, const uint8_t* keys,
                                   const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
                                   uint8_t* out) {
-  if (!c || (nrec && (!off || !seq || !ksz || !vsz_raw || !keys || !key_off || !out))) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  launch_encode(nrec, off, seq, ksz, vsz_raw, keys, key_off, vals, val_off, out, c->stream);
-  launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
-  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || (nrec && (!off || !seq || !ksz || !vsz_raw || !keys || !key_off || !out))) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    launch_encode(nrec, off, seq, ksz, vsz_raw, keys, key_off, vals, val_off, out, c->stream);
+    launch_encode_checksum(nrec, off, ksz, vsz_raw, out, c->stream);
+    if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
+    return CASK_OK;
+  });
 }
 
 extern "C" int cask_read_entries_device(cask_ctx* c, const uint8_t* const* srcs, const uint64_t* src_len, uint32_t nsrc,
                                         const uint32_t* src, const uint64_t* pos, uint64_t n, uint64_t* len,
                                         uint8_t* status, uint32_t* expected, uint32_t* found) {
-  if (!c || (n && (!srcs || !src_len || !src || !pos || !len || !status || !expected || !found))) return CASK_E_INVALID_ARG;
-  for (uint64_t r = 0; r < n; ++r)
-    if (src[r] >= nsrc) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (!n) return CASK_OK;
-  const size_t a8 = align_up(8 * n, 256), a4 = align_up(4 * n, 256), a1 = align_up(n, 256), as = align_up(8ull * nsrc, 256);
-  if (!c->gather.ensure(4 * a8 + 3 * a4 + a1 + 2 * as)) return CASK_E_NOMEM;
-  uint8_t* b = c->gather.as<uint8_t>();
-  uint64_t* d_pos = (uint64_t*)b;
-  uint64_t* d_len = (uint64_t*)(b + a8);
-  uint32_t* d_src = (uint32_t*)(b + 2 * a8);
-  uint32_t* d_exp = (uint32_t*)(b + 2 * a8 + a4);
-  uint32_t* d_fnd = (uint32_t*)(b + 2 * a8 + 2 * a4);
-  uint8_t* d_st = b + 2 * a8 + 3 * a4;
-  const uint8_t** d_srcs = (const uint8_t**)(b + 2 * a8 + 3 * a4 + a1);
-  uint64_t* d_slen = (uint64_t*)(b + 2 * a8 + 3 * a4 + a1 + as);
-  hipStream_t st = c->stream;
-  bool ok = true;
-  auto H = [&](hipError_t e) { ok = ok && e == hipSuccess; };
-  H(hipMemcpyAsync(d_pos, pos, 8 * n, hipMemcpyHostToDevice, st));
-  H(hipMemcpyAsync(d_src, src, 4 * n, hipMemcpyHostToDevice, st));
-  H(hipMemcpyAsync(d_srcs, srcs, 8ull * nsrc, hipMemcpyHostToDevice, st));
-  H(hipMemcpyAsync(d_slen, src_len, 8ull * nsrc, hipMemcpyHostToDevice, st));
-  launch_read_entries(d_pos, d_src, n, d_srcs, d_slen, d_len, d_st, d_exp, d_fnd, st);
-  H(hipGetLastError());
-  H(hipMemcpyAsync(len, d_len, 8 * n, hipMemcpyDeviceToHost, st));
-  H(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
-  H(hipMemcpyAsync(expected, d_exp, 4 * n, hipMemcpyDeviceToHost, st));
-  H(hipMemcpyAsync(found, d_fnd, 4 * n, hipMemcpyDeviceToHost, st));
-  H(hipStreamSynchronize(st));
-  return ok ? CASK_OK : CASK_E_DEVICE;
-}
-
-extern "C" int cask_gather_device(cask_ctx* c, const uint8_t* const* srcs, uint32_t nsrc, const uint32_t* src,
-                                  const uint64_t* pos, const uint64_t* dst_off, const uint32_t* len, uint64_t nrec,
-                                  uint8_t* dst) {
-  if (!c || (nrec && (!srcs || !src || !pos || !dst_off || !len || !dst))) return CASK_E_INVALID_ARG;
-  std::lock_guard<std::mutex> g(c->mu);
-  if (set_dev(c)) return CASK_E_DEVICE;
-  if (!nrec) return CASK_OK;
-  std::vector<GatherRec> recs(nrec);
-  for (uint64_t r = 0; r < nrec; ++r) {
-    if (src[r] >= nsrc) return CASK_E_INVALID_ARG;
-    recs[r] = GatherRec{pos[r], dst_off[r], src[r], len[r]};
-  }
-  const size_t rb = align_up(sizeof(GatherRec) * nrec, 256);
-  if (!c->gather.ensure(rb + sizeof(void*) * nsrc)) return CASK_E_NOMEM;
-  uint8_t* base = c->gather.as<uint8_t>();
-  if (hipMemcpyAsync(base, recs.data(), sizeof(GatherRec) * nrec, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
-      hipMemcpyAsync(base + rb, srcs, sizeof(void*) * nsrc, hipMemcpyHostToDevice, c->stream) != hipSuccess)
-    return CASK_E_DEVICE;
-  launch_gather((const GatherRec*)base, nrec, (const uint8_t* const*)(base + rb), dst, c->stream);
-  if (hipStreamSynchronize(c->stream) != hipSuccess || hipGetLastError() != hipSuccess) return CASK_E_DEVICE;
-  return CASK_OK;
+  return cask_abi::guard([&]() -> int {
+    cask_abi::maybe_throw(c);
+    if (!c || (n && (!srcs || !src_len || !src || !pos || !len || !status || !expected || !found))) return CASK_E_INVALID_ARG;
+    for (uint64_t r = 0; r < n; ++r)
+      if (src[r] >= nsrc) return CASK_E_INVALID_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (set_dev(c)) return CASK_E_DEVICE;
+    if (!n) return CASK_OK;
+    const size_t a8 = align_up(8 * n, 256), a4 = align_up(4 * n, 256), a1 = align_up(n, 256), as = align_up(8ull * nsrc, 256);
+    if (!c->gather.ensure(4 * a8 + 3 * a4 + a1 + 2 * as)) return CASK_E_NOMEM;
+    uint8_t* b = c->gather.as<uint8_t>();
+    uint64_t* d_pos = (uint64_t*)b;
+    uint64_t* d_len = (uint64_t*)(b + a8);
+    uint32_t* d_src = (uint32_t*)(b + 2 * a8);
+    uint32_t* d_exp = (uint32_t*)(b + 2 * a8 + a4);
+    uint32_t* d_fnd = (uint32_t*)(b + 2 * a8 + 2 * a4);
+    uint8_t* d_st = b + 2 * a8 + 3 * a4;
+    const uint8_t** d_srcs = (const uint8_t**)(b + 2 * a8 + 3 * a4 + a1);
+    uint64_t* d_slen = (uint64_t*)(b + 2 * a8 + 3 * a4 + a1 + as);
+    hipStream_t st = c->stream;
+    bool ok = true;
+    auto H = [&](hipError_t e) { ok = ok && e == hipSuccess; };
+    H(hipMemcpyAsync(d_pos, pos, 8 * n, hipMemcpyHostToDevice, st));
+    H(hipMemcpyAsync(d_src, src, 4 * n, hipMemcpyHostToDevice, st));
+    H(hipMemcpyAsync(d_srcs, srcs, 8ull * nsrc, hipMemcpyHostToDevice, st));
+    H(hipMemcpyAsync(d_slen, src_len, 8ull * nsrc, hipMemcpyHostToDevice, st));
+    launch_read_entries(d_pos, d_src, n, d_srcs, d_slen, d_len, d_st, d_exp, d_fnd, st);
+    H(hipGetLastError());
+    H(hipMemcpyAsync(len, d_len, 8 * n, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(expected, d_exp, 4 * n, hipMemcpyDeviceToHost, st));
+    H(hipMemcpyAsync(found, d_fnd, 4 * n, hipMemcpyDeviceToHost, st));
+    H(hipStreamSynchronize(st));
+    return ok ? CASK_OK : CASK_E_DEVICE;
+  });
 }
 
 #ifdef CASK_STAMPS

@@ -177,14 +177,6 @@ int64_t cask_log_write(const char* dir, uint32_t first_file_id, uint64_t max_fil
                        const uint8_t* keys, const uint64_t* key_off, const uint8_t* vals, const uint64_t* val_off,
                        uint32_t* file_ids, uint64_t cap);
 
-/* Compaction rewrite (Cask::compact_files_aux, cask.rs:505-513; LogWriter::write, log.rs:282-306):
- * nrec records copied byte for byte into dst (device memory). Record r is len[r] bytes of source
- * file src[r] (device pointer srcs[src[r]]) from byte pos[r], written at dst[dst_off[r]]. The
- * record arrays and srcs are host memory. Synchronous. */
-int cask_gather_device(cask_ctx* ctx, const uint8_t* const* srcs, uint32_t nsrc, const uint32_t* src,
-                       const uint64_t* pos, const uint64_t* dst_off, const uint32_t* len, uint64_t nrec,
-                       uint8_t* dst);
-
 /* Log::read_entry + Entry::from_read at caller positions (log.rs:150-166, data.rs:161-206), on the
  * device — what compaction does for each live record (cask.rs:505-508), without re-scanning whole
  * files. Record r is read at byte pos[r] of source src[r] (srcs[src[r]]: device pointer to src_len
@@ -402,6 +394,14 @@ int cask_keydir_gather_rccl(cask_ctx* ctx, void* comm, const void* block, uint64
                             uint64_t* gathered, uint64_t* max_seq);
 int cask_keydir_exchange_rccl(cask_ctx* ctx, void* comm, const void* block, uint64_t bytes, cask_db* db,
                               uint64_t* sent, uint64_t* received);
+
+/* Test hook (effective only with CASK_TEST_HOOKS=1 in the environment; CASK_E_INVALID_ARG
+ * otherwise): force failures on one context — bit 1 the gather root's receive buffer cannot be
+ * allocated, 2 cask_keydir_partition runs out of device memory, 4 the exchange cannot read its
+ * per-file terms, 8 the next entry point called with it throws std::bad_alloc inside the library
+ * (which must come back as CASK_E_NOMEM), 16 the fold of the received blocks fails. Lets a
+ * multi-rank test make one rank fail at a chosen point. */
+int cask_debug_inject(cask_ctx* ctx, uint32_t bits);
 
 /* Cask::open over several GPUs of this process (replaces cask.rs:346-382 like cask_db_open): the
  * data files are split into contiguous ranges, one per entry of `devices` (a device may appear more
