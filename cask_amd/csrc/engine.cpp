@@ -14,6 +14,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <deque>
 #include <atomic>
 #include <condition_variable>
 #include <cerrno>
@@ -419,6 +420,27 @@ bool write_raw(const std::string& p, const uint8_t* b, size_t n) {
 
 // find_data_files (log.rs:483-510): regex "(\d+).cask.data$" (unescaped '.', unanchored),
 // regular files only (DirEntry::metadata does not follow symlinks), u32 parse, ascending.
+// Files a compaction renamed away (`<id>.cask.data.gone`, `<id>.cask.hint.gone`: no longer
+// matched by find_data_files) are unlinked by the db's reclaim thread; a process that ended before
+// that thread ran leaves them behind. Log::open removes them once it holds the lock (no compaction
+// of this database can be running then). Not in the reference, whose swap_files removes the
+// compacted files itself (log.rs:198-217).
+static void remove_gone_files(const std::string& dir) {
+  DIR* d = opendir(dir.c_str());
+  if (!d) return;
+  std::vector<std::string> dead;
+  auto ends = [](const std::string& n, const char* suf) {
+    const size_t k = strlen(suf);
+    return n.size() > k && n.compare(n.size() - k, k, suf) == 0;
+  };
+  while (struct dirent* e = readdir(d)) {
+    const std::string name = e->d_name;
+    if (ends(name, ".cask.data.gone") || ends(name, ".cask.hint.gone")) dead.push_back(dir + "/" + name);
+  }
+  closedir(d);
+  for (const std::string& f : dead) (void)unlink(f.c_str());
+}
+
 bool find_data_files(const std::string& dir, std::vector<uint32_t>& out) {
   DIR* d = opendir(dir.c_str());
   if (!d) return false;
@@ -1020,6 +1042,7 @@ static cask_db* open_log(const char* path_c, const cask_options* opts_in, cask_o
     set_err(err, CASK_E_LOCKED);
     return nullptr;
   }
+  remove_gone_files(path);
   if (!find_data_files(path, db->files)) {
     delete db;
     set_err(err, CASK_E_IO);
@@ -1671,18 +1694,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     int fd = -1;
     std::vector<uint8_t> hints;
   };
-  std::vector<OutFile> outs;
-  // (reserved: the writer thread below holds references into `outs` while placement appends to it.
-  // Two consecutive files hold more than max_file_size together — the second was opened because
-  // the first could not take its first record — so there are at most 2 x bytes / max + 1 of them.)
-  {
-    uint64_t in_bytes = del_key_bytes.size() + 18ull * del_seq.size();
-    for (uint32_t f : srcs) {
-      struct stat stt;
-      if (stat(data_path(path, f).c_str(), &stt) == 0) in_bytes += (uint64_t)stt.st_size;
-    }
-    outs.reserve(2 * (in_bytes / std::max<uint64_t>(db->opts.max_file_size, 1)) + 4);
-  }
+  // (a deque: the writer thread below holds references into `outs` while placement appends to it,
+  // and push_back on a deque never moves the elements already there)
+  std::deque<OutFile> outs;
   std::vector<uint32_t> new_files, tomb_files;
   uint64_t cur = 0;
   auto place = [&](uint64_t size, bool live) -> size_t {  // LogWriter::write's rollover

@@ -136,6 +136,23 @@ def test_engine_fold_edge_cases_via_hints(native, tmp_path):
         assert db.current_sequence == py.current_sequence
 
 
+def test_open_removes_files_a_compaction_left_behind(native, tmp_path):
+    """A compaction renames the compacted files to `*.cask.data.gone` / `*.cask.hint.gone` and
+    unlinks them on the db's reclaim thread; if the process ends first they stay on disk. The next
+    open removes them (holding the lock), and they never count as data files (log.rs:483-510)."""
+    from cask_amd import CaskOptions
+    path = str(tmp_path / "db")
+    _write_db_with_hints(path, [[R.entry_new(1, b"k", b"v")]])
+    left = [path + "/0000000007.cask.data.gone", path + "/0000000007.cask.hint.gone"]
+    for f in left:
+        with open(f, "wb") as fh:
+            fh.write(b"x" * 4096)
+    with CaskOptions().open(path) as db:
+        assert db.current_sequence == 2 and len(db) == 1
+    assert not any(os.path.exists(f) for f in left)
+    assert sorted(os.listdir(path)) == ["0000000001.cask.data", "0000000001.cask.hint", "cask.lock"]
+
+
 def test_engine_truncated_hint_body_is_eof(native, tmp_path):
     """A hint file whose trailer is valid but whose last hint is cut short: Hint::from_read fails
     with UnexpectedEof and open() returns it (data.rs:258-265, cask.rs:360)."""
