@@ -14,8 +14,8 @@
 // (spec[c] == T[c]) like any other.
 //
 // First start of a run (its first chunk's c0 != 0): the lowest offset >= c0 holding a record of at
-// most kSearchShort bytes whose XXH32 matches (pass A, windows staged in LDS); then, going back, the
-// lowest offset >= c0 whose header gives a record longer than kSearchShort that ends exactly at the
+// most ScanArgs::search_short bytes whose XXH32 matches (windows staged in LDS); then, going back, the
+// lowest offset >= c0 whose header gives a record longer than that which ends exactly at the
 // start found (repeated: a chain of long records before the first verified one).
 #include "device_util.h"
 
@@ -28,8 +28,6 @@ namespace cask_dev {
 
 constexpr uint32_t kWalkWin = 4096;                   // LDS window (16-B aligned)
 constexpr uint32_t kWalkUse = kWalkWin - 16;          // bytes usable from any start in the window
-constexpr uint32_t kSearchShort = 2048;               // pass A verifies records up to this long
-constexpr uint32_t kStepA = kWalkUse - 18;            // candidate offsets per pass-A window
 constexpr uint32_t kStepB = kWalkUse - 18;            // candidate offsets per hop-back window
 constexpr uint32_t kSearchPast = 1u << 20;            // pass A looks this far past the run's end
 constexpr uint32_t kLongList = 256;  // pass A's long candidates kept for the hop back (64: no faster)
@@ -51,13 +49,6 @@ struct WalkLds {
   // records of the window waiting for their checksum (walk_flush): LDS byte, length, chunk, row
   uint32_t hx[16], hrl[16], hj[16], hr[16];
   u32x4 hrow[16];
-};
-// LDS of a searching wave (k_walk_search): a 4-KiB window, the short candidates of a step and the
-// long candidates kept for the hop back.
-struct SearchLds {
-  uint32_t win[kWalkWin / 4 + 16];
-  uint32_t cand[64];             // pass A: plausible short candidates of a block, in offset order
-  uint64_t lx[kLongList], le[kLongList];  // pass A: long candidates x and their ends x + rl
 };
 
 // A single-wave workgroup's claim of the next item of a work counter: every lane takes part in the
@@ -101,145 +92,16 @@ constexpr uint32_t kChaseNL = 1;                 // the chase's windows: 1 KiB
 constexpr uint32_t kChaseUse = kChaseNL * 1024 - 16;
 static_assert(kChaseUse == kWalkHashMax, "the walker hashes records that fit its window");
 
-// The first record start >= b0 of the chain, speculatively (see the file comment); kNone if pass A
-// finds no verified short record before min(len, b1 + kSearchPast).
-// Pass A, 256 offsets a step (4 per lane): the length fields of every offset are decoded; offsets whose record is
-// at most kSearchShort long and fits the file are hashed 16 at a time by quads (from LDS when the
-// record is staged, else from HBM), in offset order, until one matches its stored checksum. Offsets
-// whose record is longer and ends within the search horizon are listed (x, x + rl) for the hop back,
-// so it needs no second pass over the bytes (random bytes give an end that close ~1e-5 of the time).
-__device__ __forceinline__ uint64_t walk_search(SearchLds& L, const uint8_t* data, uint64_t len, uint64_t b0, uint64_t b1) {
-  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
-  const uint64_t lim = (b1 + kSearchPast < len) ? b1 + kSearchPast : len;
-  const unsigned long long below = lane ? (~0ull >> (64 - lane)) : 0ull;  // lanes < this one
-  uint64_t kA = kNone;
-  uint32_t nl = 0;  // long candidates listed
-  bool over = false;  // the list overflowed: the hop back rescans instead
-  for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kStepA) {
-    const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
-    const uint64_t wend = (wb + kWalkUse < len) ? wb + kWalkUse : len;  // staged bytes end here
-    // 256 offsets per step: lane l decodes the length fields of offsets k0 + 4l .. k0 + 4l + 3
-    // from the four aligned dwords that cover them
-    for (uint32_t k0 = 0; k0 < kStepA && kA == kNone; k0 += 256) {
-      const uint32_t o = k0 + 4 * lane;
-      const uint32_t B = x0 + o + 12, i0 = B >> 2, sh = B & 3;
-      const uint32_t d0 = L.win[i0], d1 = L.win[i0 + 1], d2 = L.win[i0 + 2], d3 = L.win[i0 + 3];
-      uint32_t sm = 0, lm = 0;  // bit s: offset o + s is a short / long candidate
-      uint64_t rls[4];
-#pragma unroll
-      for (uint32_t e = 0; e < 4; ++e) {
-        const uint32_t t = sh + e;
-        const uint32_t w3 = t < 4 ? fun(d0, d1, t) : fun(d1, d2, t - 4);
-        const uint32_t w4 = t < 4 ? fun(d1, d2, t) : fun(d2, d3, t - 4);
-        const uint32_t ksz = w3 & 0xFFFFu, vsz = (w3 >> 16) | (w4 << 16);
-        const uint64_t rl = 18ull + ksz + ((vsz == 0xFFFFFFFFu) ? 0ull : (uint64_t)vsz);
-        const uint64_t x = wb + o + e;
-        const bool valid = o + e < kStepA && x < lim && x + 18 <= len;
-        rls[e] = rl;
-        sm |= (uint32_t)(valid && rl <= kSearchShort && x + rl <= len) << e;
-        lm |= (uint32_t)(valid && rl > kSearchShort && x + rl <= lim) << e;
-      }
-      // ranks in offset order (lane-major, then e)
-      unsigned long long mS[4], mL[4];
-      uint32_t nS = 0, nL = 0, rS = 0, rL = 0;  // totals; this lane's first ranks
-#pragma unroll
-      for (uint32_t e = 0; e < 4; ++e) {
-        mS[e] = __ballot((sm >> e) & 1u);
-        mL[e] = __ballot((lm >> e) & 1u);
-        nS += (uint32_t)__builtin_popcountll(mS[e]);
-        nL += (uint32_t)__builtin_popcountll(mL[e]);
-        rS += (uint32_t)__builtin_popcountll(mS[e] & below);
-        rL += (uint32_t)__builtin_popcountll(mL[e] & below);
-      }
-      if (nL) {  // long candidates, appended in offset order
-        uint32_t r = nl + rL;
-#pragma unroll
-        for (uint32_t e = 0; e < 4; ++e)
-          if ((lm >> e) & 1u) {
-            if (r < kLongList) {
-              L.lx[r] = wb + o + e;
-              L.le[r] = wb + o + e + rls[e];
-            }
-            ++r;
-          }
-        nl += nL;
-        if (nl > kLongList) over = true;
-      }
-      // short candidates: 16 at a time (ranks [r0, r0 + 16)), one per quad, in offset order
-      for (uint32_t r0 = 0; r0 < nS && kA == kNone; r0 += 16) {
-        uint32_t r = rS;
-#pragma unroll
-        for (uint32_t e = 0; e < 4; ++e)
-          if ((sm >> e) & 1u) {
-            if (r >= r0 && r < r0 + 16) L.cand[r - r0] = o + e;
-            ++r;
-          }
-        __syncthreads();
-        const uint32_t nc = nS - r0 < 16 ? nS - r0 : 16u;
-        bool ok = false;
-        if (q < nc) {
-          const uint32_t ko = L.cand[q];
-          const uint64_t xc = wb + ko;
-          const uint64_t rlc = lds_reclen(L.win, x0 + ko);
-          const uint32_t st = lds_u32(L.win, x0 + ko);
-          const uint32_t h = (xc + rlc <= wend) ? quad_xxh32(L.win, x0 + ko + 4, (uint32_t)rlc - 4, qa)
-                                                 : quad_gbl_xxh32<2>(data + xc + 4, rlc - 4, qa);
-          ok = qa == 0 && h == st;
-        }
-        const unsigned long long mo = __ballot(ok);
-        if (mo) kA = wb + L.cand[__builtin_ctzll(mo) >> 2];  // quads are in offset order
-        __syncthreads();
-      }
-    }
-  }
-  if (kA == kNone) return kNone;
-  // hop back over long records ending exactly at the current target: from the list (it holds every
-  // long candidate before kA whose end is in the horizon), or by rescanning if it overflowed
-  uint64_t target = kA;
-  for (int it = 0; it < 64; ++it) {
-    uint64_t found = kNone;
-    if (!over) {
-      const uint32_t n = nl < kLongList ? nl : kLongList;
-      for (uint32_t i0 = 0; i0 < n && found == kNone; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        const bool hit = i < n && L.lx[i] < target && L.le[i] == target;
-        const unsigned long long m = __ballot(hit);
-        if (m) found = L.lx[i0 + __builtin_ctzll(m)];
-      }
-    } else {
-      for (uint64_t wb = b0; wb < target && found == kNone; wb += kStepB) {
-        const uint32_t x0 = walk_stage<kSearchNL>(L.win, data, len, wb);
-        for (uint32_t k0 = 0; k0 < kStepB; k0 += 64) {
-          const uint64_t x = wb + k0 + lane;
-          bool hit = false;
-          if (k0 + lane < kStepB && x < target && x + 18 <= len) {
-            const uint64_t rl = lds_reclen(L.win, x0 + k0 + lane);
-            hit = rl > kSearchShort && x + rl == target;
-          }
-          const unsigned long long m = __ballot(hit);
-          if (m) {
-            found = wb + k0 + (uint64_t)__builtin_ctzll(m);
-            break;
-          }
-        }
-      }
-    }
-    if (found == kNone) break;
-    target = found;
-  }
-  return target;
-}
-
-// The same search with a cheaper pass A (k_walk_search's default): a record's value_size field ends
+// The first record start >= b0 of the chain, speculatively (see the file comment); kNone if no
+// verified short record is found before min(len, b1 + kSearchPast). A record's value_size field ends
 // 17 bytes into its header, and a record that ends within the search horizon (or a tombstone) has a
 // last value_size byte of 0x00 (0xFF) — only offsets whose byte +17 is 0x00 or 0xFF are decoded,
 // found four at a time per aligned dword (SWAR zero-byte test), in 8-KiB windows. The short
 // candidates of a window are hashed 16 at a time in offset order (lane l scans the window's dwords
 // [32l, 32l + 32): lane order is offset order) until one verifies; long ones are listed for the hop
-// back. Same answer as walk_search for every input whose keys are at most 4,351 B: the filter skips
-// offsets whose record could neither be short nor end within the horizon, and offsets whose
-// key_size is larger (a run start after such a key is found later and k_finish's check sends the
-// run to the repair: speed only).
+// back. The filter skips offsets whose record could neither be short nor end within the horizon,
+// and offsets whose key_size is over 4,351 B (a run start after such a key is found later and
+// k_finish's check sends the run to the repair: speed only).
 #ifndef CASK_SW_NL  // (A/B variant: the window in KiB)
 #define CASK_SW_NL 8
 #endif
@@ -686,8 +548,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     const uint64_t se = fend < tend ? fend : tend;
     const uint64_t b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
     const uint64_t b1 = ((se - fd.first_chunk) * (uint64_t)a.chunk < fd.len) ? (se - fd.first_chunk) * (uint64_t)a.chunk : fd.len;
+#ifdef CASK_STAMPS
+    const uint64_t rt0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t win0 = wst[5];
+#endif
     const uint64_t s0 = b0 == 0 ? 0 : walk_search_sw(L, fd.data, fd.len, b0, b1, wst, a.search_short);
     if (threadIdx.x == 0) a.tin[t] = s0;
+#ifdef CASK_STAMPS
+    if (a.stamps && threadIdx.x == 0 && r < kStampRuns) {  // per search: start, end, windows, wave
+      unsigned long long* sr = a.stamps + 16 + 2ull * kStampWaves + 4 * r;
+      sr[0] = rt0;
+      sr[1] = __builtin_amdgcn_s_memrealtime();
+      sr[2] = wst[5] - win0;
+      sr[3] = blockIdx.x;
+    }
+#endif
   }
 #ifdef CASK_STAMPS
   if (a.stamps && threadIdx.x == 0)

@@ -251,6 +251,8 @@ void launch_hash_fix(const ScanArgs& a, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
 constexpr uint32_t kProbeRegions = 8;
 constexpr uint32_t kStampWaves = 8192;  // diagnostic builds: waves with start/end stamps
+constexpr uint32_t kStampRuns = 65536;  // diagnostic builds: searches with start/end/windows stamps
+constexpr uint64_t kStampWords = 16 + 2ull * kStampWaves + 4ull * kStampRuns;
 void launch_probe_regions(const FileDesc* files, uint32_t nfiles, unsigned long long* out, void* stream);
 void launch_err_detail(const ScanArgs& a, uint32_t fi, uint64_t slot, uint32_t* out, void* stream);
 void launch_encode_synth(uint64_t nrec, const uint64_t* off, const uint64_t* seq,

@@ -469,7 +469,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   }
   a.epoch = ++c->epoch;
 #ifdef CASK_STAMPS
-  if (c->stamps.ensure(8ull * (16 + 2 * kStampWaves))) a.stamps = c->stamps.as<unsigned long long>();
+  if (c->stamps.ensure(8ull * kStampWords)) a.stamps = c->stamps.as<unsigned long long>();
 #endif
 
   bool ok = true;
@@ -787,7 +787,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipMemsetAsync(a.ctr, 0, sizeof(Counters), st), "memset counters");
     H(hipMemsetAsync(d_ferr, 0xFF, 8ull * (nfiles + 1), st), "memset file_err");
     H(hipMemsetAsync(d_fbad, 0xFF, 8ull * (nfiles + 1), st), "memset first_bad");
-    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 8ull * (16 + 2 * kStampWaves), st));
+    if (a.stamps) H(hipMemsetAsync(a.stamps, 0, 8ull * kStampWords, st));
   };
   uint64_t nlong_total = 0;  // records hashed by k_long over all passes (each pass queues only chunks it scanned)
   // validation, long records and summary after a scan of the chunks (events 2..4 when timed)
@@ -1310,6 +1310,13 @@ extern "C" int cask_debug_stamps(cask_ctx* c, uint64_t* out16) {
 extern "C" int cask_debug_wave_stamps(cask_ctx* c, uint64_t* out, uint64_t n) {
   if (!c || !c->stamps.p || n > 2ull * kStampWaves) return CASK_E_INVALID_ARG;
   if (hipMemcpy(out, (uint8_t*)c->stamps.p + 16 * 8, n * 8, hipMemcpyDeviceToHost) != hipSuccess) return CASK_E_DEVICE;
+  return CASK_OK;
+}
+// Diagnostic build only: k_walk_search's per-search records (start, end real time, windows, wave).
+extern "C" int cask_debug_search_stamps(cask_ctx* c, uint64_t* out, uint64_t n) {
+  if (!c || !c->stamps.p || n > 4ull * kStampRuns) return CASK_E_INVALID_ARG;
+  if (hipMemcpy(out, (uint8_t*)c->stamps.p + (16 + 2ull * kStampWaves) * 8, n * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return CASK_E_DEVICE;
   return CASK_OK;
 }
 // Diagnostic build only: per-chunk spec / exit / tin / count of the last (unrepaired) pass.

@@ -39,6 +39,32 @@ def main():
     print(f"shares: stage {st[1] / tot:.2f} phase1 {st[2] / tot:.2f} phase2 {st[3] / tot:.2f} hop {st[4] / tot:.2f}; "
           f"per search: {st[0] / ns:.0f} cycles, {st[5] / ns:.2f} windows, {st[6] / ns:.2f} hash rounds")
     print("timings", ctx.last_timings(), "counters", ctx.last_counters(), "rows", res.count)
+    # per-search records of the last call: start / end (100 MHz real-time clock), windows, wave
+    import numpy as np
+    nr = 65536
+    L.cask_debug_search_stamps.restype = C.c_int
+    L.cask_debug_search_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64]
+    buf = (C.c_uint64 * (4 * nr))()
+    L.cask_debug_search_stamps(ctx._h, buf, 4 * nr)
+    a = np.frombuffer(buf, np.uint64).reshape(nr, 4).astype(np.int64)
+    a = a[a[:, 1] > 0]
+    if a.size:
+        t0 = a[:, 0].min()
+        st, en, win = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0, a[:, 2]
+        dur = en - st
+        print(f"searches {len(a)}: kernel span {en.max():.1f} us; per search us mean {dur.mean():.1f} "
+              f"p50/p90/p99/max {' / '.join(f'{x:.1f}' for x in np.percentile(dur, [50, 90, 99, 100]))}")
+        print(f"windows mean {win.mean():.2f} max {win.max()}; us per window {dur.sum() / max(win.sum(), 1):.2f}")
+        w_last = a[np.argmax(a[:, 1]), 3]
+        mine = a[a[:, 3] == w_last]
+        print(f"last wave {w_last}: {len(mine)} searches, windows {mine[:, 2].tolist()}, "
+              f"durations {[round(x, 1) for x in ((mine[:, 1] - mine[:, 0]) / 100.0).tolist()]}")
+        ends = {}
+        for e_, w_ in zip(en, a[:, 3]):
+            ends[w_] = max(ends.get(w_, 0.0), e_)
+        ev = np.array(sorted(ends.values()))
+        print(f"waves {len(ev)}: end percentiles 0/10/50/90/99/100 = "
+              f"{' / '.join(f'{x:.1f}' for x in np.percentile(ev, [0, 10, 50, 90, 99, 100]))} us")
 
 
 if __name__ == "__main__":
