@@ -454,6 +454,10 @@ def main():
              # (HIP events), per GPU; `value` above is the wall clock, host gap included
              "device_gibps_per_gpu": bytes_per_step / (breakdown["pipeline_ms"] * 1e-3) / 2 ** 30,
              "cold_call_ms": sorted(cold)[len(cold) // 2],
+             # device scratch the context holds for this workload (chunk table, slot rows, call
+             # blocks, repair state), beside the log bytes it scans
+             "scratch_bytes": ctx.scratch_bytes(),
+             "scratch_bytes_per_log_byte": ctx.scratch_bytes() / bytes_per_step,
              "step_note": ("every timed step is one cask_scan_device call over the same resident files: the "
                            "region probe and the device file table are cached on the context across steps; "
                            "cold_call_ms is the median of 3 calls made right after a call over another file "

@@ -138,6 +138,7 @@ SIGNATURES = [
                                     C.POINTER(C.c_void_p), c_u64p]),
     ("cask_copy", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     ("cask_debug_inject", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("cask_ctx_scratch_bytes", C.c_uint64, [C.c_void_p]),
     ("cask_rccl_unique_id", C.c_int, [C.c_void_p]),
     ("cask_rccl_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("cask_rccl_comm_destroy", C.c_int, [C.c_void_p]),

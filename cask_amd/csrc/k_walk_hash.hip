@@ -62,9 +62,15 @@ __device__ __forceinline__ u32x4 shr_bytes(const u32x4& v, uint32_t s) {
   return u32x4{fun(w0, w1, b), fun(w1, w2, b), fun(w2, w3, b), fun(w3, 0u, b)};
 }
 
-// One chunk's table entries (lane 0 of the quad).
+// One chunk's table entries. A chunk with more records than its slot rows (a.slot_cap: small in a
+// walk-mode call) keeps slot_cap of them and flags the call, which the host then redoes with full
+// slot rows: every later kernel reads rows r < count only, so nothing reads past the slots.
 __device__ __forceinline__ void put_chunk(const ScanArgs& a, uint64_t t, uint64_t spec, uint64_t ex, uint32_t count,
                                           uint32_t cerr) {
+  if (count > a.slot_cap) {
+    a.ctr->slot_overflow = 1u;
+    count = a.slot_cap;
+  }
   ((g_u64*)a.spec)[t] = spec;
   ((g_u64*)a.exit)[t] = ex;
   ((g_u32*)a.count)[t] = count;
@@ -185,7 +191,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
         const uint32_t r = open_record(a, W, p, csh, true, &j);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
+        if (r < a.slot_cap) *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
         if (r < W.ccerr) W.ccerr = r;
         term = true;
         break;
@@ -198,7 +204,8 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       h = gld16g((const g_u8*)(W.S.data + pl));
       const uint32_t r = open_record(a, W, p, csh, true, &j);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-      *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
+      if (r < a.slot_cap)
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
       if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
         if (r < W.ccerr) W.ccerr = r;
         term = true;

@@ -51,6 +51,7 @@ struct Counters {
   unsigned int walk_next[8];     // k_walk_runs: next run of each walk group to hand out (kWalkGroups)
   unsigned int search_next[8];   // k_walk_search: the same, for the searches
   unsigned int hash_next;        // k_walk_hash: next run to hand out (after the first by index)
+  unsigned int slot_overflow;    // k_walk_chase: a chunk had more records than the slot rows sized
 };
 
 // Layout of the call block: Counters, then row_off[nfiles + 1] (each file's first dense row,
@@ -180,6 +181,10 @@ __host__ __device__ __forceinline__ bool lds_hashed(uint64_t p, uint64_t rl, uin
 constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // Walk mode (k_walk.hip): chunks per run, and the mean record length (bytes, sampled at the heads
 // of the files by k_probe) from which a call takes it.
+// Slot rows per chunk of a pure walk-mode call (records average >= kWalkMean bytes: 32 per 32-KiB
+// chunk on average; configs[2], mean 5,114 B: at most 60 in 11 M chunks). A chunk with more sets
+// Counters::slot_overflow and the call is redone with the full count (chunk / 18 + 2).
+constexpr uint32_t kWalkSlotCap = 128;
 constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk runs 2 % faster than 64)
 // Chunk mode: the short-halo geometry (kGeoShortHalo, a 1,008-B halo) when the records at the file
 // heads average at most kShortHaloMean bytes and none is longer than kShortHaloMax; else the wide

@@ -106,6 +106,7 @@ struct cask_ctx {
   DevBuf mruns;      // mixed call: walk-mode run indices | chunk-mode [first, end) stretches
   uint32_t epoch = 0;
   uint32_t inject = 0;  // test hooks: cask_debug_inject (abi_guard.h)
+  bool full_slots_next = false;  // the next call (a redo) sizes its slot rows in full
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
   uint64_t* dbg_tin = nullptr;
@@ -269,6 +270,15 @@ int cask_last_timings8(const cask_ctx* c, float* ms8) {
 
 int cask_last_dense(const cask_ctx* c) { return c ? c->last_dense : 0; }
 
+uint64_t cask_ctx_scratch_bytes(const cask_ctx* c) {
+  if (!c) return 0;
+  const DevBuf* bufs[] = {&c->chunk, &c->slots, &c->filebuf, &c->err2, &c->gather, &c->stamps, &c->repair, &c->lq,
+                          &c->tstate, &c->keyat, &c->cdesc, &c->probe, &c->mruns, &c->stage_data, &c->stage_rows};
+  uint64_t t = 0;
+  for (const DevBuf* b : bufs) t += b->cap;
+  return t;
+}
+
 int cask_last_walk(const cask_ctx* c) { return c ? c->last_walk : 0; }
 
 int cask_last_geometry(const cask_ctx* c) { return c ? c->last_geo : -1; }
@@ -304,8 +314,9 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   int geo = c->geo >= 0 ? c->geo : kDefaultGeometry;
   const uint32_t chunk = geometry_chunk(geo);
   // slot rows per chunk, rounded to 8 rows: every chunk's rows start on a 128-B line, so the
-  // scan's 1-KiB row stores cover whole lines and need no fill from HBM
-  const uint32_t slot_cap = ((chunk / 18 + 2) + 7) & ~7u;
+  // scan's 1-KiB row stores cover whole lines and need no fill from HBM. The full count holds every
+  // record a chunk can start (18-B records); a walk-mode call uses kWalkSlotCap (below).
+  const uint32_t slot_full = ((chunk / 18 + 2) + 7) & ~7u;
   uint64_t total_chunks = 0, total_tiles = 0;
   const size_t head_words = sizeof(SummaryHead) / 8;
   const size_t sum_words = head_words + (nfiles + 1) + 4ull * nfiles;
@@ -335,7 +346,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   bool fb_fresh = false;  // (a new allocation may reuse the old address: never resident)
   if (!c->filebuf.ensure(fd_bytes + 2 * callb + 3 * pf_bytes + sum_bytes, &fb_fresh)) return CASK_E_NOMEM;
   if (!c->chunk.ensure(C * (4 * 8 + 4 + 4 + 16 + 8) + (total_tiles + 1) * 4 * 8 + 1024)) return CASK_E_NOMEM;
-  if (!c->slots.ensure((total_chunks * slot_cap + 1) * 16)) return CASK_E_NOMEM;
   const size_t runs_bytes = align_up(16ull * (total_chunks + 1), 256), cerr_bytes = align_up(4ull * (total_chunks + 1), 256),
                redo_bytes = align_up(total_chunks + 1, 256);
   if (!c->repair.ensure(runs_bytes + cerr_bytes + 2 * redo_bytes)) return CASK_E_NOMEM;
@@ -370,7 +380,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   a.exact = 0;
   a.total_chunks = total_chunks;
   a.chunk = chunk;
-  a.slot_cap = slot_cap;
   a.spec = cb;
   a.exit = cb + C;
   a.base = cb + 2 * C;
@@ -390,7 +399,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.tile_pmax = tb + 2 * TT;
     a.tile_psum = tb + 3 * TT;
   }
-  a.slots = c->slots.as<uint32_t>();
   a.file_total = d_ftot;
   a.file_err = d_ferr;
   a.first_bad = d_fbad;
@@ -623,6 +631,15 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     a.run_tail = ~0ull;  // (the chunk scan's short tail runs were sized for its own run length)
   }
   c->last_walk = mixed ? 2 : walk ? 1 : 0;
+  // Slot rows: kWalkSlotCap per chunk in a walk-mode call over data files with dense rows (the
+  // chase is their only writer; 2 KiB per 32-KiB chunk instead of 29 KiB), else the full count. The
+  // small size is redone at full size when a chunk overflows it (Counters::slot_overflow) or the
+  // call needs the repair path, whose exact chunk scans may write up to the full count.
+  const bool small_slots = walk && !mixed && !hint && dense && !c->full_slots_next;
+  c->full_slots_next = false;
+  a.slot_cap = small_slots ? kWalkSlotCap : slot_full;
+  if (!c->slots.ensure((total_chunks * (uint64_t)a.slot_cap + 1) * 16)) return CASK_E_NOMEM;
+  a.slots = c->slots.as<uint32_t>();
   H(hipEventRecord(c->ev[1], st));
   // walk mode on data files: the runs in G groups; per group the walk (which hashes the records
   // that fit its window) and the long records' queueing on the call's stream, then their hashing
@@ -713,6 +730,10 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     if (!ok) return CASK_E_DEVICE;
   }
 
+  if (small_slots && (hc->slot_overflow || hc->any_invalid)) {
+    c->full_slots_next = true;
+    return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, hint);
+  }
   c->last_dense = 0;
   if (dense && !hc->any_invalid) {
     // every speculated start held: the rows are final but for the long records' checksums

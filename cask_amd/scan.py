@@ -210,6 +210,10 @@ class ScanContext:
         return ScanResult(c, pos[:c], seq[:c], vsz[:c], ksz[:c], status[:c], list(off), _err(e))
 
     # -- instrumentation ----------------------------------------------------------------------
+    def scratch_bytes(self) -> int:
+        """Device scratch this context holds (cask_ctx_scratch_bytes)."""
+        return int(self.lib.cask_ctx_scratch_bytes(self._h))
+
     def last_error(self) -> str:
         v = self.lib.cask_ctx_last_error(self._h)
         return v.decode() if v else ""

@@ -66,6 +66,10 @@ void* cask_ctx_stream(cask_ctx* ctx);
  * inputs another library is still producing. */
 int cask_ctx_wait_stream(cask_ctx* ctx, void* hip_stream);
 int cask_ctx_device(const cask_ctx* ctx);
+/* Device scratch the context holds now, in bytes (its buffers only grow; cask_ctx_destroy frees
+ * them): chunk table, slot rows, call blocks, repair state, host-scan staging. */
+uint64_t cask_ctx_scratch_bytes(const cask_ctx* ctx);
+
 /* Human-readable cause of the last CASK_E_DEVICE returned on this context ("" if none). */
 const char* cask_ctx_last_error(const cask_ctx* ctx);
 /* Chunk size in bytes used by the scan kernels (the unit of speculation and staging). */

@@ -301,6 +301,28 @@ def test_zipf_sizes_long_records(gpu_ctx, seed):
     assert cnt["walked"] == 0, cnt
 
 
+def test_walk_slot_rows_overflow_redo(gpu_ctx):
+    """A walk-mode call sizes its slot rows for kWalkSlotCap (128) records per 32-KiB chunk: a log of
+    long records with a burst of ~600 tiny ones inside one chunk overflows them, and the call is
+    redone with full slot rows — same rows as the oracle either way; the Zipf log alone keeps the
+    small slots (its scratch is a fraction of its bytes)."""
+    import torch
+    rng = random.Random(77)
+    head = make_records(rng, 300, lambda r: 16, _zipf_vsz(rng))
+    burst = make_records(rng, 600, lambda r: 4, lambda r: 20, seq0=301)  # 42-B records
+    tail = make_records(rng, 300, lambda r: 16, _zipf_vsz(rng), seq0=901)
+    check_against_oracle(gpu_ctx, [head + burst + tail], device=True)
+    if os.environ.get("CASK_SCAN_MODE") in (None, "walk"):
+        zipf = make_records(rng, 3000, lambda r: 16, _zipf_vsz(rng), tomb_p=0.02)
+        ctx2 = type(gpu_ctx)(0)  # a fresh context: its scratch is this call's alone
+        t = torch.from_numpy(np.frombuffer(zipf, np.uint8).copy()).cuda()
+        res = ctx2.scan_device([(1, t)])
+        assert res.error is None
+        if ctx2.last_counters()["walk_mode"] == 1:
+            nch = (len(zipf) + 32767) // 32768
+            assert ctx2.scratch_bytes() < 8192 * nch + (8 << 20), (ctx2.scratch_bytes(), nch)
+
+
 @pytest.mark.parametrize("corrupt", [False, True])
 def test_mixed_modes_in_one_call(gpu_ctx, corrupt):
     """One call over a file of fixed 290-B records (configs[1] shape), a file of Zipf-length records
