@@ -57,6 +57,14 @@ def main():
               f"0/10/50/90/99/100 = {' / '.join(f'{x:.1f}' for x in q)} us")
         print(f"idle after finishing: {np.mean(span - en) / span:.3f} of wave-time; "
               f"tail (max - median end) {span - q[2]:.1f} us")
+        # per XCD (workgroups are dealt to the 8 XCDs round-robin: XCD = workgroup % 8)
+        wid = np.flatnonzero(np.frombuffer(ws, np.uint64).reshape(nw, 2)[:, 1] > 0)
+        xcd = (wid // 4) % 8
+        for x in range(8):
+            e = en[xcd == x]
+            if e.size:
+                print(f"  XCD {x}: {e.size} waves, end p10/p50/p90/max "
+                      f"{' / '.join(f'{v:.0f}' for v in np.percentile(e, [10, 50, 90, 100]))} us")
 
 
 if __name__ == "__main__":
