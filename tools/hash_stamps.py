@@ -57,6 +57,19 @@ def main():
               f"0/10/50/90/99/100 = {' / '.join(f'{x:.1f}' for x in q)} us")
         print(f"idle after finishing: {np.mean(span - en) / span:.3f} of wave-time; "
               f"tail (max - median end) {span - q[2]:.1f} us")
+        # per wave: when its runs ran out (the claim counter was past the last unit) -> its end
+        L.cask_debug_dry_stamps.restype = C.c_int
+        L.cask_debug_dry_stamps.argtypes = [C.c_void_p, C.POINTER(C.c_uint64), C.c_uint64]
+        dr = (C.c_uint64 * nw)()
+        L.cask_debug_dry_stamps(ctx._h, dr, nw)
+        full = np.frombuffer(ws, np.uint64).reshape(nw, 2).astype(np.int64)
+        dry = np.frombuffer(dr, np.uint64).astype(np.int64)
+        ok = (full[:, 1] > 0) & (dry > 0)
+        if ok.any():
+            dry_t = (dry[ok] - t0) / 100.0
+            drain = (full[ok, 1] - dry[ok]) / 100.0
+            print(f"runs ran out at p10/p50/p90/max {' / '.join(f'{x:.0f}' for x in np.percentile(dry_t, [10, 50, 90, 100]))} us; "
+                  f"drain after that p10/p50/p90/max {' / '.join(f'{x:.0f}' for x in np.percentile(drain, [10, 50, 90, 100]))} us")
         # per XCD (workgroups are dealt to the 8 XCDs round-robin: XCD = workgroup % 8)
         wid = np.flatnonzero(np.frombuffer(ws, np.uint64).reshape(nw, 2)[:, 1] > 0)
         xcd = (wid // 4) % 8
