@@ -18,7 +18,6 @@
 // lowest offset >= c0 whose header gives a record longer than that which ends exactly at the
 // start found (repeated: a chain of long records before the first verified one).
 #include "device_util.h"
-#include "walk_chase.h"
 
 #include <stdlib.h>
 
@@ -569,70 +568,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
   if (a.stamps && threadIdx.x == 0)
     for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[i], (unsigned long long)wst[i]);
 #endif
-}
-
-// one run of the chase
-__device__ __forceinline__ void chase_run(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t i,
-                                                    uint64_t p_in) {
-  uint64_t t0, t1;
-  walk_run_chunks(a, i, &t0, &t1);
-  (void)chase_range(a, files, t0, t1, p_in);
-}
-
-// The search and the chase in one kernel (k_walk_find): a wave claims runs and searches their first
-// starts as k_walk_search does, keeping each run and its start in LDS; once it holds 64 of them, or
-// the runs are all claimed, its lanes chase those runs at once (lane i the i-th, chase_range). No
-// wave waits for another: a wave whose searches ended early chases while others still search, and
-// the chase of the runs searched last is the only part after the last search.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_walk_find(ScanArgs a, const FileDesc* __restrict__ files) {
-  __shared__ SearchLdsSw L;
-  __shared__ uint64_t s_run[64], s_start[64];
-  uint64_t wst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  (void)wst;
-  const uint64_t R = a.run;
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
-  uint32_t held = 0;
-  for (uint64_t k = blockIdx.x;; k = gridDim.x + wave_claim(&a.ctr->search_next[a.grp])) {
-    const bool done = k >= nruns;
-    if (!done) {
-      const uint64_t t = (a.wruns ? a.wruns[k] : k) * R;
-      const uint32_t fi = find_file(files, a.nfiles, t);
-      const FileDesc fd = files[fi];
-      const uint64_t fend = fd.first_chunk + fd.nchunks;
-      const uint64_t tend = (t + R < a.total_chunks) ? t + R : a.total_chunks;
-      const uint64_t se = fend < tend ? fend : tend;
-      const uint64_t b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
-      const uint64_t b1 = ((se - fd.first_chunk) * (uint64_t)a.chunk < fd.len) ? (se - fd.first_chunk) * (uint64_t)a.chunk : fd.len;
-      const uint64_t s0 = b0 == 0 ? 0 : walk_search_sw(L, fd.data, fd.len, b0, b1, wst, a.search_short);
-      if (threadIdx.x == 0) {
-        a.tin[t] = s0;
-        s_run[held] = k;
-        s_start[held] = s0;
-      }
-      ++held;
-    }
-    if (held == 64 || (done && held)) {
-      __syncthreads();
-      if (threadIdx.x < held) chase_run(a, files, s_run[threadIdx.x], s_start[threadIdx.x]);
-      __syncthreads();
-      held = 0;
-    }
-    if (done) break;
-  }
-}
-void launch_walk_find(const ScanArgs& a, void* stream) {
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
-  if (!a.total_chunks || !nruns) return;
-  static int per_cu = 0;
-  if (!per_cu) {
-    int nb = 0;
-    if (cask_knobs::tune("CASK_SEARCH_WAVES")) per_cu = atoi(cask_knobs::tune("CASK_SEARCH_WAVES"));  // (tuning)
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk_find, 64, 0) == hipSuccess && nb > 0) per_cu = nb;
-    if (per_cu <= 0) per_cu = 12;
-  }
-  uint64_t grid = (uint64_t)device_cus() * (uint64_t)per_cu;
-  if (grid > nruns) grid = nruns;
-  hipLaunchKernelGGL(k_walk_find, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
 }
 
 

@@ -17,7 +17,6 @@
 // Output: the chunk table and slot rows of k_scan_chunks (spec, exit, count, cerr, long_r = none,
 // slot rows with the checksum verdict), so k_finish and the repair path run unchanged.
 #include "device_util.h"
-#include "walk_chase.h"
 
 #include <stdlib.h>
 #include "knobs.h"
@@ -36,6 +35,23 @@ namespace cask_dev {
 
 namespace {
 
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+typedef __attribute__((address_space(1))) uint64_t g_u64;
+typedef __attribute__((address_space(1))) u32x4 g_u32x4;
+
+constexpr uint32_t kNoChunk = 0xFFFFFFFFu;
+
+// The piece of a run inside one file: chunks [t0, t0 + nch) of the file at `data`.
+struct WSeg {
+  const uint8_t* data;
+  uint64_t len;
+  int64_t sl;      // the highest file offset a 16-B load may start at: such a load stays within the
+                   // 16-B granules that hold the file's bytes (sl < 0 for a file inside one granule)
+  uint64_t b0, b1; // the segment's file bytes
+  uint64_t t0;     // global index of its first chunk
+  uint32_t nch;
+};
+
 // The 16 bytes of v from byte s on (s in 0..15), zero-filled past the end.
 __device__ __forceinline__ u32x4 shr_bytes(const u32x4& v, uint32_t s) {
   const uint32_t k = s >> 2, b = s & 3;
@@ -46,10 +62,171 @@ __device__ __forceinline__ u32x4 shr_bytes(const u32x4& v, uint32_t s) {
   return u32x4{fun(w0, w1, b), fun(w1, w2, b), fun(w2, w3, b), fun(w3, 0u, b)};
 }
 
+// One chunk's table entries. A chunk with more records than its slot rows (a.slot_cap: small in a
+// walk-mode call) keeps slot_cap of them and flags the call, which the host then redoes with full
+// slot rows: every later kernel reads rows r < count only, so nothing reads past the slots.
+__device__ __forceinline__ void put_chunk(const ScanArgs& a, uint64_t t, uint64_t spec, uint64_t ex, uint32_t count,
+                                          uint32_t cerr) {
+  if (count > a.slot_cap) {
+    a.ctr->slot_overflow = 1u;
+    count = a.slot_cap;
+  }
+  ((g_u64*)a.spec)[t] = spec;
+  ((g_u64*)a.exit)[t] = ex;
+  ((g_u32*)a.count)[t] = count;
+  ((g_u32*)a.long_r)[t] = 0xFFFFFFFFu;  // every record is hashed here: nothing left for k_long
+  ((g_u32*)a.cerr)[t] = cerr;
+}
+
+// A quad's walk state (every field the same in the quad's four lanes).
+struct Walk {
+  WSeg S;
+  uint64_t run_end;  // the run's end chunk (global)
+  // chunk state of the segment
+  uint32_t cj, cn, ccerr;
+  uint64_t cspec;
+};
+
+// The chain enters the record at `pos`: close the chunks it leaves, open its chunk; returns the
+// record's row within its chunk (and the chunk in *j).
+__device__ __forceinline__ uint32_t open_record(const ScanArgs& a, Walk& W, uint64_t pos, uint32_t csh, bool writer,
+                                                uint32_t* jout) {
+  const uint32_t j = (uint32_t)((pos - W.S.b0) >> csh);
+  if (j != W.cj) {
+    if (W.cj != kNoChunk && writer) put_chunk(a, W.S.t0 + W.cj, W.cspec, pos, W.cn, W.ccerr);
+    for (uint32_t k = W.cj == kNoChunk ? 0u : W.cj + 1; k < j; ++k)
+      if (writer) put_chunk(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
+    W.cj = j;
+    W.cn = 0;
+    W.ccerr = 0xFFFFFFFFu;
+    W.cspec = pos;
+  }
+  *jout = j;
+  return W.cn++;
+}
+
+// The segment ends: the chain leaves it at `ex` (kTerm after an EOF row).
+__device__ __forceinline__ void close_segment(const ScanArgs& a, Walk& W, uint64_t ex, bool writer) {
+  uint32_t k0 = 0;
+  if (W.cj != kNoChunk) {
+    if (writer) put_chunk(a, W.S.t0 + W.cj, W.cspec, ex, W.cn, W.ccerr);
+    k0 = W.cj + 1;
+  }
+  for (uint32_t k = k0; k < W.S.nch; ++k)
+    if (writer) put_chunk(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
+  W.cj = kNoChunk;
+}
+
+// The segment of chunks [t, min(file end, W.run_end)) of the file holding chunk t.
+__device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* files, Walk& W, uint64_t t) {
+  const uint32_t fi = find_file(files, a.nfiles, t);
+  const FileDesc fd = files[fi];
+  const uint64_t fend = fd.first_chunk + fd.nchunks;
+  const uint64_t se = fend < W.run_end ? fend : W.run_end;
+  W.S.data = fd.data;
+  W.S.len = fd.len;
+  const uintptr_t end16 = ((uintptr_t)(fd.data + fd.len) + 15) & ~(uintptr_t)15;
+  W.S.sl = (int64_t)(end16 - (uintptr_t)fd.data) - 16;
+  W.S.b0 = (t - fd.first_chunk) * (uint64_t)a.chunk;
+  const uint64_t e = (se - fd.first_chunk) * (uint64_t)a.chunk;
+  W.S.b1 = e < fd.len ? e : fd.len;
+  W.S.t0 = t;
+  W.S.nch = (uint32_t)(se - t);
+  W.cj = kNoChunk;
+}
+
 }  // namespace
 
-// Split path, pass 1 — k_walk_chase: one lane per run walks its chain from the run's speculative
-// start (k_walk_search's a.tin), chase_range in walk_chase.h.
+// ---------------------------------------------------------------------------------------------
+// Split path, pass 1 — k_walk_chase: one lane per run of a.run chunks walks the record chain from
+// the run's speculative start (k_walk_search) reading only each record's 18-B header
+// (Entries::next, log.rs:403-429: each record starts where the previous one ends), and writes what
+// k_walk_runs would: slot rows (without the checksum verdict: k_run_hash adds it), the chunk table
+// (spec, exit, count, cerr, long_r = none) and, per chunk, the address of its first byte and of its
+// file's end (cdesc). A record cut short by the end of its file is its UnexpectedEof row (data.rs:163,
+// 172, 181) and ends the chain.
+// ---------------------------------------------------------------------------------------------
+// Chunks [tb, te) of one run (te <= the run's end): the chain enters the range's first segment at
+// p_in (ignored when the segment starts a file: the chain starts there at 0); returns the position
+// it leaves the range at (kTerm once an EOF row ended it, kNone if it never had a start). Chasing a
+// run as [t0, tm) and then [tm, t1) from the first range's exit writes exactly what one range
+// [t0, t1) writes: the chain is one walk either way.
+
+__device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t tb, uint64_t te,
+                                uint64_t p_in) {
+  const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
+  g_u32* slots = (g_u32*)a.slots;
+  g_u64* cd = (g_u64*)a.cdesc;
+  Walk W;
+  W.cn = 0;
+  W.ccerr = 0xFFFFFFFFu;
+  W.cspec = 0;
+  W.run_end = te;
+  uint64_t p = p_in;
+  bool term = false;
+  for (uint64_t t = tb; t < te;) {
+    seg_setup(a, files, W, t);
+    t = W.S.t0 + W.S.nch;
+    const uint64_t fend = (uint64_t)(uintptr_t)(W.S.data + W.S.len);
+    for (uint32_t c = 0; c < W.S.nch; ++c) {
+      cd[2 * (W.S.t0 + c)] = (uint64_t)(uintptr_t)(W.S.data + W.S.b0 + ((uint64_t)c << csh));
+      cd[2 * (W.S.t0 + c) + 1] = fend;
+    }
+    // the range's first segment starts at p_in; a later one starts a file (b0 == 0)
+    if (W.S.b0 == 0) p = 0ull;
+    else if (W.S.t0 != tb) p = kNone;  // (unreachable: a later segment starts a file)
+    term = false;
+    // The next record's header is loaded before this record's stores go out: a wait for a load
+    // also waits for every store issued before it (one vmcnt counts both), so loading after the
+    // stores would cost each hop a store round trip as well. Headers past the file's end are not
+    // read (an address inside the file is loaded instead).
+    const bool has = p != kNone && p < W.S.b1;
+    // one 16-B load per hop, of header bytes 2..17 (seq, key size, value size; the checksum's first
+    // two bytes are not needed)
+    const uint64_t p0 = has && p + 18 <= W.S.len ? p + 2 : 0ull;
+    u32x4 h = gld16g((const g_u8*)(W.S.data + p0));
+    asm volatile("" ::"v"(h.x), "v"(h.y), "v"(h.z), "v"(h.w));
+    while (p != kNone && p < W.S.b1) {
+      uint32_t j = 0;
+      if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
+        const uint32_t r = open_record(a, W, p, csh, true, &j);
+        const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
+        if (r < a.slot_cap) *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
+        if (r < W.ccerr) W.ccerr = r;
+        term = true;
+        break;
+      }
+      const uint32_t ksz = h.z >> 16, vsz = h.w;
+      const u32x4 row = u32x4{fun(h.x, h.y, 2), fun(h.y, h.z, 2), vsz, ksz};
+      const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+      const uint64_t pn = p + rl;
+      const uint64_t pl = pn + 18 <= W.S.len ? pn + 2 : 0ull;  // (pn < p: rl wrapped, impossible)
+      h = gld16g((const g_u8*)(W.S.data + pl));
+      const uint32_t r = open_record(a, W, p, csh, true, &j);
+      const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
+      if (r < a.slot_cap)
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
+      if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
+        if (r < W.ccerr) W.ccerr = r;
+        term = true;
+        break;
+      }
+      p = pn;
+    }
+    close_segment(a, W, term ? kTerm : p, true);
+    if (term) p = kTerm;
+  }
+  return p;
+}
+
+// The chunk range of walk run i (an index into a.wruns, or the run itself): [t0, t1).
+__device__ __forceinline__ void walk_run_chunks(const ScanArgs& a, uint64_t i, uint64_t* t0, uint64_t* t1) {
+  const uint64_t R = a.run;
+  const uint64_t k = a.wruns ? a.wruns[i] : i;
+  *t0 = k * R;
+  *t1 = k * R + R < a.total_chunks ? k * R + R : a.total_chunks;
+}
+
 __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* __restrict__ files) {
   const uint64_t R = a.run;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
@@ -83,7 +260,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   constexpr uint32_t RT = kMaxRun + 1;
   __shared__ uint32_t s_pf[4][2][RT];  // per wave, two runs: the exclusive prefix of their chunks' rows
   __shared__ uint64_t s_cd[4][2][2 * kMaxRun];  // and their chunks' first-byte and file-end addresses
-  __shared__ uint16_t s_tl[4][2][kTailMaxRecs];  // and, for a tail piece's pass, its records in that pass
   const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6;
   const bool qlead = q == 0;
   const uint64_t R = a.run;
@@ -96,8 +272,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t* pfB = s_pf[wv][1];
   uint64_t* cdA = s_cd[wv][0];
   uint64_t* cdB = s_cd[wv][1];
-  uint16_t* tlA = s_tl[wv][0];
-  uint16_t* tlB = s_tl[wv][1];
   const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
   const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;      // a line every idle load may read
 
@@ -108,7 +282,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   // arrays indexed by the slot: those go to scratch memory, whose loads wait for every load.)
   uint64_t rtA = 0, rtB = 0;
   uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
-  bool flA = false, flB = false;  // the unit's records are handed out through its list (tlA / tlB)
   bool fullB = false;
   uint32_t cur = 0;
   bool runs_left = true;
@@ -122,47 +295,21 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   // (round 5: eighths instead of quarters, over the last one or two grids' worth, measured the same
   // or 0.2 % apart; sixteenths 1.5 % slower — the tail is the longest records still in flight when
   // the runs run out, up to 64 rounds of one quad, not the units)
-  // With a.hash_ntail (walk mode over data files): the last hash_ntail runs' pieces are each handed
-  // out twice, through a list of their records — first (units [0, NT)) the records of at least
-  // kTailLong bytes, marked by the chase in a.tbits, then the other runs whole, then (the last NT
-  // units) the pieces' shorter records — so that the waves run dry on records of a few rounds each.
-  constexpr uint64_t TS = kTailSplit;
-  const bool split = a.hash_ntail != 0;
+  constexpr uint64_t TS = 4;
   const uint64_t tcap = (uint64_t)gridDim.x * 4;
-  const uint64_t ntail = split ? a.hash_ntail : nruns < tcap ? nruns : tcap;
-  const uint64_t nhead = nruns - ntail, NT = TS * ntail;
-  const uint64_t nunits = nhead + (split ? 2 * NT : NT);
+  const uint64_t ntail = nruns < tcap ? nruns : tcap;
+  const uint64_t nhead = nruns - ntail, nunits = nhead + TS * ntail;
   auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
     if (u >= nunits) return false;
-    // pass: 0 a whole head run or (no split) a tail piece, 1 a tail piece's long records, 2 its others
-    uint32_t pass = 0;
-    uint64_t piece = 0;
-    if (split) {
-      if (u < NT) {
-        pass = 1;
-        piece = u;
-      } else if (u < NT + nhead) {
-        u -= NT;
-      } else {
-        pass = 2;
-        piece = u - NT - nhead;
-      }
-    } else if (u >= nhead) {
-      piece = u - nhead;
-    }
-    const bool tl = split ? pass != 0 : u >= nhead;
-    const uint64_t k = tl ? nhead + piece / TS : u;
+    const bool tl = u >= nhead;
+    const uint64_t k = tl ? nhead + (u - nhead) / TS : u;
     const uint64_t tr = run_start(k);
     const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
-    const uint64_t qr = (R + TS - 1) / TS, c0 = tl ? (piece % TS) * qr : 0ull;
+    const uint64_t qr = (R + TS - 1) / TS, c0 = tl ? ((u - nhead) % TS) * qr : 0ull;
     const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
     const uint64_t t0 = tr + c0;
     const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
     uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
-    // the piece's long-record bits, loaded with the counts (one round trip)
-    const bool flt = pass != 0;
-    const uint32_t* tbw = a.tbits + piece * kTailBitWords;
-    uint32_t bits = flt && lane < kTailBitWords ? ((const g_u32*)tbw)[lane] : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
       if ((int)lane >= o) inc += u;
@@ -175,36 +322,15 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       cdt[2 * lane] = cd[2 * (t0 + lane)];
       cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
     }
-    uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
-    if (flt) {  // the pass's records, in order, into the unit's list
-      const uint32_t nb = 32 * lane;
-      const uint32_t valid = lane >= kTailBitWords || nb >= n ? 0u : n - nb >= 32 ? ~0u : (1u << (n - nb)) - 1u;
-      uint32_t w = (pass == 1 ? bits : ~bits) & valid;
-      const uint32_t c = (uint32_t)__builtin_popcount(w);
-      uint32_t pre = c;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(pre, o, 64);
-        if ((int)lane >= o) pre += t;
-      }
-      uint16_t* lst = intoA ? tlA : tlB;
-      uint32_t at = pre - c;
-      while (w) {
-        const uint32_t b = (uint32_t)__builtin_ctz(w);
-        w &= w - 1;
-        lst[at++] = (uint16_t)(nb + b);
-      }
-      n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)pre, 63, 64));
-    }
+    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
     if (intoA) {
       rtA = t0;
       rchA = nch;
       rnA = n;
-      flA = flt;
     } else {
       rtB = t0;
       rchB = nch;
       rnB = n;
-      flB = flt;
     }
     return true;
   };
@@ -290,20 +416,17 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     const uint32_t idx = up ? myrank - rem : cur + myrank;
     const bool claimed = want && (up ? (fullB && idx < rnB) : true);
     const uint32_t* pf = up ? pfB : pfA;
-    // the unit's idx-th record to hand out: itself, or its list's entry (a tail piece's pass)
-    const uint16_t* tlc = up ? tlB : tlA;
-    const uint32_t rec = (up ? flB : flA) ? (uint32_t)tlc[idx < kTailMaxRecs ? idx : 0u] : idx;
-    uint32_t lo = 0, hi = up ? rchB : rchA;  // the last chunk j with pf[j] <= rec
+    uint32_t lo = 0, hi = up ? rchB : rchA;  // the last chunk j with pf[j] <= idx
 #pragma unroll
     for (int it = 0; it < 6; ++it) {  // (a run is at most 64 chunks)
       const uint32_t mid = (lo + hi) >> 1;
       const bool go = hi - lo > 1;
-      const bool le = go && pf[mid] <= rec;
+      const bool le = go && pf[mid] <= idx;
       lo = le ? mid : lo;
       hi = go && !le ? mid : hi;
     }
     const uint64_t ntc = (up ? rtB : rtA) + lo;
-    const uint32_t nrc = rec - pf[lo];
+    const uint32_t nrc = idx - pf[lo];
     nt = claimed ? ntc : nt;
     nr = claimed ? nrc : nr;
     const uint64_t* cdt = up ? cdB : cdA;
@@ -325,10 +448,6 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         uint64_t* tc = cdA;
         cdA = cdB;
         cdB = tc;
-        uint16_t* tt = tlA;
-        tlA = tlB;
-        tlB = tt;
-        flA = flB;
         fullB = false;
         cur = used - rem;
       } else {
@@ -507,11 +626,11 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(tpb), 0, (hipStream_t)stream, a, a.files);
 }
 
-// The persistent grid of k_run_hash: exactly the resident workgroups, as waves (a workgroup beyond
-// them would start only as the first ones finish, holding its first run until the end).
-// CASK_HASH_WAVES (tuning knob) overrides the waves per CU.
 template <uint32_t D>
-static uint64_t hash_waves_at() {
+static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
+  // A persistent grid of exactly the resident workgroups: a workgroup beyond them would start only
+  // as the first ones finish, holding its first run (claimed by block index) until the end.
+  // CASK_HASH_WAVES (tuning knob) overrides the waves per CU.
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
@@ -520,14 +639,7 @@ static uint64_t hash_waves_at() {
       per_cu = 4 * nb;
     if (per_cu <= 0) per_cu = 8;
   }
-  return (uint64_t)device_cus() * (uint64_t)per_cu;
-}
-uint64_t run_hash_waves(int depth) {
-  return depth == 16 ? hash_waves_at<16>() : depth == 4 ? hash_waves_at<4>() : hash_waves_at<8>();
-}
-template <uint32_t D>
-static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
-  uint64_t waves = hash_waves_at<D>();
+  uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
   if (waves > nruns) waves = nruns;
   hipLaunchKernelGGL((k_run_hash<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
 }

@@ -164,18 +164,7 @@ struct ScanArgs {
   // ones are listed for the hop back (kSearchShort; CASK_SEARCH_SHORT tuning knob)
   uint32_t search_short;
   uint32_t pad_ss;
-  // walk mode: the last hash_ntail runs are hashed in kTailSplit pieces each, every piece twice —
-  // its records of at least kTailLong bytes first (before every other run), the rest last — so that
-  // the kernel ends on short records; tbits: per piece kTailBitWords words, bit i = its record i is
-  // long (written by k_walk_chase). hash_ntail 0: no split.
-  uint64_t hash_ntail;
-  uint32_t* tbits;
 };
-constexpr uint32_t kTailSplit = 4;          // pieces per tail run (and per run of the last grid's worth)
-constexpr uint32_t kTailLong = 16384;       // records at least this long go first
-constexpr uint32_t kTailMaxRecs = 1024;     // records a piece can hold: kMaxRun / kTailSplit x kWalkSlotCap
-constexpr uint32_t kTailBitWords = kTailMaxRecs / 32;
-constexpr uint64_t kTailGrids = 3;          // tail runs, in grids' worth of the hash's waves
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
 // instead of by one quad of the chunk's workgroup while the rest of it waits (configs[2]: 32 GiB of
@@ -261,10 +250,7 @@ void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each w
 // headers: slot rows, chunk table, cdesc), then k_run_hash (a wave per claimed run, a quad per record:
 // every record hashed from HBM; depth = 64-B blocks per quad in flight)
 void launch_walk_chase(const ScanArgs& a, void* stream);
-// k_walk.hip: the search and the chase in one kernel (each wave chases the runs it searched)
-void launch_walk_find(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, int depth, void* stream);
-uint64_t run_hash_waves(int depth);  // k_run_hash's grid, in waves (before the cap at the run count)
 // after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
 void launch_hash_fix(const ScanArgs& a, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
