@@ -317,10 +317,17 @@ __device__ __forceinline__ uint32_t gbl_xxh32(const uint8_t* p, uint64_t len) {
 
 // 4x4 transpose across a quad: lane q enters with stripe q of a 4-stripe block (words 0..3) and
 // leaves with word q of stripes 0..3, in order (two butterfly stages of quad DPP moves).
-#ifdef CASK_TRANSPOSE_DPP  // (A/B variant) each stage as four v_cndmask_b32_dpp: word = lane's bit
-                           // set ? own word : the partner's (the DPP operand), 8 VALU instead of 16
 __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
-  (void)q;
+  const bool b1 = q & 2, b0 = q & 1;
+  uint32_t r0 = quad_xor2(b1 ? v.x : v.z), r1 = quad_xor2(b1 ? v.y : v.w);  // swap off-diagonal 2x2 blocks
+  if (b1) { v.x = r0; v.y = r1; } else { v.z = r0; v.w = r1; }
+  r0 = quad_xor1(b0 ? v.x : v.y);  // transpose within the 2x2 blocks
+  r1 = quad_xor1(b0 ? v.z : v.w);
+  if (b0) { v.x = r0; v.z = r1; } else { v.y = r0; v.w = r1; }
+}
+// The same transpose, each stage as four v_cndmask_b32_dpp (word = the lane's bit set ? its own word :
+// the partner's, the DPP operand): 8 vector instructions instead of 16 (k_run_hash_ln).
+__device__ __forceinline__ void quad_transpose_dpp(u32x4& v) {
   uint32_t x1, y1, z1, w1, x2, y2, z2, w2;
   // stage 1, partner q ^ 2 (vcc: lanes with q & 2): off-diagonal 2x2 blocks swapped
   asm volatile(
@@ -350,16 +357,6 @@ __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
       : "vcc");
   v = u32x4{x2, y2, z2, w2};
 }
-#else
-__device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
-  const bool b1 = q & 2, b0 = q & 1;
-  uint32_t r0 = quad_xor2(b1 ? v.x : v.z), r1 = quad_xor2(b1 ? v.y : v.w);  // swap off-diagonal 2x2 blocks
-  if (b1) { v.x = r0; v.y = r1; } else { v.z = r0; v.w = r1; }
-  r0 = quad_xor1(b0 ? v.x : v.y);  // transpose within the 2x2 blocks
-  r1 = quad_xor1(b0 ? v.z : v.w);
-  if (b0) { v.x = r0; v.z = r1; } else { v.y = r0; v.w = r1; }
-}
-#endif
 
 // XXH32 (seed 0) of global bytes [p, p+len) by a quad of lanes (q = lane & 3), lane q keeping stripe
 // accumulator v_{q+1}. Lane q loads stripe q of each 64-B block (one 16-B load: the quad reads 64

@@ -580,6 +580,361 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
 
 
 // ---------------------------------------------------------------------------------------------
+// k_run_hash_ln: the same pass with whole 128-B lines per load instruction, nontemporal. The wave's
+// 16 quads are 8 pairs (lanes 8o..8o+7: quad 2o "low", h = 0, and quad 2o + 1 "high", h = 1). A
+// round of a record is its lines [La + 1 KiB i, La + 1 KiB (i + 1)) (La: the line of the body's
+// first byte), so no line is read by two rounds of one record. Instruction 2m loads line m of the
+// low quad's round (the low quad's lanes its first 64 B, the high quad's lanes its second 64 B) and
+// instruction 2m + 1 line m of the high quad's round (high lanes its first 64 B, low lanes its
+// second): every instruction reads whole lines — nontemporal loads then fetch each line once (half
+// lines per instruction fetch a line twice under that policy) — and each quad holds one 64-B block
+// of its line in its own lanes and gets the other from its partner's (lane ^ 4, ds_swizzle). A
+// body dword is funneled out of two line dwords at the body's byte offset (v_alignbyte; the lower
+// one from the previous lane by DPP, lane 0's carried from the previous block) and masked against
+// the record's full stripes; lane q keeps the stripe accumulator of its dword position.
+// ---------------------------------------------------------------------------------------------
+// v_permlane32_swap: lanes 32..63 of a trade places with lanes 0..31 of b — afterwards a holds the
+// lower halves of both, b the upper halves
+__device__ __forceinline__ void swap32(uint32_t& a, uint32_t& b) {
+  const auto r = __builtin_amdgcn_permlane32_swap(a, b, false, false);
+  a = r[0];
+  b = r[1];
+}
+__device__ __forceinline__ void swap32(u32x4& a, u32x4& b) {
+  const auto x = __builtin_amdgcn_permlane32_swap(a.x, b.x, false, false);
+  const auto y = __builtin_amdgcn_permlane32_swap(a.y, b.y, false, false);
+  const auto z = __builtin_amdgcn_permlane32_swap(a.z, b.z, false, false);
+  const auto w = __builtin_amdgcn_permlane32_swap(a.w, b.w, false, false);
+  a = u32x4{x[0], y[0], z[0], w[0]};
+  b = u32x4{x[1], y[1], z[1], w[1]};
+}
+__device__ __forceinline__ u32x4 gld16nt(uint64_t p) {
+  typedef __attribute__((address_space(1))) const u32x4 gcu32x4;
+  return __builtin_nontemporal_load((gcu32x4*)(uintptr_t)p);
+}
+
+__global__ __launch_bounds__(256) void k_run_hash_ln(ScanArgs a) {
+  constexpr uint32_t D = 8;    // lines of a record per round
+  constexpr uint32_t RW = 256; // dwords per round
+  constexpr uint32_t RT = kMaxRun + 1;
+  __shared__ uint32_t s_pf[4][2][RT];
+  __shared__ uint64_t s_cd[4][2][2 * kMaxRun];
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6, h = lane >> 5;
+  const bool qlead = q == 0;
+  const uint64_t R = a.run;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
+  g_u32* slots = (g_u32*)a.slots;
+  const g_u64* cd = (const g_u64*)a.cdesc;
+  uint32_t* pfA = s_pf[wv][0];
+  uint32_t* pfB = s_pf[wv][1];
+  uint64_t* cdA = s_cd[wv][0];
+  uint64_t* cdB = s_cd[wv][1];
+  const unsigned long long qmask = 0x1111111111111111ull;
+  const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;  // (a 128-B aligned allocation: its first line)
+
+  // the wave's record stream: as k_run_hash
+  uint64_t rtA = 0, rtB = 0;
+  uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
+  bool fullB = false;
+  uint32_t cur = 0;
+  bool runs_left = true;
+  auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
+  constexpr uint64_t TS = 4;
+  const uint64_t tcap = (uint64_t)gridDim.x * 4;
+  const uint64_t ntail = nruns < tcap ? nruns : tcap;
+  const uint64_t nhead = nruns - ntail, nunits = nhead + TS * ntail;
+  auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
+    if (u >= nunits) return false;
+    const bool tl = u >= nhead;
+    const uint64_t k = tl ? nhead + (u - nhead) / TS : u;
+    const uint64_t tr = run_start(k);
+    const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
+    const uint64_t qr = (R + TS - 1) / TS, c0 = tl ? ((u - nhead) % TS) * qr : 0ull;
+    const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
+    const uint64_t t0 = tr + c0;
+    const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
+    uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t u = __shfl_up(inc, o, 64);
+      if ((int)lane >= o) inc += u;
+    }
+    uint32_t* pf = intoA ? pfA : pfB;
+    if (lane < nch) pf[lane + 1] = inc;
+    if (lane == 0) pf[0] = 0;
+    uint64_t* cdt = intoA ? cdA : cdB;
+    if (lane < nch) {
+      cdt[2 * lane] = cd[2 * (t0 + lane)];
+      cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
+    }
+    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
+    if (intoA) {
+      rtA = t0;
+      rchA = nch;
+      rnA = n;
+    } else {
+      rtB = t0;
+      rchB = nch;
+      rnB = n;
+    }
+    return true;
+  };
+  runs_left = load_run(true, blockIdx.x * 4ull + wv);
+
+  // a quad's current record (cv) and the round of it in hand: round cri of its cnrd rounds, rfin if
+  // it is the last (the record's tail bytes in T), head if it is the first (its stored checksum in
+  // x). The body (data.rs:185-198: everything after the stored checksum) starts at cb, chl bytes;
+  // line dword t (t = 0 at cb & ~127) funneled at byte csb is body dword t - cM - 1 (cM: the dword of
+  // cb in its line); ctl: the last dword a full stripe uses. tclamp: the tail's 16 bytes were loaded
+  // from the file's last granule instead (shifted by ctsh).
+  bool cv = false, rfin = false, head = false, tclamp = false;
+  uint64_t cb = 0, cend = 0, ct_t = 0;
+  uint32_t chl = 0, cM = 0, csb = 0, ctl = 0, cnrd = 0, cri = 0, ctsh = 0;
+  uint32_t v = 0, carry = 0, mrot = 1, cstored = 0, ct_r = 0, cw3 = 0;
+  uint32_t ns = 0;
+  uint64_t nt = 0;
+  uint32_t nr = 0;
+  u32x4 nrow = u32x4{0u, 0u, 0u, 0u};
+  uint64_t ncb = 0, nce = 0;
+  uint64_t carow = safe;
+  u32x4 XA[2 * D], XB[2 * D], TA = u32x4{0u, 0u, 0u, 0u}, TB = u32x4{0u, 0u, 0u, 0u};
+  uint32_t sA = 0, sB = 0;
+#pragma unroll
+  for (uint32_t d = 0; d < 2 * D; ++d) XA[d] = XB[d] = u32x4{0u, 0u, 0u, 0u};
+#ifdef CASK_STAMPS
+  const uint64_t wid = blockIdx.x * 4ull + wv;
+  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+  auto step = [&](u32x4 (&Xm)[2 * D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[2 * D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
+    if (ns == 1) ns = 2;
+    if (runs_left && !fullB) {
+      const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
+      const bool got = load_run(false, (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old));
+      runs_left = got;
+      fullB = got;
+#ifdef CASK_STAMPS
+      if (!got && a.stamps && lane == 0 && wid < kStampWaves) a.stamps[kStampDry + wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+    }
+    // ---- plan this quad's next round (branch-free, as k_run_hash)
+    const bool cont = cv && !rfin;
+    const bool promote = !cont && ns == 2;
+    const uint32_t w3n = nrow.w, vszn = nrow.z;
+    const uint64_t bn = ncb + ((w3n >> 16) & 0x7FFFu);
+    const uint64_t en = nce;
+    const uint64_t rln = 18ull + (w3n & 0xFFFFu) + (vszn == 0xFFFFFFFFu ? 0ull : (uint64_t)vszn);
+    const bool round2 = cont || (promote && bn + rln <= en);
+    const uint64_t b2 = cont ? cb : bn + 4, end2 = cont ? cend : en;
+    const uint32_t hl2 = cont ? chl : (uint32_t)(rln - 4);
+    const uint64_t la2 = b2 & ~127ull;
+    const uint32_t M2 = cont ? cM : (uint32_t)((b2 - la2) >> 2), sb2 = cont ? csb : (uint32_t)(b2 & 3);
+    const uint32_t ns2 = hl2 >> 4;  // full stripes
+    const uint32_t tl2 = cont ? ctl : M2 + 4 * ns2;
+    const uint32_t nrd2 = cont ? cnrd : (ns2 ? (tl2 >> 8) + 1 : 1u);
+    const uint32_t ri2 = cont ? cri + 1 : 0u;
+    const uint32_t nl2 = round2 && ns2 ? (((tl2 - RW * ri2) >> 5) + 1 < D ? ((tl2 - RW * ri2) >> 5) + 1 : D) : 0u;
+    const bool fin2 = round2 && ri2 + 1 == nrd2;
+    const uint64_t pt = nt;
+    const uint32_t pr = nr, pw3 = w3n;
+    ns = promote ? 0u : ns;
+    // ---- the stream's next records to the quads that have none (as k_run_hash)
+    const bool want = ns == 0;
+    const unsigned long long wm = __ballot(qlead && want) & qmask;
+    const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
+    const uint32_t l0 = lane & ~3u;
+    const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (l0 ? (~0ull >> (64 - l0)) : 0ull));
+    const uint32_t rem = rnA - cur;
+    const bool up = myrank >= rem;
+    const uint32_t idx = up ? myrank - rem : cur + myrank;
+    const bool claimed = want && (up ? (fullB && idx < rnB) : true);
+    const uint32_t* pf = up ? pfB : pfA;
+    uint32_t lo = 0, hi = up ? rchB : rchA;
+#pragma unroll
+    for (int it = 0; it < 6; ++it) {
+      const uint32_t mid = (lo + hi) >> 1;
+      const bool go = hi - lo > 1;
+      const bool le = go && pf[mid] <= idx;
+      lo = le ? mid : lo;
+      hi = go && !le ? mid : hi;
+    }
+    const uint64_t ntc = (up ? rtB : rtA) + lo;
+    const uint32_t nrc = idx - pf[lo];
+    nt = claimed ? ntc : nt;
+    nr = claimed ? nrc : nr;
+    const uint64_t* cdt = up ? cdB : cdA;
+    const uint64_t cbc = cdt[2 * lo], cec = cdt[2 * lo + 1];
+    ncb = claimed ? cbc : ncb;
+    nce = claimed ? cec : nce;
+    carow = claimed ? (uint64_t)(uintptr_t)(slots + (ntc * (uint64_t)a.slot_cap + nrc) * 4) : promote ? safe : carow;
+    uint64_t arow = carow;
+    if (nw) {
+      const uint32_t avail = rem + (fullB ? rnB : 0u);
+      const uint32_t used = nw < avail ? nw : avail;
+      if (used >= rem && fullB) {
+        rtA = rtB;
+        rnA = rnB;
+        rchA = rchB;
+        uint32_t* t = pfA;
+        pfA = pfB;
+        pfB = t;
+        uint64_t* tc = cdA;
+        cdA = cdB;
+        cdB = tc;
+        fullB = false;
+        cur = used - rem;
+      } else {
+        cur += used;
+      }
+    }
+    ns = claimed ? 1u : ns;
+    // ---- issue the round: the record's tail (its last hl % 16 bytes, into T) and stored checksum
+    // (first round) as plain loads, first, then the octet's 2 x D line loads (a line past the
+    // round's last is that last line again: the same line, merged with its first request; a quad
+    // with no lines reads the safe line)
+    const uint64_t end16 = (end2 + 15) & ~15ull;
+    const bool tail2 = round2 && fin2 && (hl2 & 15) != 0;
+    const uint64_t tp = b2 + 16ull * ns2;
+    const bool tclamp2 = tail2 && tp + 16 > end16;
+    uint64_t ta = tail2 ? (tclamp2 ? end16 - 16 : tp) : safe;
+    uint64_t sa = round2 && !cont ? b2 - 4 : safe;
+    const uint64_t rb = la2 + 1024ull * ri2;
+    // the pair's two rounds: quad j of the lower half (lanes 0..31) with quad j of the upper half;
+    // a quad with no lines reads the safe line (as one line)
+    const uint64_t rbq = nl2 ? rb : safe;
+    const uint32_t nlq = nl2 ? nl2 - 1 : 0u;  // its last line
+    uint32_t a0 = (uint32_t)rbq, a1 = a0, c0 = (uint32_t)(rbq >> 32), c1 = c0, n0 = nlq, n1 = nlq;
+    swap32(a0, a1);  // a0: the lower quad's, a1: the upper quad's
+    swap32(c0, c1);
+    swap32(n0, n1);
+    // this lane's 16 B of each line: the lower half of the wave reads a line's first 64 B, the upper
+    // half its second (lanes j and j + 32 have the same q)
+    const uint64_t lof = 64ull * h + 16ull * q;
+    const uint64_t rb0 = (((uint64_t)c0 << 32) | a0) + lof, rb1 = (((uint64_t)c1 << 32) | a1) + lof;
+    uint64_t ya[2 * D];
+#pragma unroll
+    for (uint32_t m = 0; m < D; ++m) {
+      ya[2 * m] = rb0 + 128ull * (m < n0 ? m : n0);
+      ya[2 * m + 1] = rb1 + 128ull * (m < n1 ? m : n1);
+    }
+    asm volatile("" : "+v"(arow), "+v"(sa), "+v"(ta));
+#pragma unroll
+    for (uint32_t d = 0; d < 2 * D; ++d) asm volatile("" : "+v"(ya[d]));
+    {  // (the 8 bytes used: the dead half of a 16-B destination is a register the compiler reuses,
+       // and writing it would wait for this load)
+      const uint64_t zw = *(const g_u64*)(uintptr_t)(arow + 8);
+      nrow = u32x4{0u, 0u, (uint32_t)zw, (uint32_t)(zw >> 32)};
+    }
+    Ti = gld16g((const g_u8*)(uintptr_t)ta);
+    xi = gld4g((const g_u8*)(uintptr_t)sa);
+#pragma unroll
+    for (uint32_t d = 0; d < 2 * D; ++d) Xi[d] = gld16nt(ya[d]);
+    // the round in hand is used from here on: nothing that reads it (the pair selects included) nor
+    // the wait for it is scheduled above the loads
+    asm volatile("" : "+v"(xm)::"memory");
+#pragma unroll
+    for (uint32_t d = 0; d < 2 * D; ++d) asm volatile("" : "+v"(Xm[d]));
+    // ---- mix the round in hand (every lane: the swizzles need both quads of a pair). The elements
+    // the record's full stripes use: dword t = 256 cri + 16 d + 4 k + q of its lines (lane q, block
+    // d, word k after the transpose) for t in [cM + 1, ctl], i.e. e = 4 d + k in [e_lo, e_lo + span]
+    // (e_lo <= 8: only the first elements of a first round can precede the first stripe)
+    {
+      const int32_t A = (int32_t)(cM + 1 - q) - (int32_t)(RW * cri), B = (int32_t)(ctl - q) - (int32_t)(RW * cri);
+      int32_t e_lo = A <= 0 ? 0 : (A + 3) >> 2;
+      int32_t e_hi = !cv || B < 0 ? -1 : (B >> 2 < 63 ? B >> 2 : 63);
+      const bool none = e_hi < e_lo;  // (no element: both tests fail)
+      e_lo = none ? 64 : e_lo;
+      e_hi = none ? -1 : e_hi;
+      const uint32_t span = (uint32_t)(e_hi - e_lo);
+#pragma unroll
+      for (uint32_t m = 0; m < D; ++m) {
+        const u32x4 xa = Xm[2 * m], xb = Xm[2 * m + 1];
+        // line m of the lower quad's round (its first 64 B in the lower half of the wave, its second
+        // in the upper half) and of the upper quad's: after the swap each half holds its line
+        u32x4 blk[2] = {xa, xb};
+        swap32(blk[0], blk[1]);
+#pragma unroll
+        for (uint32_t e = 0; e < 2; ++e) {
+          const uint32_t d = 2 * m + e;
+          const u32x4 gg = blk[e];
+          const uint32_t dv = (uint32_t)__builtin_amdgcn_mov_dpp((int)gg.w, 0x93, 0xF, 0xF, false);  // [3,0,1,2]
+          const uint32_t p0 = q == 0 ? carry : dv;
+          carry = dv;
+          u32x4 x = u32x4{fun(p0, gg.x, csb), fun(gg.x, gg.y, csb), fun(gg.y, gg.z, csb), fun(gg.z, gg.w, csb)};
+          quad_transpose_dpp(x);
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t el = 4 * d + k;
+            const bool ok = el < 8 ? (uint32_t)((int32_t)el - e_lo) <= span : (int32_t)el <= e_hi;
+            uint32_t w = xround(v, x[k]);
+            asm volatile("" : "+v"(w));
+            v = ok ? w : v;
+          }
+        }
+      }
+    }
+    if (cv && head) cstored = xm;
+    if (cv && rfin) {  // merge, length, tail, avalanche (data.rs:185-198)
+      const uint32_t tb = chl & 15;
+      uint32_t m = rotl_var(v, mrot);
+      m += quad_xor1(m);
+      m += quad_xor2(m);
+      uint32_t hh = (chl >= 16 ? m : P5) + chl;
+      const u32x4 tw = shr_bytes(Tm, tclamp ? ctsh : 0u);
+      const uint32_t n4 = tb >> 2, n1 = tb & 3;
+      hh = n4 > 0 ? tail4(hh, tw.x) : hh;
+      hh = n4 > 1 ? tail4(hh, tw.y) : hh;
+      hh = n4 > 2 ? tail4(hh, tw.z) : hh;
+      const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
+      hh = n1 > 0 ? tail1(hh, lw & 0xFFu) : hh;
+      hh = n1 > 1 ? tail1(hh, (lw >> 8) & 0xFFu) : hh;
+      hh = n1 > 2 ? tail1(hh, (lw >> 16) & 0xFFu) : hh;
+      hh = avalanche(hh);
+      if (hh != cstored && qlead) {  // InvalidChecksum{expected: stored, found: hh} (data.rs:193-198)
+        slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
+        atomicMin(&a.cerr[ct_t], ct_r);
+      }
+    }
+    // ---- state for the next iteration
+    if (cont) {
+      cri = ri2;
+      rfin = fin2;
+      tclamp = tclamp2;
+      ctsh = (uint32_t)(tp - (end16 - 16));
+      head = false;
+    } else {
+      cv = promote && round2;
+      cb = b2;
+      cend = end2;
+      chl = hl2;
+      cM = M2;
+      csb = sb2;
+      ctl = tl2;
+      cnrd = nrd2;
+      cri = 0;
+      rfin = fin2;
+      tclamp = tclamp2;
+      ctsh = (uint32_t)(tp - (end16 - 16));
+      head = true;
+      // lane q holds the words of stripe accumulator j = w mod 4 = (q - cM - 1) mod 4
+      const uint32_t j = (q - M2 - 1) & 3;
+      v = j == 0 ? P1 + P2 : j == 1 ? P2 : j == 2 ? 0u : 0u - P1;
+      mrot = j == 0 ? 1u : j == 1 ? 7u : j == 2 ? 12u : 18u;
+      ct_t = pt;
+      ct_r = pr;
+      cw3 = pw3;
+    }
+    const bool stream_left = rnA != cur || (fullB && rnB != 0) || runs_left;
+    return __builtin_amdgcn_readfirstlane((int)(stream_left || __any(cv || ns != 0))) != 0;
+  };
+  for (;;) {
+    (void)step(XA, TA, sA, XB, TB, sB);
+    if (!step(XB, TB, sB, XA, TA, sA)) break;
+  }
+#ifdef CASK_STAMPS
+  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[17 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+// ---------------------------------------------------------------------------------------------
 // Walk mode with k_finish running beside k_run_hash (it needs only the chase's output, so it runs
 // in the slots the hash's last waves leave): the checksum verdicts k_finish may have read before
 // the hash wrote them. Every chunk with a failing row has cerr set (the chase's EOF rows, the
@@ -649,6 +1004,21 @@ void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
   hipStream_t s = (hipStream_t)stream;
+  // k_run_hash_ln: whole lines per load instruction, nontemporal (CASK_HASH_LINES=0, a tuning knob:
+  // k_run_hash, a quad's 64 B per instruction)
+  static const bool lines = !(cask_knobs::tune("CASK_HASH_LINES") && atoi(cask_knobs::tune("CASK_HASH_LINES")) == 0);
+  if (lines) {
+    static int per_cu = 0;
+    if (!per_cu) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash_ln, 256, 0) == hipSuccess && nb > 0) per_cu = 4 * nb;
+      if (per_cu <= 0) per_cu = 8;
+    }
+    uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
+    if (waves > nruns) waves = nruns;
+    hipLaunchKernelGGL(k_run_hash_ln, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
+    return;
+  }
   if (depth == 16)  // (18 blocks, the most that keep 2 waves per SIMD: no faster, profiles/r04_ab_variants.txt)
     run_hash_at<16>(a, nruns, s);
   else if (depth == 4)

@@ -15,10 +15,14 @@ P=(
 )
 for spec in "$@"; do
   name=${spec%%=*}; lib=${spec#*=}
+  envs=()
+  if [[ "$lib" == *@* ]]; then  # NAME=PATH@VAR=VALUE[,VAR=VALUE]: that build's environment
+    IFS=',' read -ra envs <<< "${lib#*@}"; lib=${lib%%@*}
+  fi
   for p in "${P[@]}"; do
     set -- $p; pn=$1; shift
     echo "=== $name $pn"; date
-    timeout -s KILL 300 rocprofv3 --pmc "$@" -d "$O/${name}_$pn" -o ${name}_$pn --output-format csv -- \
+    env "${envs[@]}" timeout -s KILL 300 rocprofv3 --pmc "$@" -d "$O/${name}_$pn" -o ${name}_$pn --output-format csv -- \
       python3 tools/ab.py --child "$lib" --steps 3 --zipf-gib 32 > "$O/${name}_$pn.log" 2>&1
     rc=$?
     echo "rc=$rc"; tail -1 "$O/${name}_$pn.log" | cut -c1-160
