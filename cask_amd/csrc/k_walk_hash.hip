@@ -23,15 +23,6 @@
 
 namespace cask_dev {
 
-#ifdef CASK_STAMPS  // diagnostic build: k_run_hash phase cycle sums -> a.stamps[8..15] (tools/hash_stamps.py)
-#define HST(v) const uint64_t v = __builtin_amdgcn_s_memtime();
-#define HADD(i, v) hst[i] += __builtin_amdgcn_s_memtime() - (v);
-#define HCNT(i) hst[i] += 1;
-#else
-#define HST(v)
-#define HADD(i, v)
-#define HCNT(i)
-#endif
 
 namespace {
 
@@ -240,358 +231,33 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
 // ---------------------------------------------------------------------------------------------
 // Split path, pass 2 — k_run_hash: Entry::from_read's checksum (data.rs:185-198) of every record the
 // chase found. A wave claims runs and hands their records, in order, to its 16 quads: a quad hashes
-// its record straight from HBM (lane q keeps stripe accumulator q, quad_transpose), and takes the next
-// record of the wave's stream as it starts one (its slot row and chunk address are loaded one
-// iteration ahead). A failed record gets the bad bit in its slot row and lowers its chunk's first
-// failing row (cerr), which k_finish reads. The wave's stream runs on from one claimed run to the
-// next (the next run's row counts are loaded one iteration before they are needed), so no quad
-// waits for a run's last record.
+// its record straight from HBM, and takes the next record of the wave's stream as it starts one (its
+// slot row and chunk address are loaded one iteration ahead). A failed record gets the bad bit in its
+// slot row and lowers its chunk's first failing row (cerr), which k_finish reads. The wave's stream
+// runs on from one claimed run to the next (the next run's row counts are loaded one iteration
+// before they are needed), so no quad waits for a run's last record.
 //
-// The pipeline: iteration i issues round i (up to D 64-B blocks of each quad's record, its partial
-// last stripe, the stored checksum of a record's first round) and then mixes round i - 1. Every
-// quad issues every one of those loads (a quad with nothing to load reads one safe line), and the
-// two rounds live in two register sets used in turn (the loop body twice, no copies), so the
-// compiler's counted waits wait for round i - 1 only and round i stays in flight while it is mixed.
-// The loads whose results the next iteration's bookkeeping needs (slot rows, chunk addresses, the
-// next run's counts) are issued before the round's, so waiting for them never waits for the round.
-// ---------------------------------------------------------------------------------------------
-template <uint32_t D>
-__global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
-  constexpr uint32_t RT = kMaxRun + 1;
-  __shared__ uint32_t s_pf[4][2][RT];  // per wave, two runs: the exclusive prefix of their chunks' rows
-  __shared__ uint64_t s_cd[4][2][2 * kMaxRun];  // and their chunks' first-byte and file-end addresses
-  const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6;
-  const bool qlead = q == 0;
-  const uint64_t R = a.run;
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
-  const uint32_t vinit = q == 0 ? P1 + P2 : q == 1 ? P2 : q == 2 ? 0u : 0u - P1;
-  const uint32_t mrot = q == 0 ? 1u : q == 1 ? 7u : q == 2 ? 12u : 18u;
-  g_u32* slots = (g_u32*)a.slots;
-  const g_u64* cd = (const g_u64*)a.cdesc;
-  uint32_t* pfA = s_pf[wv][0];  // the run records are handed out from (A) and the one after it (B)
-  uint32_t* pfB = s_pf[wv][1];
-  uint64_t* cdA = s_cd[wv][0];
-  uint64_t* cdB = s_cd[wv][1];
-  const unsigned long long qmask = 0x1111111111111111ull;  // lane 0 of each quad
-  const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;      // a line every idle load may read
-
-  // The wave's record stream (uniform): two runs, A (records are handed out from it, at cursor
-  // cur) and B (the next one, once loaded: fullB), each as its first chunk, chunk count and row
-  // count. B is refilled from the claim counter as soon as it is free (at the top of an iteration:
-  // the wait for the claim also waits for the round in flight, once a run). (Plain variables, not
-  // arrays indexed by the slot: those go to scratch memory, whose loads wait for every load.)
-  uint64_t rtA = 0, rtB = 0;
-  uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
-  bool fullB = false;
-  uint32_t cur = 0;
-  bool runs_left = true;
-  auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
-  // run k's chunk-row prefix into LDS and its bounds into A or B; false if there is no run k (the
-  // flags are set by the callers: a store to one of two flags chosen at run time is what the
-  // compiler merges into a store through a selected pointer, which keeps both in scratch memory)
-  // Units of work: the runs in order, except that the last grid's worth of runs (one per wave) is
-  // handed out in quarters, so that the waves run dry within about a quarter of a run of each other
-  // instead of a whole one (configs[2]: a run is ~0.4 ms of one wave's hashing).
-  // (round 5: eighths instead of quarters, over the last one or two grids' worth, measured the same
-  // or 0.2 % apart; sixteenths 1.5 % slower — the tail is the longest records still in flight when
-  // the runs run out, up to 64 rounds of one quad, not the units)
-  constexpr uint64_t TS = 4;
-  const uint64_t tcap = (uint64_t)gridDim.x * 4;
-  const uint64_t ntail = nruns < tcap ? nruns : tcap;
-  const uint64_t nhead = nruns - ntail, nunits = nhead + TS * ntail;
-  auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
-    if (u >= nunits) return false;
-    const bool tl = u >= nhead;
-    const uint64_t k = tl ? nhead + (u - nhead) / TS : u;
-    const uint64_t tr = run_start(k);
-    const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
-    const uint64_t qr = (R + TS - 1) / TS, c0 = tl ? ((u - nhead) % TS) * qr : 0ull;
-    const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
-    const uint64_t t0 = tr + c0;
-    const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
-    uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t u = __shfl_up(inc, o, 64);
-      if ((int)lane >= o) inc += u;
-    }
-    uint32_t* pf = intoA ? pfA : pfB;
-    if (lane < nch) pf[lane + 1] = inc;
-    if (lane == 0) pf[0] = 0;
-    uint64_t* cdt = intoA ? cdA : cdB;
-    if (lane < nch) {
-      cdt[2 * lane] = cd[2 * (t0 + lane)];
-      cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
-    }
-    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
-    if (intoA) {
-      rtA = t0;
-      rchA = nch;
-      rnA = n;
-    } else {
-      rtB = t0;
-      rchB = nch;
-      rnB = n;
-    }
-    return true;
-  };
-  runs_left = load_run(true, blockIdx.x * 4ull + wv);  // the wave's first run, by its index
-
-  // a quad's current record (cv) and the round of it in hand: blocks [rlb, rlb + rnl) of its full
-  // 64-B blocks, rfin if the record ends in this round (its partial block in T), head if it is the
-  // record's first (its stored checksum in xst)
-  bool cv = false, rfin = false, head = false;
-  uint64_t cbase = 0, crl = 0, ct_t = 0;
-  uint32_t cnblk = 0, crem = 0, rlb = 0, rnl = 0, v = 0, cstored = 0, ct_r = 0, cw3 = 0;
-  // its next record: ns = 0 none, 1 slot row + chunk address loading (issued last iteration), 2 ready
-  uint32_t ns = 0;
-  uint64_t nt = 0;
-  uint32_t nr = 0;
-  u32x4 nrow = u32x4{0u, 0u, 0u, 0u};
-  uint64_t ncb = 0, nce = 0;  // its chunk's first byte and its file's end (from the run's LDS table)
-  // where the slot row is read from: every iteration reloads it (a quad that has claimed a record it
-  // cannot start yet reads the same slot row again; one with no record reads the safe line)
-  uint64_t carow = safe;
-  u32x4 XA[D], XB[D], TA = u32x4{0u, 0u, 0u, 0u}, TB = u32x4{0u, 0u, 0u, 0u};
-  uint32_t sA = 0, sB = 0;
-#pragma unroll
-  for (uint32_t d = 0; d < D; ++d) XA[d] = XB[d] = u32x4{0u, 0u, 0u, 0u};
-
-  uint64_t hst[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  (void)hst;
-  HST(h_all)
-#ifdef CASK_STAMPS
-  const uint64_t wid = blockIdx.x * 4ull + wv;
-  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-  // One iteration: round in hand in (Xm, Tm, xm), the next round into (Xi, Ti, xi): D full blocks
-  // in X, a record's partial last block in T, its stored checksum in x. False: done.
-  auto step = [&](u32x4 (&Xm)[D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
-    HCNT(6)
-    HST(h0)
-    if (ns == 1) ns = 2;
-    if (runs_left && !fullB) {  // (every lane takes part in the atomic, lane 0 adding 1)
-      const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
-      const bool got = load_run(false, (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old));
-      runs_left = got;
-      fullB = got;
-#ifdef CASK_STAMPS
-      if (!got && a.stamps && lane == 0 && wid < kStampWaves) a.stamps[kStampDry + wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-    }
-    // ---- plan this quad's next round: the rest of its record, or the next record from its slot row
-    // and its chunk's address (branch-free: every lane computes both and selects, so the counted
-    // waits see one path)
-    const bool cont = cv && !rfin;
-    const bool promote = !cont && ns == 2;
-    const uint32_t w3n = nrow.w, vszn = nrow.z;
-    const uint64_t bn = ncb + ((w3n >> 16) & 0x7FFFu);
-    const uint64_t en = nce;
-    const uint64_t rln = 18ull + (w3n & 0xFFFFu) + (vszn == 0xFFFFFFFFu ? 0ull : (uint64_t)vszn);
-    // (an UnexpectedEof row, cut by the file's end, has failed already: nothing to hash)
-    const bool round2 = cont || (promote && bn + rln <= en);
-    const uint32_t lb2 = cont ? rlb + D : 0u;
-    const uint64_t base2 = cont ? cbase : bn, rl2 = cont ? crl : rln;
-    const uint32_t nblk2 = cont ? cnblk : (uint32_t)((rln - 4) >> 6);
-    const uint32_t rb2 = cont ? crem : (uint32_t)((rln - 4) & 63);
-    const uint32_t left = nblk2 - lb2;
-    const uint32_t nl2 = round2 ? (left < D ? left : D) : 0u;
-    const bool fin2 = round2 && (left < D || (left == D && rb2 == 0));
-    const uint64_t pt = nt;
-    const uint32_t pr = nr, pw3 = w3n;
-    ns = promote ? 0u : ns;
-    HADD(1, h0)
-    HST(h1)
-    // ---- the stream's next records to the quads that have none (in lane order)
-    const bool want = ns == 0;
-    const unsigned long long wm = __ballot(qlead && want) & qmask;
-    const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
-    // every lane loads a slot row and a chunk address every iteration (the safe line when it takes
-    // no record): a load into a loop-carried register only under a branch is a copy after the
-    // merge, and the copy waits for every load in flight
-    // (branch-free for the lanes: the rank, chunk search and addresses are computed by every lane)
-    const uint32_t l0 = lane & ~3u;
-    const uint32_t myrank = (uint32_t)__builtin_popcountll(wm & (l0 ? (~0ull >> (64 - l0)) : 0ull));
-    const uint32_t rem = rnA - cur;
-    const bool up = myrank >= rem;
-    const uint32_t idx = up ? myrank - rem : cur + myrank;
-    const bool claimed = want && (up ? (fullB && idx < rnB) : true);
-    const uint32_t* pf = up ? pfB : pfA;
-    uint32_t lo = 0, hi = up ? rchB : rchA;  // the last chunk j with pf[j] <= idx
-#pragma unroll
-    for (int it = 0; it < 6; ++it) {  // (a run is at most 64 chunks)
-      const uint32_t mid = (lo + hi) >> 1;
-      const bool go = hi - lo > 1;
-      const bool le = go && pf[mid] <= idx;
-      lo = le ? mid : lo;
-      hi = go && !le ? mid : hi;
-    }
-    const uint64_t ntc = (up ? rtB : rtA) + lo;
-    const uint32_t nrc = idx - pf[lo];
-    nt = claimed ? ntc : nt;
-    nr = claimed ? nrc : nr;
-    const uint64_t* cdt = up ? cdB : cdA;
-    const uint64_t cbc = cdt[2 * lo], cec = cdt[2 * lo + 1];
-    ncb = claimed ? cbc : ncb;
-    nce = claimed ? cec : nce;
-    carow = claimed ? (uint64_t)(uintptr_t)(slots + (ntc * (uint64_t)a.slot_cap + nrc) * 4) : promote ? safe : carow;
-    uint64_t arow = carow;
-    if (nw) {
-      const uint32_t avail = rem + (fullB ? rnB : 0u);
-      const uint32_t used = nw < avail ? nw : avail;
-      if (used >= rem && fullB) {  // run A is handed out: the stream moves on to B
-        rtA = rtB;
-        rnA = rnB;
-        rchA = rchB;
-        uint32_t* t = pfA;
-        pfA = pfB;
-        pfB = t;
-        uint64_t* tc = cdA;
-        cdA = cdB;
-        cdB = tc;
-        fullB = false;
-        cur = used - rem;
-      } else {
-        cur += used;
-      }
-    }
-    ns = claimed ? 1u : ns;
-    // ---- issue the round: D blocks, the last partial block, the stored checksum (first round);
-    // every quad issues every load (the ones it does not need read the safe line). Every address
-    // of the iteration's loads is in a register before the first load issues: an address built
-    // after a load may be built in that load's destination, a write that waits for every load in
-    // flight.
-    const uint64_t bpa = base2 + 4 + 64ull * lb2 + 16ull * q;
-    uint64_t ya[D];
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) ya[d] = round2 && d < nl2 ? bpa + 64ull * d : safe;
-    // the record's partial last block, into T: the lanes of its full stripes load them, the lane of
-    // its partial stripe the record's last 16 bytes (ending where the record ends: no load reaches
-    // past the record into a line that the next record's quad reads at another time, nor past the
-    // file's end), the others the safe line
-    const bool tail2 = round2 && fin2 && rb2 != 0;
-    const uint32_t rq2 = rb2 >> 4;
-    const uint64_t tq = base2 + 4 + 64ull * nblk2 + 16ull * q;
-    uint64_t ta = tail2 && q < rq2 ? tq : tail2 && q == rq2 && (rb2 & 15) != 0 ? base2 + rl2 - 16 : safe;
-    uint64_t sa = round2 && !cont ? base2 : safe;
-    asm volatile("" : "+v"(arow), "+v"(sa), "+v"(ta));
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) asm volatile("" : "+v"(ya[d]));
-    nrow = *(const g_u32x4*)(uintptr_t)arow;
-#pragma unroll
-    for (uint32_t d = 0; d < D; ++d) Xi[d] = gld16g((const g_u8*)(uintptr_t)ya[d]);
-    Ti = gld16g((const g_u8*)(uintptr_t)ta);
-    xi = gld4g((const g_u8*)(uintptr_t)sa);
-    // the round in hand's last block and checksum are used from here on: nothing that reads them
-    // (nor the wait for them, one counted past this round's loads) is scheduled above the loads
-    asm volatile("" : "+v"(xm)::"memory");
-    HADD(2, h1)
-    HST(h2)
-    // ---- mix the round in hand
-    if (cv) {
-#pragma unroll
-      for (uint32_t d = 0; d < D; ++d) {
-        u32x4 x = Xm[d];
-        quad_transpose(x, q);
-        const uint32_t w = xround(xround(xround(xround(v, x.x), x.y), x.z), x.w);
-        v = d < rnl ? w : v;
-      }
-      if (head) cstored = xm;
-      HST(h3)
-      if (rfin) {  // the last partial block, merge, length, tail, avalanche (data.rs:185-198)
-        const uint32_t rem = crem >> 4, tb = crem & 15;
-        const u32x4 T = Tm;
-        u32x4 t = T;
-        quad_transpose(t, q);
-        uint32_t vv = v;
-        vv = rem > 0 ? xround(vv, t.x) : vv;
-        vv = rem > 1 ? xround(vv, t.y) : vv;
-        vv = rem > 2 ? xround(vv, t.z) : vv;
-        uint32_t m = rotl_var(vv, mrot);
-        m += quad_xor1(m);
-        m += quad_xor2(m);
-        const uint64_t hl = crl - 4;
-        uint32_t h = (hl >= 16 ? m : P5) + (uint32_t)hl;
-        const int src = (int)((lane & ~3u) | rem);
-        u32x4 tw;
-        tw.x = (uint32_t)__shfl((int)T.x, src, 64);
-        tw.y = (uint32_t)__shfl((int)T.y, src, 64);
-        tw.z = (uint32_t)__shfl((int)T.z, src, 64);
-        tw.w = (uint32_t)__shfl((int)T.w, src, 64);
-        // the partial stripe's lane loaded the record's last 16 bytes: the stripe from byte 16 - tb on
-        tw = shr_bytes(tw, tb ? 16u - tb : 0u);
-        const uint32_t n4 = tb >> 2, n1 = tb & 3;
-        h = n4 > 0 ? tail4(h, tw.x) : h;
-        h = n4 > 1 ? tail4(h, tw.y) : h;
-        h = n4 > 2 ? tail4(h, tw.z) : h;
-        const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
-        h = n1 > 0 ? tail1(h, lw & 0xFFu) : h;
-        h = n1 > 1 ? tail1(h, (lw >> 8) & 0xFFu) : h;
-        h = n1 > 2 ? tail1(h, (lw >> 16) & 0xFFu) : h;
-        h = avalanche(h);
-        if (h != cstored && qlead) {  // InvalidChecksum{expected: stored, found: h} (data.rs:193-198)
-          slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
-          atomicMin(&a.cerr[ct_t], ct_r);
-        }
-      }
-      HADD(4, h3)
-    }
-    HADD(3, h2)
-    // ---- state for the next iteration
-    if (cont) {
-      rlb = lb2;
-      rnl = nl2;
-      rfin = fin2;
-      head = false;
-    } else {
-      cv = promote && round2;
-      cbase = base2;
-      crl = rl2;
-      cnblk = nblk2;
-      crem = rb2;
-      rlb = 0;
-      rnl = nl2;
-      rfin = fin2;
-      head = true;
-      v = vinit;
-      ct_t = pt;
-      ct_r = pr;
-      cw3 = pw3;
-    }
-    const bool stream_left = rnA != cur || (fullB && rnB != 0) || runs_left;
-    // (uniform by construction, and made visibly so: a loop exit the compiler must treat as divergent
-    // becomes an exec-mask loop in which the exit after the first step also reaches the loop header,
-    // so the header's waits count the first step's loads as possibly in flight and wait for them)
-    return __builtin_amdgcn_readfirstlane((int)(stream_left || __any(cv || ns != 0))) != 0;
-  };
-  // (one exit, after the second step: a wave that finishes in the first step runs the second as a
-  // no-op — nothing left to claim or load but safe lines — so that no path from the middle of the
-  // body reaches the loop header with the first step's loads in flight)
-  for (;;) {
-    (void)step(XA, TA, sA, XB, TB, sB);
-    if (!step(XB, TB, sB, XA, TA, sA)) break;
-  }
-#ifdef CASK_STAMPS
-  HADD(0, h_all)
-  if (a.stamps && lane == 0)
-    for (int i = 0; i < 8; ++i) atomicAdd(&a.stamps[8 + i], (unsigned long long)hst[i]);
-  if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[17 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-}
-
-
-// ---------------------------------------------------------------------------------------------
-// k_run_hash_ln: the same pass with whole 128-B lines per load instruction, nontemporal. The wave's
-// 16 quads are 8 pairs (lanes 8o..8o+7: quad 2o "low", h = 0, and quad 2o + 1 "high", h = 1). A
-// round of a record is its lines [La + 1 KiB i, La + 1 KiB (i + 1)) (La: the line of the body's
-// first byte), so no line is read by two rounds of one record. Instruction 2m loads line m of the
-// low quad's round (the low quad's lanes its first 64 B, the high quad's lanes its second 64 B) and
-// instruction 2m + 1 line m of the high quad's round (high lanes its first 64 B, low lanes its
-// second): every instruction reads whole lines — nontemporal loads then fetch each line once (half
-// lines per instruction fetch a line twice under that policy) — and each quad holds one 64-B block
-// of its line in its own lanes and gets the other from its partner's (lane ^ 4, ds_swizzle). A
-// body dword is funneled out of two line dwords at the body's byte offset (v_alignbyte; the lower
-// one from the previous lane by DPP, lane 0's carried from the previous block) and masked against
-// the record's full stripes; lane q keeps the stripe accumulator of its dword position.
+// Loads: whole 128-B lines per instruction, nontemporal. The quads are pairs across the two halves
+// of the wave (quad j of lanes 0..31 with quad j of lanes 32..63). A round of a record is its lines
+// [La + 1 KiB i, La + 1 KiB (i + 1)) (La: the line of the body's first byte), so no line is read by
+// two rounds of one record. Instruction 2m loads line m of the lower quad's round, 2m + 1 line m of
+// the upper quad's, the lower half of the wave a line's first 64 B and the upper half its second:
+// every instruction reads whole lines — nontemporal loads then fetch each line once (a quad's 64 B
+// per instruction fetched a line twice under that policy, and rounds starting mid-line fetched the
+// line at each round boundary twice under the default one: 1.11x the log bytes) — and one
+// v_permlane32_swap per dword hands each half its own line. A body dword is funneled out of two line
+// dwords at the body's byte offset (v_alignbyte; the lower one from the previous lane by DPP, lane
+// 0's carried from the previous block), quad_transpose_dpp gives lane q its dword position's words,
+// and the words outside the record's full stripes are masked; lane q keeps the stripe accumulator of
+// its dword position ((q - cM - 1) mod 4).
+//
+// The pipeline: iteration i issues round i (2 x 8 line loads, the record's last partial stripe, the
+// stored checksum of a record's first round) and then mixes round i - 1. Every quad issues every
+// one of those loads (past a round's last line a quad reads that line again; a quad with nothing to
+// load reads one safe line), and the two rounds live in two register sets used in turn (the loop
+// body twice, no copies), so the compiler's counted waits wait for round i - 1 only and round i
+// stays in flight while it is mixed. The loads whose results the next iteration's bookkeeping needs
+// (slot rows, chunk addresses, the next run's counts) are issued before the round's.
 // ---------------------------------------------------------------------------------------------
 // v_permlane32_swap: lanes 32..63 of a trade places with lanes 0..31 of b — afterwards a holds the
 // lower halves of both, b the upper halves
@@ -613,7 +279,7 @@ __device__ __forceinline__ u32x4 gld16nt(uint64_t p) {
   return __builtin_nontemporal_load((gcu32x4*)(uintptr_t)p);
 }
 
-__global__ __launch_bounds__(256) void k_run_hash_ln(ScanArgs a) {
+__global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   constexpr uint32_t D = 8;    // lines of a record per round
   constexpr uint32_t RW = 256; // dwords per round
   constexpr uint32_t RT = kMaxRun + 1;
@@ -632,7 +298,13 @@ __global__ __launch_bounds__(256) void k_run_hash_ln(ScanArgs a) {
   const unsigned long long qmask = 0x1111111111111111ull;
   const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;  // (a 128-B aligned allocation: its first line)
 
-  // the wave's record stream: as k_run_hash
+  // The wave's record stream (uniform): two runs, A (records are handed out from it, at cursor
+  // cur) and B (the next one, once loaded: fullB), each as its first chunk, chunk count and row
+  // count. B is refilled from the claim counter as soon as it is free. (Plain variables, not arrays
+  // indexed by the slot: those go to scratch memory, whose loads wait for every load.) Units of
+  // work: the runs in order, except that the last grid's worth of runs is handed out in quarters,
+  // so that the waves run dry within about a quarter of a run of each other (round 5: eighths or
+  // sixteenths no faster).
   uint64_t rtA = 0, rtB = 0;
   uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
   bool fullB = false;
@@ -715,7 +387,9 @@ __global__ __launch_bounds__(256) void k_run_hash_ln(ScanArgs a) {
       if (!got && a.stamps && lane == 0 && wid < kStampWaves) a.stamps[kStampDry + wid] = __builtin_amdgcn_s_memrealtime();
 #endif
     }
-    // ---- plan this quad's next round (branch-free, as k_run_hash)
+    // ---- plan this quad's next round: the rest of its record, or the next record from its slot row
+    // and its chunk's address (branch-free: every lane computes both and selects, so the counted
+    // waits see one path)
     const bool cont = cv && !rfin;
     const bool promote = !cont && ns == 2;
     const uint32_t w3n = nrow.w, vszn = nrow.z;
@@ -736,7 +410,8 @@ __global__ __launch_bounds__(256) void k_run_hash_ln(ScanArgs a) {
     const uint64_t pt = nt;
     const uint32_t pr = nr, pw3 = w3n;
     ns = promote ? 0u : ns;
-    // ---- the stream's next records to the quads that have none (as k_run_hash)
+    // ---- the stream's next records to the quads that have none (in lane order; branch-free for
+    // the lanes: every lane loads a slot row every iteration, the safe line when it takes none)
     const bool want = ns == 0;
     const unsigned long long wm = __ballot(qlead && want) & qmask;
     const uint32_t nw = (uint32_t)__builtin_popcountll(wm);
@@ -981,50 +656,21 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(k_walk_chase, dim3(grid), dim3(tpb), 0, (hipStream_t)stream, a, a.files);
 }
 
-template <uint32_t D>
-static void run_hash_at(const ScanArgs& a, uint64_t nruns, hipStream_t s) {
-  // A persistent grid of exactly the resident workgroups: a workgroup beyond them would start only
-  // as the first ones finish, holding its first run (claimed by block index) until the end.
-  // CASK_HASH_WAVES (tuning knob) overrides the waves per CU.
+// A persistent grid of exactly the resident workgroups: a workgroup beyond them would start only as
+// the first ones finish, holding its first run (claimed by block index) until the end.
+void launch_run_hash(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
+  if (!nruns) return;
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (cask_knobs::tune("CASK_HASH_WAVES")) per_cu = atoi(cask_knobs::tune("CASK_HASH_WAVES"));
-    else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash<D>, 256, 0) == hipSuccess && nb > 0)
-      per_cu = 4 * nb;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash, 256, 0) == hipSuccess && nb > 0) per_cu = 4 * nb;
     if (per_cu <= 0) per_cu = 8;
   }
   uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
   if (waves > nruns) waves = nruns;
-  hipLaunchKernelGGL((k_run_hash<D>), dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
-}
-
-void launch_run_hash(const ScanArgs& a, int depth, void* stream) {
-  if (!a.total_chunks) return;
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
-  if (!nruns) return;
-  hipStream_t s = (hipStream_t)stream;
-  // k_run_hash_ln: whole lines per load instruction, nontemporal (CASK_HASH_LINES=0, a tuning knob:
-  // k_run_hash, a quad's 64 B per instruction)
-  static const bool lines = !(cask_knobs::tune("CASK_HASH_LINES") && atoi(cask_knobs::tune("CASK_HASH_LINES")) == 0);
-  if (lines) {
-    static int per_cu = 0;
-    if (!per_cu) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash_ln, 256, 0) == hipSuccess && nb > 0) per_cu = 4 * nb;
-      if (per_cu <= 0) per_cu = 8;
-    }
-    uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
-    if (waves > nruns) waves = nruns;
-    hipLaunchKernelGGL(k_run_hash_ln, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, s, a);
-    return;
-  }
-  if (depth == 16)  // (18 blocks, the most that keep 2 waves per SIMD: no faster, profiles/r04_ab_variants.txt)
-    run_hash_at<16>(a, nruns, s);
-  else if (depth == 4)
-    run_hash_at<4>(a, nruns, s);
-  else
-    run_hash_at<8>(a, nruns, s);
+  hipLaunchKernelGGL(k_run_hash, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
 }
 
 }  // namespace cask_dev

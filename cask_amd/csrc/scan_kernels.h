@@ -248,9 +248,9 @@ void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: hint bod
 void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each walk run's speculative start
 // k_walk_hash.hip: k_walk_chase (a lane per run of a.run chunks chases the record
 // headers: slot rows, chunk table, cdesc), then k_run_hash (a wave per claimed run, a quad per record:
-// every record hashed from HBM; depth = 64-B blocks per quad in flight)
+// every record hashed from HBM, whole 128-B lines per load instruction)
 void launch_walk_chase(const ScanArgs& a, void* stream);
-void launch_run_hash(const ScanArgs& a, int depth, void* stream);
+void launch_run_hash(const ScanArgs& a, void* stream);
 // after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
 void launch_hash_fix(const ScanArgs& a, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)

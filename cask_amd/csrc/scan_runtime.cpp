@@ -647,8 +647,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   // hash on HBM bandwidth). Long records hashed before k_finish mark their rows like any failed
   // check (slot bad bit, cerr), so k_finish sees them.
   bool long_pre = false;
-  // CASK_HASH_D (tuning knob): 64-B blocks in flight per quad of the hashing kernel
-  static const int hash_depth = cask_knobs::tune("CASK_HASH_D") ? atoi(cask_knobs::tune("CASK_HASH_D")) : 16;  // (16: 5 % faster than 8)
   bool fused = false;
   bool fin_done = false;  // k_finish already launched (beside the hash)
   if (mixed) {  // the walk-mode runs (split path), then the chunk-mode runs, then k_finish for all
@@ -665,7 +663,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_walk_chase(aw, st);
     L("k_walk_chase");
     H(hipEventRecord(c->ev[7], st));
-    launch_run_hash(aw, hash_depth, st);
+    launch_run_hash(aw, st);
     L("k_run_hash");
     ScanArgs ac = a;
     ac.runs = c->mruns.as<uint64_t>() + c->mixed_nw;
@@ -689,7 +687,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     launch_walk_chase(a, st);
     L("k_walk_chase");
     H(hipEventRecord(c->ev[7], st));
-    launch_run_hash(a, hash_depth, st);
+    launch_run_hash(a, st);
     L("k_run_hash");
     // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
     // starts): on a side stream it runs in the slots the hash's last waves leave, and k_hash_fix
