@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--cpu-sample-files", type=int, default=2, help="configs[2] files timed by the CPU baseline")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-resident (H2D+D2H) measurement")
     ap.add_argument("--no-cfg1", action="store_true", help="skip the secondary configs[1] measurement")
+    ap.add_argument("--no-cold", action="store_true",
+                    help="skip cold_call_ms (its calls over one file are small launches of the same kernels: "
+                         "a profiled run without them has per-kernel averages over the full-size steps only)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the keydir gather + fold after the loop")
     ap.add_argument("--no-cfg5", action="store_true",
                     help="N>1: skip the cfg5 shard (290-B records) scan + key-hash partitioned keydir")
@@ -424,7 +427,7 @@ def main():
     # table already on the device — so a call over another set in between makes the next full call
     # pay both again. Reported beside `value`, never in it.
     cold = []
-    for _ in range(3):
+    for _ in range(0 if args.no_cold else 3):
         ctx.scan_device(views[:1], rows)
         torch.cuda.synchronize(dev)
         t_c = time.perf_counter()
@@ -453,7 +456,7 @@ def main():
              # SURVEY §8d's definition: device time from the first to the last kernel of a step
              # (HIP events), per GPU; `value` above is the wall clock, host gap included
              "device_gibps_per_gpu": bytes_per_step / (breakdown["pipeline_ms"] * 1e-3) / 2 ** 30,
-             "cold_call_ms": sorted(cold)[len(cold) // 2],
+             "cold_call_ms": sorted(cold)[len(cold) // 2] if cold else None,
              # device scratch the context holds for this workload (chunk table, slot rows, call
              # blocks, repair state), beside the log bytes it scans
              "scratch_bytes": ctx.scratch_bytes(),

@@ -484,11 +484,12 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     // half its second (lanes j and j + 32 have the same q)
     const uint64_t lof = 64ull * h + 16ull * q;
     const uint64_t rb0 = (((uint64_t)c0 << 32) | a0) + lof, rb1 = (((uint64_t)c1 << 32) | a1) + lof;
+    const uint32_t e0 = 128 * n0, e1 = 128 * n1;  // the last line's offset
     uint64_t ya[2 * D];
 #pragma unroll
     for (uint32_t m = 0; m < D; ++m) {
-      ya[2 * m] = rb0 + 128ull * (m < n0 ? m : n0);
-      ya[2 * m + 1] = rb1 + 128ull * (m < n1 ? m : n1);
+      ya[2 * m] = rb0 + (uint64_t)(128 * m < e0 ? 128 * m : e0);
+      ya[2 * m + 1] = rb1 + (uint64_t)(128 * m < e1 ? 128 * m : e1);
     }
     asm volatile("" : "+v"(arow), "+v"(sa), "+v"(ta));
 #pragma unroll

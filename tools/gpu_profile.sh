@@ -17,11 +17,14 @@ if [ -z "$SKIP_BENCH" ]; then
   TAILN=1 step bench_full 600 python bench.py
 fi
 export TMPDIR=/tmp
-B="$R/bench.py --steps ${PSTEPS:-20} --warmup ${PWARM:-3} --no-cpu-baseline --no-e2e --no-cfg1"
+B="$R/bench.py --steps ${PSTEPS:-20} --warmup ${PWARM:-3} --no-cpu-baseline --no-e2e --no-cfg1 --no-cold"
 rm -rf "$R/gpurun_out/prof_$TAG"
 TAILN=1 step prof_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG/kt" -o kt --output-format csv -- python3 $B
 step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_$TAG/fetch" -o fetch --output-format csv -- python3 $B
 step prof_write 600 rocprofv3 --pmc WRITE_SIZE -d "$R/gpurun_out/prof_$TAG/write" -o write --output-format csv -- python3 $B
+# memory-side read requests by size: FETCH_SIZE x2 under-reports nontemporal whole-line reads (round 5:
+# 31.5 GB for k_run_hash's 34.4 GB of log bytes), the request count does not
+step prof_rdreq 600 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum -d "$R/gpurun_out/prof_$TAG/rdreq" -o rdreq --output-format csv -- python3 $B
 if [ -n "$CFG2" ]; then  # configs[2] (32 GiB Zipf): the same three passes over tools/bench_configs.py cfg3
   C="$R/tools/bench_configs.py cfg3 --steps 2"
   rm -rf "$R/gpurun_out/prof_${TAG}_cfg2"
