@@ -520,6 +520,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       e_lo = none ? 64 : e_lo;
       e_hi = none ? -1 : e_hi;
       const uint32_t span = (uint32_t)(e_hi - e_lo);
+      const bool hi1 = e_hi & 1, hi2 = e_hi & 2;  // (e_hi % 4 = 3: that block is whole)
 #pragma unroll
       for (uint32_t m = 0; m < D; ++m) {
         const u32x4 xa = Xm[2 * m], xb = Xm[2 * m + 1];
@@ -536,13 +537,22 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
           carry = dv;
           u32x4 x = u32x4{fun(p0, gg.x, csb), fun(gg.x, gg.y, csb), fun(gg.y, gg.z, csb), fun(gg.z, gg.w, csb)};
           quad_transpose_dpp(x);
+          if (d < 2) {  // (a first round's first stripe can start in these: each word masked)
 #pragma unroll
-          for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t el = 4 * d + k;
-            const bool ok = el < 8 ? (uint32_t)((int32_t)el - e_lo) <= span : (int32_t)el <= e_hi;
-            uint32_t w = xround(v, x[k]);
-            asm volatile("" : "+v"(w));
-            v = ok ? w : v;
+            for (uint32_t k = 0; k < 4; ++k) {
+              const uint32_t el = 4 * d + k;
+              const bool ok = (uint32_t)((int32_t)el - e_lo) <= span;
+              uint32_t w = xround(v, x[k]);
+              asm volatile("" : "+v"(w));
+              v = ok ? w : v;
+            }
+          } else {  // the whole block, or its first e_hi % 4 + 1 words (the record's last full stripe's
+                    // block), or none of it
+            uint32_t w1 = xround(v, x.x), w2 = xround(w1, x.y), w3 = xround(w2, x.z), w4 = xround(w3, x.w);
+            asm volatile("" : "+v"(w1), "+v"(w2), "+v"(w3), "+v"(w4));
+            const uint32_t part = hi2 ? w3 : hi1 ? w2 : w1;
+            const int32_t e0 = (int32_t)(4 * d);
+            v = e0 + 3 <= e_hi ? w4 : e0 <= e_hi ? part : v;
           }
         }
       }
@@ -554,7 +564,8 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       m += quad_xor1(m);
       m += quad_xor2(m);
       uint32_t hh = (chl >= 16 ? m : P5) + chl;
-      const u32x4 tw = shr_bytes(Tm, tclamp ? ctsh : 0u);
+      u32x4 tw = Tm;
+      if (__any(tclamp)) tw = shr_bytes(Tm, tclamp ? ctsh : 0u);  // (rare: the file ends in the tail's 16 B)
       const uint32_t n4 = tb >> 2, n1 = tb & 3;
       hh = n4 > 0 ? tail4(hh, tw.x) : hh;
       hh = n4 > 1 ? tail4(hh, tw.y) : hh;
