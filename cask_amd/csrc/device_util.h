@@ -326,12 +326,13 @@ __device__ __forceinline__ void quad_transpose(u32x4& v, uint32_t q) {
   if (b0) { v.x = r0; v.z = r1; } else { v.y = r0; v.w = r1; }
 }
 // The same transpose, each stage as four v_cndmask_b32_dpp (word = the lane's bit set ? its own word :
-// the partner's, the DPP operand): 8 vector instructions instead of 16 (k_run_hash_ln).
+// the partner's, the DPP operand): 8 vector instructions instead of 16 (k_run_hash). The two
+// s_mov to vcc before each stage are the two wait states a DPP read of a VGPR the previous vector
+// instruction wrote needs (no s_nop).
 __device__ __forceinline__ void quad_transpose_dpp(u32x4& v) {
   uint32_t x1, y1, z1, w1, x2, y2, z2, w2;
   // stage 1, partner q ^ 2 (vcc: lanes with q & 2): off-diagonal 2x2 blocks swapped
   asm volatile(
-      "s_nop 1\n"
       "s_mov_b32 vcc_lo, 0xcccccccc\n"
       "s_mov_b32 vcc_hi, 0xcccccccc\n"
       "v_cndmask_b32_dpp %2, %4, %6, vcc quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf\n"
@@ -344,7 +345,6 @@ __device__ __forceinline__ void quad_transpose_dpp(u32x4& v) {
       : "vcc");
   // stage 2, partner q ^ 1 (vcc: lanes with q & 1): the 2x2 blocks transposed
   asm volatile(
-      "s_nop 1\n"
       "s_mov_b32 vcc_lo, 0xaaaaaaaa\n"
       "s_mov_b32 vcc_hi, 0xaaaaaaaa\n"
       "v_cndmask_b32_dpp %1, %4, %5, vcc quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf\n"
