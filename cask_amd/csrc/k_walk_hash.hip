@@ -285,6 +285,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   constexpr uint32_t RT = kMaxRun + 1;
   __shared__ uint32_t s_pf[4][2][RT];
   __shared__ uint64_t s_cd[4][2][2 * kMaxRun];
+  __shared__ uint32_t s_fq[4][64][12];  // per wave: records whose checksums are to be finished
   const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6, h = lane >> 5;
   const bool qlead = q == 0;
   const uint64_t R = a.run;
@@ -372,6 +373,31 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t sA = 0, sB = 0;
 #pragma unroll
   for (uint32_t d = 0; d < 2 * D; ++d) XA[d] = XB[d] = u32x4{0u, 0u, 0u, 0u};
+  // the queued checksums (s_fq): lane i finishes record i (merged accumulators + length, tail bytes,
+  // their count, the stored checksum, where its slot row is) and marks a mismatch
+  uint32_t fq_n = 0;  // (uniform)
+  auto fq_flush = [&]() __attribute__((always_inline)) {
+    if (lane < fq_n) {
+      const uint32_t* e = s_fq[wv][lane];
+      uint32_t hh = e[0];
+      const u32x4 tw = u32x4{e[1], e[2], e[3], e[4]};
+      const uint32_t tb = e[5], n4 = tb >> 2, n1 = tb & 3;
+      hh = n4 > 0 ? tail4(hh, tw.x) : hh;
+      hh = n4 > 1 ? tail4(hh, tw.y) : hh;
+      hh = n4 > 2 ? tail4(hh, tw.z) : hh;
+      const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
+      hh = n1 > 0 ? tail1(hh, lw & 0xFFu) : hh;
+      hh = n1 > 1 ? tail1(hh, (lw >> 8) & 0xFFu) : hh;
+      hh = n1 > 2 ? tail1(hh, (lw >> 16) & 0xFFu) : hh;
+      hh = avalanche(hh);
+      if (hh != e[6]) {  // InvalidChecksum{expected: stored, found: hh} (data.rs:193-198)
+        const uint64_t t = (uint64_t)e[8] | ((uint64_t)e[9] << 32);
+        const uint32_t r = e[7];
+        slots[(t * (uint64_t)a.slot_cap + r) * 4 + 3] = e[10] | kSlotBad;
+        atomicMin(&a.cerr[t], r);
+      }
+    }
+  };
 #ifdef CASK_STAMPS
   const uint64_t wid = blockIdx.x * 4ull + wv;
   if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[16 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
@@ -558,26 +584,36 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       }
     }
     if (cv && head) cstored = xm;
-    if (cv && rfin) {  // merge, length, tail, avalanche (data.rs:185-198)
-      const uint32_t tb = chl & 15;
+    // ---- a record that ends with this round: its stripe accumulators merged in the quad, the rest of
+    // its checksum (data.rs:185-198: length, tail bytes, avalanche, the compare) queued per wave and
+    // finished up to 64 at once, a record per lane (a few of the 16 quads finish a record in an
+    // iteration, and per quad every lane of the wave would run those steps every iteration)
+    const bool fin_now = cv && rfin;
+    const unsigned long long fm = __ballot(fin_now && qlead) & qmask;
+    if (fm) {
       uint32_t m = rotl_var(v, mrot);
       m += quad_xor1(m);
       m += quad_xor2(m);
-      uint32_t hh = (chl >= 16 ? m : P5) + chl;
       u32x4 tw = Tm;
-      if (__any(tclamp)) tw = shr_bytes(Tm, tclamp ? ctsh : 0u);  // (rare: the file ends in the tail's 16 B)
-      const uint32_t n4 = tb >> 2, n1 = tb & 3;
-      hh = n4 > 0 ? tail4(hh, tw.x) : hh;
-      hh = n4 > 1 ? tail4(hh, tw.y) : hh;
-      hh = n4 > 2 ? tail4(hh, tw.z) : hh;
-      const uint32_t lw = n4 == 0 ? tw.x : n4 == 1 ? tw.y : n4 == 2 ? tw.z : tw.w;
-      hh = n1 > 0 ? tail1(hh, lw & 0xFFu) : hh;
-      hh = n1 > 1 ? tail1(hh, (lw >> 8) & 0xFFu) : hh;
-      hh = n1 > 2 ? tail1(hh, (lw >> 16) & 0xFFu) : hh;
-      hh = avalanche(hh);
-      if (hh != cstored && qlead) {  // InvalidChecksum{expected: stored, found: hh} (data.rs:193-198)
-        slots[(ct_t * (uint64_t)a.slot_cap + ct_r) * 4 + 3] = cw3 | kSlotBad;
-        atomicMin(&a.cerr[ct_t], ct_r);
+      if (__any(fin_now && tclamp)) tw = shr_bytes(Tm, tclamp ? ctsh : 0u);  // (rare: the file ends in the tail's 16 B)
+      if (fin_now && qlead) {
+        uint32_t* e = s_fq[wv][fq_n + (uint32_t)__builtin_popcountll(fm & (lane ? (~0ull >> (64 - lane)) : 0ull))];
+        e[0] = (chl >= 16 ? m : P5) + chl;
+        e[1] = tw.x;
+        e[2] = tw.y;
+        e[3] = tw.z;
+        e[4] = tw.w;
+        e[5] = chl & 15;
+        e[6] = cstored;
+        e[7] = ct_r;
+        e[8] = (uint32_t)ct_t;
+        e[9] = (uint32_t)(ct_t >> 32);
+        e[10] = cw3;
+      }
+      fq_n += (uint32_t)__builtin_popcountll(fm);
+      if (fq_n > 64 - 16) {
+        fq_flush();
+        fq_n = 0;
       }
     }
     // ---- state for the next iteration
@@ -616,6 +652,7 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     (void)step(XA, TA, sA, XB, TB, sB);
     if (!step(XB, TB, sB, XA, TA, sA)) break;
   }
+  if (fq_n) fq_flush();
 #ifdef CASK_STAMPS
   if (a.stamps && lane == 0 && wid < kStampWaves) a.stamps[17 + 2 * wid] = __builtin_amdgcn_s_memrealtime();
 #endif
