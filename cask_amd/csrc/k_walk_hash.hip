@@ -303,16 +303,16 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   // cur) and B (the next one, once loaded: fullB), each as its first chunk, chunk count and row
   // count. B is refilled from the claim counter as soon as it is free. (Plain variables, not arrays
   // indexed by the slot: those go to scratch memory, whose loads wait for every load.) Units of
-  // work: the runs in order, except that the last grid's worth of runs is handed out in quarters,
-  // so that the waves run dry within about a quarter of a run of each other (round 5: eighths or
-  // sixteenths no faster).
+  // work: the runs in order, except that the last grid's worth of runs is handed out in eighths, so
+  // that the waves run dry within about an eighth of a run of each other (A/B: quarters 0.3 % and
+  // sixteenths 0.7 % slower, halves 1.2 %; eighths over the last two grids' worth 0.3 %).
   uint64_t rtA = 0, rtB = 0;
   uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
   bool fullB = false;
   uint32_t cur = 0;
   bool runs_left = true;
   auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
-  constexpr uint64_t TS = 4;
+  constexpr uint64_t TS = 8;
   const uint64_t tcap = (uint64_t)gridDim.x * 4;
   const uint64_t ntail = nruns < tcap ? nruns : tcap;
   const uint64_t nhead = nruns - ntail, nunits = nhead + TS * ntail;
