@@ -24,7 +24,8 @@ pytestmark = pytest.mark.gpu
 def scan_mode(request, monkeypatch):
     """Every test here runs three times: the mode the library picks (k_scan_chunks for these mostly
     short records — with the short 1,008-B halo when the file heads hold short records — and the
-    walk for the long-record cases), the walk mode forced (k_walk_runs), and the chunk scan forced
+    walk for the long-record cases), the walk mode forced (k_walk_search, k_walk_chase, k_run_hash),
+    and the chunk scan forced
     with the wide 4,080-B halo (there host-resident inputs and rows also go through the pinned
     staging ring, CASK_STAGE_MIN=0)."""
     if request.param == "auto":
@@ -392,6 +393,42 @@ def test_long_record_hash_every_length_residue(gpu_ctx):
     cnt = gpu_ctx.last_counters()
     assert cnt["long_records"] > 0 or cnt["walk_mode"] >= 1, cnt
     assert res.error is not None
+
+
+def test_line_rounds_every_offset_and_length(gpu_ctx):
+    """k_run_hash reads a record in rounds of whole 128-B lines from the line of its body's first
+    byte and funnels the body out of them (walk mode): bodies starting at every offset in a line
+    (each residue mod 128 many times), body lengths around the 16-B stripe, 64-B block, 128-B line and
+    1-KiB round boundaries, stored checksums that start in the line before the body's, a third of
+    the records corrupted in the body, the stored checksum or the tail, and files ending inside the
+    last record's 16-B tail granule — row for row as the oracle."""
+    rng = random.Random(71)
+    lens = [14, 15, 16, 17, 31, 32, 33, 63, 64, 65, 127, 128, 129, 1007, 1008, 1009, 1023, 1024, 1025,
+            1039, 1040, 1041, 2047, 2048, 2049, 3071, 3072, 3073, 4095, 4096, 4097]
+    files, seq = [], 1
+    for f in range(3):
+        recs = []
+        for _ in range(900):
+            body = rng.choice(lens) if rng.random() < 0.7 else rng.randrange(14, 9000)
+            ksz = rng.randrange(0, 24)
+            vsz = max(0, body - 14 - ksz)  # body = 14 + ksz + vsz (header past the checksum + key + value)
+            rec = bytearray(R.entry_new(seq, rng.randbytes(ksz), rng.randbytes(vsz)).write_bytes())
+            seq += 1
+            x = rng.random()
+            if x < 0.11:
+                rec[4 + rng.randrange(len(rec) - 4)] ^= 1 << rng.randrange(8)  # body
+            elif x < 0.22:
+                rec[rng.randrange(4)] ^= 0x01  # stored checksum
+            elif x < 0.33:
+                rec[-1 - rng.randrange(min(15, len(rec) - 1))] ^= 0x80  # the tail bytes
+            recs.append(bytes(rec))
+        files.append(b"".join(recs))
+    # the last file cut inside its last record's tail: an UnexpectedEof row at the end
+    files.append(files[0][: len(files[0]) - 7])
+    res = check_against_oracle(gpu_ctx, files, device=True)
+    assert res.error is not None
+    starts = np.concatenate([O.scan(b)["pos"] for b in files[:3]]).astype(np.int64)
+    assert len(set(((starts + 4) % 128).tolist())) == 128  # every body offset in a line was exercised
 
 
 def test_records_past_walk_hash_limit(gpu_ctx):
