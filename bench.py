@@ -228,6 +228,18 @@ def time_loop(torch, dev, run, timings, steps, barrier, dist, backend):
     return elapsed, [[float(x) for x in t] for t in tbuf]
 
 
+def secondary(extra: dict, key: str, fn):
+    """A measurement reported beside the metric: its result goes to extra[key]; an exception does not
+    end the run — it is reported as extra[key + "_error"] and the caller goes on (restoring whatever
+    it dropped for the measurement's memory) to print the line."""
+    try:
+        extra[key] = fn()
+        return True
+    except Exception as e:  # noqa: BLE001 - reported in the line
+        extra[key + "_error"] = f"{type(e).__name__}: {e}"[:300]
+        return False
+
+
 def cfg1_secondary(ctx, torch, dev, steps):
     """configs[1] (8 x 1 GiB of fixed 290-B records): the regular-chunk path, for reference."""
     from cask_amd.workloads import cfg2_files
@@ -603,17 +615,13 @@ def main():
         # (the workload is kept by `zf` whatever happens inside; only the generator's views are dropped
         # for the shard's memory, and the rows are rebuilt after it, failed or not)
         zf = (files, vsz, rl)
-        try:
-            res = None
-            files = vsz = rl = None
-            rows = None
-            torch.cuda.empty_cache()
-            extra["cfg5_shard"] = cfg5_shard_secondary(ctx, torch, dev, rank, world, dist, args.dist_backend,
-                                                       args.same_device, max(3, min(args.steps, 10)), barrier)
-        except Exception as e:  # noqa: BLE001 - reported in the line
-            extra["cfg5_shard_error"] = f"{type(e).__name__}: {e}"[:300]
-        finally:
-            files, vsz, rl = zf
+        res = None
+        files = vsz = rl = None
+        rows = None
+        torch.cuda.empty_cache()
+        secondary(extra, "cfg5_shard", lambda: cfg5_shard_secondary(
+            ctx, torch, dev, rank, world, dist, args.dist_backend, args.same_device, max(3, min(args.steps, 10)), barrier))
+        files, vsz, rl = zf
         try:
             res = ctx.scan_device(views, ctx.alloc_rows(n + 16))
         except Exception as e:  # noqa: BLE001 - reported in the line
