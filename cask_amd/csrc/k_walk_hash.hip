@@ -404,7 +404,11 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
 #endif
   auto step = [&](u32x4 (&Xm)[2 * D], u32x4& Tm, uint32_t& xm, u32x4 (&Xi)[2 * D], u32x4& Ti, uint32_t& xi) __attribute__((always_inline)) -> bool {
     if (ns == 1) ns = 2;
-    if (runs_left && !fullB) {
+    // the next unit is claimed once the current one has at most 16 records left to hand out (the
+    // stream still never waits: B is loaded an iteration before it is needed), so that a wave holds
+    // one unit's worth of records, not two, when the units run out (A/B: 0.5 % faster than claiming
+    // as soon as B is free)
+    if (runs_left && !fullB && rnA - cur <= 16) {
       const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
       const bool got = load_run(false, (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old));
       runs_left = got;
