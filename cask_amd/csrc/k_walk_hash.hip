@@ -143,11 +143,50 @@ __device__ __forceinline__ void seg_setup(const ScanArgs& a, const FileDesc* fil
 // run as [t0, tm) and then [tm, t1) from the first range's exit writes exactly what one range
 // [t0, t1) writes: the chain is one walk either way.
 
+// A run among the last a.hash_ntail (k_run_hash's tail runs) also marks, per piece of it
+// (kTailSplit per run), which of the piece's records are at least kTailLong bytes long: bit i of the
+// piece's kTailBitWords words in a.tbits, record i counted from the piece's first chunk.
+struct TailBits {
+  bool on = false;
+  uint64_t r0 = 0, unit0 = 0;  // the run's first chunk, its first piece
+  uint64_t qr = 1;             // chunks per piece
+  uint64_t q = ~0ull;          // the piece being marked
+  uint32_t i = 0, word = 0;    // its next record, the bits of its current word
+  __device__ __forceinline__ void flush(const ScanArgs& a) {
+    if (q != ~0ull && (i & 31) && i <= kTailMaxRecs) a.tbits[(unit0 + q) * kTailBitWords + ((i - 1) >> 5)] = word;
+  }
+  __device__ __forceinline__ void record(const ScanArgs& a, uint64_t t, bool longr) {
+    const uint64_t qq = (t - r0) / qr;
+    if (qq != q) {
+      flush(a);
+      q = qq;
+      i = 0;
+      word = 0;
+    }
+    word |= (longr ? 1u : 0u) << (i & 31);
+    ++i;
+    if (!(i & 31)) {
+      if (i <= kTailMaxRecs) a.tbits[(unit0 + q) * kTailBitWords + ((i - 1) >> 5)] = word;
+      word = 0;
+    }
+  }
+};
+
 __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t tb, uint64_t te,
                                 uint64_t p_in) {
   const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   g_u32* slots = (g_u32*)a.slots;
   g_u64* cd = (g_u64*)a.cdesc;
+  TailBits tbt;
+  {
+    const uint64_t R = a.run, nruns = (a.total_chunks + R - 1) / R, k = tb / R;
+    if (a.hash_ntail && k >= nruns - a.hash_ntail) {
+      tbt.on = true;
+      tbt.r0 = k * R;
+      tbt.qr = (R + kTailSplit - 1) / kTailSplit;
+      tbt.unit0 = (k - (nruns - a.hash_ntail)) * kTailSplit;
+    }
+  }
   Walk W;
   W.cn = 0;
   W.ccerr = 0xFFFFFFFFu;
@@ -181,6 +220,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       uint32_t j = 0;
       if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
         const uint32_t r = open_record(a, W, p, csh, true, &j);
+        if (tbt.on) tbt.record(a, W.S.t0 + j, false);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
         if (r < a.slot_cap) *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
         if (r < W.ccerr) W.ccerr = r;
@@ -194,6 +234,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       const uint64_t pl = pn + 18 <= W.S.len ? pn + 2 : 0ull;  // (pn < p: rl wrapped, impossible)
       h = gld16g((const g_u8*)(W.S.data + pl));
       const uint32_t r = open_record(a, W, p, csh, true, &j);
+      if (tbt.on) tbt.record(a, W.S.t0 + j, rl >= kTailLong);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
       if (r < a.slot_cap)
         *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
@@ -207,6 +248,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
     close_segment(a, W, term ? kTerm : p, true);
     if (term) p = kTerm;
   }
+  if (tbt.on) tbt.flush(a);
   return p;
 }
 
@@ -279,14 +321,15 @@ __device__ __forceinline__ u32x4 gld16nt(uint64_t p) {
   return __builtin_nontemporal_load((gcu32x4*)(uintptr_t)p);
 }
 
-__global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_run_hash(ScanArgs a) {
   constexpr uint32_t D = 8;    // lines of a record per round
   constexpr uint32_t RW = 256; // dwords per round
   constexpr uint32_t RT = kMaxRun + 1;
   __shared__ uint32_t s_pf[4][2][RT];
   __shared__ uint64_t s_cd[4][2][2 * kMaxRun];
   __shared__ uint32_t s_fq[4][64][12];  // per wave: records whose checksums are to be finished
-  const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = threadIdx.x >> 6, h = lane >> 5;
+  __shared__ uint16_t s_tl[4][2][kTailMaxRecs];  // per wave, two units: a tail piece's pass's records
+  const uint32_t lane = threadIdx.x & 63, q = lane & 3, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), h = lane >> 5;
   const bool qlead = q == 0;
   const uint64_t R = a.run;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + R - 1) / R;
@@ -296,6 +339,9 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t* pfB = s_pf[wv][1];
   uint64_t* cdA = s_cd[wv][0];
   uint64_t* cdB = s_cd[wv][1];
+  uint16_t* tlA = s_tl[wv][0];  // a tail piece's pass: its records in that pass
+  uint16_t* tlB = s_tl[wv][1];
+  bool flA = false, flB = false;  // the unit's records are handed out through its list
   const unsigned long long qmask = 0x1111111111111111ull;
   const uint64_t safe = (uint64_t)(uintptr_t)a.cdesc;  // (a 128-B aligned allocation: its first line)
 
@@ -312,21 +358,31 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
   uint32_t cur = 0;
   bool runs_left = true;
   auto run_start = [&](uint64_t k) __attribute__((always_inline)) { return (a.wruns ? a.wruns[k] : k) * R; };
-  constexpr uint64_t TS = 8;
+  constexpr uint64_t TS = kTailSplit;
+  // With a.hash_ntail (walk mode over data files): the last hash_ntail runs' pieces are each handed
+  // out twice, through a list of their records: the records of at least kTailLong bytes right after
+  // the other runs (units [nhead, nhead + NT)), the shorter ones last — so that no long record is
+  // still being hashed when the units run out
+  const bool split = a.hash_ntail != 0;
   const uint64_t tcap = (uint64_t)gridDim.x * 4;
-  const uint64_t ntail = nruns < tcap ? nruns : tcap;
-  const uint64_t nhead = nruns - ntail, nunits = nhead + TS * ntail;
+  const uint64_t ntail = split ? a.hash_ntail : nruns < tcap ? nruns : tcap;
+  const uint64_t nhead = nruns - ntail, NT = TS * ntail, nunits = nhead + (split ? 2 * NT : NT);
   auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
     if (u >= nunits) return false;
+    // pass: 0 a whole head run or (no split) a tail piece, 1 a tail piece's long records, 2 its others
     const bool tl = u >= nhead;
-    const uint64_t k = tl ? nhead + (u - nhead) / TS : u;
+    const uint64_t piece = tl ? (u - nhead) % NT : 0ull;
+    const uint32_t pass = split && tl ? (u - nhead < NT ? 1u : 2u) : 0u;
+    const uint64_t k = tl ? nhead + piece / TS : u;
     const uint64_t tr = run_start(k);
     const uint64_t nk = a.total_chunks - tr < R ? a.total_chunks - tr : R;
-    const uint64_t qr = (R + TS - 1) / TS, c0 = tl ? ((u - nhead) % TS) * qr : 0ull;
+    const uint64_t qr = (R + TS - 1) / TS, c0 = tl ? (piece % TS) * qr : 0ull;
     const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
     const uint64_t t0 = tr + c0;
     const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
     uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
+    // (the piece's long-record bits, loaded with the counts: one round trip)
+    const uint32_t bits = pass && lane < kTailBitWords ? ((const g_u32*)a.tbits)[piece * kTailBitWords + lane] : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
       if ((int)lane >= o) inc += u;
@@ -339,15 +395,36 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
       cdt[2 * lane] = cd[2 * (t0 + lane)];
       cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
     }
-    const uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
+    uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
+    if (pass) {  // the pass's records, in order, into the unit's list
+      const uint32_t nb = 32 * lane;
+      const uint32_t valid = lane >= kTailBitWords || nb >= n ? 0u : n - nb >= 32 ? ~0u : (1u << (n - nb)) - 1u;
+      uint32_t w = (pass == 1 ? bits : ~bits) & valid;
+      const uint32_t c = (uint32_t)__builtin_popcount(w);
+      uint32_t pre = c;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(pre, o, 64);
+        if ((int)lane >= o) pre += t;
+      }
+      uint16_t* lst = intoA ? tlA : tlB;
+      uint32_t at = pre - c;
+      while (w) {
+        const uint32_t b = (uint32_t)__builtin_ctz(w);
+        w &= w - 1;
+        lst[at++] = (uint16_t)(nb + b);
+      }
+      n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)pre, 63, 64));
+    }
     if (intoA) {
       rtA = t0;
       rchA = nch;
       rnA = n;
+      flA = pass != 0;
     } else {
       rtB = t0;
       rchB = nch;
       rnB = n;
+      flB = pass != 0;
     }
     return true;
   };
@@ -452,17 +529,20 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
     const uint32_t idx = up ? myrank - rem : cur + myrank;
     const bool claimed = want && (up ? (fullB && idx < rnB) : true);
     const uint32_t* pf = up ? pfB : pfA;
+    // the unit's idx-th record to hand out: itself, or its list's entry (a tail piece's pass)
+    const uint16_t* tlc = up ? tlB : tlA;
+    const uint32_t rec = (up ? flB : flA) ? (uint32_t)tlc[idx < kTailMaxRecs ? idx : 0u] : idx;
     uint32_t lo = 0, hi = up ? rchB : rchA;
 #pragma unroll
     for (int it = 0; it < 6; ++it) {
       const uint32_t mid = (lo + hi) >> 1;
       const bool go = hi - lo > 1;
-      const bool le = go && pf[mid] <= idx;
+      const bool le = go && pf[mid] <= rec;
       lo = le ? mid : lo;
       hi = go && !le ? mid : hi;
     }
     const uint64_t ntc = (up ? rtB : rtA) + lo;
-    const uint32_t nrc = idx - pf[lo];
+    const uint32_t nrc = rec - pf[lo];
     nt = claimed ? ntc : nt;
     nr = claimed ? nrc : nr;
     const uint64_t* cdt = up ? cdB : cdA;
@@ -484,6 +564,10 @@ __global__ __launch_bounds__(256) void k_run_hash(ScanArgs a) {
         uint64_t* tc = cdA;
         cdA = cdB;
         cdB = tc;
+        uint16_t* tt = tlA;
+        tlA = tlB;
+        tlB = tt;
+        flA = flB;
         fullB = false;
         cur = used - rem;
       } else {
@@ -711,17 +795,22 @@ void launch_walk_chase(const ScanArgs& a, void* stream) {
 
 // A persistent grid of exactly the resident workgroups: a workgroup beyond them would start only as
 // the first ones finish, holding its first run (claimed by block index) until the end.
-void launch_run_hash(const ScanArgs& a, void* stream) {
-  if (!a.total_chunks) return;
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
-  if (!nruns) return;
+uint64_t run_hash_waves() {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash, 256, 0) == hipSuccess && nb > 0) per_cu = 4 * nb;
     if (per_cu <= 0) per_cu = 8;
   }
-  uint64_t waves = (uint64_t)device_cus() * (uint64_t)per_cu;
+  return (uint64_t)device_cus() * (uint64_t)per_cu;
+}
+
+void launch_run_hash(const ScanArgs& a, void* stream) {
+  if (!a.total_chunks) return;
+  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
+  if (!nruns) return;
+  uint64_t waves = run_hash_waves();
+  if (const char* e = cask_knobs::tune("CASK_HASH_WAVES_PER_CU")) waves = (uint64_t)device_cus() * (uint64_t)atoi(e);
   if (waves > nruns) waves = nruns;
   hipLaunchKernelGGL(k_run_hash, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
 }

@@ -164,6 +164,12 @@ struct ScanArgs {
   // ones are listed for the hop back (kSearchShort; CASK_SEARCH_SHORT tuning knob)
   uint32_t search_short;
   uint32_t pad_ss;
+  // walk mode, k_run_hash's tail: the last hash_ntail runs are handed out in kTailSplit pieces,
+  // each piece twice — its records of at least kTailLong bytes right after the other runs, its
+  // shorter ones last — so that the kernel ends on short records; tbits: per piece kTailBitWords
+  // words, bit i = its record i is long (written by k_walk_chase). hash_ntail 0: one pass.
+  uint64_t hash_ntail;
+  uint32_t* tbits;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -186,6 +192,13 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // Counters::slot_overflow and the call is redone with the full count (chunk / 18 + 2).
 constexpr uint32_t kWalkSlotCap = 128;
 constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk runs 2 % faster than 64)
+constexpr uint32_t kTailSplit = 8;  // pieces per tail run (k_run_hash)
+#ifndef CASK_TAIL_LONG
+#define CASK_TAIL_LONG 16384
+#endif
+constexpr uint32_t kTailLong = CASK_TAIL_LONG;  // a tail piece's records at least this long go first
+constexpr uint32_t kTailMaxRecs = kWalkRun / kTailSplit * kWalkSlotCap;  // records a piece can hold
+constexpr uint32_t kTailBitWords = kTailMaxRecs / 32;
 // Chunk mode: the short-halo geometry (kGeoShortHalo, a 1,008-B halo) when the records at the file
 // heads average at most kShortHaloMean bytes and none is longer than kShortHaloMax; else the wide
 // halo (kDefaultGeometry, 4,080 B). Speed only: a record that crosses the window goes to k_long.
@@ -251,6 +264,7 @@ void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each w
 // every record hashed from HBM, whole 128-B lines per load instruction)
 void launch_walk_chase(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, void* stream);
+uint64_t run_hash_waves();  // k_run_hash's persistent grid, in waves
 // after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
 void launch_hash_fix(const ScanArgs& a, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)

@@ -102,6 +102,7 @@ struct cask_ctx {
   DevBuf tstate;     // k_finish look-back granules (8 per tile), tagged with `epoch`
   DevBuf keyat;      // cask_shard_keydir_hints: per row, its key's offset in its hint body
   DevBuf cdesc;      // walk mode, split path: per chunk its address and its file's end (2 x u64)
+  DevBuf tbits;      // walk mode: the tail pieces' long-record bits (kTailBitWords per piece)
   DevBuf probe;      // k_probe_regions: 3 u64 per region of each file
   DevBuf mruns;      // mixed call: walk-mode run indices | chunk-mode [first, end) stretches
   uint32_t epoch = 0;
@@ -273,7 +274,7 @@ int cask_last_dense(const cask_ctx* c) { return c ? c->last_dense : 0; }
 uint64_t cask_ctx_scratch_bytes(const cask_ctx* c) {
   if (!c) return 0;
   const DevBuf* bufs[] = {&c->chunk, &c->slots, &c->filebuf, &c->err2, &c->gather, &c->stamps, &c->repair, &c->lq,
-                          &c->tstate, &c->keyat, &c->cdesc, &c->probe, &c->mruns, &c->stage_data, &c->stage_rows};
+                          &c->tstate, &c->keyat, &c->cdesc, &c->tbits, &c->probe, &c->mruns, &c->stage_data, &c->stage_rows};
   uint64_t t = 0;
   for (const DevBuf* b : bufs) t += b->cap;
   return t;
@@ -684,6 +685,17 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipEventRecord(c->ev[6], st));
     a.walk_pre = 1;
     a.cdesc = c->cdesc.as<uint64_t>();
+    // The hash's tail: the last grid's worth of runs, in pieces whose long records are hashed before
+    // their short ones (k_run_hash). Only with small slot rows (a piece's records fit its list).
+    // CASK_TAIL_SPLIT=0 (tuning knob) turns it off.
+    static const bool tail_on = !(cask_knobs::tune("CASK_TAIL_SPLIT") && atoi(cask_knobs::tune("CASK_TAIL_SPLIT")) == 0);
+    const uint64_t qr = (a.run + kTailSplit - 1) / kTailSplit;
+    a.hash_ntail = 0;
+    if (tail_on && small_slots && qr * a.slot_cap <= kTailMaxRecs) {
+      a.hash_ntail = std::min<uint64_t>(nruns, run_hash_waves());
+      if (!c->tbits.ensure(4ull * kTailBitWords * kTailSplit * a.hash_ntail + 256)) return CASK_E_NOMEM;
+      a.tbits = c->tbits.as<uint32_t>();
+    }
     launch_walk_chase(a, st);
     L("k_walk_chase");
     H(hipEventRecord(c->ev[7], st));

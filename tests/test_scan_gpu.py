@@ -624,3 +624,43 @@ def test_cfg2_full_size_properties(gpu_ctx):
         assert np.array_equal(want["vsz_raw"].astype(np.uint32), res.vsz[sl].cpu().numpy().view(np.uint32))
         assert np.array_equal(want["status"].astype(np.uint8), res.status[sl].cpu().numpy())
         del host, want
+
+
+def test_zipf_head_and_tail_units(gpu_ctx):
+    """configs[2] record shape at 4.5 GiB in 2-GiB files: over 4,000 walk runs, so k_run_hash hands out
+    whole runs first and then the last grid's worth of runs in pieces, each piece twice (its records
+    of at least 16 KiB, marked by k_walk_chase, then its shorter ones). Bit flips in the bodies of
+    records all over both parts; every row of every file and the call's first error as the C oracle's
+    scan of the same bytes."""
+    import torch
+    from cask_amd.workloads import zipf_files
+    fs, _, n, rl = zipf_files(gpu_ctx, 4.5, 2 ** 31)
+    rl_h = rl[:n].cpu().numpy()
+    rng = np.random.default_rng(5)
+    hosts = []
+    for f, idx in fs:
+        i0, i1 = int(idx[0]), int(idx[-1]) + 1
+        off = np.concatenate([[0], np.cumsum(rl_h[i0:i1])[:-1]])
+        host = f.data.cpu().numpy().copy()
+        for r in rng.choice(i1 - i0, size=16, replace=False):
+            b = int(off[r]) + 18 + int(rng.integers(int(rl_h[i0 + r]) - 18))
+            host[b] ^= np.uint8(1 << int(rng.integers(8)))
+        f.data.copy_(torch.from_numpy(host))
+        hosts.append(host)
+    res = gpu_ctx.scan_device([(f.file_id, f.data) for f, _ in fs])
+    first_err = None
+    for i, ((f, _), host) in enumerate(zip(fs, hosts)):
+        want = O.scan(host)
+        sl = res.file_rows(i)
+        assert sl.stop - sl.start == len(want)
+        assert np.array_equal(want["pos"], res.pos[sl].cpu().numpy().astype(np.uint64))
+        assert np.array_equal(want["seq"], res.seq[sl].cpu().numpy().astype(np.uint64))
+        assert np.array_equal(want["ksz"].astype(np.uint16), res.ksz[sl].cpu().numpy().view(np.uint16))
+        assert np.array_equal(want["vsz_raw"].astype(np.uint32), res.vsz[sl].cpu().numpy().view(np.uint32))
+        assert np.array_equal(want["status"].astype(np.uint8), res.status[sl].cpu().numpy())
+        assert int((want["status"] != 0).sum()) == 16
+        if first_err is None:
+            r = want[np.flatnonzero(want["status"] != 0)[0]]
+            first_err = (int(r["status"]), f.file_id, int(r["pos"]), int(r["expected"]), int(r["found"]))
+    e = res.error
+    assert (e.kind, e.file_id, e.pos, e.expected, e.found) == first_err

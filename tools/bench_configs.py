@@ -141,9 +141,33 @@ def compact(ctx, torch, nfiles, workdir):
     return out
 
 
+def open_ab(ctx, torch, nfiles, workdir, rounds=2):
+    """Cask::open of the same configs[3]-shaped files by cask_db_open (threaded host fold) and by
+    cask_db_open_multi on device 0 (keydir blocks reduced on the device, merged on the host), in turn;
+    no hint files are written, so every open scans."""
+    from cask_amd import CaskOptions
+    from cask_amd.keydir import open_multi
+    path = os.path.join(workdir, "db")
+    os.makedirs(path)
+    nbytes, live_want, n, write_s = write_cfg3(ctx, torch, nfiles, path)
+    out = {"files": nfiles, "records": n, "bytes": nbytes, "open_s": [], "open_multi_s": []}
+    for _ in range(rounds):
+        t0 = time.perf_counter()
+        with CaskOptions().write_hints(False).open(path) as db:
+            out["open_s"].append(time.perf_counter() - t0)
+            assert len(db) == live_want
+        print(f"open {out['open_s'][-1]:.2f} s", file=sys.stderr, flush=True)
+        t0 = time.perf_counter()
+        with open_multi(path, [0], CaskOptions().write_hints(False)) as db:
+            out["open_multi_s"].append(time.perf_counter() - t0)
+            assert len(db) == live_want
+        print(f"open_multi {out['open_multi_s'][-1]:.2f} s", file=sys.stderr, flush=True)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("what", nargs="+", choices=["cfg3", "compact"])
+    ap.add_argument("what", nargs="+", choices=["cfg3", "compact", "openab"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--gib", type=float, default=32.0)
     ap.add_argument("--max-file", type=int, default=2 ** 31)
@@ -162,7 +186,7 @@ def main():
         else:
             wd = tempfile.mkdtemp(prefix="cask_compact_", dir=args.dir)
             try:
-                r = compact(ctx, torch, args.files, wd)
+                r = (compact if w == "compact" else open_ab)(ctx, torch, args.files, wd)
             finally:
                 shutil.rmtree(wd, ignore_errors=True)
         r["what"] = w
