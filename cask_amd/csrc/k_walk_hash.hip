@@ -151,15 +151,16 @@ struct TailBits {
   uint64_t r0 = 0, unit0 = 0;  // the run's first chunk, its first piece
   uint64_t qr = 1;             // chunks per piece
   uint64_t q = ~0ull;          // the piece being marked
+  uint64_t qe = 0;             // the first chunk after it (the chain only moves forward)
   uint32_t i = 0, word = 0;    // its next record, the bits of its current word
   __device__ __forceinline__ void flush(const ScanArgs& a) {
     if (q != ~0ull && (i & 31) && i <= kTailMaxRecs) a.tbits[(unit0 + q) * kTailBitWords + ((i - 1) >> 5)] = word;
   }
   __device__ __forceinline__ void record(const ScanArgs& a, uint64_t t, bool longr) {
-    const uint64_t qq = (t - r0) / qr;
-    if (qq != q) {
+    if (t >= qe) {  // (a division per piece, not per record)
       flush(a);
-      q = qq;
+      q = (uint32_t)(t - r0) / (uint32_t)qr;
+      qe = r0 + (q + 1) * qr;
       i = 0;
       word = 0;
     }
