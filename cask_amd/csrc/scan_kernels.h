@@ -192,7 +192,10 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // Counters::slot_overflow and the call is redone with the full count (chunk / 18 + 2).
 constexpr uint32_t kWalkSlotCap = 128;
 constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk runs 2 % faster than 64)
-constexpr uint32_t kTailSplit = 8;  // pieces per tail run (k_run_hash)
+#ifndef CASK_TAIL_SPLIT_N  // (A/B variant)
+#define CASK_TAIL_SPLIT_N 4
+#endif
+constexpr uint32_t kTailSplit = CASK_TAIL_SPLIT_N;  // pieces per tail run (k_run_hash)
 #ifndef CASK_TAIL_LONG
 #define CASK_TAIL_LONG 16384
 #endif
