@@ -197,7 +197,7 @@ constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk ru
 #endif
 constexpr uint32_t kTailSplit = CASK_TAIL_SPLIT_N;  // pieces per tail run (k_run_hash)
 #ifndef CASK_TAIL_LONG
-#define CASK_TAIL_LONG 16384
+#define CASK_TAIL_LONG 24576
 #endif
 constexpr uint32_t kTailLong = CASK_TAIL_LONG;  // a tail piece's records at least this long go first
 constexpr uint32_t kTailMaxRecs = kWalkRun / kTailSplit * kWalkSlotCap;  // records a piece can hold
