@@ -350,9 +350,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   // cur) and B (the next one, once loaded: fullB), each as its first chunk, chunk count and row
   // count. B is refilled from the claim counter as soon as it is free. (Plain variables, not arrays
   // indexed by the slot: those go to scratch memory, whose loads wait for every load.) Units of
-  // work: the runs in order, except that the last grid's worth of runs is handed out in eighths, so
-  // that the waves run dry within about an eighth of a run of each other (A/B: quarters 0.3 % and
-  // sixteenths 0.7 % slower, halves 1.2 %; eighths over the last two grids' worth 0.3 %).
+  // work: the runs in order, except that the tail runs (a.hash_ntail: two grids' worth; else one) are
+  // handed out in kTailSplit pieces, each twice with a.hash_ntail (long records, then short ones), so
+  // that the waves run dry close together (A/B in DESIGN §4 and profiles/r05_hash_lines_ab.txt).
   uint64_t rtA = 0, rtB = 0;
   uint32_t rnA = 0, rnB = 0, rchA = 0, rchB = 0;
   bool fullB = false;

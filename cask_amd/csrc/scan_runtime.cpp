@@ -685,14 +685,17 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     H(hipEventRecord(c->ev[6], st));
     a.walk_pre = 1;
     a.cdesc = c->cdesc.as<uint64_t>();
-    // The hash's tail: the last grid's worth of runs, in pieces whose long records are hashed before
+    // The hash's tail: the last runs, in pieces whose long records are hashed before
     // their short ones (k_run_hash). Only with small slot rows (a piece's records fit its list).
     // CASK_TAIL_SPLIT=0 (tuning knob) turns it off.
     static const bool tail_on = !(cask_knobs::tune("CASK_TAIL_SPLIT") && atoi(cask_knobs::tune("CASK_TAIL_SPLIT")) == 0);
     const uint64_t qr = (a.run + kTailSplit - 1) / kTailSplit;
     a.hash_ntail = 0;
     if (tail_on && small_slots && qr * a.slot_cap <= kTailMaxRecs) {
-      a.hash_ntail = std::min<uint64_t>(nruns, run_hash_waves());
+      // the last two grids' worth of runs (configs[2], A/B: one grid's worth 0.8 % slower, four 0.5 %,
+      // half 1.7 %); CASK_TAIL_PCT (tuning knob): the tail runs as a percentage of the hash's grid
+      static const uint64_t tail_pct = cask_knobs::tune("CASK_TAIL_PCT") ? (uint64_t)atoi(cask_knobs::tune("CASK_TAIL_PCT")) : 200u;
+      a.hash_ntail = std::min<uint64_t>(nruns, std::max<uint64_t>(1, run_hash_waves() * tail_pct / 100));
       if (!c->tbits.ensure(4ull * kTailBitWords * kTailSplit * a.hash_ntail + 256)) return CASK_E_NOMEM;
       a.tbits = c->tbits.as<uint32_t>();
     }

@@ -628,7 +628,7 @@ def test_cfg2_full_size_properties(gpu_ctx):
 
 def test_zipf_head_and_tail_units(gpu_ctx):
     """configs[2] record shape at 4.5 GiB in 2-GiB files: over 4,000 walk runs, so k_run_hash hands out
-    whole runs first and then the last grid's worth of runs in pieces, each piece twice (its records
+    whole runs first and then the last two grids' worth of runs in pieces, each piece twice (its records
     of at least 24 KiB, marked by k_walk_chase, then its shorter ones). Bit flips in the bodies of
     records all over both parts; every row of every file and the call's first error as the C oracle's
     scan of the same bytes."""
