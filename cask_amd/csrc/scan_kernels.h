@@ -193,7 +193,7 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 constexpr uint32_t kWalkSlotCap = 128;
 constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk runs 2 % faster than 64)
 #ifndef CASK_TAIL_SPLIT_N  // (A/B variant)
-#define CASK_TAIL_SPLIT_N 4
+#define CASK_TAIL_SPLIT_N 2
 #endif
 constexpr uint32_t kTailSplit = CASK_TAIL_SPLIT_N;  // pieces per tail run (k_run_hash)
 #ifndef CASK_TAIL_LONG
