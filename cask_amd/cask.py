@@ -189,7 +189,7 @@ class Cask:
         e = L.IndexEntry()
         kb = bytes(key)
         ok = L.lib().cask_db_get_entry(self._handle(), kb, len(kb), C.byref(e))
-        if not ok:
+        if ok != 1:  # (1: found; 0: not found)
             return None
         return IndexEntry(e.file_id, e.entry_pos, e.entry_size, e.sequence)
 

@@ -1735,8 +1735,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     }
   } remove_on_throw{remove_outs};
   // one record's bytes into its file, and its hint (Hint::new(entry, entry_pos), data.rs:218-226)
-  auto append = [&](size_t oi, const uint8_t* rec, uint64_t n) -> bool {
-    OutFile& o = outs[oi];
+  auto append = [&](OutFile& o, const uint8_t* rec, uint64_t n) -> bool {
     if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) return false;
     const uint16_t k = rd16(rec + 12);
     uint8_t h[22];
@@ -1769,8 +1768,12 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     std::vector<HostBuf> regions;       // per source file of the batch: its live records' bytes, in order
     std::vector<const uint8_t*> at;     // per record: its bytes (in a region)
     std::vector<uint64_t> len, foff;    // per record: length, offset in its output file
-    std::vector<size_t> oi;             // per record: its output file
-    size_t complete = 0;                // outs[0, complete) take no record after this batch
+    std::vector<OutFile*> op;           // per record: its output file
+    // outs[done, complete) take no record after this batch: the writer finishes them. (The writer
+    // never indexes `outs`: placement appends to it meanwhile, which may rewrite the deque's block
+    // map; the elements themselves never move, so pointers resolved at placement stay valid.)
+    std::vector<OutFile*> fin;
+    size_t complete = 0;
   };
   struct Writer {
     std::thread th;
@@ -1797,16 +1800,16 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     ~Writer() { stop(); }
   } writer;
   auto write_batch = [&](WBatch& B) -> int {  // (on the writer thread)
-    const uint64_t n = B.oi.size();
+    const uint64_t n = B.op.size();
     std::vector<std::pair<uint64_t, uint64_t>> runs;
     for (uint64_t k = 0; k < n;) {
       uint64_t e = k;
-      while (e < n && B.oi[e] == B.oi[k]) ++e;
+      while (e < n && B.op[e] == B.op[k]) ++e;
       runs.emplace_back(k, e);
       k = e;
     }
     for (const auto& r : runs) {  // (fds opened here, on one thread)
-      OutFile& o = outs[B.oi[r.first]];
+      OutFile& o = *B.op[r.first];
       if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) {
         writer.fail_fid = o.fid;
         return CASK_E_IO;
@@ -1835,16 +1838,16 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     parallel_for(ntw, [&](unsigned t) {
       for (size_t x = t; x < ntask; x += ntw) {
         if (x < runs.size()) {
-          for (uint64_t j = runs[x].first; j < runs[x].second; ++j) append(B.oi[j], B.at[j], B.len[j]);
+          for (uint64_t j = runs[x].first; j < runs[x].second; ++j) append(*B.op[j], B.at[j], B.len[j]);
         } else {
           const Piece& pc = pieces[x - runs.size()];
-          if (!pwrite_all(outs[B.oi[runs[pc.run].first]].fd, pc.at, pc.n, pc.foff)) ok[pc.run] = 0;
+          if (!pwrite_all(B.op[runs[pc.run].first]->fd, pc.at, pc.n, pc.foff)) ok[pc.run] = 0;
         }
       }
     });
     for (size_t r = 0; r < runs.size(); ++r)
       if (!ok[r]) {
-        writer.fail_fid = outs[B.oi[runs[r].first]].fid;
+        writer.fail_fid = B.op[runs[r].first]->fid;
         return CASK_E_IO;
       }
     return CASK_OK;
@@ -1858,14 +1861,16 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   // Output files [lo, hi) finished: hint file (HintWriter: body + XXH32 trailer) written and data
   // file closed, a file per thread (the first failure in file order is the error). The writer thread
   // finishes each output file once no later batch can add to it; this thread the rest at the end.
-  size_t hints_done = 0;
-  auto finish_outputs = [&](size_t lo, size_t hi, uint32_t* fail) -> int {
+  size_t hints_done = 0;  // (the writer's; read here only once it has stopped)
+  size_t fin_next = 0;    // (this thread's: the output files already handed to the writer to finish)
+  auto finish_outputs = [&](const std::vector<OutFile*>& fo, uint32_t* fail) -> int {
+    const size_t lo = 0, hi = fo.size();
     if (hi <= lo) return CASK_OK;
     std::vector<char> okh(hi - lo, 1);
     const unsigned nth = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)(hi - lo)));
     parallel_for(nth, [&](unsigned t) {
       for (size_t i = lo + t; i < hi; i += nth) {
-        OutFile& o = outs[i];
+        OutFile& o = *fo[i];
         if (o.fd < 0 && (o.fd = open(data_path(path, o.fid).c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644)) < 0) {
           okh[i - lo] = 0;
           continue;
@@ -1878,7 +1883,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     });
     for (size_t i = lo; i < hi; ++i)
       if (!okh[i - lo]) {
-        *fail = outs[i].fid;
+        *fail = fo[i]->fid;
         return CASK_E_IO;
       }
     return CASK_OK;
@@ -1897,7 +1902,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
         const auto tw0 = std::chrono::steady_clock::now();
         int st = writer.status == CASK_OK ? abi_status([&] { return write_batch(*B); }) : writer.status;
         if (st == CASK_OK && B->complete > hints_done) {  // (output files no later batch adds to)
-          st = abi_status([&] { return finish_outputs(hints_done, B->complete, &writer.fail_fid); });
+          st = abi_status([&] { return finish_outputs(B->fin, &writer.fail_fid); });
           if (st == CASK_OK) hints_done = B->complete;
         }
         const double dt = ms_since(tw0);
@@ -2068,13 +2073,15 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       t_verify += ms_since(tv);
       // placement (LogWriter::write's rollover, log.rs:282-306), in write order
       auto tg = std::chrono::steady_clock::now();
-      WB->oi.resize(n);
+      WB->op.resize(n);
       WB->foff.resize(n);
       for (uint64_t k = 0; k < n; ++k) {
-        WB->oi[k] = place(WB->len[k], true);
+        WB->op[k] = &outs[place(WB->len[k], true)];
         WB->foff[k] = cur - WB->len[k];  // (its offset in its file: placement just added it)
       }
       WB->complete = outs.empty() ? 0 : outs.size() - 1;  // (the last output file may take more)
+      for (size_t i = fin_next; i < WB->complete; ++i) WB->fin.push_back(&outs[i]);
+      fin_next = std::max(fin_next, WB->complete);
       t_gather += ms_since(tg);
       // hand the batch to the writer once it has taken the previous one
       auto tw = std::chrono::steady_clock::now();
@@ -2171,7 +2178,9 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   // the output files the writer thread has not finished (the last live one, the tombstone tail's)
   {
     uint32_t ff = 0;
-    if (finish_outputs(hints_done, outs.size(), &ff) != CASK_OK) return abort_with(CASK_E_IO, ff);
+    std::vector<OutFile*> rest;
+    for (size_t i = hints_done; i < outs.size(); ++i) rest.push_back(&outs[i]);
+    if (finish_outputs(rest, &ff) != CASK_OK) return abort_with(CASK_E_IO, ff);
   }
   t_write += ms_since(tw);
   tp = tw;
@@ -2986,13 +2995,17 @@ void cask_db_close(cask_db* db) { delete db; }
 uint64_t cask_db_len(const cask_db* db) { return db ? db->index.live() : 0; }
 
 int cask_db_get_entry(const cask_db* db, const uint8_t* key, uint64_t ksz, cask_index_entry* out) {
-  return cask_abi::guard([&]() -> int {
+  // 1 (found) or 0 by contract: not under cask_abi::guard, whose negative statuses a caller testing
+  // for 0 would take as "found"; the lookup allocates nothing, and anything thrown is "not found"
+  try {
     if (!db || (ksz && !key) || ksz > 0xFFFF) return 0;
     const cask_index_entry* e = db->index.get(key, (uint32_t)ksz);
     if (!e) return 0;
     if (out) *out = *e;
     return 1;
-  });
+  } catch (...) {
+    return 0;
+  }
 }
 
 int64_t cask_db_export(const cask_db* db, uint8_t* key_bytes, uint64_t key_cap, uint64_t* key_off,

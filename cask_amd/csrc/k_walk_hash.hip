@@ -776,6 +776,25 @@ __global__ __launch_bounds__(256) void k_hash_fix(ScanArgs a) {
   atomicMax(&a.err_inv[fi], ~(unsigned long long)(base + ce));
 }
 
+// A walk-mode call that needs the repair path: its slot rows (kWalkSlotCap per chunk, every chunk's
+// count within them: no slot_overflow) moved to the full stride, one thread per slot row.
+__global__ __launch_bounds__(256) void k_restride(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                  const uint32_t* __restrict__ count, uint64_t nchunks,
+                                                  uint32_t cap_src, uint32_t cap_dst) {
+  const uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x;
+  const uint64_t c = i / cap_src;
+  const uint32_t r = (uint32_t)(i - c * cap_src);
+  if (c >= nchunks || r >= (count[c] & kCountMask)) return;
+  *(u32x4*)(dst + (c * cap_dst + r) * 4) = *(const u32x4*)(src + (c * cap_src + r) * 4);
+}
+
+void launch_restride(const ScanArgs& a, uint32_t* dst, uint32_t cap_dst, void* stream) {
+  const uint64_t n = a.total_chunks * (uint64_t)a.slot_cap;
+  if (!n) return;
+  hipLaunchKernelGGL(k_restride, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a.slots, dst,
+                     a.count, a.total_chunks, a.slot_cap, cap_dst);
+}
+
 void launch_hash_fix(const ScanArgs& a, void* stream) {
   if (!a.total_chunks) return;
   hipLaunchKernelGGL(k_hash_fix, dim3((uint32_t)((a.total_chunks + 255) / 256)), dim3(256), 0, (hipStream_t)stream, a);

@@ -230,7 +230,8 @@ static int gather_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes
   // goes through the all-gather with root 0 in its place, then every rank stops at the agreement)
   int status = (bytes && !block) ? CASK_E_INVALID_ARG : CASK_OK;
   std::vector<uint64_t> all, off;
-  if (!host_alloc(all, 2ull * nranks) || !host_alloc(off, (uint64_t)nranks + 1)) status = CASK_E_NOMEM;
+  if (!host_alloc(all, 3ull * nranks) || !host_alloc(off, (uint64_t)nranks + 1)) status = CASK_E_NOMEM;
+  const uint64_t root_given = (uint64_t)(int64_t)root;  // (compared across the ranks below)
   if (root < 0 || root >= nranks) {
     status = CASK_E_INVALID_ARG;
     root = 0;
@@ -242,15 +243,20 @@ static int gather_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes
   if (has_hd && (hipMemcpyAsync(&hd, block, sizeof(hd), hipMemcpyDeviceToHost, st) != hipSuccess ||
                  hipStreamSynchronize(st) != hipSuccess))
     status = CASK_E_DEVICE;
-  // every rank's block size and max sequence + 1 (ncclAllGather of two u64 per rank): the global
-  // maximum sequence is the largest of them on every rank, with no collective of its own
-  const uint64_t mine[2] = {status == CASK_OK ? bytes : 0, has_hd ? hd.max_seq_p1 : 0};
-  if (!allgather_u64(K, st, mine, 2, all)) return CASK_E_DEVICE;
+  // every rank's block size, max sequence + 1 and root (ncclAllGather of three u64 per rank): the
+  // global maximum sequence is the largest of them on every rank, with no collective of its own; ranks
+  // that name different roots would each post the root's receives, and the grouped send/recv would
+  // never match — every rank sees the disagreement here and stops at the agreement instead
+  const uint64_t mine[3] = {status == CASK_OK ? bytes : 0, has_hd ? hd.max_seq_p1 : 0, root_given};
+  if (!allgather_u64(K, st, mine, 3, all)) return CASK_E_DEVICE;
+  if (status == CASK_OK && !all.empty())
+    for (int r = 0; r < nranks; ++r)
+      if (all[3ull * r + 2] != root_given) status = CASK_E_INVALID_ARG;
   if (status == CASK_OK) {
     uint64_t mx = 0;
-    for (int r = 0; r < nranks; ++r) mx = std::max(mx, all[2ull * r + 1]);
+    for (int r = 0; r < nranks; ++r) mx = std::max(mx, all[3ull * r + 1]);
     if (max_seq) *max_seq = mx ? mx - 1 : 0;
-    for (int r = 0; r < nranks; ++r) off[r + 1] = off[r] + ((all[2ull * r] + 255) & ~255ull);
+    for (int r = 0; r < nranks; ++r) off[r + 1] = off[r] + ((all[3ull * r] + 255) & ~255ull);
     if (gathered) *gathered = rank == root ? off[nranks] : bytes;
   }
   // the root's receive and host buffers, then the agreed status: every rank goes on, or every one stops
@@ -266,12 +272,12 @@ static int gather_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes
   bool sent = true;
   if (rank == root) {
     for (int r = 0; r < nranks; ++r) {
-      if (!all[2ull * r]) continue;
+      if (!all[3ull * r]) continue;
       uint8_t* dst = (uint8_t*)buf.p + off[r];
       if (r == root)
         sent = sent && hipMemcpyAsync(dst, block, bytes, hipMemcpyDeviceToDevice, st) == hipSuccess;
       else
-        sent = sent && K.R->Recv(dst, all[2ull * r], ncclUint8, r, K.c, st) == ncclSuccess;
+        sent = sent && K.R->Recv(dst, all[3ull * r], ncclUint8, r, K.c, st) == ncclSuccess;
     }
   } else if (bytes) {
     sent = K.R->Send(block, bytes, ncclUint8, root, K.c, st) == ncclSuccess;
@@ -283,7 +289,7 @@ static int gather_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes
     if (off[nranks] && hipMemcpy(host.data(), buf.p, off[nranks], hipMemcpyDeviceToHost) != hipSuccess) fst = CASK_E_DEVICE;
     if (fst == CASK_OK && cask_abi::take_inject(ctx, cask_abi::kInjFold)) fst = CASK_E_NOMEM;
     for (int r = 0; r < nranks && fst == CASK_OK; ++r)
-      if (all[2ull * r]) fst = cask_keydir_merge(db, host.data() + off[r], all[2ull * r]);
+      if (all[3ull * r]) fst = cask_keydir_merge(db, host.data() + off[r], all[3ull * r]);
   }
   return agree(K, st, fst);
 }

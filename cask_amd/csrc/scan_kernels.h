@@ -202,6 +202,10 @@ constexpr uint32_t kTailSplit = CASK_TAIL_SPLIT_N;  // pieces per tail run (k_ru
 constexpr uint32_t kTailLong = CASK_TAIL_LONG;  // a tail piece's records at least this long go first
 constexpr uint32_t kTailMaxRecs = kWalkRun / kTailSplit * kWalkSlotCap;  // records a piece can hold
 constexpr uint32_t kTailBitWords = kTailMaxRecs / 32;
+// k_run_hash loads a piece's bit words one per lane and lists its records in LDS: a variant with
+// more words than lanes would leave records unhashed, so it must not compile
+static_assert(kTailBitWords <= 64, "a tail piece's long-record bits are loaded one word per lane");
+static_assert(4 * 2 * kTailMaxRecs * 2 <= 32768, "k_run_hash's tail lists outgrew their LDS budget");
 // Chunk mode: the short-halo geometry (kGeoShortHalo, a 1,008-B halo) when the records at the file
 // heads average at most kShortHaloMean bytes and none is longer than kShortHaloMax; else the wide
 // halo (kDefaultGeometry, 4,080 B). Speed only: a record that crosses the window goes to k_long.
@@ -270,6 +274,9 @@ void launch_run_hash(const ScanArgs& a, void* stream);
 uint64_t run_hash_waves();  // k_run_hash's persistent grid, in waves
 // after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
 void launch_hash_fix(const ScanArgs& a, void* stream);
+// the slot rows of a walk-mode call re-strided from a.slot_cap to cap_dst rows per chunk (the
+// repair path's exact chunk scans may write a chunk's full count)
+void launch_restride(const ScanArgs& a, uint32_t* dst, uint32_t cap_dst, void* stream);
 // k_walk.hip: record lengths at kProbeRegions points of every file, 3 u64 per point (k_probe_regions)
 constexpr uint32_t kProbeRegions = 8;
 constexpr uint32_t kStampWaves = 8192;  // diagnostic builds: waves with start/end stamps

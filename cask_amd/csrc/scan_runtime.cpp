@@ -54,6 +54,10 @@ struct DevBuf {
   }
   template <typename T>
   T* as() const { return (T*)p; }
+  void swap(DevBuf& o) {
+    std::swap(p, o.p);
+    std::swap(cap, o.cap);
+  }
 };
 
 struct HostPinned {
@@ -93,6 +97,7 @@ struct cask_ctx {
   // Members are destroyed in reverse order: every buffer is freed before the context goes.
   DevBuf chunk;      // spec | exit | base | tin (u64 x4) | count (u32) | tiles | long_r | desc | gbase
   DevBuf slots;      // 16-B slot rows, slot_cap per chunk
+  DevBuf slots_alt;  // walk mode's repair path: the slot rows re-strided to the full count
   DevBuf filebuf;    // FileDesc[] | call block (CallLayout) | file_err[] | first_bad[] | file_total[] | summary
   DevBuf err2;       // error detail words
   DevBuf gather;     // cask_read_entries_device: positions, sources and outputs of one batch
@@ -743,9 +748,20 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     if (!ok) return CASK_E_DEVICE;
   }
 
-  if (small_slots && (hc->slot_overflow || hc->any_invalid)) {
+  if (small_slots && hc->slot_overflow) {  // a chunk's rows were cut at kWalkSlotCap: redo in full
     c->full_slots_next = true;
     return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, hint);
+  }
+  if (small_slots && hc->any_invalid) {
+    // the repair path's exact chunk scans may write a chunk's full count: the rows found so far
+    // move to the full stride (every chunk's count is within kWalkSlotCap), and only the chunks
+    // validation flagged are scanned again
+    if (!c->slots_alt.ensure((total_chunks * (uint64_t)slot_full + 1) * 16)) return CASK_E_NOMEM;
+    launch_restride(a, c->slots_alt.as<uint32_t>(), slot_full, st);
+    L("k_restride");
+    c->slots.swap(c->slots_alt);
+    a.slots = c->slots.as<uint32_t>();
+    a.slot_cap = slot_full;
   }
   c->last_dense = 0;
   if (dense && !hc->any_invalid) {

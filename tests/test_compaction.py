@@ -249,6 +249,27 @@ def test_engine_compact_many_batches_matches_oracle(native, tmp_path, batch, mon
 
 
 @pytest.mark.gpu
+def test_engine_compact_into_many_output_files(native, tmp_path, monkeypatch):
+    """Over a hundred output files placed while the writer thread finishes earlier ones (4-KiB
+    files, small source batches): placement appends to the output list as the writer works through
+    the batch before, which must not disturb the files the writer holds. Files, stats and keydir
+    equal the oracle's."""
+    from cask_amd import CaskOptions
+    monkeypatch.setenv("CASK_COMPACT_BATCH", "40000")
+    rng = random.Random(77)
+    mfs = 4 << 10
+    path, ref = _both(tmp_path, _workload(rng, 9000, 3000, vmax=400), mfs)
+    rdb = R.replay(ref)
+    with CaskOptions().max_file_size(mfs).open(path) as db:
+        files = db.files()
+        rep = db.compact_files(files)
+        rc, rn = R.compact_files(ref, rdb, files, mfs)
+        assert rep["compacted"] == len(rc) and rep["new_files"] == len(rn)
+        assert len(rn) >= 100, len(rn)
+        _check_same(db, path, rdb, ref)
+
+
+@pytest.mark.gpu
 def test_engine_compact_failure_in_a_later_batch(native, tmp_path, monkeypatch):
     """A checksum failure in the last source file, with one file per batch: the earlier batches
     were already handed to the writer thread; the error is the reference's and every file the call

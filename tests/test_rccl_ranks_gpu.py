@@ -154,10 +154,11 @@ def test_gather_ranks_fold_equals_replay(fake_rccl, tmp_path, nranks, root):
             rk.close()
 
 
-@pytest.mark.parametrize("case", ["root_alloc", "bad_root", "root_fold"])
+@pytest.mark.parametrize("case", ["root_alloc", "bad_root", "root_mismatch", "root_fold"])
 def test_gather_failure_on_one_rank_is_agreed(fake_rccl, tmp_path, case):
-    """A root that cannot allocate the gathered blocks, one rank passing a root out of range, a root
-    whose fold fails: every rank returns the same status (rccl_gather.cpp agree()), none blocks."""
+    """A root that cannot allocate the gathered blocks, one rank passing a root out of range, one
+    rank naming a different (valid) root than the others, a root whose fold fails: every rank
+    returns the same status (rccl_gather.cpp agree()), none blocks."""
     lib = fake_rccl
     path = str(tmp_path / "db")
     _make_db(path, 50, nfiles=3)
@@ -165,9 +166,9 @@ def test_gather_failure_on_one_rank_is_agreed(fake_rccl, tmp_path, case):
     inj = {"root_alloc": {0: INJ_ROOT_ALLOC}, "root_fold": {0: INJ_FOLD}}.get(case, {})
     ranks = _setup(lib, path, nranks, inj)
     try:
-        roots = [0, 99 if case == "bad_root" else 0, 0]
+        roots = [0, {"bad_root": 99, "root_mismatch": 2}.get(case, 0), 0]
         res, took = _run_ranks(nranks, lambda r: ranks[r].gather(roots[r]))
-        want = {"root_alloc": -13, "bad_root": -10, "root_fold": -13}[case]
+        want = {"root_alloc": -13, "bad_root": -10, "root_mismatch": -10, "root_fold": -13}[case]
         assert [x[0] for x in res] == [want] * nranks
         assert max(took) < TIMEOUT_S / 2, took  # no rank waited for the stand-in to give up
         for x in res:
