@@ -59,6 +59,8 @@ def parse():
     ap.add_argument("--no-cold", action="store_true",
                     help="skip cold_call_ms (its calls over one file are small launches of the same kernels: "
                          "a profiled run without them has per-kernel averages over the full-size steps only)")
+    ap.add_argument("--no-shard-n1", action="store_true",
+                    help="N=1: skip configs4_shard_n1 (the N>1 lines' per-GPU shard timed on one GPU)")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the keydir gather + fold after the loop")
     ap.add_argument("--no-cfg5", action="store_true",
                     help="N>1: skip the cfg5 shard (290-B records) scan + key-hash partitioned keydir")
@@ -117,12 +119,25 @@ def cpu_baseline(files, nfiles: int, cfg: str):
         O.replay_fast(buf, paths[0][0], ix2)
         dt_fast = time.perf_counter() - t1
         del ix, ix2, buf
-        hosts = [np.fromfile(p, dtype=np.uint8) for _, p in paths]
+        # N cores: the sample cut at record boundaries into one independent data file per thread (a
+        # file's records are a chain walked in order, cask.rs:348 / log.rs:403-429: one thread per
+        # file, as the GPU path gives one lane per run), each piece with its own file id
         ncores = max(1, min(16, len(os.sched_getaffinity(0))))
+        per = -(-ncores // len(paths))
+        hosts, hids = [], []
+        for fid, p in paths:
+            b = np.fromfile(p, dtype=np.uint8)
+            starts = O.scan(b)["pos"].astype(np.int64)
+            cuts = [0] + [int(starts[np.searchsorted(starts, b.size * k // per)]) for k in range(1, per)] + [b.size]
+            for k in range(per):
+                if cuts[k + 1] > cuts[k]:
+                    hosts.append(b[cuts[k]:cuts[k + 1]])
+                    hids.append(len(hids) + 1)
         t2 = time.perf_counter()
-        pr, _ = O.replay_parallel(hosts, [fid for fid, _ in paths], ncores)
+        pr, _ = O.replay_parallel(hosts, hids, ncores)
         dt_par = time.perf_counter() - t2
         assert pr.err_kind == 0 and pr.records == recs, (pr.err_kind, pr.records, recs)
+        npieces = len(hosts)
         del hosts
     finally:
         for name in os.listdir(tmp):
@@ -145,11 +160,9 @@ def cpu_baseline(files, nfiles: int, cfg: str):
         "seconds": dt, "host_cpu": cpu, "nproc": os.cpu_count(),
         "fast_restatement_gibps_1core": files[0].data.numel() / dt_fast / 2 ** 30,
         "fast_restatement_gibps_Ncores": total / dt_par / 2 ** 30, "fast_restatement_cores": ncores,
-        # BASELINE.md:43 names N = nproc; this box's share per GPU is 16 of them (the pool's rule), so
-        # the nproc figure is the 16-core measurement scaled linearly — an upper bound, not a run
-        "fast_restatement_gibps_nproc_projected": total / dt_par / 2 ** 30 * (os.cpu_count() or ncores) / ncores,
-        "fast_restatement_nproc_note": (f"measured on {ncores} threads (the box's CPU share per GPU); "
-                                        f"nproc = {os.cpu_count()} projected linearly from it, not run"),
+        "fast_restatement_Ncores_sample": (f"the same {total} B cut at record boundaries into {npieces} data "
+                                           f"files, replayed on {ncores} threads (the box's CPU share per GPU; "
+                                           f"nproc {os.cpu_count()} is not this process's to use)"),
     }
 
 
@@ -260,6 +273,38 @@ def cfg1_secondary(ctx, torch, dev, steps):
     out = {"gibps": nb * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps, "kernel": "k_scan_chunks",
            "kernel_ms_avg": k, "kernel_frac_of_8TBps": nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS, "bytes": nb}
     del fs, views, rows
+    torch.cuda.empty_cache()
+    return out
+
+
+def cfg4_shard_n1_secondary(ctx, torch, dev, steps):
+    """N = 1, reported beside the metric: the exact per-rank workload of the N > 1 lines (rank 0's
+    configs[4] shard: 32 data files of up to 1 GiB, configs[2]'s record distribution, the same
+    generator seed, file ids and sequences), timed on this one GPU the same way — so that a 1 -> N
+    efficiency computed from this point has no file-shape term (configs[2] at N = 1 is 17 files of
+    2 GiB)."""
+    from cask_amd.workloads import zipf_files
+    files, vsz, n, rl = zipf_files(ctx, CFG4_FILES_PER_RANK * (CFG4_FILE - CFG2_MAX_RECORD) / 2 ** 30, CFG4_FILE,
+                                   seed=0x5A1F, first_file_id=1, first_seq=1, first_key=0)
+    assert len(files) == CFG4_FILES_PER_RANK, (len(files), CFG4_FILES_PER_RANK)
+    torch.cuda.synchronize(dev)
+    views = [(f.file_id, f.data) for f, _ in files]
+    rows = ctx.alloc_rows(n + 16)
+    res = ctx.scan_device(views, rows)
+    assert res.count == n, (res.count, n)
+    check_rows(torch, rows, res, files, vsz, rl, 1)
+    run, timings = ctx.prepare_scan(views, rows)
+    for _ in range(3):
+        run()
+    el, tt = time_loop(torch, dev, run, timings, steps, lambda: torch.cuda.synchronize(dev), None, "nccl")
+    nb = sum(f.data.numel() for f, _ in files)
+    k = sum(t[1] for t in tt) / len(tt)
+    out = {"workload": "configs[4] shard of rank 0: 32 x 1 GiB data files, configs[2]'s record distribution "
+                       "(the N > 1 lines' per-GPU workload, timed at N = 1)",
+           "files": len(files), "records": n, "bytes": nb,
+           "gibps": nb * steps / el / 2 ** 30, "ms_per_step": el * 1e3 / steps, "steps": steps,
+           "kernel": "k_run_hash", "kernel_ms_avg": k, "kernel_frac_of_8TBps": nb / (k * 1e-3) / 1e9 / HBM_PEAK_GBPS}
+    del files, vsz, rl, views, rows, res
     torch.cuda.empty_cache()
     return out
 
@@ -646,11 +691,15 @@ def main():
         cpu = cpu_baseline([f for f, _ in files], max(1, min(args.cpu_sample_files, len(files))), cfg)
         line["cpu_baseline"] = cpu
 
-    if rank == 0 and world == 1 and not args.no_cfg1:
+    if rank == 0 and world == 1 and not (args.no_cfg1 and args.no_shard_n1):
         res = None
         rows = views = None
-        files = None
+        files = vsz = rl = None
+        run = timings = None
         torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_shard_n1:
+        secondary(extra, "configs4_shard_n1", lambda: cfg4_shard_n1_secondary(ctx, torch, dev, args.steps))
+    if rank == 0 and world == 1 and not args.no_cfg1:
         extra["configs1_secondary"] = cfg1_secondary(ctx, torch, dev, max(10, args.steps))
 
     if watchdog is not None:

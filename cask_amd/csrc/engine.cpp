@@ -712,6 +712,61 @@ struct EngineDev {
     return (rg ? rg : &ring)->d2h(ps) ? CASK_OK : CASK_E_DEVICE;
   }
 
+  // open() with the keydir built on the device: every batch's rows, appended in file order (the
+  // block needs the rows of all the scanned files at once; the data files stay resident anyway)
+  struct AllRows {
+    uint8_t* p = nullptr;
+    uint64_t cap = 0, n = 0;
+    ~AllRows() {
+      if (p) (void)hipFree(p);
+    }
+    static uint64_t a(uint64_t c, uint32_t w) { return (c * w + 255) & ~255ull; }
+    cask_rows view() const {
+      cask_rows r{};
+      r.capacity = cap;
+      r.count = n;
+      r.pos = (uint64_t*)p;
+      r.seq = (uint64_t*)(p + a(cap, 8));
+      r.vsz = (uint32_t*)(p + 2 * a(cap, 8));
+      r.ksz = (uint16_t*)(p + 2 * a(cap, 8) + a(cap, 4));
+      r.status = p + 2 * a(cap, 8) + a(cap, 4) + a(cap, 2);
+      return r;
+    }
+    // rows [0, m) of `src` after the n already here (the buffer grows by half again when short)
+    int append(const cask_rows& src, uint64_t m, hipStream_t st) {
+      if (n + m > cap) {
+        const uint64_t nc = std::max<uint64_t>(n + m, cap + cap / 2);
+        uint8_t* q = nullptr;
+        if (hipMalloc(&q, 2 * a(nc, 8) + a(nc, 4) + a(nc, 2) + nc + 256) != hipSuccess) return CASK_E_NOMEM;
+        AllRows grown;
+        grown.p = q;
+        grown.cap = nc;
+        if (n) {
+          const cask_rows o = view(), g = grown.view();
+          if (hipMemcpyAsync(g.pos, o.pos, 8 * n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+              hipMemcpyAsync(g.seq, o.seq, 8 * n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+              hipMemcpyAsync(g.vsz, o.vsz, 4 * n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+              hipMemcpyAsync(g.ksz, o.ksz, 2 * n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+              hipMemcpyAsync(g.status, o.status, n, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+              hipStreamSynchronize(st) != hipSuccess)
+            return CASK_E_DEVICE;
+        }
+        std::swap(p, grown.p);
+        std::swap(cap, grown.cap);
+      }
+      const cask_rows d = view();
+      if (m && (hipMemcpyAsync(d.pos + n, src.pos, 8 * m, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(d.seq + n, src.seq, 8 * m, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(d.vsz + n, src.vsz, 4 * m, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(d.ksz + n, src.ksz, 2 * m, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(d.status + n, src.status, m, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess))
+        return CASK_E_DEVICE;
+      n += m;
+      return CASK_OK;
+    }
+  };
+
   // Device rows sized from a guess (average record >= 48 B), once more at the exact count if short.
   int scan(const std::vector<cask_file_view>& v, std::vector<uint64_t>& row_off, cask_scan_error& se) {
     uint64_t total = 0;
@@ -1127,6 +1182,19 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
     vcut.push_back(views.size());
   }
   const size_t nbat = vcut.size() - 1;
+  // Every file scanned (no valid hint file): the keydir is reduced on the device — each batch's rows
+  // kept, and after the last batch one block of the whole replay (cask_shard_keydir: per key only the
+  // records that can decide the final keydir; configs[3]: a fifth of the records) that this thread
+  // merges (cask_keydir_merge + cask_keydir_finish, as the multi-GPU open folds its ranges' blocks)
+  // instead of folding every hint record. A replay that also has hint files folds on the host
+  // (CASK_OPEN_DEVFOLD=0, a test hook, forces the host fold).
+  const char* dfh = cask_knobs::hook("CASK_OPEN_DEVFOLD");
+  const bool dev_fold = !views.empty() && scan_idx.size() == nf && !(dfh && !strcmp(dfh, "0"));
+  std::vector<uint64_t> roff_all(views.size() + 1, 0);  // (dev_fold) each view's first row
+  EngineDev::AllRows all_rows;
+  std::vector<uint8_t> dblock;  // (dev_fold) the block, on the host
+  int dblock_st = CASK_E_IO;    // (dev_fold) CASK_OK once the block is here
+  bool dblock_done = false;
   struct Batch {
     RawBytes hb;                // hint bodies of the batch's files
     std::vector<uint64_t> fo;   // view k of the batch: hb[fo[k], fo[k + 1])
@@ -1203,12 +1271,39 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
           std::vector<uint64_t> ro(vb.size() + 1);
           int ds = ed->scan(vb, ro, bat[b].se);
           if (ds == CASK_OK) ds = ed->hints(vb, ro, bat[b].hb, bat[b].fo);
+          if (ds == CASK_OK && dev_fold && !bat[b].se.kind) {  // the batch's rows, kept for the block
+            for (size_t k = 0; k <= vb.size(); ++k) roff_all[vcut[b] + k] = all_rows.n + ro[k];
+            ds = all_rows.append(ed->r, ro[vb.size()], (hipStream_t)cask_ctx_stream(ed->ctx));
+          }
           return ds;
         });
       }
       t_dev += ms_since(td);
       mark(b, st, true);
     }
+    // (dev_fold) every batch scanned clean: the replay's block, reduced on the device, to the host
+    bool clean = dev_fold;
+    for (size_t b = 0; b < nbat && clean; ++b) clean = bat[b].st == CASK_OK && !bat[b].se.kind && !stop.load();
+    int bs = CASK_E_IO;
+    if (clean) {
+      const auto td = std::chrono::steady_clock::now();
+      bs = abi_status([&] {
+        const cask_rows r = all_rows.view();
+        const void* blk = nullptr;
+        uint64_t nb = 0;
+        int st = cask_shard_keydir(ed->ctx, views.data(), (uint32_t)views.size(), &r, roff_all.data(), &blk, &nb);
+        if (st != CASK_OK) return st;
+        dblock.resize(nb);
+        return ed->to_host(dblock.data(), (const uint8_t*)blk, nb);
+      });
+      t_dev += ms_since(td);
+    }
+    {
+      std::lock_guard<std::mutex> g(bm);
+      dblock_st = bs;
+      dblock_done = true;
+    }
+    bcv.notify_all();
   };
   std::thread th_read, th_dev;
   bool threaded = false;
@@ -1232,6 +1327,7 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
     }
   } else {
     for (size_t b = 0; b < nbat; ++b) bat[b].read_done = bat[b].ready = true;
+    dblock_done = true;
   }
   auto join_all = [&]() {
     stop = true;
@@ -1294,7 +1390,9 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
       }
     }
     const unsigned nt = std::max(1u, std::min<unsigned>(ntb, (unsigned)std::max<size_t>(fe - fi, 1)));
-    parallel_for(nt, [&](unsigned t) {
+    // (dev_fold: the bodies were built on the device from the scan's rows — whole records, and the
+    // block carries the highest sequence — so only their hint files are written below)
+    if (!dev_fold) parallel_for(nt, [&](unsigned t) {
       for (size_t i = fi + t; i < fe; i += nt) {
         Body& B = bodies[i];
         B.cut.clear();
@@ -1376,12 +1474,31 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
     // Index::update + Stats over the batch's records (their keys stay in hints[] / the batch's
     // bodies until here)
     auto tf2 = std::chrono::steady_clock::now();
-    parallel_fold(srcs, db->index, &fscratch);
+    if (!dev_fold) parallel_fold(srcs, db->index, &fscratch);
     t_fold += ms_since(tf2);
     RawBytes().p.swap(bat[b].hb.p);  // (the batch's bodies are no longer needed)
     for (size_t i = fi; i < fe; ++i)
       if (use_hint[i]) std::vector<uint8_t>().swap(hints[i]);
     fi = fe;
+  }
+  if (dev_fold && fail == CASK_OK) {  // the whole replay's block, merged in one fold
+    auto tf3 = std::chrono::steady_clock::now();
+    {
+      std::unique_lock<std::mutex> lk(bm);
+      bcv.wait(lk, [&] { return dblock_done; });
+    }
+    int st = dblock_st;
+    if (st == CASK_OK) {
+      db->merging = true;
+      st = cask_keydir_merge(db, dblock.data(), dblock.size());
+      if (st == CASK_OK) st = cask_keydir_finish(db);
+    }
+    std::vector<uint8_t>().swap(dblock);
+    if (st != CASK_OK) {
+      fail = st;
+      fail_fid = 0;
+    }
+    t_fold += ms_since(tf3);
   }
   join_all();
   edlock = std::unique_lock<std::mutex>();
@@ -2685,28 +2802,29 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
     sh[r].hi = nf * (size_t)(r + 1) / (size_t)ndev;
   }
   const bool write_hints = db->opts.write_hints != 0;
-  // one stretch [lo, hi) of files of one kind on device `dev`; false on failure (s.e set)
-  auto run_stretch = [&](Shard& s, int dev, cask_ctx* ctx, size_t lo, size_t hi, bool hint) -> bool {
+  // one stretch [lo, hi) of files of one kind on device `dev` (its EngineDev `ed`, locked by the
+  // caller: its pinned ring reads data files to the device); false on failure (s.e set)
+  auto run_stretch = [&](Shard& s, int dev, EngineDev* ed, cask_ctx* ctx, size_t lo, size_t hi, bool hint) -> bool {
     auto fail = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
       s.e = cask_open_error{st, fid, pos, e, f};
       return false;
     };
     auto tr = std::chrono::steady_clock::now();
     const size_t n = hi - lo;
-    std::vector<std::vector<uint8_t>> data(n);
     std::vector<uint64_t> blen(n);
+    std::vector<std::string> paths;
     uint64_t total = 0;
     for (size_t i = 0; i < n; ++i) {
       if (hint) {
         blen[i] = hints[lo + i].size() - 4;  // the body: Take(size - 4) (log.rs:129)
-      } else {
-        if (!read_file(data_path(path, db->files[lo + i]), data[i])) return fail(CASK_E_IO, db->files[lo + i]);
-        blen[i] = data[i].size();
+      } else {  // File::open + metadata (log.rs:190-196): a file that cannot be read is its Io error
+        struct stat stt;
+        paths.push_back(data_path(path, db->files[lo + i]));
+        if (stat(paths.back().c_str(), &stt) != 0) return fail(CASK_E_IO, db->files[lo + i]);
+        blen[i] = (uint64_t)stt.st_size;
       }
       total += (blen[i] + 255) & ~255ull;
     }
-    s.ms_read += ms_since(tr);
-    auto ts = std::chrono::steady_clock::now();
     uint8_t* dbuf = nullptr;
     void* drows = nullptr;
     uint8_t* dhint = nullptr;
@@ -2724,27 +2842,49 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
     std::vector<cask_file_view> views(n);
     uint64_t off = 0;
     for (size_t i = 0; i < n; ++i) {
-      const uint8_t* src = hint ? hints[lo + i].data() : data[i].data();
-      if (blen[i] && hipMemcpy(dbuf + off, src, blen[i], hipMemcpyHostToDevice) != hipSuccess) return fail(CASK_E_DEVICE);
       views[i] = cask_file_view{db->files[lo + i], CASK_VIEW_DEVICE, dbuf + off, blen[i]};
       off += (blen[i] + 255) & ~255ull;
     }
+    if (hint) {  // (the bodies are in host memory already)
+      for (size_t i = 0; i < n; ++i)
+        if (blen[i] && hipMemcpy((void*)views[i].data, hints[lo + i].data(), blen[i], hipMemcpyHostToDevice) != hipSuccess)
+          return fail(CASK_E_DEVICE);
+    } else {  // the data files straight to the device: reader threads through the pinned ring
+      std::vector<char> ok(n, 1);
+      const int rs = ed->read_to_device(paths, views, ok);
+      if (rs != CASK_OK) return fail(rs);
+      for (size_t i = 0; i < n; ++i)
+        if (!ok[i]) return fail(CASK_E_IO, db->files[lo + i]);
+    }
+    s.ms_read += ms_since(tr);
+    auto ts = std::chrono::steady_clock::now();
+    // rows sized from a guess (records of at least 48 B, as EngineDev::scan; hint records are at
+    // least 22 B), and once more at the exact count if that was short
     const uint64_t bound = cask_rows_bound(views.data(), (uint32_t)n);
-    const uint64_t a8 = (bound * 8 + 255) & ~255ull, a4 = (bound * 4 + 255) & ~255ull, a2 = (bound * 2 + 255) & ~255ull;
-    if (hipMalloc(&drows, 2 * a8 + a4 + a2 + bound + 256) != hipSuccess) return fail(CASK_E_DEVICE);
-    uint8_t* rb = (uint8_t*)drows;
+    uint64_t cap = std::min<uint64_t>(bound, total / (hint ? 22 : 48) + n + 1024);
     cask_rows rows{};
-    rows.capacity = bound;
-    rows.pos = (uint64_t*)rb;
-    rows.seq = (uint64_t*)(rb + a8);
-    rows.vsz = (uint32_t*)(rb + 2 * a8);
-    rows.ksz = (uint16_t*)(rb + 2 * a8 + a4);
-    rows.status = rb + 2 * a8 + a4 + a2;
     std::vector<uint64_t> roff(n + 1);
     cask_scan_error se{};
-    int st = hint ? cask_parse_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se)
-                  : cask_scan_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
-    if (st != CASK_OK) return fail(st);
+    int st = CASK_E_CAPACITY;
+    for (int attempt = 0; attempt < 2 && st == CASK_E_CAPACITY; ++attempt) {
+      if (drows) (void)hipFree(drows);
+      drows = nullptr;
+      const uint64_t a8 = (cap * 8 + 255) & ~255ull, a4 = (cap * 4 + 255) & ~255ull, a2 = (cap * 2 + 255) & ~255ull;
+      if (hipMalloc(&drows, 2 * a8 + a4 + a2 + cap + 256) != hipSuccess) return fail(CASK_E_NOMEM);
+      uint8_t* rb = (uint8_t*)drows;
+      rows = cask_rows{};
+      rows.capacity = cap;
+      rows.pos = (uint64_t*)rb;
+      rows.seq = (uint64_t*)(rb + a8);
+      rows.vsz = (uint32_t*)(rb + 2 * a8);
+      rows.ksz = (uint16_t*)(rb + 2 * a8 + a4);
+      rows.status = rb + 2 * a8 + a4 + a2;
+      se = cask_scan_error{};
+      st = hint ? cask_parse_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se)
+                : cask_scan_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
+      cap = rows.count;
+    }
+    if (st != CASK_OK) return fail(st == CASK_E_CAPACITY ? CASK_E_DEVICE : st);
     if (!hint && write_hints) {  // RecreateHints (log.rs:137-148): every Ok row of each file, trailer
       std::vector<uint64_t> fo(n + 1, 0);
       st = cask_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), nullptr, 0, fo.data());
@@ -2781,8 +2921,14 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
   auto run_shard = [&](int r) {
     Shard& s = sh[r];
     if (s.lo == s.hi) return;
-    int st = CASK_OK;
-    cask_ctx* ctx = cask_ctx_create(devices[r], &st);
+    EngineDev* ed = engine_dev(devices[r]);  // (its pinned ring, for the reads; one user at a time)
+    if (!ed) {
+      s.e = cask_open_error{CASK_E_DEVICE, 0, 0, 0, 0};
+      return;
+    }
+    std::lock_guard<std::mutex> edg(ed->mu);
+    int st = ed->prepare();
+    cask_ctx* ctx = st == CASK_OK ? cask_ctx_create(devices[r], &st) : nullptr;
     if (!ctx) {
       s.e = cask_open_error{st, 0, 0, 0, 0};
       return;
@@ -2791,7 +2937,7 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
       size_t j = i + 1;
       while (j < s.hi && use_hint[j] == use_hint[i]) ++j;
       // (an exception in a stretch is its failure, so the context is still destroyed below)
-      const int st = abi_status([&] { return run_stretch(s, devices[r], ctx, i, j, use_hint[i] != 0) ? CASK_OK : 1; });
+      const int st = abi_status([&] { return run_stretch(s, devices[r], ed, ctx, i, j, use_hint[i] != 0) ? CASK_OK : 1; });
       if (st != CASK_OK) {
         if (st != 1) s.e = cask_open_error{st, 0, 0, 0, 0};
         break;

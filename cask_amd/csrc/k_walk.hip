@@ -108,11 +108,18 @@ static_assert(kChaseUse == kWalkHashMax, "the walker hashes records that fit its
 constexpr uint32_t kSwNL = CASK_SW_NL, kSwWin = kSwNL * 1024, kSwUse = kSwWin - 16, kSwStep = kSwUse - 18;
 constexpr uint32_t kSwDw = 4 * kSwNL;  // dwords of candidate bytes per lane per window (64 x 32 x 4 >= kSwStep)
 static_assert(64 * kSwDw * 4 >= kSwStep, "every candidate byte of a window is scanned");
+#ifndef CASK_SW_PROBE  // (A/B variant: 0 = no chain probe)
+#define CASK_SW_PROBE 16
+#endif
+constexpr uint32_t kProbeHops = CASK_SW_PROBE;  // phase 3: headers a long candidate's chain is followed for
 struct SearchLdsSw {
   uint32_t wins[1][kSwWin / 4 + 16];
   uint32_t cand[16];
   uint32_t nl;
   uint32_t pad[3];
+  // phase 3: a round's short records reached from long candidates (file offset, length, candidate)
+  uint64_t pp[16];
+  uint32_t prl[16], pcx[16];
   // long candidates as offsets from the run's first byte (x - b0 and x + rl - b0: both within the
   // run and kSearchPast past it, far below 2^32), 2 KiB instead of 4: more searching waves per CU
   uint32_t lx[kLongList], le[kLongList];
@@ -127,6 +134,7 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
   uint64_t kA = kNone;
   if (lane == 0) L.nl = 0;
   bool over = false;
+  uint32_t nl0 = 0;  // long candidates already followed by phase 3
   // (staging the next window into registers while this one is searched measured no faster: 207
   // VGPRs, 2 waves per SIMD instead of 3)
   for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kSwStep) {
@@ -239,6 +247,81 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
       if (mo) break;
     }
     WADD(3, tw2)
+    // phase 3 (no short record of this window verified): each long candidate listed from this
+    // window has its chain followed header to header (a lane each, one 16-B load per hop:
+    // Entries::next, log.rs:403-429) to the first record of at most sshort bytes, within the horizon;
+    // the lowest candidate whose chain reaches a record whose XXH32 matches is the start, as the
+    // windows scanned one by one would find it — that record is the first short one after the
+    // candidate, and the hop back below reaches the candidate from it. A stretch of 64-KiB records
+    // then costs a few dependent loads instead of a window per 8 KiB. A false candidate (value bytes
+    // that look like a header) lands on some true record start about once per mean record length
+    // of its random "length", and its chain would then verify too: each hop must also raise the
+    // sequence number by at most 2^32 (LogWriter appends records in sequence order: cask.rs:132-136,
+    // log.rs:282-306), which random bytes pass about once in 2^32. A log whose sequence numbers do
+    // not rise along a chain (a compaction's tombstone tail) is scanned window by window as before.
+    // (Speed only: any start taken is checked by k_finish.)
+    if (kProbeHops && kA == kNone) {
+      __syncthreads();
+      const uint32_t n1 = L.nl < kLongList ? L.nl : kLongList;
+      uint64_t best = kNone;  // (uniform) the lowest verified candidate, as an offset from b0
+      for (uint32_t c0 = nl0; c0 < n1; c0 += 64) {
+        const uint32_t ci = c0 + lane;
+        uint64_t tp = kNone;
+        uint32_t trl = 0;
+        if (ci < n1) {
+          uint64_t p = b0 + L.le[ci];
+          // the candidate's sequence number, from its header in this window
+          uint64_t sq = lds_hdr(W, x0 + (uint32_t)(b0 + L.lx[ci] - wb)).seq;
+          for (uint32_t hop = 0; hop < kProbeHops; ++hop) {
+            if (p >= lim || p + 18 > len) break;
+            const u32x4 hd = gld16g((const g_u8*)(data + p + 2));  // header bytes 2..17
+            const uint32_t ksz = hd.z >> 16, vsz = hd.w;
+            const uint64_t sn = (uint64_t)fun(hd.x, hd.y, 2) | ((uint64_t)fun(hd.y, hd.z, 2) << 32);
+            if (ksz > 4351u || ((vsz >> 24) != 0u && vsz != 0xFFFFFFFFu)) break;  // (not a record)
+            if (sn <= sq || sn - sq > (1ull << 32)) break;  // (sequence numbers rise along a log)
+            sq = sn;
+            const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
+            if (rl <= sshort) {
+              if (p + rl <= len) {
+                tp = p;
+                trl = (uint32_t)rl;
+              }
+              break;
+            }
+            p += rl;
+          }
+        }
+        // the reached records, 16 per round (a quad each), in candidate-list order
+        const unsigned long long hm = __ballot(tp != kNone);
+        const uint32_t nh = (uint32_t)__builtin_popcountll(hm);
+        const uint32_t rank = (uint32_t)__builtin_popcountll(hm & (lane ? (~0ull >> (64 - lane)) : 0ull));
+        for (uint32_t r0 = 0; r0 < nh; r0 += 16) {
+          if (tp != kNone && rank >= r0 && rank < r0 + 16) {
+            L.pp[rank - r0] = tp;
+            L.prl[rank - r0] = trl;
+            L.pcx[rank - r0] = L.lx[ci];
+          }
+          __syncthreads();
+          const uint32_t nq = nh - r0 < 16 ? nh - r0 : 16u;
+          uint64_t x = kNone;
+          if (q < nq) {
+            const uint64_t pq = L.pp[q];
+            const uint32_t rq = L.prl[q];
+            const uint32_t st = gld4g((const g_u8*)(data + pq));
+            const uint32_t h = quad_gbl_xxh32<2>(data + pq + 4, rq - 4, qa);
+            if (qa == 0 && h == st) x = L.pcx[q];
+          }
+          for (int s = 32; s; s >>= 1) {
+            const uint64_t y = __shfl_xor(x, s, 64);
+            x = y < x ? y : x;
+          }
+          best = x < best ? x : best;
+          __syncthreads();
+        }
+      }
+      nl0 = n1;
+      if (best != kNone) kA = b0 + best;
+    }
   }
   over = __any(over) || L.nl > kLongList;
   WST(th0)
@@ -653,7 +736,7 @@ void launch_walk_runs(const ScanArgs& a, void* stream) {
   hipLaunchKernelGGL(k_walk_runs, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
 }
 
-void launch_walk_search(const ScanArgs& a, void* stream) {
+void launch_walk_search(const ScanArgs& a, void* stream, int cus) {
   const uint64_t nruns = launch_runs(a);
   if (!a.total_chunks || !nruns) return;
   // A persistent grid of exactly the resident workgroups (LDS-bound: ~12 per CU): a workgroup
@@ -666,7 +749,7 @@ void launch_walk_search(const ScanArgs& a, void* stream) {
     else if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_walk_search, 64, 0) == hipSuccess && nb > 0) per_cu = nb;
     if (per_cu <= 0) per_cu = 12;
   }
-  uint64_t grid = (uint64_t)device_cus() * (uint64_t)per_cu;
+  uint64_t grid = (uint64_t)(cus > 0 ? cus : device_cus()) * (uint64_t)per_cu;
   if (grid > nruns) grid = nruns;
   hipLaunchKernelGGL(k_walk_search, dim3((uint32_t)grid), dim3(64), 0, (hipStream_t)stream, a, a.files);
 }

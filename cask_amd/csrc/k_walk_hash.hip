@@ -825,11 +825,12 @@ uint64_t run_hash_waves() {
   return (uint64_t)device_cus() * (uint64_t)per_cu;
 }
 
-void launch_run_hash(const ScanArgs& a, void* stream) {
+void launch_run_hash(const ScanArgs& a, void* stream, int cus) {
   if (!a.total_chunks) return;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
   uint64_t waves = run_hash_waves();
+  if (cus > 0) waves = waves / (uint64_t)device_cus() * (uint64_t)cus;
   if (const char* e = cask_knobs::tune("CASK_HASH_WAVES_PER_CU")) waves = (uint64_t)device_cus() * (uint64_t)atoi(e);
   if (waves > nruns) waves = nruns;
   hipLaunchKernelGGL(k_run_hash, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);

@@ -265,12 +265,13 @@ int hint_pack(void* scratch, const FileDesc* files_host, uint32_t nfiles, const 
               uint64_t n, uint8_t* out, uint64_t cap, uint64_t* file_start, void* stream);
 void launch_walk(const ScanArgs& a, const uint64_t* summary, void* stream);
 void launch_walk_runs(const ScanArgs& a, void* stream);  // k_walk.hip: hint bodies (cask_parse_hints_device)
-void launch_walk_search(const ScanArgs& a, void* stream);  // k_walk.hip: each walk run's speculative start
+// (cus: the compute units the launch's stream may use, for its persistent grid; 0 = all of them)
+void launch_walk_search(const ScanArgs& a, void* stream, int cus = 0);  // k_walk.hip: each walk run's speculative start
 // k_walk_hash.hip: k_walk_chase (a lane per run of a.run chunks chases the record
 // headers: slot rows, chunk table, cdesc), then k_run_hash (a wave per claimed run, a quad per record:
 // every record hashed from HBM, whole 128-B lines per load instruction)
 void launch_walk_chase(const ScanArgs& a, void* stream);
-void launch_run_hash(const ScanArgs& a, void* stream);
+void launch_run_hash(const ScanArgs& a, void* stream, int cus = 0);
 uint64_t run_hash_waves();  // k_run_hash's persistent grid, in waves
 // after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
 void launch_hash_fix(const ScanArgs& a, void* stream);

@@ -93,6 +93,7 @@ struct cask_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t side = nullptr;  // walk mode: k_finish beside k_run_hash
+  hipStream_t masked[2] = {};  // diagnostic builds: streams held to some of the CUs (CASK_HASH_CUS, CASK_PRE_CUS)
   hipStream_t stream = nullptr;
   // Members are destroyed in reverse order: every buffer is freed before the context goes.
   DevBuf chunk;      // spec | exit | base | tin (u64 x4) | count (u32) | tiles | long_r | desc | gbase
@@ -164,6 +165,8 @@ struct cask_ctx {
     if (kd) kd_scratch_destroy(kd);
     if (own) (void)hipStreamDestroy(own);
     if (side) (void)hipStreamDestroy(side);
+    for (hipStream_t m : masked)
+      if (m) (void)hipStreamDestroy(m);
     if (evf) (void)hipEventDestroy(evf);
   }
 };
@@ -685,9 +688,33 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     as.run_lo = 0;
     as.run_hi = nruns;
     if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
-    launch_walk_search(as, st);
+    // CASK_PRE_CUS / CASK_HASH_CUS (tuning knobs, diagnostics): the search + chase, or the hash, on a
+    // stream held to that many CUs (hipExtStreamCreateWithCUMask, the excluded ones spread evenly),
+    // each grid sized for them — what reserving CUs for an overlapped pre-hash would cost each side
+    static const int pre_cus = cask_knobs::tune("CASK_PRE_CUS") ? atoi(cask_knobs::tune("CASK_PRE_CUS")) : 0;
+    static const int hash_cus = cask_knobs::tune("CASK_HASH_CUS") ? atoi(cask_knobs::tune("CASK_HASH_CUS")) : 0;
+    auto masked = [&](int k, int ncu) -> hipStream_t {
+      const int all = device_cus();
+      if (ncu <= 0 || ncu >= all) return st;
+      if (!c->masked[k]) {
+        std::vector<uint32_t> m((all + 31) / 32, 0u);
+        for (int i = 0, kept = 0; i < all; ++i)
+          if ((int64_t)(i + 1) * ncu / all > kept) {  // ncu of the all bits, spread evenly
+            m[i / 32] |= 1u << (i % 32);
+            ++kept;
+          }
+        if (hipExtStreamCreateWithCUMask(&c->masked[k], (uint32_t)m.size(), m.data()) != hipSuccess) c->masked[k] = nullptr;
+      }
+      return c->masked[k] ? c->masked[k] : st;
+    };
+    hipStream_t ps = masked(0, pre_cus), hs = masked(1, hash_cus);
+    if (ps != st) {
+      H(hipEventRecord(c->evw, st));
+      H(hipStreamWaitEvent(ps, c->evw, 0));
+    }
+    launch_walk_search(as, ps, ps != st ? pre_cus : 0);
     L("k_walk_search");
-    H(hipEventRecord(c->ev[6], st));
+    H(hipEventRecord(c->ev[6], ps));
     a.walk_pre = 1;
     a.cdesc = c->cdesc.as<uint64_t>();
     // The hash's tail: the last runs, in pieces whose long records are hashed before
@@ -704,10 +731,18 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       if (!c->tbits.ensure(4ull * kTailBitWords * kTailSplit * a.hash_ntail + 256)) return CASK_E_NOMEM;
       a.tbits = c->tbits.as<uint32_t>();
     }
-    launch_walk_chase(a, st);
+    launch_walk_chase(a, ps);
     L("k_walk_chase");
-    H(hipEventRecord(c->ev[7], st));
-    launch_run_hash(a, st);
+    H(hipEventRecord(c->ev[7], ps));
+    if (ps != st) H(hipStreamWaitEvent(st, c->ev[7], 0));
+    if (hs != st) {
+      H(hipStreamWaitEvent(hs, c->ev[7], 0));
+      launch_run_hash(a, hs, hash_cus);
+      H(hipEventRecord(c->evw, hs));
+      H(hipStreamWaitEvent(st, c->evw, 0));
+    } else {
+      launch_run_hash(a, st);
+    }
     L("k_run_hash");
     // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
     // starts): on a side stream it runs in the slots the hash's last waves leave, and k_hash_fix

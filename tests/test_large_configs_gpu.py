@@ -1,8 +1,9 @@
 """BASELINE configs[3] and configs[4] at full size on one MI355X, checked against the C oracle.
 
 configs[3] (compaction merge, 64 x 1,073,741,820 B with 80 % of the records overwritten or deleted):
-the files are generated on the device and written to /dev/shm, opened by the product (scan + hint
-files), compacted by the product (cask_db_compact_files) and by the oracle's restatement of
+the files are generated on the device and written to /dev/shm, opened by cask_db_open_multi over two
+ranges on the one device and by the product's open (scan, keydir reduced on the device, hint files) —
+each keydir's digest, stats and sequence against the oracle's threaded replay —, compacted by the product (cask_db_compact_files) and by the oracle's restatement of
 Cask::compact_files_aux (orc_compact_files_fn, cask.rs:451-523) from the same directory before it:
 every new data and hint file must be byte-identical (the live region in file order; the tombstone
 tail, whose order the reference leaves to a HashMap, in first-seen order on both sides — checked as a
@@ -129,11 +130,35 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
         del kid, vsz
         torch.cuda.empty_cache()
         ids = list(range(1, nfiles + 1))
-        # the product's open: scan on the device, hint files recreated (they must be the oracle's)
+        maps = [np.memmap(os.path.join(path, f"{i:010}.cask.data"), np.uint8, "r") for i in ids]
+        # the oracle's keydir (threaded replay), kept for the liveness of its compaction below
+        _say("cfg3: oracle replay")
+        pix = _beat("cfg3 oracle replay", O.PIndex, maps, ids, THREADS)
+        assert pix.result.err_kind == 0 and pix.result.live == live_want
+        # cask_db_open_multi over two ranges of the files on this one device (32 x 1 GiB each, read
+        # to the device by the pinned ring's threads, rows sized from the record estimate), no hint
+        # files written: keydir digest, stats and sequence equal the oracle's
+        from cask_amd.keydir import open_multi
+        _say("cfg3: open_multi devices=[0, 0]")
+        t_m = time.time()
+        with _beat("cfg3 open_multi", open_multi, path, [ctx.device, ctx.device],
+                   CaskOptions().max_file_size(1 << 30).write_hints(False)) as mdb:
+            _say(f"cfg3: open_multi took {time.time() - t_m:.2f} s")
+            dg, nk = _beat("cfg3 open_multi digest", _digest_of_export, mdb)
+            assert nk == live_want and dg == pix.result.digest
+            assert _stats_rows(mdb) == pix.stats
+            assert mdb.current_sequence == pix.result.max_seq + 1
+        assert not any(f.endswith(".cask.hint") for f in os.listdir(path))
+        # the product's open: scan on the device, keydir reduced there (every file scanned), hint
+        # files recreated (they must be the oracle's)
         _say("cfg3: product open")
+        t_o = time.time()
         with CaskOptions().max_file_size(1 << 30).open(path) as db:
+            _say(f"cfg3: open took {time.time() - t_o:.2f} s")
             assert len(db) == live_want
-            maps = [np.memmap(os.path.join(path, f"{i:010}.cask.data"), np.uint8, "r") for i in ids]
+            dg, nk = _beat("cfg3 open digest", _digest_of_export, db)
+            assert nk == live_want and dg == pix.result.digest
+            assert db.current_sequence == pix.result.max_seq + 1
 
             def check_hint(i, m):  # (the oracle's C calls drop the GIL: files checked on threads)
                 hb = np.fromfile(os.path.join(path, f"{i:010}.cask.hint"), np.uint8)
@@ -148,10 +173,8 @@ def test_cfg3_full_size_compaction_against_oracle(gpu_ctx):
                     assert ok, i
                     if i % 16 == 0:
                         _say(f"cfg3: hint file {i} checked")
-            _say("cfg3: hint files checked; oracle replay")
-            # the oracle's keydir (threaded replay) and its compaction of the same files, first
-            pix = _beat("cfg3 oracle replay", O.PIndex, maps, ids, THREADS)
-            assert pix.result.err_kind == 0 and pix.result.live == live_want
+            _say("cfg3: hint files checked")
+            # the oracle's compaction of the same files, first
             assert pix.stats == _stats_rows(db)
             want_dir = os.path.join(work, "oracle")
             os.makedirs(want_dir)

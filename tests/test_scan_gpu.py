@@ -120,13 +120,17 @@ def test_golden_rows_device(gpu_ctx, case):
     check_against_oracle(gpu_ctx, bufs, device=True)
 
 
-@pytest.mark.parametrize("par_fold", [False, True], ids=["fold", "sharded_fold"])
+@pytest.mark.parametrize("fold", ["devfold", "fold", "sharded_fold"])
 @pytest.mark.parametrize("case", golden_cases())
-def test_golden_engine_open(native, case, tmp_path, monkeypatch, par_fold):
+def test_golden_engine_open(native, case, tmp_path, monkeypatch, fold):
     """Cask::open on the fixture directory: keydir, stats, sequence or error, hint files — with the
-    fold on one thread and sharded by key hash over threads (CASK_PAR_FOLD_MIN=0 forces it), the
-    latter with every data file a pipeline batch of its own (read, scanned and folded in turn)."""
+    keydir reduced on the device and merged (the default when every file is scanned), and with the
+    host fold (CASK_OPEN_DEVFOLD=0) on one thread and sharded by key hash over threads
+    (CASK_PAR_FOLD_MIN=0 forces it); the last two with every data file a pipeline batch of its own
+    (read, scanned and folded in turn)."""
     from cask_amd import CaskOptions, errors
+    par_fold = fold != "fold"
+    monkeypatch.setenv("CASK_OPEN_DEVFOLD", "1" if fold == "devfold" else "0")
     monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if par_fold else str(1 << 62))
     if par_fold:  # and the hint bodies' copy to the host staged through the pinned ring
         monkeypatch.setenv("CASK_STAGE_MIN", "0")
@@ -166,9 +170,14 @@ def make_records(rng, n, ksz_fn, vsz_fn, seq0=1, tomb_p=0.0):
     return b"".join(out)
 
 
-def test_sharded_fold_matches_single_thread(native, tmp_path, monkeypatch):
+@pytest.mark.parametrize("batch", [None, "1"], ids=["batches", "file_batches"])
+def test_sharded_fold_matches_single_thread(native, tmp_path, monkeypatch, batch):
     """Many files of overwrites, stale and live tombstones and out-of-order sequences: the sharded
-    fold must give the single-thread fold's keydir, stats and sequence (Index::update, Stats)."""
+    fold and the device-reduced block merged on the host must give the single-thread fold's keydir,
+    stats and sequence (Index::update, Stats); the device path also with every file a batch of its
+    own (its rows gathered batch after batch into one block)."""
+    if batch:
+        monkeypatch.setenv("CASK_OPEN_BATCH", batch)
     from cask_amd import CaskOptions
     rng = random.Random(53)
     keys = [rng.randbytes(rng.randrange(0, 24)) for _ in range(700)]
@@ -188,14 +197,15 @@ def test_sharded_fold_matches_single_thread(native, tmp_path, monkeypatch):
         with open(R.data_file_path(str(d), fid), "wb") as f:
             f.write(b"".join(recs))
     got = []
-    for par in (False, True):
+    for par, devfold in ((False, "0"), (True, "0"), (False, "1")):
         for h in d.glob("*.cask.hint"):
-            h.unlink()  # both opens take the scan path
+            h.unlink()  # every open takes the scan path
         monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if par else str(1 << 62))
+        monkeypatch.setenv("CASK_OPEN_DEVFOLD", devfold)
         with CaskOptions().open(str(d)) as db:
             got.append((sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence] for k, e in db.index().items()),
                         sorted([f, *st] for f, st in db.stats().items()), db.current_sequence))
-    assert got[0] == got[1]
+    assert got[0] == got[1] == got[2]
     assert len(got[0][0]) > 100
 
 

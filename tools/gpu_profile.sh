@@ -17,7 +17,7 @@ if [ -z "$SKIP_BENCH" ]; then
   TAILN=1 step bench_full 600 python bench.py
 fi
 export TMPDIR=/tmp
-B="$R/bench.py --steps ${PSTEPS:-20} --warmup ${PWARM:-3} --no-cpu-baseline --no-e2e --no-cfg1 --no-cold"
+B="$R/bench.py --steps ${PSTEPS:-20} --warmup ${PWARM:-3} --no-cpu-baseline --no-e2e --no-cfg1 --no-shard-n1 --no-cold"
 rm -rf "$R/gpurun_out/prof_$TAG"
 TAILN=1 step prof_kt 600 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_$TAG/kt" -o kt --output-format csv -- python3 $B
 step prof_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$R/gpurun_out/prof_$TAG/fetch" -o fetch --output-format csv -- python3 $B

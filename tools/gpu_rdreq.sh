@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 TAG=${TAG:-r04a}
 O="$R/gpurun_out/rdreq_$TAG"
 rm -rf "$O"; mkdir -p "$O"
-B="$R/bench.py --steps ${PSTEPS:-4} --warmup 1 --no-cpu-baseline --no-e2e --no-cfg1"
+B="$R/bench.py --steps ${PSTEPS:-4} --warmup 1 --no-cpu-baseline --no-e2e --no-cfg1 --no-shard-n1"
 run() {  # run NAME TIMEOUT CMD...
   local name=$1 to=$2; shift 2
   echo "=== $name"; date

@@ -15,10 +15,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gib", type=float, default=32.0)
     ap.add_argument("--calls", type=int, default=3)
+    ap.add_argument("--lib", default=STAMPS_LIB, help="a stamps build (make stamps, or a variant with -DCASK_STAMPS)")
     args = ap.parse_args()
     import torch
     import cask_amd
-    cask_amd._lib.use_library(STAMPS_LIB)
+    cask_amd._lib.use_library(args.lib)
     from cask_amd.workloads import zipf_files
     L = cask_amd.lib()
     L.cask_debug_stamps.restype = C.c_int
@@ -55,6 +56,11 @@ def main():
         print(f"searches {len(a)}: kernel span {en.max():.1f} us; per search us mean {dur.mean():.1f} "
               f"p50/p90/p99/max {' / '.join(f'{x:.1f}' for x in np.percentile(dur, [50, 90, 99, 100]))}")
         print(f"windows mean {win.mean():.2f} max {win.max()}; us per window {dur.sum() / max(win.sum(), 1):.2f}")
+        hist = np.bincount(np.minimum(win, 32))
+        print("windows histogram (searches with k windows, k = 0..31, 32+):", hist.tolist())
+        for lo, hi in ((0, 2), (3, 5), (6, 10), (11, 20), (21, 1 << 30)):
+            m = (win >= lo) & (win <= hi)
+            print(f"  windows {lo}-{hi if hi < 1 << 30 else 'max'}: {int(m.sum())} searches, {dur[m].sum():.0f} us total")
         w_last = a[np.argmax(a[:, 1]), 3]
         mine = a[a[:, 3] == w_last]
         print(f"last wave {w_last}: {len(mine)} searches, windows {mine[:, 2].tolist()}, "
