@@ -473,6 +473,49 @@ bool find_data_files(const std::string& dir, std::vector<uint32_t>& out) {
 using cask_host::host_threads;
 using cask_host::parallel_for;
 
+// Per file: (live entries, their bytes) over the whole keydir, counted on threads by table (a dense
+// array per thread for the usual small file ids; the Stats that a sharded replay completes from it,
+// cask_keydir_finish, and an owner's terms).
+std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> live_by_file(const Index& ix) {
+  using Acc = std::pair<uint64_t, uint64_t>;
+  constexpr uint32_t kDense = 1u << 16;
+  const unsigned nt = std::max(1u, std::min(host_threads(), Index::kSub));
+  std::vector<std::vector<Acc>> dense(nt);
+  std::vector<std::unordered_map<uint32_t, Acc>> sparse(nt);
+  parallel_for(nt, [&](unsigned t) {
+    std::vector<Acc>& d = dense[t];
+    for (unsigned q = t; q < Index::kSub; q += nt)
+      for (const KeyDir::Slot& sl : ix.sub[q].slots) {
+        if (sl.state != 1) continue;
+        const uint32_t f = sl.e.file_id;
+        Acc* a;
+        if (f < kDense) {
+          if (f >= d.size()) d.resize(std::min<size_t>(kDense, std::max<size_t>(f + 1, 2 * d.size())));
+          a = &d[f];
+        } else {
+          a = &sparse[t][f];
+        }
+        a->first += 1;
+        a->second += sl.e.entry_size;
+      }
+  });
+  std::unordered_map<uint32_t, Acc> out;
+  for (unsigned t = 0; t < nt; ++t) {
+    for (uint32_t f = 0; f < dense[t].size(); ++f)
+      if (dense[t][f].first) {
+        Acc& a = out[f];
+        a.first += dense[t][f].first;
+        a.second += dense[t][f].second;
+      }
+    for (const auto& kv : sparse[t]) {
+      Acc& a = out[kv.first];
+      a.first += kv.second.first;
+      a.second += kv.second.second;
+    }
+  }
+  return out;
+}
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -625,6 +668,19 @@ struct EngineDev {
   static constexpr int kReaders = cask_host::PinnedRing::kThreads;
   static constexpr size_t kSlotBytes = cask_host::PinnedRing::kBytes;
   cask_rows r{};
+
+  // After a large open: the data, row and hint buffers go back to the device (they are sized for
+  // the largest batch or stretch seen; kept only while small, for the next open or compaction).
+  void trim() {
+    constexpr size_t kKeep = 4ull << 30;
+    (void)hipSetDevice(device);
+    for (Buf* b : {&data, &rows, &hint})
+      if (b->cap > kKeep) {
+        (void)hipFree(b->p);
+        b->p = nullptr;
+        b->cap = 0;
+      }
+  }
 
   int prepare() {
     if (hipSetDevice(device) != hipSuccess) return CASK_E_DEVICE;
@@ -1192,7 +1248,8 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
   const bool dev_fold = !views.empty() && scan_idx.size() == nf && !(dfh && !strcmp(dfh, "0"));
   std::vector<uint64_t> roff_all(views.size() + 1, 0);  // (dev_fold) each view's first row
   EngineDev::AllRows all_rows;
-  std::vector<uint8_t> dblock;  // (dev_fold) the block, on the host
+  RawBytes dblock;              // (dev_fold) the block, on the host
+  double t_blk = 0, t_blk_d2h = 0;  // (dev_fold) its build on the device, its copy to the host
   int dblock_st = CASK_E_IO;    // (dev_fold) CASK_OK once the block is here
   bool dblock_done = false;
   struct Batch {
@@ -1270,7 +1327,10 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
           std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)vcut[b], views.begin() + (ptrdiff_t)vcut[b + 1]);
           std::vector<uint64_t> ro(vb.size() + 1);
           int ds = ed->scan(vb, ro, bat[b].se);
-          if (ds == CASK_OK) ds = ed->hints(vb, ro, bat[b].hb, bat[b].fo);
+          // the hint bodies: for the hint files, and for the host fold (with the keydir reduced on
+          // the device and no hint files to write, none)
+          if (ds == CASK_OK && dev_fold && !opts.write_hints) bat[b].fo.assign(vb.size() + 1, 0);
+          else if (ds == CASK_OK) ds = ed->hints(vb, ro, bat[b].hb, bat[b].fo);
           if (ds == CASK_OK && dev_fold && !bat[b].se.kind) {  // the batch's rows, kept for the block
             for (size_t k = 0; k <= vb.size(); ++k) roff_all[vcut[b] + k] = all_rows.n + ro[k];
             ds = all_rows.append(ed->r, ro[vb.size()], (hipStream_t)cask_ctx_stream(ed->ctx));
@@ -1293,8 +1353,12 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
         uint64_t nb = 0;
         int st = cask_shard_keydir(ed->ctx, views.data(), (uint32_t)views.size(), &r, roff_all.data(), &blk, &nb);
         if (st != CASK_OK) return st;
-        dblock.resize(nb);
-        return ed->to_host(dblock.data(), (const uint8_t*)blk, nb);
+        t_blk = ms_since(td);
+        const auto tc = std::chrono::steady_clock::now();
+        if (!dblock.resize(nb)) return (int)CASK_E_NOMEM;
+        st = ed->to_host(dblock.data(), (const uint8_t*)blk, nb);
+        t_blk_d2h = ms_since(tc);
+        return st;
       });
       t_dev += ms_since(td);
     }
@@ -1487,13 +1551,21 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
       std::unique_lock<std::mutex> lk(bm);
       bcv.wait(lk, [&] { return dblock_done; });
     }
+    const double t_wait = ms_since(tf3);
     int st = dblock_st;
+    double t_merge = 0;
     if (st == CASK_OK) {
+      const auto tm = std::chrono::steady_clock::now();
       db->merging = true;
       st = cask_keydir_merge(db, dblock.data(), dblock.size());
+      t_merge = ms_since(tm);
       if (st == CASK_OK) st = cask_keydir_finish(db);
     }
-    std::vector<uint8_t>().swap(dblock);
+    if (cask_knobs::hook("CASK_OPEN_TRACE"))
+      fprintf(stderr, "open (device-reduced keydir): block %.1f ms on the device, %.1f ms to the host (%llu B); "
+                      "waited %.1f ms; merge %.1f ms, finish %.1f ms\n",
+              t_blk, t_blk_d2h, (unsigned long long)dblock.size(), t_wait, t_merge, ms_since(tf3) - t_wait - t_merge);
+    RawBytes().p.swap(dblock.p);
     if (st != CASK_OK) {
       fail = st;
       fail_fid = 0;
@@ -1501,6 +1573,7 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
     t_fold += ms_since(tf3);
   }
   join_all();
+  if (ed) ed->trim();
   edlock = std::unique_lock<std::mutex>();
   db->timings[0] = t_read;
   db->timings[1] = t_dev;
@@ -2473,32 +2546,73 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   const ShardRec* rec = (const ShardRec*)(blk + rec_at);
   const uint8_t* keys = blk + key_at;
   const uint64_t n = hd.nrec;
-  // 0. every record's key offset, checked before anything changes
-  std::vector<uint64_t> ko(n);
-  {
-    uint64_t o = 0;
-    for (uint64_t i = 0; i < n; ++i) {
-      ko[i] = o;
-      o += rec[i].ksz;
-      if (o > hd.key_bytes) return CASK_E_INVALID_ARG;
-    }
-  }
   // The fold of a block depends on each key's records alone, in order: on threads by keydir table
   // (parallel_fold's split), each table taking its records in block order — first the thresholds
   // against the keydir entering the shard, then the updates. Stale terms are per-file sums.
+  // Pass 1, threads by piece of the block: each record with its key hash (and its key when short)
+  // appended to its (piece, table) list, so that pass 2 streams each table's lists instead of
+  // reaching back into the block for every record.
   const char* mv = cask_knobs::hook("CASK_PAR_FOLD_MIN");
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
   const unsigned nt = n < min_par ? 1u : std::min(host_threads(), Index::kSub);
   constexpr unsigned S = Index::kSub;
-  std::vector<uint64_t> hs(n);
-  std::vector<std::vector<std::vector<uint32_t>>> lists(nt, std::vector<std::vector<uint32_t>>(S));
+  const unsigned np = nt == 1 ? 1u : 4 * nt;  // pieces
+  // every piece's first key offset (the keys lie in record order), checked before anything changes
+  std::vector<uint64_t> pko(np + 1, 0);
   parallel_for(nt, [&](unsigned t) {
-    const uint64_t lo = n * t / nt, hi = n * (t + 1) / nt;
-    for (uint64_t i = lo; i < hi; ++i) {
-      hs[i] = hash_key(keys + ko[i], rec[i].ksz);
-      lists[t][Index::sub_of(hs[i])].push_back((uint32_t)(i - lo));
+    for (unsigned g = t; g < np; g += nt) {
+      uint64_t o = 0;
+      for (uint64_t i = n * g / np, e = n * (g + 1) / np; i < e; ++i) o += rec[i].ksz;
+      pko[g + 1] = o;
     }
   });
+  for (unsigned g = 0; g < np; ++g) pko[g + 1] += pko[g];
+  if (pko[np] > hd.key_bytes) return CASK_E_INVALID_ARG;
+  struct Item {
+    uint64_t hash, seq, pos;
+    uint32_t file_id, vsz;
+    uint16_t ksz;
+    uint8_t kind, pad0;
+    uint32_t pad1;
+    union {
+      uint8_t kin[KeyDir::kInline];
+      const uint8_t* kp;  // ksz > kInline: the key in the block
+    };
+    const uint8_t* key() const { return ksz <= KeyDir::kInline ? kin : kp; }
+  };
+  std::vector<std::vector<Item>> lists((size_t)np * S);
+  std::vector<uint64_t> nconds(np, 0);
+  parallel_for(nt, [&](unsigned t) {
+    for (unsigned g = t; g < np; g += nt) {
+      const uint64_t lo = n * g / np, hi = n * (g + 1) / np;
+      std::vector<Item>* L = &lists[(size_t)g * S];
+      for (unsigned q = 0; q < S; ++q) L[q].reserve((hi - lo) / S + (hi - lo) / (4 * S) + 16);
+      uint64_t ko = pko[g];
+      for (uint64_t i = lo; i < hi; ++i) {
+        const ShardRec& r = rec[i];
+        Item it;
+        it.ksz = r.ksz;
+        it.hash = hash_key(keys + ko, r.ksz);
+        it.seq = r.seq;
+        it.pos = r.pos;
+        it.file_id = r.file_id;
+        it.vsz = r.vsz;
+        it.kind = r.kind;
+        it.pad0 = 0;
+        it.pad1 = 0;
+        if (r.ksz <= KeyDir::kInline) memcpy(it.kin, keys + ko, r.ksz);
+        else it.kp = keys + ko;
+        nconds[g] += r.kind == kCond;
+        L[Index::sub_of(it.hash)].push_back(it);
+        ko += r.ksz;
+      }
+    }
+  });
+  // phase 0 (the thresholds) only for a block with conditional tombstones, against a keydir that
+  // holds something (an empty one stales none of them)
+  uint64_t ncond = 0;
+  for (uint64_t c : nconds) ncond += c;
+  const int first_phase = ncond && db->index.live() ? 0 : 1;
   std::vector<std::unordered_map<uint32_t, cask_db::ShardTerms>> sterms(nt);
   parallel_for(nt, [&](unsigned t) {
     auto stale = [&](uint32_t fid, uint32_t ksz) {  // Stats add + remove of a stale tombstone
@@ -2509,29 +2623,36 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     for (unsigned q = t; q < S; q += nt) {
       KeyDir& kd = db->index.sub[q];
       uint64_t cnt = 0;  // room for every record's key: a block holds about one record per key
-      for (unsigned g = 0; g < nt; ++g) cnt += lists[g][q].size();
+      for (unsigned g = 0; g < np; ++g) cnt += lists[(size_t)g * S + q].size();
       kd.reserve(kd.live + cnt);
-      for (int phase = 0; phase < 2; ++phase)
-        for (unsigned g = 0; g < nt; ++g) {
-          const uint64_t lo = n * g / nt;
-          const std::vector<uint32_t>& Lq = lists[g][q];
-          for (size_t jj = 0; jj < Lq.size(); ++jj) {
-            if (jj + 8 < Lq.size()) kd.prefetch(hs[lo + Lq[jj + 8]]);
-            if (jj + 4 < Lq.size()) kd.prefetch_key(hs[lo + Lq[jj + 4]]);
-            const uint64_t i = lo + Lq[jj];
-            const ShardRec& r = rec[i];
-            const uint8_t* k = keys + ko[i];
-            const int64_t f = kd.find(k, r.ksz, hs[i]);
-            const cask_index_entry* e = f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
+      for (int phase = first_phase; phase < 2; ++phase)
+        for (unsigned g = 0; g < np; ++g) {
+          const std::vector<Item>& Lq = lists[(size_t)g * S + q];
+          const size_t m = Lq.size();
+          for (size_t jj = 0; jj < m; ++jj) {
+            if (jj + 16 < m) kd.prefetch(Lq[jj + 16].hash);
+            if (jj + 4 < m) kd.prefetch_key(Lq[jj + 4].hash);
+            const Item& r = Lq[jj];
+            auto entry = [&]() -> const cask_index_entry* {
+              const int64_t f = kd.find(r.key(), r.ksz, r.hash);
+              return f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
+            };
             if (phase == 0) {  // 1. thresholds, against the keydir entering the shard
-              if (r.kind == kCond && (e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+              if (r.kind == kCond) {
+                const cask_index_entry* e = entry();
+                if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+              }
               continue;
             }
             // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
             if (r.kind == kCond) continue;
-            if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE && e && e->sequence > r.seq) stale(r.file_id, r.ksz);
-            kd.update_kd(k, r.ksz, r.file_id, r.pos, r.vsz, r.seq, hs[i]);
+            if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
+              const cask_index_entry* e = entry();
+              if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+            }
+            kd.update_kd(r.key(), r.ksz, r.file_id, r.pos, r.vsz, r.seq, r.hash);
           }
+          if (phase == 1) std::vector<Item>().swap(lists[(size_t)g * S + q]);
         }
     }
   });
@@ -2560,12 +2681,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
 int cask_keydir_finish(cask_db* db) {
   return cask_abi::guard([&]() -> int {
     if (!db || !db->merging) return CASK_E_INVALID_ARG;
-    std::unordered_map<uint32_t, std::pair<uint64_t, uint64_t>> live;  // file -> (entries, bytes)
-    db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& sl) {
-      auto& l = live[sl.e.file_id];
-      l.first += 1;
-      l.second += sl.e.entry_size;
-    });
+    const auto live = live_by_file(db->index);  // file -> (entries, bytes)
     db->index.stats.clear();
     for (const auto& kv : db->terms) {
       const cask_db::ShardTerms& t = kv.second;
@@ -2677,12 +2793,12 @@ static int64_t keydir_terms_impl(const cask_db* db, uint8_t* out, uint64_t cap) 
     x.stale_bytes += kv.second.stale_bytes;
   }
   for (uint32_t f : db->files) t[f].file_id = f;  // (files with no terms still travel)
-  db->index.for_each_live([&](const KeyDir&, const KeyDir::Slot& sl) {
-    KeydirTerm& x = t[sl.e.file_id];
-    x.file_id = sl.e.file_id;
-    x.live += 1;
-    x.live_bytes += sl.e.entry_size;
-  });
+  for (const auto& kv : live_by_file(db->index)) {
+    KeydirTerm& x = t[kv.first];
+    x.file_id = kv.first;
+    x.live += kv.second.first;
+    x.live_bytes += kv.second.second;
+  }
   const uint64_t need = sizeof(KeydirTerm) * t.size();
   if (out && cap >= need) {
     uint64_t o = 0;
@@ -2791,7 +2907,7 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
   }
   struct Shard {
     size_t lo = 0, hi = 0;
-    std::vector<std::vector<uint8_t>> blocks;
+    std::vector<RawBytes> blocks;
     std::vector<uint32_t> parts;  // hint files written under their temporary names, in order
     cask_open_error e{};
     double ms_read = 0, ms_scan = 0;
@@ -2802,13 +2918,20 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
     sh[r].hi = nf * (size_t)(r + 1) / (size_t)ndev;
   }
   const bool write_hints = db->opts.write_hints != 0;
-  // one stretch [lo, hi) of files of one kind on device `dev` (its EngineDev `ed`, locked by the
-  // caller: its pinned ring reads data files to the device); false on failure (s.e set)
-  auto run_stretch = [&](Shard& s, int dev, EngineDev* ed, cask_ctx* ctx, size_t lo, size_t hi, bool hint) -> bool {
+  // One stretch [lo, hi) of files of one kind on device `dev` through its EngineDev `ed` (locked by
+  // the caller; its context, pinned rings and buffers), reduced to one keydir block; false on failure
+  // (s.e set). Hint bodies: parsed on the device (cask_parse_hints_device). Data files: read straight
+  // to the device by the pinned ring's reader threads (the stretch's bytes stay resident: the block
+  // reads its keys there), scanned in batches of at most an eighth of the stretch (at least 1 GiB:
+  // the scan's scratch stays bounded), each batch's hint bodies written under their temporary names
+  // and its rows kept, then one block over every row of the stretch (as open() does).
+  auto run_stretch = [&](Shard& s, int dev, EngineDev* ed, size_t lo, size_t hi, bool hint) -> bool {
     auto fail = [&](int st, uint32_t fid = 0, uint64_t pos = 0, uint32_t e = 0, uint32_t f = 0) {
       s.e = cask_open_error{st, fid, pos, e, f};
       return false;
     };
+    cask_ctx* ctx = ed->ctx;
+    hipStream_t cst = (hipStream_t)cask_ctx_stream(ctx);
     auto tr = std::chrono::steady_clock::now();
     const size_t n = hi - lo;
     std::vector<uint64_t> blen(n);
@@ -2826,93 +2949,106 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
       total += (blen[i] + 255) & ~255ull;
     }
     uint8_t* dbuf = nullptr;
-    void* drows = nullptr;
-    uint8_t* dhint = nullptr;
     struct Free {
       uint8_t*& a;
-      void*& b;
-      uint8_t*& c;
       ~Free() {
         if (a) (void)hipFree(a);
-        if (b) (void)hipFree(b);
-        if (c) (void)hipFree(c);
       }
-    } release{dbuf, drows, dhint};
-    if (hipSetDevice(dev) != hipSuccess || hipMalloc(&dbuf, total + 256) != hipSuccess) return fail(CASK_E_DEVICE);
+    } release{dbuf};
+    if (hipSetDevice(dev) != hipSuccess) return fail(CASK_E_DEVICE);
+    if (hipMalloc(&dbuf, total + 256) != hipSuccess) return fail(CASK_E_NOMEM);
     std::vector<cask_file_view> views(n);
     uint64_t off = 0;
     for (size_t i = 0; i < n; ++i) {
       views[i] = cask_file_view{db->files[lo + i], CASK_VIEW_DEVICE, dbuf + off, blen[i]};
       off += (blen[i] + 255) & ~255ull;
     }
+    std::vector<uint64_t> roff(n + 1, 0);
+    EngineDev::AllRows all;
+    auto ts = std::chrono::steady_clock::now();
     if (hint) {  // (the bodies are in host memory already)
       for (size_t i = 0; i < n; ++i)
         if (blen[i] && hipMemcpy((void*)views[i].data, hints[lo + i].data(), blen[i], hipMemcpyHostToDevice) != hipSuccess)
           return fail(CASK_E_DEVICE);
-    } else {  // the data files straight to the device: reader threads through the pinned ring
-      std::vector<char> ok(n, 1);
-      const int rs = ed->read_to_device(paths, views, ok);
-      if (rs != CASK_OK) return fail(rs);
-      for (size_t i = 0; i < n; ++i)
-        if (!ok[i]) return fail(CASK_E_IO, db->files[lo + i]);
-    }
-    s.ms_read += ms_since(tr);
-    auto ts = std::chrono::steady_clock::now();
-    // rows sized from a guess (records of at least 48 B, as EngineDev::scan; hint records are at
-    // least 22 B), and once more at the exact count if that was short
-    const uint64_t bound = cask_rows_bound(views.data(), (uint32_t)n);
-    uint64_t cap = std::min<uint64_t>(bound, total / (hint ? 22 : 48) + n + 1024);
-    cask_rows rows{};
-    std::vector<uint64_t> roff(n + 1);
-    cask_scan_error se{};
-    int st = CASK_E_CAPACITY;
-    for (int attempt = 0; attempt < 2 && st == CASK_E_CAPACITY; ++attempt) {
-      if (drows) (void)hipFree(drows);
-      drows = nullptr;
+      s.ms_read += ms_since(tr);
+      ts = std::chrono::steady_clock::now();
+      // rows sized from the body bytes (hint records are at least 22 B)
+      cask_rows rows{};
+      const uint64_t cap = cask_rows_bound(views.data(), (uint32_t)n);
+      if (!ed->rows.ensure(cap * 23 + 5 * 256)) return fail(CASK_E_NOMEM);
       const uint64_t a8 = (cap * 8 + 255) & ~255ull, a4 = (cap * 4 + 255) & ~255ull, a2 = (cap * 2 + 255) & ~255ull;
-      if (hipMalloc(&drows, 2 * a8 + a4 + a2 + cap + 256) != hipSuccess) return fail(CASK_E_NOMEM);
-      uint8_t* rb = (uint8_t*)drows;
-      rows = cask_rows{};
       rows.capacity = cap;
-      rows.pos = (uint64_t*)rb;
-      rows.seq = (uint64_t*)(rb + a8);
-      rows.vsz = (uint32_t*)(rb + 2 * a8);
-      rows.ksz = (uint16_t*)(rb + 2 * a8 + a4);
-      rows.status = rb + 2 * a8 + a4 + a2;
-      se = cask_scan_error{};
-      st = hint ? cask_parse_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se)
-                : cask_scan_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
-      cap = rows.count;
-    }
-    if (st != CASK_OK) return fail(st == CASK_E_CAPACITY ? CASK_E_DEVICE : st);
-    if (!hint && write_hints) {  // RecreateHints (log.rs:137-148): every Ok row of each file, trailer
-      std::vector<uint64_t> fo(n + 1, 0);
-      st = cask_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), nullptr, 0, fo.data());
-      if (st == CASK_E_CAPACITY || st == CASK_OK) {
-        st = hipMalloc(&dhint, fo[n] + 256) == hipSuccess ? CASK_OK : CASK_E_DEVICE;
-        if (st == CASK_OK) st = cask_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), dhint, fo[n] + 256, fo.data());
-      }
-      std::vector<uint8_t> hb(fo[n]);
-      if (st == CASK_OK && !hb.empty()) st = cask_copy(ctx, hb.data(), dhint, hb.size());
+      rows.pos = (uint64_t*)ed->rows.p;
+      rows.seq = (uint64_t*)(ed->rows.p + a8);
+      rows.vsz = (uint32_t*)(ed->rows.p + 2 * a8);
+      rows.ksz = (uint16_t*)(ed->rows.p + 2 * a8 + a4);
+      rows.status = ed->rows.p + 2 * a8 + a4 + a2;
+      cask_scan_error se{};
+      int st = cask_parse_hints_device(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &se);
       if (st != CASK_OK) return fail(st);
-      // files up to the first failing one (that one included: the drain on drop, log.rs:466-470)
-      for (size_t i = 0; i < n; ++i) {
-        s.parts.push_back(db->files[lo + i]);
-        if (!write_file_raw2(part_path(hint_path(path, db->files[lo + i])), hb.data() + fo[i], fo[i + 1] - fo[i],
-                             cask_xxh::xxh32(hb.data() + fo[i], fo[i + 1] - fo[i], 0)))
-          return fail(CASK_E_IO, db->files[lo + i]);
-        if (se.kind && se.file_id == db->files[lo + i]) break;
+      if (se.kind)  // a hint record cut short: Cask::open's `?` (cask.rs:360,365)
+        return fail(CASK_E_EOF, se.file_id, se.pos, se.expected, se.found);
+      const void* blk = nullptr;
+      uint64_t nb = 0;
+      st = cask_shard_keydir_hints(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb);
+      if (st == CASK_OK) {
+        s.blocks.emplace_back();
+        st = s.blocks.back().resize(nb) ? ed->to_host(s.blocks.back().data(), (const uint8_t*)blk, nb) : CASK_E_NOMEM;
       }
+      if (st != CASK_OK) return fail(st);
+      s.ms_scan += ms_since(ts);
+      return true;
     }
-    if (se.kind)  // the stretch's first failing record: Cask::open's `?` (cask.rs:360,365)
-      return fail(se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF, se.file_id, se.pos, se.expected, se.found);
+    // data files: batches of consecutive files
+    const uint64_t bb = std::max<uint64_t>(1ull << 30, total / 8);
+    for (size_t b0 = 0; b0 < n;) {
+      size_t b1 = b0 + 1;
+      uint64_t acc = blen[b0];
+      while (b1 < n && acc + blen[b1] <= bb) acc += blen[b1++];
+      const std::vector<cask_file_view> vb(views.begin() + (ptrdiff_t)b0, views.begin() + (ptrdiff_t)b1);
+      const std::vector<std::string> pb(paths.begin() + (ptrdiff_t)b0, paths.begin() + (ptrdiff_t)b1);
+      auto tb = std::chrono::steady_clock::now();
+      std::vector<char> ok(vb.size(), 1);
+      int st = ed->read_to_device(pb, vb, ok);
+      if (st != CASK_OK) return fail(st);
+      for (size_t k = 0; k < vb.size(); ++k)
+        if (!ok[k]) return fail(CASK_E_IO, vb[k].file_id);
+      s.ms_read += ms_since(tb);
+      tb = std::chrono::steady_clock::now();
+      std::vector<uint64_t> ro(vb.size() + 1);
+      cask_scan_error se{};
+      st = ed->scan(vb, ro, se);
+      if (st != CASK_OK) return fail(st);
+      if (write_hints) {  // RecreateHints (log.rs:137-148): every Ok row of each file, trailer
+        RawBytes hb;
+        std::vector<uint64_t> fo;
+        st = ed->hints(vb, ro, hb, fo);
+        if (st != CASK_OK) return fail(st);
+        // files up to the first failing one (that one included: the drain on drop, log.rs:466-470)
+        for (size_t k = 0; k < vb.size(); ++k) {
+          s.parts.push_back(vb[k].file_id);
+          if (!write_file_raw2(part_path(hint_path(path, vb[k].file_id)), hb.data() + fo[k], fo[k + 1] - fo[k],
+                               cask_xxh::xxh32(hb.data() + fo[k], fo[k + 1] - fo[k], 0)))
+            return fail(CASK_E_IO, vb[k].file_id);
+          if (se.kind && se.file_id == vb[k].file_id) break;
+        }
+      }
+      if (se.kind)  // the stretch's first failing record: Cask::open's `?` (cask.rs:360,365)
+        return fail(se.kind == CASK_ROW_CHECKSUM ? CASK_E_CHECKSUM : CASK_E_EOF, se.file_id, se.pos, se.expected, se.found);
+      for (size_t k = 0; k <= vb.size(); ++k) roff[b0 + k] = all.n + ro[k];
+      st = all.append(ed->r, ro[vb.size()], cst);
+      if (st != CASK_OK) return fail(st);
+      s.ms_scan += ms_since(tb);
+      b0 = b1;
+    }
+    ts = std::chrono::steady_clock::now();
+    const cask_rows rows = all.view();
     const void* blk = nullptr;
     uint64_t nb = 0;
-    st = hint ? cask_shard_keydir_hints(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb)
-              : cask_shard_keydir(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb);
+    int st = cask_shard_keydir(ctx, views.data(), (uint32_t)n, &rows, roff.data(), &blk, &nb);
     if (st == CASK_OK) {
-      s.blocks.emplace_back(nb);
-      if (hipMemcpy(s.blocks.back().data(), blk, nb, hipMemcpyDeviceToHost) != hipSuccess) st = CASK_E_DEVICE;
+      s.blocks.emplace_back();
+      st = s.blocks.back().resize(nb) ? ed->to_host(s.blocks.back().data(), (const uint8_t*)blk, nb) : CASK_E_NOMEM;
     }
     if (st != CASK_OK) return fail(st);
     s.ms_scan += ms_since(ts);
@@ -2927,24 +3063,23 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
       return;
     }
     std::lock_guard<std::mutex> edg(ed->mu);
-    int st = ed->prepare();
-    cask_ctx* ctx = st == CASK_OK ? cask_ctx_create(devices[r], &st) : nullptr;
-    if (!ctx) {
-      s.e = cask_open_error{st, 0, 0, 0, 0};
+    const int st0 = ed->prepare();
+    if (st0 != CASK_OK) {
+      s.e = cask_open_error{st0, 0, 0, 0, 0};
       return;
     }
     for (size_t i = s.lo; i < s.hi;) {  // maximal stretches of one kind, in order
       size_t j = i + 1;
       while (j < s.hi && use_hint[j] == use_hint[i]) ++j;
-      // (an exception in a stretch is its failure, so the context is still destroyed below)
-      const int st = abi_status([&] { return run_stretch(s, devices[r], ed, ctx, i, j, use_hint[i] != 0) ? CASK_OK : 1; });
+      // (an exception in a stretch is its failure)
+      const int st = abi_status([&] { return run_stretch(s, devices[r], ed, i, j, use_hint[i] != 0) ? CASK_OK : 1; });
       if (st != CASK_OK) {
         if (st != 1) s.e = cask_open_error{st, 0, 0, 0, 0};
         break;
       }
       i = j;
     }
-    cask_ctx_destroy(ctx);
+    ed->trim();
   };
   // one thread per distinct device; a device's shards run in order on its thread
   std::vector<int> devs;

@@ -142,28 +142,32 @@ def compact(ctx, torch, nfiles, workdir):
 
 
 def open_ab(ctx, torch, nfiles, workdir, rounds=2):
-    """Cask::open of the same configs[3]-shaped files by cask_db_open (threaded host fold) and by
-    cask_db_open_multi on device 0 (keydir blocks reduced on the device, merged on the host), in turn;
-    no hint files are written, so every open scans."""
+    """Cask::open of the same configs[3]-shaped files, in turn: cask_db_open with the keydir reduced
+    on the device (the default when every file is scanned), cask_db_open with the host fold of every
+    hint row (CASK_OPEN_DEVFOLD=0, a test hook), and cask_db_open_multi over one and two ranges on
+    device 0; no hint files are written, so every open scans. Timings: [read, device, hint files,
+    fold, total] ms."""
     from cask_amd import CaskOptions
     from cask_amd.keydir import open_multi
     path = os.path.join(workdir, "db")
     os.makedirs(path)
     nbytes, live_want, n, write_s = write_cfg3(ctx, torch, nfiles, path)
-    out = {"files": nfiles, "records": n, "bytes": nbytes, "open_s": [], "open_timings_ms": [], "open_multi_s": []}
-    for _ in range(rounds):
-        t0 = time.perf_counter()
-        with CaskOptions().write_hints(False).open(path) as db:
-            out["open_s"].append(time.perf_counter() - t0)
-            out["open_timings_ms"].append(db.open_timings())
-            assert len(db) == live_want
-        print(f"open {out['open_s'][-1]:.2f} s {out['open_timings_ms'][-1]}", file=sys.stderr, flush=True)
-        if os.environ.get("OPENAB_MULTI") == "1":  # (holds every file in host and device memory at once)
+    out = {"files": nfiles, "records": n, "bytes": nbytes, "runs": []}
+    for r in range(rounds):
+        for name in ("open_devfold", "open_hostfold", "open_multi_1", "open_multi_2"):
+            os.environ["CASK_OPEN_DEVFOLD"] = "0" if name == "open_hostfold" else "1"
             t0 = time.perf_counter()
-            with open_multi(path, [0], CaskOptions().write_hints(False)) as db:
-                out["open_multi_s"].append(time.perf_counter() - t0)
+            if name.startswith("open_multi"):
+                db = open_multi(path, [0] * int(name[-1]), CaskOptions().write_hints(False))
+            else:
+                db = CaskOptions().write_hints(False).open(path)
+            with db:
+                dt = time.perf_counter() - t0
+                tm = db.open_timings()
                 assert len(db) == live_want
-            print(f"open_multi {out['open_multi_s'][-1]:.2f} s", file=sys.stderr, flush=True)
+            out["runs"].append({"round": r, "what": name, "s": dt, "timings_ms": tm})
+            print(f"{name} {dt:.2f} s {tm}", file=sys.stderr, flush=True)
+    os.environ.pop("CASK_OPEN_DEVFOLD", None)
     return out
 
 
@@ -177,6 +181,8 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--dir", default=None, help="parent directory of the compaction database")
     args = ap.parse_args()
+    if "openab" in args.what:  # (open_ab switches the open's fold with a test hook)
+        os.environ["CASK_TEST_HOOKS"] = "1"
     import torch
     torch.cuda.set_device(0)
     from cask_amd import ScanContext
