@@ -247,26 +247,6 @@ __device__ __forceinline__ uint32_t gld4(const uint8_t* p) {
   __builtin_memcpy(&v, (g_u8*)p, 4);
   return v;
 }
-// Agent-scope (sc1) accesses: written through to memory / read past this CU's L1 — how the
-// overlapped walk's kernels hand data to one another while they run (MI355X_MICROARCH.md, visibility:
-// every byte of a hand-off stored sc1, the storing wave's vmcnt(0), then the flag; every load of it sc1).
-typedef __attribute__((address_space(1))) uint32_t g_u32a;
-typedef __attribute__((address_space(1))) uint64_t g_u64a;
-__device__ __forceinline__ void st_agent(uint32_t* p, uint32_t v) {
-  __hip_atomic_store((g_u32a*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
-  __hip_atomic_store((g_u64a*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_agent(const uint32_t* p) {
-  return __hip_atomic_load((g_u32a*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
-  return __hip_atomic_load((g_u64a*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// every memory operation this wave has issued is complete (before a hand-off's flag)
-__device__ __forceinline__ void drain_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 __device__ __forceinline__ u32x4 gld16g(const g_u8* p) {
   u32x4 v;
   __builtin_memcpy(&v, p, 16);

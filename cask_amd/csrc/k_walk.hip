@@ -636,13 +636,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     const uint64_t win0 = wst[5];
 #endif
     const uint64_t s0 = b0 == 0 ? 0 : walk_search_sw(L, fd.data, fd.len, b0, b1, wst, a.search_short);
-    if (a.sready) {  // the overlapped walk: tin written through to memory, then the run's flag
-      if (threadIdx.x == 0) st_agent(&a.tin[t], s0);
-      drain_vm();
-      if (threadIdx.x == 0) st_agent(&a.sready[r], a.epoch);
-    } else if (threadIdx.x == 0) {
-      a.tin[t] = s0;
-    }
+    if (threadIdx.x == 0) a.tin[t] = s0;
 #ifdef CASK_STAMPS
     if (a.stamps && threadIdx.x == 0 && r < kStampRuns) {  // per search: start, end, windows, wave
       unsigned long long* sr = a.stamps + 16 + 2ull * kStampWaves + 4 * r;

@@ -53,24 +53,9 @@ __device__ __forceinline__ u32x4 shr_bytes(const u32x4& v, uint32_t s) {
   return u32x4{fun(w0, w1, b), fun(w1, w2, b), fun(w2, w3, b), fun(w3, 0u, b)};
 }
 
-// Stores of what k_run_hash reads: agent-scope (written through) when the hash runs at the same time
-// (PUB, the overlapped walk), plain otherwise.
-template <bool PUB>
-__device__ __forceinline__ void st32(uint32_t* p, uint32_t v) {
-  if (PUB) st_agent(p, v);
-  else *(g_u32*)p = v;
-}
-template <bool PUB>
-__device__ __forceinline__ void st64(uint64_t* p, uint64_t v) {
-  if (PUB) st_agent(p, v);
-  else *(g_u64*)p = v;
-}
-
 // One chunk's table entries. A chunk with more records than its slot rows (a.slot_cap: small in a
 // walk-mode call) keeps slot_cap of them and flags the call, which the host then redoes with full
 // slot rows: every later kernel reads rows r < count only, so nothing reads past the slots.
-// (spec, exit and long_r are read by k_finish only, after the chase's kernel has ended.)
-template <bool PUB = false>
 __device__ __forceinline__ void put_chunk(const ScanArgs& a, uint64_t t, uint64_t spec, uint64_t ex, uint32_t count,
                                           uint32_t cerr) {
   if (count > a.slot_cap) {
@@ -79,9 +64,9 @@ __device__ __forceinline__ void put_chunk(const ScanArgs& a, uint64_t t, uint64_
   }
   ((g_u64*)a.spec)[t] = spec;
   ((g_u64*)a.exit)[t] = ex;
-  st32<PUB>(a.count + t, count);
+  ((g_u32*)a.count)[t] = count;
   ((g_u32*)a.long_r)[t] = 0xFFFFFFFFu;  // every record is hashed here: nothing left for k_long
-  st32<PUB>(a.cerr + t, cerr);
+  ((g_u32*)a.cerr)[t] = cerr;
 }
 
 // A quad's walk state (every field the same in the quad's four lanes).
@@ -95,14 +80,13 @@ struct Walk {
 
 // The chain enters the record at `pos`: close the chunks it leaves, open its chunk; returns the
 // record's row within its chunk (and the chunk in *j).
-template <bool PUB = false>
 __device__ __forceinline__ uint32_t open_record(const ScanArgs& a, Walk& W, uint64_t pos, uint32_t csh, bool writer,
                                                 uint32_t* jout) {
   const uint32_t j = (uint32_t)((pos - W.S.b0) >> csh);
   if (j != W.cj) {
-    if (W.cj != kNoChunk && writer) put_chunk<PUB>(a, W.S.t0 + W.cj, W.cspec, pos, W.cn, W.ccerr);
+    if (W.cj != kNoChunk && writer) put_chunk(a, W.S.t0 + W.cj, W.cspec, pos, W.cn, W.ccerr);
     for (uint32_t k = W.cj == kNoChunk ? 0u : W.cj + 1; k < j; ++k)
-      if (writer) put_chunk<PUB>(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
+      if (writer) put_chunk(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
     W.cj = j;
     W.cn = 0;
     W.ccerr = 0xFFFFFFFFu;
@@ -113,15 +97,14 @@ __device__ __forceinline__ uint32_t open_record(const ScanArgs& a, Walk& W, uint
 }
 
 // The segment ends: the chain leaves it at `ex` (kTerm after an EOF row).
-template <bool PUB = false>
 __device__ __forceinline__ void close_segment(const ScanArgs& a, Walk& W, uint64_t ex, bool writer) {
   uint32_t k0 = 0;
   if (W.cj != kNoChunk) {
-    if (writer) put_chunk<PUB>(a, W.S.t0 + W.cj, W.cspec, ex, W.cn, W.ccerr);
+    if (writer) put_chunk(a, W.S.t0 + W.cj, W.cspec, ex, W.cn, W.ccerr);
     k0 = W.cj + 1;
   }
   for (uint32_t k = k0; k < W.S.nch; ++k)
-    if (writer) put_chunk<PUB>(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
+    if (writer) put_chunk(a, W.S.t0 + k, kNone, 0ull, 0u, 0xFFFFFFFFu);
   W.cj = kNoChunk;
 }
 
@@ -170,14 +153,12 @@ struct TailBits {
   uint64_t q = ~0ull;          // the piece being marked
   uint64_t qe = 0;             // the first chunk after it (the chain only moves forward)
   uint32_t i = 0, word = 0;    // its next record, the bits of its current word
-  template <bool PUB = false>
   __device__ __forceinline__ void flush(const ScanArgs& a) {
-    if (q != ~0ull && (i & 31) && i <= kTailMaxRecs) st32<PUB>(a.tbits + (unit0 + q) * kTailBitWords + ((i - 1) >> 5), word);
+    if (q != ~0ull && (i & 31) && i <= kTailMaxRecs) a.tbits[(unit0 + q) * kTailBitWords + ((i - 1) >> 5)] = word;
   }
-  template <bool PUB = false>
   __device__ __forceinline__ void record(const ScanArgs& a, uint64_t t, bool longr) {
     if (t >= qe) {  // (a division per piece, not per record)
-      flush<PUB>(a);
+      flush(a);
       q = (uint32_t)(t - r0) / (uint32_t)qr;
       qe = r0 + (q + 1) * qr;
       i = 0;
@@ -186,7 +167,7 @@ struct TailBits {
     word |= (longr ? 1u : 0u) << (i & 31);
     ++i;
     if (!(i & 31)) {
-      if (i <= kTailMaxRecs) st32<PUB>(a.tbits + (unit0 + q) * kTailBitWords + ((i - 1) >> 5), word);
+      if (i <= kTailMaxRecs) a.tbits[(unit0 + q) * kTailBitWords + ((i - 1) >> 5)] = word;
       word = 0;
     }
   }
@@ -291,140 +272,6 @@ __global__ __launch_bounds__(256) void k_walk_chase(ScanArgs a, const FileDesc* 
 }
 
 // ---------------------------------------------------------------------------------------------
-// The overlapped walk's chase: one lane per run of a.run chunks, as k_walk_chase, but running at the
-// same time as k_walk_search (on CUs of its own) and k_run_hash. Each lane waits for its run's start
-// (a.sready, published by the search), follows the run's chain one hop per iteration of a loop the
-// wave shares (a lane's segments and hops in sequence, so a lane whose run is done leaves the others
-// to it), and publishes the run (a.cready) as soon as its last chunk entry is out: every byte
-// k_run_hash reads is stored agent-scope (written through), the wave drains its memory operations,
-// then the lane's flag. The hash takes the runs in order and waits only for runs not published yet.
-// A lane that has waited for its search longer than kChaseWaitTicks (the search kernel failed to
-// run) gives the call up (Counters::hash_stall: the host redoes it with the kernels in sequence).
-// ---------------------------------------------------------------------------------------------
-constexpr uint64_t kChaseWaitTicks = 100000000ull;  // 1 s of the 100-MHz real-time counter
-
-__global__ __launch_bounds__(64) void k_walk_chase_pub(ScanArgs a, const FileDesc* __restrict__ files) {
-  const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
-  g_u32* slots = (g_u32*)a.slots;
-  const uint64_t R = a.run, nruns = (a.total_chunks + R - 1) / R;
-  const uint64_t k = blockIdx.x * 64ull + threadIdx.x;  // this lane's run
-  // stage: 0 waiting for the run's start, 1 the next segment, 2 following the chain, 3 done
-  uint32_t stage = k < nruns ? 0u : 3u;
-  const uint64_t tb = k < nruns ? k * R : 0ull;
-  const uint64_t te = k < nruns ? (tb + R < a.total_chunks ? tb + R : a.total_chunks) : 0ull;
-  TailBits tbt;
-  if (k < nruns && a.hash_ntail && k >= nruns - a.hash_ntail) {
-    tbt.on = true;
-    tbt.r0 = k * R;
-    tbt.qr = (R + kTailSplit - 1) / kTailSplit;
-    tbt.unit0 = (k - (nruns - a.hash_ntail)) * kTailSplit;
-  }
-  Walk W;
-  W.cn = 0;
-  W.ccerr = 0xFFFFFFFFu;
-  W.cspec = 0;
-  W.run_end = te;
-  W.cj = kNoChunk;
-  uint64_t t = tb, p = kNone;
-  bool term = false;
-  u32x4 h = u32x4{0u, 0u, 0u, 0u};
-  const uint64_t t_wait0 = __builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    if (!__any(stage != 3)) break;
-    bool fin = false;
-    if (stage == 0) {
-      if (ld_agent(a.sready + k) == a.epoch) {
-        p = ld_agent(a.tin + tb);
-        stage = 1;
-      } else if (__builtin_amdgcn_s_memrealtime() - t_wait0 > kChaseWaitTicks) {
-        st_agent(&a.ctr->hash_stall, 1u);
-        stage = 3;  // (not published: the hash gives up on it too)
-      }
-    }
-    if (stage == 1) {  // the next segment of the run (chunks of one file), or the run is done
-      if (t >= te) {
-        fin = true;
-        stage = 3;
-      } else {
-        seg_setup(a, files, W, t);
-        t = W.S.t0 + W.S.nch;
-        const uint64_t fend = (uint64_t)(uintptr_t)(W.S.data + W.S.len);
-        for (uint32_t c = 0; c < W.S.nch; ++c) {
-          st64<true>(a.cdesc + 2 * (W.S.t0 + c), (uint64_t)(uintptr_t)(W.S.data + W.S.b0 + ((uint64_t)c << csh)));
-          st64<true>(a.cdesc + 2 * (W.S.t0 + c) + 1, fend);
-        }
-        if (W.S.b0 == 0) p = 0ull;  // a later segment starts a file
-        else if (W.S.t0 != tb) p = kNone;
-        term = false;
-        const bool has = p != kNone && p < W.S.b1;
-        const uint64_t p0 = has && p + 18 <= W.S.len ? p + 2 : 0ull;
-        h = gld16g((const g_u8*)(W.S.data + p0));
-        stage = 2;
-      }
-    } else if (stage == 2) {  // one hop (Entries::next, log.rs:403-429), or the segment closes
-      bool close = !(p != kNone && p < W.S.b1);
-      if (!close) {
-        uint32_t j = 0;
-        if (p + 18 > W.S.len) {  // header cut short: Io(UnexpectedEof) (data.rs:163)
-          const uint32_t r = open_record<true>(a, W, p, csh, true, &j);
-          if (tbt.on) tbt.record<true>(a, W.S.t0 + j, false);
-          const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-          if (r < a.slot_cap) {
-            uint64_t* sr = (uint64_t*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4);
-            st64<true>(sr, 0ull);
-            st64<true>(sr + 1, (uint64_t)(off << 16) << 32);
-          }
-          if (r < W.ccerr) W.ccerr = r;
-          term = true;
-          close = true;
-        } else {
-          const uint32_t ksz = h.z >> 16, vsz = h.w;
-          const u32x4 row = u32x4{fun(h.x, h.y, 2), fun(h.y, h.z, 2), vsz, ksz};
-          const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-          const uint64_t pn = p + rl;
-          const uint64_t pl = pn + 18 <= W.S.len ? pn + 2 : 0ull;
-          h = gld16g((const g_u8*)(W.S.data + pl));  // (before this record's stores: see chase_range)
-          const uint32_t r = open_record<true>(a, W, p, csh, true, &j);
-          if (tbt.on) tbt.record<true>(a, W.S.t0 + j, rl >= kTailLong);
-          const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-          if (r < a.slot_cap) {
-            uint64_t* sr = (uint64_t*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4);
-            st64<true>(sr, (uint64_t)row.x | ((uint64_t)row.y << 32));
-            st64<true>(sr + 1, (uint64_t)row.z | ((uint64_t)(row.w | (off << 16)) << 32));
-          }
-          if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
-            if (r < W.ccerr) W.ccerr = r;
-            term = true;
-            close = true;
-          } else {
-            p = pn;
-          }
-        }
-      }
-      if (close) {
-        close_segment<true>(a, W, term ? kTerm : p, true);
-        if (term) p = kTerm;
-        stage = 1;
-      }
-    }
-    if (__any(fin)) {  // the runs done in this iteration: their last stores out, then their flags
-      if (fin && tbt.on) tbt.flush<true>(a);
-      drain_vm();
-      if (fin) st_agent(a.cready + k, a.epoch);
-    }
-    if (__all(stage == 0 || stage == 3)) __builtin_amdgcn_s_sleep(4);  // (only waiting lanes left)
-  }
-}
-
-void launch_walk_chase_pub(const ScanArgs& a, void* stream, int cus) {
-  (void)cus;
-  if (!a.total_chunks) return;
-  const uint64_t nruns = (a.total_chunks + a.run - 1) / a.run;
-  hipLaunchKernelGGL(k_walk_chase_pub, dim3((uint32_t)((nruns + 63) / 64)), dim3(64), 0, (hipStream_t)stream, a,
-                     a.files);
-}
-
-// ---------------------------------------------------------------------------------------------
 // Split path, pass 2 — k_run_hash: Entry::from_read's checksum (data.rs:185-198) of every record the
 // chase found. A wave claims runs and hands their records, in order, to its 16 quads: a quad hashes
 // its record straight from HBM, and takes the next record of the wave's stream as it starts one (its
@@ -475,12 +322,6 @@ __device__ __forceinline__ u32x4 gld16nt(uint64_t p) {
   return __builtin_nontemporal_load((gcu32x4*)(uintptr_t)p);
 }
 
-// PUB (the overlapped walk): the chase runs at the same time — a unit's run is taken once the chase has
-// published it (a.cready), and everything the chase wrote is read agent-scope. A wave that waits for a
-// run longer than kHashWaitTicks gives the call up (Counters::hash_stall: the host redoes it in sequence).
-constexpr uint64_t kHashWaitTicks = 100000000ull;  // 1 s of the 100-MHz real-time counter
-
-template <bool PUB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_run_hash(ScanArgs a) {
   constexpr uint32_t D = 8;    // lines of a record per round
   constexpr uint32_t RW = 256; // dwords per round
@@ -524,7 +365,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
   // the other runs (units [nhead, nhead + NT)), the shorter ones last — so that no long record is
   // still being hashed when the units run out
   const bool split = a.hash_ntail != 0;
-  const uint64_t tcap = a.hash_waves_all;
+  const uint64_t tcap = (uint64_t)gridDim.x * 4;
   const uint64_t ntail = split ? a.hash_ntail : nruns < tcap ? nruns : tcap;
   const uint64_t nhead = nruns - ntail, NT = TS * ntail, nunits = nhead + (split ? 2 * NT : NT);
   auto load_run = [&](bool intoA, uint64_t u) __attribute__((always_inline)) -> bool {
@@ -540,21 +381,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     const uint64_t c1 = tl ? (c0 + qr < nk ? c0 + qr : nk) : nk;
     const uint64_t t0 = tr + c0;
     const uint32_t nch = (uint32_t)(c1 > c0 ? c1 - c0 : 0ull);
-    if (PUB) {  // the run's chase published (the wait is rare once the first units are taken)
-      const uint64_t tw0 = __builtin_amdgcn_s_memrealtime();
-      while (__builtin_amdgcn_readfirstlane(ld_agent(a.cready + k)) != a.epoch) {
-        if (__builtin_amdgcn_s_memrealtime() - tw0 > kHashWaitTicks) {
-          st_agent(&a.ctr->hash_stall, 1u);
-          return false;
-        }
-        __builtin_amdgcn_s_sleep(8);
-      }
-    }
-    uint32_t inc = lane < nch ? ((PUB ? ld_agent(a.count + t0 + lane) : ((const g_u32*)a.count)[t0 + lane]) & kCountMask) : 0u;
+    uint32_t inc = lane < nch ? (((const g_u32*)a.count)[t0 + lane] & kCountMask) : 0u;
     // (the piece's long-record bits, loaded with the counts: one round trip)
-    const uint32_t bits = pass && lane < kTailBitWords
-                              ? (PUB ? ld_agent(a.tbits + piece * kTailBitWords + lane) : ((const g_u32*)a.tbits)[piece * kTailBitWords + lane])
-                              : 0u;
+    const uint32_t bits = pass && lane < kTailBitWords ? ((const g_u32*)a.tbits)[piece * kTailBitWords + lane] : 0u;
     for (int o = 1; o < 64; o <<= 1) {
       const uint32_t u = __shfl_up(inc, o, 64);
       if ((int)lane >= o) inc += u;
@@ -564,8 +393,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     if (lane == 0) pf[0] = 0;
     uint64_t* cdt = intoA ? cdA : cdB;
     if (lane < nch) {
-      cdt[2 * lane] = PUB ? ld_agent(a.cdesc + 2 * (t0 + lane)) : cd[2 * (t0 + lane)];
-      cdt[2 * lane + 1] = PUB ? ld_agent(a.cdesc + 2 * (t0 + lane) + 1) : cd[2 * (t0 + lane) + 1];
+      cdt[2 * lane] = cd[2 * (t0 + lane)];
+      cdt[2 * lane + 1] = cd[2 * (t0 + lane) + 1];
     }
     uint32_t n = __builtin_amdgcn_readfirstlane((uint32_t)__shfl((int)inc, 63, 64));
     if (pass) {  // the pass's records, in order, into the unit's list
@@ -600,12 +429,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     }
     return true;
   };
-  if (a.hash_claim_only) {  // (a grid launched after the first one: every unit from the counter)
-    const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
-    runs_left = load_run(true, (uint64_t)a.hash_fixed + __builtin_amdgcn_readfirstlane(old));
-  } else {
-    runs_left = load_run(true, blockIdx.x * 4ull + wv);
-  }
+  runs_left = load_run(true, blockIdx.x * 4ull + wv);
 
   // a quad's current record (cv) and the round of it in hand: round cri of its cnrd rounds, rfin if
   // it is the last (the record's tail bytes in T), head if it is the first (its stored checksum in
@@ -664,7 +488,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     // as soon as B is free)
     if (runs_left && !fullB && rnA - cur <= 16) {
       const uint32_t old = atomicAdd(&a.ctr->hash_next, lane == 0 ? 1u : 0u);
-      const bool got = load_run(false, (uint64_t)a.hash_fixed + __builtin_amdgcn_readfirstlane(old));
+      const bool got = load_run(false, (uint64_t)gridDim.x * 4ull + __builtin_amdgcn_readfirstlane(old));
       runs_left = got;
       fullB = got;
 #ifdef CASK_STAMPS
@@ -787,7 +611,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
     for (uint32_t d = 0; d < 2 * D; ++d) asm volatile("" : "+v"(ya[d]));
     {  // (the 8 bytes used: the dead half of a 16-B destination is a register the compiler reuses,
        // and writing it would wait for this load)
-      const uint64_t zw = PUB ? ld_agent((const uint64_t*)(uintptr_t)(arow + 8)) : *(const g_u64*)(uintptr_t)(arow + 8);
+      const uint64_t zw = *(const g_u64*)(uintptr_t)(arow + 8);
       nrow = u32x4{0u, 0u, (uint32_t)zw, (uint32_t)(zw >> 32)};
     }
     Ti = gld16g((const g_u8*)(uintptr_t)ta);
@@ -995,41 +819,21 @@ uint64_t run_hash_waves() {
   static int per_cu = 0;
   if (!per_cu) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash<false>, 256, 0) == hipSuccess && nb > 0) per_cu = 4 * nb;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_run_hash, 256, 0) == hipSuccess && nb > 0) per_cu = 4 * nb;
     if (per_cu <= 0) per_cu = 8;
   }
   return (uint64_t)device_cus() * (uint64_t)per_cu;
-}
-
-// The waves of one k_run_hash launch over `cus` CUs (0: all of them): the resident ones, at most one
-// per unit of work.
-uint64_t run_hash_grid_waves(const ScanArgs& a, int cus) {
-  const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
-  uint64_t waves = run_hash_waves();
-  if (const char* e = cask_knobs::tune("CASK_HASH_WAVES_PER_CU")) waves = (uint64_t)device_cus() * (uint64_t)atoi(e);
-  if (cus > 0) waves = waves / (uint64_t)device_cus() * (uint64_t)cus;
-  waves = (waves + 3) / 4 * 4;
-  if (waves > 4 * ((nruns + 3) / 4)) waves = 4 * ((nruns + 3) / 4);
-  return waves;
 }
 
 void launch_run_hash(const ScanArgs& a, void* stream, int cus) {
   if (!a.total_chunks) return;
   const uint64_t nruns = a.wruns ? a.nwruns : (a.total_chunks + a.run - 1) / a.run;
   if (!nruns) return;
-  const uint64_t waves = run_hash_grid_waves(a, cus);
-  ScanArgs b = a;  // one grid: its units by index, then from the counter
-  b.hash_fixed = (uint32_t)waves;
-  b.hash_claim_only = 0;
-  b.hash_waves_all = waves;
-  hipLaunchKernelGGL(k_run_hash<false>, dim3((uint32_t)(waves / 4)), dim3(256), 0, (hipStream_t)stream, b);
-}
-
-// The overlapped walk's hash grids (the caller sets hash_fixed, hash_claim_only, hash_waves_all).
-void launch_run_hash_pub(const ScanArgs& a, void* stream, int cus) {
-  if (!a.total_chunks) return;
-  const uint64_t waves = run_hash_grid_waves(a, cus);
-  hipLaunchKernelGGL(k_run_hash<true>, dim3((uint32_t)(waves / 4)), dim3(256), 0, (hipStream_t)stream, a);
+  uint64_t waves = run_hash_waves();
+  if (cus > 0) waves = waves / (uint64_t)device_cus() * (uint64_t)cus;
+  if (const char* e = cask_knobs::tune("CASK_HASH_WAVES_PER_CU")) waves = (uint64_t)device_cus() * (uint64_t)atoi(e);
+  if (waves > nruns) waves = nruns;
+  hipLaunchKernelGGL(k_run_hash, dim3((uint32_t)((waves + 3) / 4)), dim3(256), 0, (hipStream_t)stream, a);
 }
 
 }  // namespace cask_dev

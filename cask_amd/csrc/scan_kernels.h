@@ -52,7 +52,6 @@ struct Counters {
   unsigned int search_next[8];   // k_walk_search: the same, for the searches
   unsigned int hash_next;        // k_walk_hash: next run to hand out (after the first by index)
   unsigned int slot_overflow;    // k_walk_chase: a chunk had more records than the slot rows sized
-  unsigned int hash_stall;       // overlapped walk: a k_run_hash wave gave up waiting for a run (redo)
 };
 
 // Layout of the call block: Counters, then row_off[nfiles + 1] (each file's first dense row,
@@ -171,18 +170,6 @@ struct ScanArgs {
   // words, bit i = its record i is long (written by k_walk_chase). hash_ntail 0: one pass.
   uint64_t hash_ntail;
   uint32_t* tbits;
-  // the overlapped walk (scan_runtime.cpp): k_walk_search, k_walk_chase and k_run_hash run at once
-  // on their own CUs, handing runs over through per-run flags tagged with the call's epoch —
-  // sready[k] once run k's start is in tin (written with agent-scope stores), cready[k] once its
-  // chase output (slot rows, counts, cerr, cdesc, tail bits) is, all written through to memory
-  // (agent scope) and read back the same way. Null: the kernels run one after the other.
-  uint32_t* sready;
-  uint32_t* cready;
-  // k_run_hash: units handed out by index over all the hash grids of a call (a grid with
-  // hash_claim_only takes every unit from the claim counter), and the waves of all of them
-  uint32_t hash_fixed;
-  uint32_t hash_claim_only;
-  uint64_t hash_waves_all;
 };
 
 // Default ScanArgs::big: records longer than 2 KiB are hashed by k_long_hash, many lanes at once,
@@ -204,9 +191,6 @@ constexpr uint32_t kDefaultRun = 16, kMaxRun = 64;
 // chunk on average; configs[2], mean 5,114 B: at most 60 in 11 M chunks). A chunk with more sets
 // Counters::slot_overflow and the call is redone with the full count (chunk / 18 + 2).
 constexpr uint32_t kWalkSlotCap = 128;
-// The overlapped walk: the CUs the chase (then the second hash grid) runs on; the search and the
-// first hash grid take the others (the chase runs as fast on 32 CUs as on all 256: profiles/r06_cumask_ab.txt).
-constexpr int kOverlapCUs = 32;
 constexpr uint32_t kWalkRun = 32, kWalkMean = 1024;  // (configs[2]: 32-chunk runs 2 % faster than 64)
 #ifndef CASK_TAIL_SPLIT_N  // (A/B variant)
 #define CASK_TAIL_SPLIT_N 2
@@ -288,12 +272,6 @@ void launch_walk_search(const ScanArgs& a, void* stream, int cus = 0);  // k_wal
 // every record hashed from HBM, whole 128-B lines per load instruction)
 void launch_walk_chase(const ScanArgs& a, void* stream);
 void launch_run_hash(const ScanArgs& a, void* stream, int cus = 0);
-// the overlapped walk: the chase as a lane per run that waits for its run's search, chases it and
-// publishes it (a.sready / a.cready set), on a stream of `cus` CUs; k_run_hash waiting per unit
-void launch_walk_chase_pub(const ScanArgs& a, void* stream, int cus);
-void launch_run_hash_pub(const ScanArgs& a, void* stream, int cus);
-// the waves one launch of k_run_hash over `cus` CUs holds (0: all of them)
-uint64_t run_hash_grid_waves(const ScanArgs& a, int cus);
 uint64_t run_hash_waves();  // k_run_hash's persistent grid, in waves
 // after k_finish ran beside k_run_hash: the checksum statuses of the chunks with a failing row
 void launch_hash_fix(const ScanArgs& a, void* stream);

@@ -114,8 +114,6 @@ struct cask_ctx {
   uint32_t epoch = 0;
   uint32_t inject = 0;  // test hooks: cask_debug_inject (abi_guard.h)
   bool full_slots_next = false;  // the next call (a redo) sizes its slot rows in full
-  bool serial_next = false;      // the next call (a redo) runs the walk's kernels one after the other
-  DevBuf flags;                  // the overlapped walk: per run, search done and chase done (epoch tags)
   uint64_t* dbg_spec = nullptr;
   uint64_t* dbg_exit = nullptr;
   uint64_t* dbg_tin = nullptr;
@@ -132,7 +130,6 @@ struct cask_ctx {
   hipEvent_t ev[8] = {};
   hipEvent_t evw = nullptr;  // cask_ctx_wait_stream
   hipEvent_t evf = nullptr;  // walk mode: k_finish done on the side stream
-  hipEvent_t evo[3] = {};    // the overlapped walk: call start, hash grid 1 done, hash grid 2 done
   void* kd = nullptr;        // cask_shard_keydir scratch (k_keydir.hip)
   float last_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   uint64_t last_counters[5] = {0, 0, 0, 0, 0};
@@ -171,8 +168,6 @@ struct cask_ctx {
     for (hipStream_t m : masked)
       if (m) (void)hipStreamDestroy(m);
     if (evf) (void)hipEventDestroy(evf);
-    for (hipEvent_t e : evo)
-      if (e) (void)hipEventDestroy(e);
   }
 };
 
@@ -218,7 +213,6 @@ cask_ctx* cask_ctx_create(int device, int* status) {
   for (auto& e : c->ev) (void)hipEventCreate(&e);
   (void)hipEventCreateWithFlags(&c->evw, hipEventDisableTiming);
   (void)hipEventCreateWithFlags(&c->evf, hipEventDisableTiming);
-  for (auto& e : c->evo) (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
   (void)hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking);
   if (!c->err2.ensure(64)) {
     cask_ctx_destroy(c);
@@ -664,7 +658,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
   bool long_pre = false;
   bool fused = false;
   bool fin_done = false;  // k_finish already launched (beside the hash)
-  bool overlapped = false;  // the walk's kernels ran at once (the overlapped walk)
   if (mixed) {  // the walk-mode runs (split path), then the chunk-mode runs, then k_finish for all
     fused = true;
     ScanArgs aw = a;
@@ -695,42 +688,33 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     as.run_lo = 0;
     as.run_hi = nruns;
     if (!c->cdesc.ensure(16ull * (total_chunks + 1))) return CASK_E_NOMEM;
-    // The overlapped walk (the default for a walk-mode call over data files with dense rows): the
-    // search, the chase and the hash run at once — the search (then hash grid 1) on every CU but a
-    // few, the chase (then hash grid 2) on those few (kOverlapCUs; the chase is bound by its chains'
-    // latency and runs as fast there as on all of them), the runs handed over by per-run flags: the
-    // chase follows a run as soon as its search has published its start, the hash takes a run once
-    // its chase has published it. Every stream keeps to its CUs (hipExtStreamCreateWithCUMask), so
-    // none of the three can take the CUs another waits on. CASK_WALK_OVERLAP=0 (test hook) and a
-    // redo after a hash_stall run them one after the other. CASK_OVERLAP_CUS (tuning knob): the chase's CUs.
-    const char* ovh = cask_knobs::hook("CASK_WALK_OVERLAP");
-    static const int ov_cus = cask_knobs::tune("CASK_OVERLAP_CUS") ? atoi(cask_knobs::tune("CASK_OVERLAP_CUS")) : kOverlapCUs;
-    const int all_cus = device_cus();
-    bool overlap = small_slots && dense && !c->serial_next && !(ovh && !strcmp(ovh, "0")) && ov_cus > 0 && ov_cus < all_cus &&
-                   c->side && c->evf && c->evo[0] && c->evo[1] && c->evo[2];
-    c->serial_next = false;
-    if (overlap && (!c->masked[0] || !c->masked[1])) {  // the two complementary CU masks, made once
-      std::vector<uint32_t> m0((all_cus + 31) / 32, 0u), m1((all_cus + 31) / 32, 0u);
-      for (int i = 0, kept = 0; i < all_cus; ++i) {
-        if ((int64_t)(i + 1) * ov_cus / all_cus > kept) {  // ov_cus of them, spread evenly
-          m0[i / 32] |= 1u << (i % 32);
-          ++kept;
-        } else {
-          m1[i / 32] |= 1u << (i % 32);
-        }
+    // CASK_PRE_CUS / CASK_HASH_CUS (tuning knobs, diagnostics): the search + chase, or the hash, on a
+    // stream held to that many CUs (hipExtStreamCreateWithCUMask, the excluded ones spread evenly),
+    // each grid sized for them — what reserving CUs for an overlapped pre-hash would cost each side
+    static const int pre_cus = cask_knobs::tune("CASK_PRE_CUS") ? atoi(cask_knobs::tune("CASK_PRE_CUS")) : 0;
+    static const int hash_cus = cask_knobs::tune("CASK_HASH_CUS") ? atoi(cask_knobs::tune("CASK_HASH_CUS")) : 0;
+    auto masked = [&](int k, int ncu) -> hipStream_t {
+      const int all = device_cus();
+      if (ncu <= 0 || ncu >= all) return st;
+      if (!c->masked[k]) {
+        std::vector<uint32_t> m((all + 31) / 32, 0u);
+        for (int i = 0, kept = 0; i < all; ++i)
+          if ((int64_t)(i + 1) * ncu / all > kept) {  // ncu of the all bits, spread evenly
+            m[i / 32] |= 1u << (i % 32);
+            ++kept;
+          }
+        if (hipExtStreamCreateWithCUMask(&c->masked[k], (uint32_t)m.size(), m.data()) != hipSuccess) c->masked[k] = nullptr;
       }
-      if (!c->masked[0] && hipExtStreamCreateWithCUMask(&c->masked[0], (uint32_t)m0.size(), m0.data()) != hipSuccess)
-        c->masked[0] = nullptr;
-      if (!c->masked[1] && hipExtStreamCreateWithCUMask(&c->masked[1], (uint32_t)m1.size(), m1.data()) != hipSuccess)
-        c->masked[1] = nullptr;
-      overlap = c->masked[0] && c->masked[1];
+      return c->masked[k] ? c->masked[k] : st;
+    };
+    hipStream_t ps = masked(0, pre_cus), hs = masked(1, hash_cus);
+    if (ps != st) {
+      H(hipEventRecord(c->evw, st));
+      H(hipStreamWaitEvent(ps, c->evw, 0));
     }
-    if (overlap) {
-      bool ffresh = false;
-      if (!c->flags.ensure(8ull * (nruns + 1), &ffresh)) return CASK_E_NOMEM;
-      // epoch tags 1..255: cleared when the buffer is new and whenever the tag starts again at 1
-      if (ffresh || a.epoch == 1) H(hipMemsetAsync(c->flags.p, 0, 8ull * (nruns + 1), st), "memset flags");
-    }
+    launch_walk_search(as, ps, ps != st ? pre_cus : 0);
+    L("k_walk_search");
+    H(hipEventRecord(c->ev[6], ps));
     a.walk_pre = 1;
     a.cdesc = c->cdesc.as<uint64_t>();
     // The hash's tail: the last runs, in pieces whose long records are hashed before
@@ -747,74 +731,33 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
       if (!c->tbits.ensure(4ull * kTailBitWords * kTailSplit * a.hash_ntail + 256)) return CASK_E_NOMEM;
       a.tbits = c->tbits.as<uint32_t>();
     }
+    launch_walk_chase(a, ps);
+    L("k_walk_chase");
+    H(hipEventRecord(c->ev[7], ps));
+    if (ps != st) H(hipStreamWaitEvent(st, c->ev[7], 0));
+    if (hs != st) {
+      H(hipStreamWaitEvent(hs, c->ev[7], 0));
+      launch_run_hash(a, hs, hash_cus);
+      H(hipEventRecord(c->evw, hs));
+      H(hipStreamWaitEvent(st, c->evw, 0));
+    } else {
+      launch_run_hash(a, st);
+    }
+    L("k_run_hash");
+    // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
+    // starts): on a side stream it runs in the slots the hash's last waves leave, and k_hash_fix
+    // then adds the checksum statuses it may have missed. CASK_FIN_OVERLAP=0 (tuning knob): after.
     static const bool fin_overlap = !(cask_knobs::tune("CASK_FIN_OVERLAP") && atoi(cask_knobs::tune("CASK_FIN_OVERLAP")) == 0);
-    if (overlap) {
-      hipStream_t s1 = c->masked[1], s2 = c->masked[0];
-      a.sready = c->flags.as<uint32_t>();
-      a.cready = a.sready + nruns;
-      as.sready = a.sready;
-      as.tin = a.tin;
-      as.epoch = a.epoch;
-      H(hipEventRecord(c->evo[0], st));
-      H(hipStreamWaitEvent(s1, c->evo[0], 0));
-      H(hipStreamWaitEvent(s2, c->evo[0], 0));
-      launch_walk_search(as, s1, all_cus - ov_cus);
-      L("k_walk_search (overlapped)");
-      H(hipEventRecord(c->ev[6], s1));
-      launch_walk_chase_pub(a, s2, ov_cus);
-      L("k_walk_chase_pub");
-      H(hipEventRecord(c->ev[7], s2));
-      // hash grid 1 after the search, on its CUs; grid 2 after the chase, on the chase's CUs
-      const uint64_t w1 = run_hash_grid_waves(a, all_cus - ov_cus), w2 = run_hash_grid_waves(a, ov_cus);
-      ScanArgs a1 = a;
-      a1.hash_fixed = (uint32_t)w1;
-      a1.hash_claim_only = 0;
-      a1.hash_waves_all = w1 + w2;
-      launch_run_hash_pub(a1, s1, all_cus - ov_cus);
-      L("k_run_hash (grid 1)");
-      H(hipEventRecord(c->evo[1], s1));
-      ScanArgs a2 = a1;
-      a2.hash_claim_only = 1;
-      launch_run_hash_pub(a2, s2, ov_cus);
-      L("k_run_hash (grid 2)");
-      H(hipEventRecord(c->evo[2], s2));
-      // k_finish beside the hash as soon as the chase is done; k_hash_fix once all are
+    if (dense && fin_overlap && c->side && c->evf) {
+      H(hipEventRecord(c->ev[2], st));  // (the hash's end, for the timings)
       H(hipStreamWaitEvent(c->side, c->ev[7], 0));
       launch_finish(a, c->side);
       L("k_finish (beside the hash)");
       H(hipEventRecord(c->evf, c->side));
-      H(hipStreamWaitEvent(st, c->evo[1], 0));
-      H(hipStreamWaitEvent(st, c->evo[2], 0));
-      H(hipEventRecord(c->ev[2], st));  // (the hashes' end, for the timings)
       H(hipStreamWaitEvent(st, c->evf, 0));
       launch_hash_fix(a, st);
       L("k_hash_fix");
       fin_done = true;
-      overlapped = true;
-      a.sready = a.cready = nullptr;
-    } else {
-      launch_walk_search(as, st);
-      L("k_walk_search");
-      H(hipEventRecord(c->ev[6], st));
-      launch_walk_chase(a, st);
-      L("k_walk_chase");
-      H(hipEventRecord(c->ev[7], st));
-      launch_run_hash(a, st);
-      L("k_run_hash");
-      // k_finish needs only the chase's output (the chunk table, the slot rows, the speculated
-      // starts): on a side stream it runs in the slots the hash's last waves leave, and k_hash_fix
-      // then adds the checksum statuses it may have missed. CASK_FIN_OVERLAP=0 (tuning knob): after.
-      if (dense && fin_overlap && c->side && c->evf) {
-        H(hipEventRecord(c->ev[2], st));  // (the hash's end, for the timings)
-        H(hipStreamWaitEvent(c->side, c->ev[7], 0));
-        launch_finish(a, c->side);
-        L("k_finish (beside the hash)");
-        H(hipEventRecord(c->evf, c->side));
-        H(hipStreamWaitEvent(st, c->evf, 0));
-        launch_hash_fix(a, st);
-        L("k_hash_fix");
-        fin_done = true;
-      }
     }
     a.walk_pre = 0;
     long_pre = true;
@@ -840,10 +783,6 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     if (!ok) return CASK_E_DEVICE;
   }
 
-  if (overlapped && hc->hash_stall) {  // a wave gave up waiting for a run: the call again, in sequence
-    c->serial_next = true;
-    return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, hint);
-  }
   if (small_slots && hc->slot_overflow) {  // a chunk's rows were cut at kWalkSlotCap: redo in full
     c->full_slots_next = true;
     return scan_device_impl(c, files, nfiles, rows, file_row_offset, err, hint);
@@ -877,12 +816,7 @@ static int scan_device_impl(cask_ctx* c, const cask_file_view* files, uint32_t n
     float t_all = 0, t_k1 = 0, t_fin = 0, t_long = 0, t_search = 0;
     (void)hipEventElapsedTime(&t_all, c->ev[1], more ? c->ev[4] : c->ev[3]);
     float t_chase = 0;
-    if (overlapped) {  // [6] the searches' end, [7] the chase's (beside the search), [2] the hashes'
-      (void)hipEventElapsedTime(&t_search, c->ev[1], c->ev[6]);
-      (void)hipEventElapsedTime(&t_chase, c->ev[6], c->ev[7]);  // (the chase's time after the search)
-      if (t_chase < 0) t_chase = 0;
-      (void)hipEventElapsedTime(&t_k1, c->ev[6], c->ev[2]);  // (the hash after the search)
-    } else if (fused) {  // [1] is k_run_hash alone, [6] the run searches, [7] the chase
+    if (fused) {  // [1] is k_run_hash alone, [6] the run searches, [7] the chase
       (void)hipEventElapsedTime(&t_search, c->ev[1], c->ev[6]);
       (void)hipEventElapsedTime(&t_chase, c->ev[6], c->ev[7]);
       (void)hipEventElapsedTime(&t_k1, c->ev[7], c->ev[2]);
