@@ -124,15 +124,31 @@ struct HugeAlloc {
       void* p = ::operator new(b, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
       return static_cast<T*>(p);
     }
+    // fresh anonymous pages, 2-MiB aligned (over-map by one huge page and trim): zero until first
+    // written, so a table of empty slots costs no fill pass (KeyDir::reserve)
     const size_t r = (b + kHuge - 1) & ~(kHuge - 1);
-    void* p = std::aligned_alloc(kHuge, r);
-    if (!p) throw std::bad_alloc();
-    (void)madvise(p, r, MADV_HUGEPAGE);
-    return static_cast<T*>(p);
+    void* m = mmap(nullptr, r + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) throw std::bad_alloc();
+    const uintptr_t a = ((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1);
+    if (a > (uintptr_t)m) munmap(m, a - (uintptr_t)m);
+    const uintptr_t e = (uintptr_t)m + r + kHuge;
+    if (e > a + r) munmap((void*)(a + r), e - (a + r));
+    (void)madvise((void*)a, r, MADV_HUGEPAGE);
+    return reinterpret_cast<T*>(a);
+  }
+  static bool zeroed(size_t n) { return n * sizeof(T) >= kHuge; }  // allocate(n) hands out zero bytes
+  template <class U>
+  void construct(U* p) noexcept {  // resize/size-constructor leave trivial elements uninitialized
+    ::new (static_cast<void*>(p)) U;
+  }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) {
+    ::new (static_cast<void*>(p)) U(std::forward<A>(a)...);
   }
   void deallocate(T* p, size_t n) {
-    if (n * sizeof(T) < kHuge) ::operator delete(p, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
-    else std::free(p);
+    const size_t b = n * sizeof(T);
+    if (b < kHuge) ::operator delete(p, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
+    else munmap(p, (b + kHuge - 1) & ~(kHuge - 1));
   }
   template <class U>
   bool operator==(const HugeAlloc<U>&) const { return true; }
@@ -199,7 +215,8 @@ class KeyDir {
     if (cap == slots.size() && (used + 1) * 4 <= cap * 3) return;
     std::vector<Slot, HugeAlloc<Slot>> old;
     old.swap(slots);
-    slots.assign(cap, Slot{});
+    slots.resize(cap);  // (default-initialised: a huge allocation is zero already, see HugeAlloc)
+    if (!HugeAlloc<Slot>::zeroed(cap)) memset((void*)slots.data(), 0, cap * sizeof(Slot));
     used = 0;
     const uint64_t m = cap - 1;
     for (const Slot& s : old) {
@@ -1248,8 +1265,9 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
   const bool dev_fold = !views.empty() && scan_idx.size() == nf && !(dfh && !strcmp(dfh, "0"));
   std::vector<uint64_t> roff_all(views.size() + 1, 0);  // (dev_fold) each view's first row
   EngineDev::AllRows all_rows;
-  RawBytes dblock;              // (dev_fold) the block, on the host
+  HostBuf dblock;               // (dev_fold) the block, on the host (huge pages: the copy faults 2-MiB pages)
   double t_blk = 0, t_blk_d2h = 0;  // (dev_fold) its build on the device, its copy to the host
+  uint64_t dblock_n = 0;        // (dev_fold) its bytes
   int dblock_st = CASK_E_IO;    // (dev_fold) CASK_OK once the block is here
   bool dblock_done = false;
   struct Batch {
@@ -1355,8 +1373,9 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
         if (st != CASK_OK) return st;
         t_blk = ms_since(td);
         const auto tc = std::chrono::steady_clock::now();
-        if (!dblock.resize(nb)) return (int)CASK_E_NOMEM;
-        st = ed->to_host(dblock.data(), (const uint8_t*)blk, nb);
+        if (!dblock.alloc(std::max<uint64_t>(nb, 1))) return (int)CASK_E_NOMEM;
+        dblock_n = nb;
+        st = ed->to_host(dblock.get(), (const uint8_t*)blk, nb);
         t_blk_d2h = ms_since(tc);
         return st;
       });
@@ -1557,15 +1576,15 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
     if (st == CASK_OK) {
       const auto tm = std::chrono::steady_clock::now();
       db->merging = true;
-      st = cask_keydir_merge(db, dblock.data(), dblock.size());
+      st = cask_keydir_merge(db, dblock.get(), dblock_n);
       t_merge = ms_since(tm);
       if (st == CASK_OK) st = cask_keydir_finish(db);
     }
     if (cask_knobs::hook("CASK_OPEN_TRACE"))
       fprintf(stderr, "open (device-reduced keydir): block %.1f ms on the device, %.1f ms to the host (%llu B); "
                       "waited %.1f ms; merge %.1f ms, finish %.1f ms\n",
-              t_blk, t_blk_d2h, (unsigned long long)dblock.size(), t_wait, t_merge, ms_since(tf3) - t_wait - t_merge);
-    RawBytes().p.swap(dblock.p);
+              t_blk, t_blk_d2h, (unsigned long long)dblock_n, t_wait, t_merge, ms_since(tf3) - t_wait - t_merge);
+    dblock.reset();
     if (st != CASK_OK) {
       fail = st;
       fail_fid = 0;
@@ -2557,6 +2576,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   const unsigned nt = n < min_par ? 1u : std::min(host_threads(), Index::kSub);
   constexpr unsigned S = Index::kSub;
   const unsigned np = nt == 1 ? 1u : 4 * nt;  // pieces
+  const auto tm0 = std::chrono::steady_clock::now();
   // every piece's first key offset (the keys lie in record order), checked before anything changes
   std::vector<uint64_t> pko(np + 1, 0);
   parallel_for(nt, [&](unsigned t) {
@@ -2580,34 +2600,63 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     };
     const uint8_t* key() const { return ksz <= KeyDir::kInline ? kin : kp; }
   };
-  std::vector<std::vector<Item>> lists((size_t)np * S);
+  // (a) every record's key hash, and per (piece, table) how many: (b) one array of items in (table,
+  // piece, block) order — written once, in place, no list growing, huge pages (a list per piece and
+  // table of freshly allocated small vectors cost the pass its page faults: 0.39 s per 20 M records
+  // on 8 threads, tools/merge_bench.py)
+  const auto tmA = std::chrono::steady_clock::now();
+  std::vector<uint64_t, HugeAlloc<uint64_t>> hs(n);  // (uninitialized: HugeAlloc::construct)
+  std::vector<uint64_t> cnt((size_t)np * S, 0);
   std::vector<uint64_t> nconds(np, 0);
   parallel_for(nt, [&](unsigned t) {
     for (unsigned g = t; g < np; g += nt) {
-      const uint64_t lo = n * g / np, hi = n * (g + 1) / np;
-      std::vector<Item>* L = &lists[(size_t)g * S];
-      for (unsigned q = 0; q < S; ++q) L[q].reserve((hi - lo) / S + (hi - lo) / (4 * S) + 16);
+      uint64_t* c = &cnt[(size_t)g * S];
       uint64_t ko = pko[g];
-      for (uint64_t i = lo; i < hi; ++i) {
+      uint64_t lc[S] = {}, nc = 0;  // (locals: no stores to lines other threads write)
+      for (uint64_t i = n * g / np, e = n * (g + 1) / np; i < e; ++i) {
+        const uint64_t h = hash_key(keys + ko, rec[i].ksz);
+        hs[i] = h;
+        ++lc[Index::sub_of(h)];
+        nc += rec[i].kind == kCond;
+        ko += rec[i].ksz;
+      }
+      for (unsigned q = 0; q < S; ++q) c[q] = lc[q];
+      nconds[g] = nc;
+    }
+  });
+  std::vector<uint64_t> at((size_t)np * S + 1, 0);  // (table q, piece g) starts at at[q * np + g]
+  for (unsigned q = 0, k = 0; q < S; ++q)
+    for (unsigned g = 0; g < np; ++g, ++k) at[k + 1] = at[k] + cnt[(size_t)g * S + q];
+  const auto tmB = std::chrono::steady_clock::now();
+  std::vector<Item, HugeAlloc<Item>> items(n);
+  parallel_for(nt, [&](unsigned t) {
+    for (unsigned g = t; g < np; g += nt) {
+      uint64_t w[S];
+      for (unsigned q = 0; q < S; ++q) w[q] = at[(size_t)q * np + g];
+      uint64_t ko = pko[g];
+      for (uint64_t i = n * g / np, e = n * (g + 1) / np; i < e; ++i) {
         const ShardRec& r = rec[i];
-        Item it;
-        it.ksz = r.ksz;
-        it.hash = hash_key(keys + ko, r.ksz);
+        Item& it = items[w[Index::sub_of(hs[i])]++];
+        it.hash = hs[i];
         it.seq = r.seq;
         it.pos = r.pos;
         it.file_id = r.file_id;
         it.vsz = r.vsz;
+        it.ksz = r.ksz;
         it.kind = r.kind;
         it.pad0 = 0;
         it.pad1 = 0;
         if (r.ksz <= KeyDir::kInline) memcpy(it.kin, keys + ko, r.ksz);
         else it.kp = keys + ko;
-        nconds[g] += r.kind == kCond;
-        L[Index::sub_of(it.hash)].push_back(it);
         ko += r.ksz;
       }
     }
   });
+  std::vector<uint64_t, HugeAlloc<uint64_t>>().swap(hs);
+  const bool tracing = cask_knobs::hook("CASK_OPEN_TRACE") != nullptr;
+  const auto tm1 = std::chrono::steady_clock::now();
+  if (tracing) fprintf(stderr, "keydir merge: %llu records, lists %.1f ms (pko %.1f, hash %.1f)\n", (unsigned long long)n, ms_since(tm0), std::chrono::duration<double, std::milli>(tmA - tm0).count(), std::chrono::duration<double, std::milli>(tmB - tmA).count());
+  std::vector<double> tres(nt, 0.0);
   // phase 0 (the thresholds) only for a block with conditional tombstones, against a keydir that
   // holds something (an empty one stales none of them)
   uint64_t ncond = 0;
@@ -2622,13 +2671,13 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     };
     for (unsigned q = t; q < S; q += nt) {
       KeyDir& kd = db->index.sub[q];
-      uint64_t cnt = 0;  // room for every record's key: a block holds about one record per key
-      for (unsigned g = 0; g < np; ++g) cnt += lists[(size_t)g * S + q].size();
-      kd.reserve(kd.live + cnt);
-      for (int phase = first_phase; phase < 2; ++phase)
-        for (unsigned g = 0; g < np; ++g) {
-          const std::vector<Item>& Lq = lists[(size_t)g * S + q];
-          const size_t m = Lq.size();
+      const Item* Lq = items.data() + at[(size_t)q * np];
+      const size_t m = at[(size_t)(q + 1) * np] - at[(size_t)q * np];  // the table's items, in block order
+      const auto tr = std::chrono::steady_clock::now();
+      kd.reserve(kd.live + m);  // (room for every record's key: a block holds about one record per key)
+      tres[t] += ms_since(tr);
+      for (int phase = first_phase; phase < 2; ++phase) {
+        {
           for (size_t jj = 0; jj < m; ++jj) {
             if (jj + 16 < m) kd.prefetch(Lq[jj + 16].hash);
             if (jj + 4 < m) kd.prefetch_key(Lq[jj + 4].hash);
@@ -2652,10 +2701,11 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
             }
             kd.update_kd(r.key(), r.ksz, r.file_id, r.pos, r.vsz, r.seq, r.hash);
           }
-          if (phase == 1) std::vector<Item>().swap(lists[(size_t)g * S + q]);
         }
+      }
     }
   });
+  if (tracing) fprintf(stderr, "keydir merge: tables %.1f ms (reserve %.1f per thread)\n", ms_since(tm1), tres[0]);
   for (const auto& m : sterms)
     for (const auto& kv : m) {
       cask_db::ShardTerms& x = db->terms[kv.first];
