@@ -181,11 +181,15 @@ class KeyDir {
   KeyDir() { slots.assign(256, Slot{}); }
 
   const uint8_t* key_of(const Slot& s) const { return s.ksz <= kInline ? s.kin : arena.data() + s.key_off; }
-  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[h & (slots.size() - 1)]); }
+  // a key's home slot: the hash's bits below the table bits (Index::sub_of), scaled to the table —
+  // any size, not only powers of two (a table sized to its keys: 4.5 instead of 8 GB of slots for
+  // configs[3]'s 52 M keys, all of which are first-touch page faults in the merge)
+  uint64_t home(uint64_t h) const { return (uint64_t)(((unsigned __int128)(h << 6) * slots.size()) >> 64); }
+  void prefetch(uint64_t h) const { __builtin_prefetch(&slots[home(h)]); }
   // the arena bytes of a long key on the slot h lands on, once that slot is in cache (prefetch() a
   // few records before)
   void prefetch_key(uint64_t h) const {
-    const Slot& s = slots[h & (slots.size() - 1)];
+    const Slot& s = slots[home(h)];
     if (s.state == 1 && s.hash == h && s.ksz > kInline) __builtin_prefetch(arena.data() + s.key_off);
   }
 
@@ -200,8 +204,8 @@ class KeyDir {
   }
 
   int64_t find(const uint8_t* k, uint32_t n, uint64_t h) const {
-    const uint64_t m = slots.size() - 1;
-    for (uint64_t i = h & m;; i = (i + 1) & m) {
+    const uint64_t c = slots.size();
+    for (uint64_t i = home(h);; i = i + 1 == c ? 0 : i + 1) {
       const Slot& s = slots[i];
       if (s.state == 0) return -(int64_t)i - 1;
       if (s.state == 1 && s.hash == h && s.ksz == n && key_eq(s, k, n)) return (int64_t)i;
@@ -210,19 +214,22 @@ class KeyDir {
 
   // Room for n live keys without growing; a rebuild drops the slots of deleted keys.
   void reserve(uint64_t n) {
-    uint64_t cap = slots.size();
-    while (cap * 3 < (std::max(n, live) + 1) * 4) cap *= 2;
-    if (cap == slots.size() && (used + 1) * 4 <= cap * 3) return;
+    // load 1/2 once sized (a slot is a line: each probe past the home slot is one more line;
+    // 0.39-0.7 measured within 15 % at configs[3]'s 52 M keys, tools/merge_bench.py), growing at 3/4
+    const uint64_t need = 2 * (std::max(n, live) + 1);
+    if (slots.size() >= need && (used + 1) * 4 <= slots.size() * 3) return;
+    constexpr uint64_t kG = HugeAlloc<Slot>::kHuge / sizeof(Slot);  // (whole huge pages when large)
+    const uint64_t cap = slots.size() >= need ? slots.size()  // (same size: the deleted slots dropped)
+                         : need <= 256 ? 256 : need < kG ? (need + 63) & ~63ull : (need + kG - 1) / kG * kG;
     std::vector<Slot, HugeAlloc<Slot>> old;
     old.swap(slots);
     slots.resize(cap);  // (default-initialised: a huge allocation is zero already, see HugeAlloc)
     if (!HugeAlloc<Slot>::zeroed(cap)) memset((void*)slots.data(), 0, cap * sizeof(Slot));
     used = 0;
-    const uint64_t m = cap - 1;
     for (const Slot& s : old) {
       if (s.state != 1) continue;
-      uint64_t i = s.hash & m;
-      while (slots[i].state) i = (i + 1) & m;
+      uint64_t i = home(s.hash);
+      while (slots[i].state) i = i + 1 == cap ? 0 : i + 1;
       slots[i] = s;
       ++used;
     }
@@ -618,6 +625,20 @@ struct HostBuf {
     return true;
   }
   uint8_t* get() const { return p; }
+  // unmapped on a thread of its own (a multi-GiB mapping takes a while to give back, and nothing
+  // waits for it), or here when no thread can be had
+  void reset_async() {
+    if (!p) return;
+    uint8_t* q = p;
+    const size_t m = n;
+    p = nullptr;
+    n = 0;
+    try {
+      std::thread([q, m] { munmap(q, m); }).detach();
+    } catch (...) {
+      munmap(q, m);
+    }
+  }
 };
 
 // A whole file into a HostBuf (no zero fill before the read, huge pages); false on an I/O error.
@@ -1065,6 +1086,9 @@ struct cask_db {
   std::unordered_map<uint32_t, ShardTerms> terms;
   bool merging = false;
   uint32_t shards = 0;
+  // the merge's scratch (key hashes, items), kept from block to block and given back after the
+  // last one (cask_keydir_finish), off the calling thread
+  HostBuf mhash, mitems;
   // the bytes of files a compaction took out of the database, released on a thread of their own
   // (joined before the next compaction and at close)
   std::thread reclaim;
@@ -1584,7 +1608,7 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
       fprintf(stderr, "open (device-reduced keydir): block %.1f ms on the device, %.1f ms to the host (%llu B); "
                       "waited %.1f ms; merge %.1f ms, finish %.1f ms\n",
               t_blk, t_blk_d2h, (unsigned long long)dblock_n, t_wait, t_merge, ms_since(tf3) - t_wait - t_merge);
-    dblock.reset();
+    dblock.reset_async();
     if (st != CASK_OK) {
       fail = st;
       fail_fid = 0;
@@ -2605,7 +2629,14 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   // table of freshly allocated small vectors cost the pass its page faults: 0.39 s per 20 M records
   // on 8 threads, tools/merge_bench.py)
   const auto tmA = std::chrono::steady_clock::now();
-  std::vector<uint64_t, HugeAlloc<uint64_t>> hs(n);  // (uninitialized: HugeAlloc::construct)
+  // (scratch in db: the next block reuses its pages; cask_keydir_finish gives it back)
+  auto scratch = [](HostBuf& b, uint64_t bytes) -> uint8_t* {
+    if (b.n >= bytes) return b.get();
+    b.reset_async();
+    if (!b.alloc(bytes)) throw std::bad_alloc();
+    return b.get();
+  };
+  uint64_t* hs = (uint64_t*)scratch(db->mhash, std::max<uint64_t>(n, 1) * sizeof(uint64_t));
   std::vector<uint64_t> cnt((size_t)np * S, 0);
   std::vector<uint64_t> nconds(np, 0);
   parallel_for(nt, [&](unsigned t) {
@@ -2628,7 +2659,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   for (unsigned q = 0, k = 0; q < S; ++q)
     for (unsigned g = 0; g < np; ++g, ++k) at[k + 1] = at[k] + cnt[(size_t)g * S + q];
   const auto tmB = std::chrono::steady_clock::now();
-  std::vector<Item, HugeAlloc<Item>> items(n);
+  Item* items = (Item*)scratch(db->mitems, std::max<uint64_t>(n, 1) * sizeof(Item));
   parallel_for(nt, [&](unsigned t) {
     for (unsigned g = t; g < np; g += nt) {
       uint64_t w[S];
@@ -2652,7 +2683,6 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
       }
     }
   });
-  std::vector<uint64_t, HugeAlloc<uint64_t>>().swap(hs);
   const bool tracing = cask_knobs::hook("CASK_OPEN_TRACE") != nullptr;
   const auto tm1 = std::chrono::steady_clock::now();
   if (tracing) fprintf(stderr, "keydir merge: %llu records, lists %.1f ms (pko %.1f, hash %.1f)\n", (unsigned long long)n, ms_since(tm0), std::chrono::duration<double, std::milli>(tmA - tm0).count(), std::chrono::duration<double, std::milli>(tmB - tmA).count());
@@ -2671,7 +2701,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     };
     for (unsigned q = t; q < S; q += nt) {
       KeyDir& kd = db->index.sub[q];
-      const Item* Lq = items.data() + at[(size_t)q * np];
+      const Item* Lq = items + at[(size_t)q * np];
       const size_t m = at[(size_t)(q + 1) * np] - at[(size_t)q * np];  // the table's items, in block order
       const auto tr = std::chrono::steady_clock::now();
       kd.reserve(kd.live + m);  // (room for every record's key: a block holds about one record per key)
@@ -2706,6 +2736,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     }
   });
   if (tracing) fprintf(stderr, "keydir merge: tables %.1f ms (reserve %.1f per thread)\n", ms_since(tm1), tres[0]);
+  const auto tm2 = std::chrono::steady_clock::now();
   for (const auto& m : sterms)
     for (const auto& kv : m) {
       cask_db::ShardTerms& x = db->terms[kv.first];
@@ -2723,6 +2754,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   }
   if (hd.max_seq_p1 && hd.max_seq_p1 - 1 > db->sequence) db->sequence = hd.max_seq_p1 - 1;
   ++db->shards;
+  if (tracing) fprintf(stderr, "keydir merge: terms %.1f ms\n", ms_since(tm2));
   return CASK_OK;
 }
 
@@ -2747,6 +2779,8 @@ int cask_keydir_finish(cask_db* db) {
     db->files.erase(std::unique(db->files.begin(), db->files.end()), db->files.end());
     db->file_seq = db->files.empty() ? 0u : db->files.back();
     db->merging = false;
+    db->mhash.reset_async();
+    db->mitems.reset_async();
     return CASK_OK;
   });
 }
