@@ -110,23 +110,32 @@ class StatsDelta {
 
 // Allocator for large tables: 2-MiB-aligned and advised as transparent huge pages (a keydir fold
 // hits random slots of tables of tens of MB; with 4-KiB pages nearly every access also misses the
-// TLB). Small allocations take the ordinary heap.
+// TLB). Small allocations take the ordinary heap; up to kMap the heap's huge-aligned blocks (which a
+// later table of the process reuses without new page faults: the host fold's 16-MB tables), above it
+// fresh anonymous pages, zero until first written, so a table of empty slots costs no fill pass
+// (KeyDir::reserve; configs[3]'s merge tables of ~90 MB, which the heap would map afresh anyway).
 template <class T>
 struct HugeAlloc {
   using value_type = T;
   HugeAlloc() = default;
   template <class U>
   HugeAlloc(const HugeAlloc<U>&) {}
-  static constexpr size_t kHuge = 2ull << 20;
+  static constexpr size_t kHuge = 2ull << 20, kMap = 32ull << 20;
+  static size_t rounded(size_t b) { return (b + kHuge - 1) & ~(kHuge - 1); }
   T* allocate(size_t n) {
     const size_t b = n * sizeof(T);
     if (b < kHuge) {
       void* p = ::operator new(b, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
       return static_cast<T*>(p);
     }
-    // fresh anonymous pages, 2-MiB aligned (over-map by one huge page and trim): zero until first
-    // written, so a table of empty slots costs no fill pass (KeyDir::reserve)
-    const size_t r = (b + kHuge - 1) & ~(kHuge - 1);
+    const size_t r = rounded(b);
+    if (b < kMap) {
+      void* p = std::aligned_alloc(kHuge, r);
+      if (!p) throw std::bad_alloc();
+      (void)madvise(p, r, MADV_HUGEPAGE);
+      return static_cast<T*>(p);
+    }
+    // (over-map by one huge page and trim to a 2-MiB-aligned range)
     void* m = mmap(nullptr, r + kHuge, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
     if (m == MAP_FAILED) throw std::bad_alloc();
     const uintptr_t a = ((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1);
@@ -136,7 +145,7 @@ struct HugeAlloc {
     (void)madvise((void*)a, r, MADV_HUGEPAGE);
     return reinterpret_cast<T*>(a);
   }
-  static bool zeroed(size_t n) { return n * sizeof(T) >= kHuge; }  // allocate(n) hands out zero bytes
+  static bool zeroed(size_t n) { return n * sizeof(T) >= kMap; }  // allocate(n) hands out zero bytes
   template <class U>
   void construct(U* p) noexcept {  // resize/size-constructor leave trivial elements uninitialized
     ::new (static_cast<void*>(p)) U;
@@ -148,7 +157,8 @@ struct HugeAlloc {
   void deallocate(T* p, size_t n) {
     const size_t b = n * sizeof(T);
     if (b < kHuge) ::operator delete(p, std::align_val_t(alignof(T) < 64 ? 64 : alignof(T)));
-    else munmap(p, (b + kHuge - 1) & ~(kHuge - 1));
+    else if (b < kMap) std::free(p);
+    else munmap(p, rounded(b));
   }
   template <class U>
   bool operator==(const HugeAlloc<U>&) const { return true; }
@@ -214,12 +224,16 @@ class KeyDir {
 
   // Room for n live keys without growing; a rebuild drops the slots of deleted keys.
   void reserve(uint64_t n) {
-    // load 1/2 once sized (a slot is a line: each probe past the home slot is one more line;
-    // 0.39-0.7 measured within 15 % at configs[3]'s 52 M keys, tools/merge_bench.py), growing at 3/4
-    const uint64_t need = 2 * (std::max(n, live) + 1);
-    if (slots.size() >= need && (used + 1) * 4 <= slots.size() * 3) return;
+    // A table holds up to 3/4 of its slots; one that must grow is sized to 3/5 (a slot is a line:
+    // each probe past the home slot is one more line, each slot a first-touch fault; loads 0.39-0.6
+    // measured within 15 % at configs[3]'s 52 M keys, profiles/r06h_merge_loadsweep.txt, and 0.63
+    // against 0.42 faster in the host fold, tools/fold_bench.py)
+    const uint64_t m = std::max(n, live) + 1;
+    const bool fits = slots.size() * 3 >= m * 4;
+    if (fits && (used + 1) * 4 <= slots.size() * 3) return;
     constexpr uint64_t kG = HugeAlloc<Slot>::kHuge / sizeof(Slot);  // (whole huge pages when large)
-    const uint64_t cap = slots.size() >= need ? slots.size()  // (same size: the deleted slots dropped)
+    const uint64_t need = m * 5 / 3 + 1;
+    const uint64_t cap = fits ? slots.size()  // (same size: the deleted slots dropped)
                          : need <= 256 ? 256 : need < kG ? (need + 63) & ~63ull : (need + kG - 1) / kG * kG;
     std::vector<Slot, HugeAlloc<Slot>> old;
     old.swap(slots);

@@ -9,4 +9,6 @@ timeout -k 10 300 python -u tools/merge_bench.py 52000000 > gpurun_out/r06h_merg
 rc=$?; cat gpurun_out/r06h_merge.log; echo "merge rc=$rc"; [ $rc -ne 0 ] && exit $rc
 CASK_OPEN_TRACE=1 timeout -k 10 500 python -u tools/bench_configs.py openab --files 64 --dir /dev/shm --out gpurun_out/r06h_openab.json > gpurun_out/r06h_openab.log 2>&1
 rc=$?; grep -E "^open|device-reduced|keydir merge" gpurun_out/r06h_openab.log; echo "openab rc=$rc"; [ $rc -ne 0 ] && { tail -30 gpurun_out/r06h_openab.log; exit $rc; }
-exit 0
+[ -n "$NOBIG" ] && exit 0
+timeout -k 10 400 python -u tools/bigkeys_bench.py --gib 8 --out gpurun_out/r06h_bigkeys.json > gpurun_out/r06h_bigkeys.log 2>&1
+rc=$?; grep -v amdgpu.ids gpurun_out/r06h_bigkeys.log | tail -8; echo "bigkeys rc=$rc"; exit $rc
