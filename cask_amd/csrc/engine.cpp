@@ -2647,8 +2647,8 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   auto scratch = [](HostBuf& b, uint64_t bytes) -> uint8_t* {
     if (b.n >= bytes) return b.get();
     b.reset_async();
-    if (!b.alloc(bytes)) throw std::bad_alloc();
-    return b.get();
+    if (!b.alloc(bytes + bytes / 2)) throw std::bad_alloc();  // (headroom for a larger next block:
+    return b.get();                                            // untouched pages cost nothing)
   };
   uint64_t* hs = (uint64_t*)scratch(db->mhash, std::max<uint64_t>(n, 1) * sizeof(uint64_t));
   std::vector<uint64_t> cnt((size_t)np * S, 0);
