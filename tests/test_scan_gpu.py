@@ -312,6 +312,47 @@ def test_zipf_sizes_long_records(gpu_ctx, seed):
     assert cnt["walked"] == 0, cnt
 
 
+@pytest.mark.parametrize("seqs", ["rising", "shuffled", "jumps", "corrupt"])
+def test_walk_search_long_stretches(gpu_ctx, seqs):
+    """k_walk_search where a run's first short record lies behind stretches of 4-8 records of ~64 KiB
+    (>= 30 windows of 8 KiB): the probe follows the long candidates' chains header to header to the
+    first short record and hashes it (k_walk.hip, phase 3). Its chains must raise the sequence by at
+    most 2^32 per hop: with rising sequences it takes that path; with the sequences shuffled, or
+    jumping by 2^33 at every stretch, it must fall back to the windows; with a byte flipped in some
+    of the short records behind the stretches (their checksums fail) it must move on to a later
+    candidate. Rows and the first error equal the oracle's row for row (24 MiB: many 1-MiB runs
+    start inside a stretch)."""
+    rng = random.Random(0x5EA)
+    recs, seq, bad = [], 1, []
+    seqlist = list(range(1, 4000))
+    if seqs == "shuffled":
+        rng.shuffle(seqlist)
+    total = 0
+    while total < 24 << 20:
+        for _ in range(rng.randrange(4, 9)):
+            s = seqlist[len(recs)] if seqs == "shuffled" else seq
+            recs.append(R.entry_new(s, rng.randbytes(16), rng.randbytes(rng.randrange(60000, 65536))).write_bytes())
+            seq += 1
+            total += len(recs[-1])
+        if seqs == "jumps":
+            seq += 1 << 33
+        for j in range(rng.randrange(1, 4)):
+            s = seqlist[len(recs)] if seqs == "shuffled" else seq
+            r = bytearray(R.entry_new(s, rng.randbytes(16), rng.randbytes(rng.randrange(0, 200))).write_bytes())
+            if seqs == "corrupt" and j == 0 and rng.random() < 0.3:
+                r[len(r) - 1 if len(r) > 34 else 20] ^= 0x40
+                bad.append(len(recs))
+            recs.append(bytes(r))
+            seq += 1
+            total += len(recs[-1])
+    assert seqs != "corrupt" or bad
+    buf = b"".join(recs)
+    check_against_oracle(gpu_ctx, [buf, buf[: len(buf) // 2 + 12345]], device=True)
+    cnt = gpu_ctx.last_counters()
+    if os.environ.get("CASK_SCAN_MODE") in (None, "walk") and seqs != "corrupt":
+        assert cnt["walk_mode"] >= 1 and cnt["walked"] == 0, cnt
+
+
 def test_walk_slot_rows_overflow_redo(gpu_ctx):
     """A walk-mode call sizes its slot rows for kWalkSlotCap (128) records per 32-KiB chunk: a log of
     long records with a burst of ~600 tiny ones inside one chunk overflows them, and the call is
