@@ -173,45 +173,10 @@ struct TailBits {
   }
 };
 
-#ifndef CASK_CHASE_STAGE  // (A/B variant: a lane's slot rows staged in LDS, stored a line at a time)
-#define CASK_CHASE_STAGE 0
-#endif
-// A lane's slot rows of one 128-B line of its chunk, held in LDS until the chain leaves the line
-// (CASK_CHASE_STAGE): the line's rows then go out in consecutive stores instead of one per hop.
-struct RowStage {
-  u32x4* buf;      // the lane's 8 rows in LDS
-  uint64_t at = 0; // slot index (in rows) of the staged line's first row
-  uint32_t n = 0;  // rows staged (rows at..at+n-1)
-  __device__ __forceinline__ void flush(g_u32* slots) {
-    for (uint32_t k = 0; k < n; ++k) *(g_u32x4*)(slots + (at + k) * 4) = buf[k];
-    n = 0;
-  }
-  __device__ __forceinline__ void put(g_u32* slots, uint64_t idx, const u32x4& row) {
-    const uint64_t line = idx & ~7ull;
-    if (n && (line != at || idx != at + n)) flush(slots);
-    if (!n) at = line;
-    // (rows of a chunk come in order from 0; a line's first row is its first staged row)
-    if (idx != at + n) {
-      *(g_u32x4*)(slots + idx * 4) = row;
-      return;
-    }
-    buf[n++] = row;
-    if (n == 8) flush(slots);
-  }
-};
-
 __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ files, uint64_t tb, uint64_t te,
                                 uint64_t p_in) {
   const uint32_t csh = (uint32_t)__builtin_ctz(a.chunk);
   g_u32* slots = (g_u32*)a.slots;
-#if CASK_CHASE_STAGE
-  __shared__ u32x4 s_rows[256][8];
-  RowStage stg;
-  stg.buf = s_rows[threadIdx.x];
-#define CASK_ROW_STORE(idx, row) stg.put(slots, (idx), (row))
-#else
-#define CASK_ROW_STORE(idx, row) (*(g_u32x4*)(slots + (idx) * 4) = (row))
-#endif
   g_u64* cd = (g_u64*)a.cdesc;
   TailBits tbt;
   {
@@ -258,7 +223,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
         const uint32_t r = open_record(a, W, p, csh, true, &j);
         if (tbt.on) tbt.record(a, W.S.t0 + j, false);
         const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
-        if (r < a.slot_cap) CASK_ROW_STORE((W.S.t0 + j) * (uint64_t)a.slot_cap + r, (u32x4{0u, 0u, 0u, off << 16}));
+        if (r < a.slot_cap) *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{0u, 0u, 0u, off << 16};
         if (r < W.ccerr) W.ccerr = r;
         term = true;
         break;
@@ -273,7 +238,7 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
       if (tbt.on) tbt.record(a, W.S.t0 + j, rl >= kTailLong);
       const uint32_t off = (uint32_t)(p - W.S.b0 - ((uint64_t)j << csh));
       if (r < a.slot_cap)
-        CASK_ROW_STORE((W.S.t0 + j) * (uint64_t)a.slot_cap + r, (u32x4{row.x, row.y, row.z, row.w | (off << 16)}));
+        *(g_u32x4*)(slots + ((W.S.t0 + j) * (uint64_t)a.slot_cap + r) * 4) = u32x4{row.x, row.y, row.z, row.w | (off << 16)};
       if (pn > W.S.len) {  // key or value cut short (data.rs:172,181)
         if (r < W.ccerr) W.ccerr = r;
         term = true;
@@ -285,10 +250,6 @@ __device__ uint64_t chase_range(const ScanArgs& a, const FileDesc* __restrict__ 
     if (term) p = kTerm;
   }
   if (tbt.on) tbt.flush(a);
-#if CASK_CHASE_STAGE
-  stg.flush(slots);
-#endif
-#undef CASK_ROW_STORE
   return p;
 }
 
