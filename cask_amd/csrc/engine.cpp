@@ -224,15 +224,16 @@ class KeyDir {
 
   // Room for n live keys without growing; a rebuild drops the slots of deleted keys.
   void reserve(uint64_t n) {
-    // A table holds up to 3/4 of its slots; one that must grow is sized to 3/5 (a slot is a line:
-    // each probe past the home slot is one more line, each slot a first-touch fault; loads 0.39-0.6
-    // measured within 15 % at configs[3]'s 52 M keys, profiles/r06h_merge_loadsweep.txt, and 0.63
-    // against 0.42 faster in the host fold, tools/fold_bench.py)
+    // A table holds up to 3/4 of its slots; one that must grow is sized to 2/5 (a slot is a line:
+    // each probe past the home slot is one more line, each slot a first-touch fault. configs[3]'s
+    // 52 M-key merge: loads 0.39-0.6 within 15 % of each other, 0.39 the fastest,
+    // profiles/r06h_merge_loadsweep.txt; its compaction's 42 M lookups: 0.70-0.74 s at 0.39 against
+    // 0.86-0.87 at 0.6, profiles/r06k_compaction_ab.txt)
     const uint64_t m = std::max(n, live) + 1;
     const bool fits = slots.size() * 3 >= m * 4;
     if (fits && (used + 1) * 4 <= slots.size() * 3) return;
     constexpr uint64_t kG = HugeAlloc<Slot>::kHuge / sizeof(Slot);  // (whole huge pages when large)
-    const uint64_t need = m * 5 / 3 + 1;
+    const uint64_t need = m * 5 / 2 + 1;
     const uint64_t cap = fits ? slots.size()  // (same size: the deleted slots dropped)
                          : need <= 256 ? 256 : need < kG ? (need + 63) & ~63ull : (need + kG - 1) / kG * kG;
     std::vector<Slot, HugeAlloc<Slot>> old;
@@ -1058,7 +1059,11 @@ void parallel_fold(const std::vector<FoldSrc>& src, Index& out, FoldScratch* kee
         double est = 0.7213 / (1 + 1.079 / kReg) * kReg * kReg / z;
         if (est < 2.5 * kReg && zeros) est = kReg * std::log((double)kReg / zeros);
         const uint64_t want = std::min<uint64_t>(cnt, (uint64_t)(est * 1.15) + 64);
-        kd.reserve(kd.live + want);
+        // A fresh table is sized for its keys at once. A table holding keys grows when it fills
+        // (update()): how many of the batch's keys it holds already is not known here, and sizing
+        // for all of them as new rebuilt every table of compact_files' re-index, whose keys are all
+        // in the keydir (0.36 -> 0.63-0.74 s on configs[3], profiles/r06k_compaction_ab.txt).
+        if (!kd.live) kd.reserve(want);
       }
       StatsDelta sd(delta[q], &out.stats);
       for (size_t k = 0; k < ns; ++k) {
@@ -2718,7 +2723,9 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
       const Item* Lq = items + at[(size_t)q * np];
       const size_t m = at[(size_t)(q + 1) * np] - at[(size_t)q * np];  // the table's items, in block order
       const auto tr = std::chrono::steady_clock::now();
-      kd.reserve(kd.live + m);  // (room for every record's key: a block holds about one record per key)
+      // (a fresh table: room for every record's key — a block holds about one record per key; a
+      // table holding keys grows when it fills, as in parallel_fold)
+      if (!kd.live) kd.reserve(m);
       tres[t] += ms_since(tr);
       for (int phase = first_phase; phase < 2; ++phase) {
         {

@@ -180,11 +180,15 @@ def main():
     ap.add_argument("--files", type=int, default=4)
     ap.add_argument("--out", default="")
     ap.add_argument("--dir", default=None, help="parent directory of the compaction database")
+    ap.add_argument("--lib", default="", help="an A/B build of the library (cask_amd._lib.use_library)")
     args = ap.parse_args()
     if "openab" in args.what:  # (open_ab switches the open's fold with a test hook)
         os.environ["CASK_TEST_HOOKS"] = "1"
     import torch
     torch.cuda.set_device(0)
+    if args.lib:
+        import cask_amd
+        cask_amd._lib.use_library(args.lib)
     from cask_amd import ScanContext
     ctx = ScanContext(0)
     results = []

@@ -71,7 +71,11 @@ def main():
     ap.add_argument("--files", type=int, default=16)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--dir", default="/dev/shm" if os.path.isdir("/dev/shm") else None)
+    ap.add_argument("--lib", default="", help="an A/B build of the library (cask_amd._lib.use_library)")
     args = ap.parse_args()
+    if args.lib:
+        import cask_amd
+        cask_amd._lib.use_library(args.lib)
     from cask_amd import CaskOptions
     work = tempfile.mkdtemp(prefix="cask_fold_", dir=args.dir)
     try:
