@@ -21,6 +21,7 @@
 
 #include "device_util.h"
 #include "keydir_format.h"
+#include "knobs.h"
 
 namespace cask_dev {
 
@@ -50,12 +51,25 @@ struct KdArgs {
   uint64_t* eoff;     // exclusive sums
   uint64_t* koff;
   uint32_t* seg;      // segment starts
+  // per sorted position i, row is[i]'s fields (k_kd_gather): what k_kd_segs and k_kd_write read,
+  // in segment order instead of one scattered load per field per record
+  uint64_t* sseq;
+  uint32_t* svsz;
+  uint32_t* sf;       // file index
+  uint16_t* sksz;
+  u32x4* skey;        // the key's first 16 bytes, zero-filled past its end
+  // per row, in row order (k_kd_hash, written as it reads the rows): (seq lo, seq hi, vsz, file
+  // index) and the key's first 16 bytes — two 16-B loads per row for k_kd_gather instead of five
+  // scattered fields and a byte loop over the key
+  u32x4* rfld;
+  u32x4* rkey;
   uint32_t* nseg;
   uint64_t* fstat;    // per file: puts, put_bytes, stale, stale_bytes
   unsigned long long* tot;  // [0] max seq + 1, [1] records, [2] key bytes
   uint8_t* out;       // the block
   uint64_t rec_at, key_at;
   const uint64_t* key_at_row;  // per row: offset of its key in its file's bytes (null: pos + 18)
+  uint64_t hmask;     // the key hash's bits that group rows (all but under CASK_KD_HASH_BITS)
 };
 
 // key_hash: keydir_format.h (shared with the host's partition and owner lookups)
@@ -86,10 +100,48 @@ __global__ __launch_bounds__(256) void k_kd_hash(KdArgs a) {
     if (in) {
       f = row_file(a, d);
       const uint32_t k = a.ksz[d], v = a.vsz[d];
-      a.h[d] = key_hash(row_key(a, d, f), k);
+      const uint8_t* kp = row_key(a, d, f);
+      // the key's first 16 bytes from the aligned dwords that hold them (a dword read past the key
+      // stays inside the dword of its last byte), zero past its end; a key of at most 16 bytes is
+      // hashed from them (key_hash's words), a longer one by key_hash itself
+      uint32_t w[4] = {0u, 0u, 0u, 0u};
+      const uint32_t m = k < 16u ? k : 16u;
+      if (m) {
+        const uint32_t sh = (uint32_t)((uintptr_t)kp & 3), nd = (sh + m + 3) >> 2;
+        const uint32_t* q = (const uint32_t*)((uintptr_t)kp - sh);
+        uint32_t x[5];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) x[j] = j < nd ? q[j] : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t b0 = 4 * j;  // key bytes b0..b0+3
+          const uint32_t v4 = fun(x[j], x[j + 1], sh);
+          w[j] = b0 >= m ? 0u : m - b0 >= 4 ? v4 : v4 & ((1u << (8 * (m - b0))) - 1u);
+        }
+      }
+      uint64_t hk;
+      if (k <= 16) {
+        const uint64_t w0 = (uint64_t)w[0] | ((uint64_t)w[1] << 32), w1 = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+        uint64_t hh = 0x9E3779B97F4A7C15ull ^ ((uint64_t)k * 0xD6E8FEB86659FD93ull), t = w0;
+        if (k >= 8) {
+          hh = mix64(hh ^ w0);
+          t = w1;
+          if (k >= 16) {
+            hh = mix64(hh ^ w1);
+            t = 0;
+          }
+        }
+        hk = mix64(hh ^ t ^ 0xA0761D6478BD642Full);
+      } else {
+        hk = key_hash(kp, k);
+      }
+      a.h[d] = hk & a.hmask;
       a.idx[d] = (uint32_t)d;
       a.fidx[d] = f;
-      const unsigned long long s1 = (unsigned long long)a.seq[d] + 1;
+      const uint64_t sq = a.seq[d];
+      a.rfld[d] = u32x4{(uint32_t)sq, (uint32_t)(sq >> 32), v, f};
+      a.rkey[d] = u32x4{w[0], w[1], w[2], w[3]};
+      const unsigned long long s1 = (unsigned long long)sq + 1;
       mx = mx > s1 ? mx : s1;
       if (v != 0xFFFFFFFFu) {
         put = 1;
@@ -124,13 +176,32 @@ __global__ __launch_bounds__(256) void k_kd_heads(KdArgs a) {
     a.head[i] = (i == 0 || a.hs[i] != a.hs[i - 1]) ? 1 : 0;
 }
 
-__device__ __forceinline__ bool same_key(const KdArgs& a, uint64_t d0, uint32_t f0, uint64_t d1, uint32_t f1) {
-  const uint32_t k = a.ksz[d0];
-  if (a.ksz[d1] != k) return false;
-  const uint8_t* x = row_key(a, d0, f0);
-  const uint8_t* y = row_key(a, d1, f1);
-  for (uint32_t i = 0; i < k; ++i)
-    if (x[i] != y[i]) return false;
+// Every row's fields in sorted order (a thread per sorted position: independent scattered loads,
+// many in flight), the key's first 16 bytes with them: two 16-B loads of k_kd_hash's packed rows.
+__global__ __launch_bounds__(256) void k_kd_gather(KdArgs a) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < a.n; i += (uint64_t)gridDim.x * 256ull) {
+    const uint64_t d = a.is[i];
+    const u32x4 r = a.rfld[d];
+    a.sseq[i] = (uint64_t)r.x | ((uint64_t)r.y << 32);
+    a.svsz[i] = r.z;
+    a.sf[i] = r.w;
+    a.sksz[i] = a.ksz[d];
+    a.skey[i] = a.rkey[d];
+  }
+}
+
+// Sorted positions i0 and i1 hold the same key: sizes and first 16 bytes from the gathered arrays,
+// the rest of a longer key from the files.
+__device__ __forceinline__ bool same_key(const KdArgs& a, uint64_t i0, uint64_t i1) {
+  const uint32_t k = a.sksz[i0];
+  if (a.sksz[i1] != k) return false;
+  const u32x4 x = a.skey[i0], y = a.skey[i1];
+  if (x.x != y.x || x.y != y.y || x.z != y.z || x.w != y.w) return false;
+  if (k <= 16) return true;
+  const uint8_t* p = row_key(a, a.is[i0], a.sf[i0]);
+  const uint8_t* q = row_key(a, a.is[i1], a.sf[i1]);
+  for (uint32_t j = 16; j < k; ++j)
+    if (p[j] != q[j]) return false;
   return true;
 }
 
@@ -139,23 +210,20 @@ __global__ __launch_bounds__(256) void k_kd_segs(KdArgs a) {
   const uint32_t ns = *a.nseg;
   for (uint64_t j = blockIdx.x * 256ull + threadIdx.x; j < ns; j += (uint64_t)gridDim.x * 256ull) {
     const uint64_t s = a.seg[j], e = (j + 1 < ns) ? a.seg[j + 1] : a.n;
-    const uint64_t d0 = a.is[s];
-    const uint32_t f0 = a.fidx[d0];
     bool raw = false;
-    for (uint64_t i = s + 1; i < e && !raw; ++i) raw = !same_key(a, d0, f0, a.is[i], a.fidx[a.is[i]]);
+    for (uint64_t i = s + 1; i < e && !raw; ++i) raw = !same_key(a, s, i);
     if (raw) {  // a 64-bit collision between different keys: every record, folded one by one
       for (uint64_t i = s; i < e; ++i) {
-        const uint64_t d = a.is[i];
         a.kind[i] = 4;
         a.ecnt[i] = 1;
-        a.ekey[i] = a.ksz[d];
+        a.ekey[i] = a.sksz[i];
       }
       continue;
     }
     // keydir: suffix-strict maxima (sequence + 1 > every later record's)
     unsigned long long later = 0;
     for (uint64_t i = e; i-- > s;) {
-      const unsigned long long q = (unsigned long long)a.seq[a.is[i]] + 1;
+      const unsigned long long q = (unsigned long long)a.sseq[i] + 1;
       a.kind[i] = q > later ? 1 : 0;
       later = later > q ? later : q;
     }
@@ -163,17 +231,16 @@ __global__ __launch_bounds__(256) void k_kd_segs(KdArgs a) {
     // shard (sequence + 1, 0 = vacant): x > L ? max(x, A) : C
     unsigned long long L = 0, A = 0, C = 0;
     for (uint64_t i = s; i < e; ++i) {
-      const uint64_t d = a.is[i];
-      const unsigned long long q = (unsigned long long)a.seq[d] + 1;
+      const unsigned long long q = (unsigned long long)a.sseq[i] + 1;
       uint8_t kd = a.kind[i];
-      if (a.vsz[d] != 0xFFFFFFFFu) {
+      if (a.svsz[i] != 0xFFFFFFFFu) {
         A = A > q ? A : q;
         C = C > q ? C : q;
       } else {
         if (C > q) {  // stale whatever entered the shard
-          const uint32_t f = a.fidx[d];
+          const uint32_t f = a.sf[i];
           atomicAdd((unsigned long long*)&a.fstat[4ull * f + 2], 1ull);
-          atomicAdd((unsigned long long*)&a.fstat[4ull * f + 3], 18ull + a.ksz[d]);
+          atomicAdd((unsigned long long*)&a.fstat[4ull * f + 3], 18ull + a.sksz[i]);
         } else {      // stale iff x > T
           kd |= 2;
           a.tval[i] = A > q ? L : (L > q ? L : q);
@@ -187,7 +254,7 @@ __global__ __launch_bounds__(256) void k_kd_segs(KdArgs a) {
       a.kind[i] = kd;
       const uint32_t m = (kd & 1) + ((kd >> 1) & 1);
       a.ecnt[i] = m;
-      a.ekey[i] = (uint64_t)m * a.ksz[d];
+      a.ekey[i] = (uint64_t)m * a.sksz[i];
     }
   }
 }
@@ -198,22 +265,23 @@ __global__ void k_kd_totals(KdArgs a) {
   a.tot[2] = a.koff[a.n - 1] + a.ekey[a.n - 1];
 }
 
-__device__ __forceinline__ void kd_emit(const KdArgs& a, uint64_t r, uint64_t ko, uint64_t d, uint32_t f, uint8_t kind,
+__device__ __forceinline__ void kd_emit(const KdArgs& a, uint64_t r, uint64_t ko, uint64_t i, uint64_t d, uint8_t kind,
                                         uint64_t seq) {
   ShardRec* rec = (ShardRec*)(a.out + a.rec_at) + r;
+  const uint32_t f = a.sf[i];
   ShardRec x;
   x.pos = a.pos[d];
   x.seq = seq;
   x.file_id = a.file_ids[f];
-  x.vsz = a.vsz[d];
-  x.ksz = a.ksz[d];
+  x.vsz = a.svsz[i];
+  x.ksz = a.sksz[i];
   x.kind = kind;
   x.pad0 = 0;
   x.pad1 = 0;
   *rec = x;
   const uint8_t* k = row_key(a, d, f);
   uint8_t* o = a.out + a.key_at + ko;
-  for (uint32_t i = 0; i < x.ksz; ++i) o[i] = k[i];
+  for (uint32_t j = 0; j < x.ksz; ++j) o[j] = k[j];
 }
 
 __global__ __launch_bounds__(256) void k_kd_write(KdArgs a) {
@@ -221,18 +289,17 @@ __global__ __launch_bounds__(256) void k_kd_write(KdArgs a) {
     const uint8_t kd = a.kind[i];
     if (!kd) continue;
     const uint64_t d = a.is[i];
-    const uint32_t f = a.fidx[d];
     uint64_t r = a.eoff[i], ko = a.koff[i];
     if (kd & 4) {
-      kd_emit(a, r, ko, d, f, kRaw, a.seq[d]);
+      kd_emit(a, r, ko, i, d, kRaw, a.sseq[i]);
       continue;
     }
     if (kd & 2) {  // the threshold first: rank 0 resolves it before it folds the shard's rows
-      kd_emit(a, r, ko, d, f, kCond, a.tval[i]);
+      kd_emit(a, r, ko, i, d, kCond, a.tval[i]);
       ++r;
-      ko += a.ksz[d];
+      ko += a.sksz[i];
     }
-    if (kd & 1) kd_emit(a, r, ko, d, f, kKept, a.seq[d]);
+    if (kd & 1) kd_emit(a, r, ko, i, d, kKept, a.sseq[i]);
   }
 }
 
@@ -341,6 +408,8 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
                  o_idx = take(4 * n1), o_fidx = take(4 * n1), o_hs = take(8 * n1), o_is = take(4 * n1),
                  o_head = take(n1), o_kind = take(n1), o_tval = take(8 * n1), o_ecnt = take(8 * n1),
                  o_ekey = take(8 * n1), o_eoff = take(8 * n1), o_koff = take(8 * n1), o_seg = take(4 * n1),
+                 o_sf = take(4 * n1), o_sksz = take(2 * n1), o_skey = take(16 * n1), o_rfld = take(16 * n1),
+                 o_rkey = take(16 * n1),
                  o_nseg = take(8), o_fstat = take(32ull * (nfiles + 1)), o_tot = take(64), o_tmp = take(tmp);
   if (!S_.ensure(o)) return -13;
   uint8_t* b = (uint8_t*)S_.p;
@@ -355,6 +424,13 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   a.ksz = ksz;
   a.n = n;
   a.key_at_row = key_at;
+  // CASK_KD_HASH_BITS=b (test hook): rows grouped by b bits of their key hash, so that different
+  // keys share segments and take the collision path (kRaw) — the fold of the block is the same
+  {
+    const char* hb = cask_knobs::hook("CASK_KD_HASH_BITS");
+    const int bits = hb ? atoi(hb) : 64;
+    a.hmask = bits >= 64 ? ~0ull : bits <= 0 ? 0ull : (1ull << bits) - 1;
+  }
   a.h = (uint64_t*)(b + o_h);
   a.idx = (uint32_t*)(b + o_idx);
   a.fidx = (uint32_t*)(b + o_fidx);
@@ -368,6 +444,13 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   a.eoff = (uint64_t*)(b + o_eoff);
   a.koff = (uint64_t*)(b + o_koff);
   a.seg = (uint32_t*)(b + o_seg);
+  a.sseq = (uint64_t*)(b + o_h);    // (the sort's inputs are dead once it has run)
+  a.svsz = (uint32_t*)(b + o_idx);
+  a.sf = (uint32_t*)(b + o_sf);
+  a.sksz = (uint16_t*)(b + o_sksz);
+  a.skey = (u32x4*)(b + o_skey);
+  a.rfld = (u32x4*)(b + o_rfld);
+  a.rkey = (u32x4*)(b + o_rkey);
   a.nseg = (uint32_t*)(b + o_nseg);
   a.fstat = (uint64_t*)(b + o_fstat);
   a.tot = (unsigned long long*)(b + o_tot);
@@ -389,6 +472,7 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
     tb = tmp;
     H(hipcub::DeviceSelect::Flagged(tmpp, tb, hipcub::CountingInputIterator<uint32_t>(0), a.head, a.seg, a.nseg,
                                      (int)n, st));
+    hipLaunchKernelGGL(k_kd_gather, dim3(grid), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_kd_segs, dim3(grid), dim3(256), 0, st, a);
     tb = tmp;
     H(hipcub::DeviceScan::ExclusiveSum(tmpp, tb, a.ecnt, a.eoff, (int)n, st));

@@ -1,7 +1,7 @@
 // Environment knobs, of two kinds; a plain run of the product library reads neither:
 //  * test hooks force the paths the tests cover — CASK_SCAN_MODE (walk|chunk|wide|narrow),
 //    CASK_HOST_THREADS, CASK_OPEN_BATCH, CASK_OPEN_DEVFOLD, CASK_OPEN_TRACE, CASK_PAR_FOLD_MIN, CASK_STAGE_MIN, CASK_LOCAL_REPAIRS,
-//    CASK_NO_REPAIR — and are read only when CASK_TEST_HOOKS=1 is in the environment when the library
+//    CASK_NO_REPAIR, CASK_KD_HASH_BITS — and are read only when CASK_TEST_HOOKS=1 is in the environment when the library
 //    is first used (tests/conftest.py sets it; bench.py refuses to run with it);
 //  * tuning knobs (the A/B studies recorded in DESIGN.md: run lengths, grid sizes, hash depth, ...)
 //    exist only in diagnostic builds compiled with -DCASK_TUNING (`make -C cask_amd variant

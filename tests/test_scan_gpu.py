@@ -209,6 +209,49 @@ def test_sharded_fold_matches_single_thread(native, tmp_path, monkeypatch, batch
     assert len(got[0][0]) > 100
 
 
+def test_devfold_forced_hash_collisions(native, tmp_path, monkeypatch):
+    """The device-reduced keydir where different keys share a key-hash segment (CASK_KD_HASH_BITS
+    groups rows by 4 bits of the hash, then by none): k_kd_segs must tell the keys apart — short
+    keys by their gathered 16 bytes, longer ones sharing those 16 bytes by the rest from the files —
+    and send such segments whole (kRaw); the merged keydir, stats and sequence equal the host
+    fold's, as with the full hash."""
+    from cask_amd import CaskOptions
+    rng = random.Random(71)
+    prefixes = [rng.randbytes(16) for _ in range(4)]
+    keys = [rng.randbytes(rng.randrange(0, 17)) for _ in range(150)]
+    keys += [rng.choice(prefixes) + rng.randbytes(rng.randrange(1, 30)) for _ in range(150)]
+    keys += [p[:rng.randrange(0, 17)] for p in prefixes]
+    d = tmp_path / "db"
+    d.mkdir()
+    seq = 1
+    for fid in range(1, 4):
+        recs = []
+        for _ in range(3000):
+            k = rng.choice(keys)
+            s = seq if rng.random() < 0.9 else max(1, seq - rng.randrange(1, 2000))
+            seq += 1
+            if rng.random() < 0.15:
+                recs.append(R.entry_deleted(s, k).write_bytes())
+            else:
+                recs.append(R.entry_new(s, k, rng.randbytes(rng.randrange(0, 200))).write_bytes())
+        with open(R.data_file_path(str(d), fid), "wb") as f:
+            f.write(b"".join(recs))
+    got = []
+    for devfold, bits in (("0", None), ("1", None), ("1", "4"), ("1", "0")):
+        for h in d.glob("*.cask.hint"):
+            h.unlink()
+        monkeypatch.setenv("CASK_OPEN_DEVFOLD", devfold)
+        if bits is None:
+            monkeypatch.delenv("CASK_KD_HASH_BITS", raising=False)
+        else:
+            monkeypatch.setenv("CASK_KD_HASH_BITS", bits)
+        with CaskOptions().open(str(d)) as db:
+            got.append((sorted([k.hex(), e.file_id, e.entry_pos, e.entry_size, e.sequence] for k, e in db.index().items()),
+                        sorted([f, *st] for f, st in db.stats().items()), db.current_sequence))
+    assert got[0] == got[1] == got[2] == got[3]
+    assert len(got[0][0]) > 200
+
+
 def test_uniform_290(gpu_ctx):
     rng = random.Random(1)
     buf = make_records(rng, 20000, lambda r: 16, lambda r: 256)
