@@ -279,8 +279,16 @@ __device__ __forceinline__ void kd_emit(const KdArgs& a, uint64_t r, uint64_t ko
   x.pad0 = 0;
   x.pad1 = 0;
   *rec = x;
-  const uint8_t* k = row_key(a, d, f);
   uint8_t* o = a.out + a.key_at + ko;
+  if (x.ksz <= 16) {  // (the key's bytes are in its gathered prefix: no load from the files)
+    const u32x4 w = a.skey[i];
+    const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (uint32_t j = 0; j < 16; ++j)  // (unrolled: ww stays in registers)
+      if (j < x.ksz) o[j] = (uint8_t)(ww[j >> 2] >> (8 * (j & 3)));
+    return;
+  }
+  const uint8_t* k = row_key(a, d, f);
   for (uint32_t j = 0; j < x.ksz; ++j) o[j] = k[j];
 }
 
