@@ -66,16 +66,17 @@ def cfg3(ctx, torch, steps, total_gib, max_file):
             "counters": counters, "parity": "rows == generator (count, pos, seq, ksz, vsz, status)"}
 
 
-def write_cfg3(ctx, torch, nfiles, path):
+def write_cfg3(ctx, torch, nfiles, path, live=0.2):
     """configs[3]-shaped data files 1..nfiles in `path`: 290-B records, a key space of a fifth of
-    the records, 10 % of keys ending in a tombstone. Returns (bytes, live keys, records, seconds)."""
+    the records (`live`: another fraction), 10 % of keys ending in a tombstone. Returns (bytes,
+    live keys, records, seconds)."""
     from cask_amd.workloads import CFG2_RECORDS_PER_FILE, variable_file
     dev = torch.device("cuda", ctx.device)
     rpf = CFG2_RECORDS_PER_FILE
     n = nfiles * rpf
     g = torch.Generator(device=dev)
     g.manual_seed(0xC0FFEE)
-    nkeys = n // 5
+    nkeys = max(1, int(n * live))
     kid = torch.randint(0, nkeys, (n,), generator=g, device=dev, dtype=torch.int64)
     last = torch.full((nkeys,), -1, dtype=torch.int64, device=dev)
     last.scatter_reduce_(0, kid, torch.arange(n, device=dev), reduce="amax")
@@ -104,16 +105,16 @@ def write_cfg3(ctx, torch, nfiles, path):
     return nbytes, live_want, n, write_s
 
 
-def compact(ctx, torch, nfiles, workdir):
+def compact(ctx, torch, nfiles, workdir, live=0.2):
     from cask_amd import CaskOptions
     from cask_amd.workloads import CFG2_RECORDS_PER_FILE
     rpf = CFG2_RECORDS_PER_FILE
     path = os.path.join(workdir, "db")
     os.makedirs(path)
-    nbytes, live_want, n, write_s = write_cfg3(ctx, torch, nfiles, path)
+    nbytes, live_want, n, write_s = write_cfg3(ctx, torch, nfiles, path, live)
     out = {"config": f"configs[3] shape scaled to {nfiles} files x {rpf} records (290 B, 80 % overwritten/"
                      f"deleted, 10 % of keys end in a tombstone), on disk, 1 GPU",
-           "files": nfiles, "records": n, "bytes": nbytes, "write_files_s": write_s}
+           "files": nfiles, "records": n, "bytes": nbytes, "write_files_s": write_s, "key_space_fraction": live}
     t0 = time.perf_counter()
     print(f"files written in {write_s:.1f} s; opening", file=sys.stderr, flush=True)
     with CaskOptions().max_file_size(1 << 30).open(path) as db:
@@ -181,6 +182,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--dir", default=None, help="parent directory of the compaction database")
     ap.add_argument("--lib", default="", help="an A/B build of the library (cask_amd._lib.use_library)")
+    ap.add_argument("--live", type=float, default=0.2, help="compact: key space as a fraction of the records")
     args = ap.parse_args()
     if "openab" in args.what:  # (open_ab switches the open's fold with a test hook)
         os.environ["CASK_TEST_HOOKS"] = "1"
@@ -198,7 +200,7 @@ def main():
         else:
             wd = tempfile.mkdtemp(prefix="cask_compact_", dir=args.dir)
             try:
-                r = (compact if w == "compact" else open_ab)(ctx, torch, args.files, wd)
+                r = compact(ctx, torch, args.files, wd, args.live) if w == "compact" else open_ab(ctx, torch, args.files, wd)
             finally:
                 shutil.rmtree(wd, ignore_errors=True)
         r["what"] = w
