@@ -38,12 +38,6 @@
 #include "../../include/cask_scan.h"
 #include "host_ring.h"
 #include "keydir_format.h"
-
-namespace cask_internal {  // scan_runtime.cpp
-int read_gather_device(cask_ctx* c, const uint8_t* const* srcs, const uint64_t* src_len, uint32_t nsrc,
-                       const uint32_t* src, const uint64_t* pos, uint64_t n, uint64_t* len, uint8_t* status,
-                       uint32_t* expected, uint32_t* found, uint64_t* off, uint8_t* out, uint64_t out_cap, uint64_t* total);
-}
 #include "xxh32.h"
 #include "knobs.h"
 
@@ -715,7 +709,7 @@ struct EngineDev {
       cap = b + b / 8 + 4096;
       return true;
     }
-  } data, rows, hint, gath;  // (gath: compaction's live records gathered in write order)
+  } data, rows, hint;
   // pinned staging: reads of data files to the device, copies of results back to the host
   cask_host::PinnedRing ring;
   // open(): hint bodies back to the host while `ring` reads files in. Hint bodies are ~1/8 of the data
@@ -733,7 +727,7 @@ struct EngineDev {
   void trim() {
     constexpr size_t kKeep = 4ull << 30;
     (void)hipSetDevice(device);
-    for (Buf* b : {&data, &rows, &hint, &gath})
+    for (Buf* b : {&data, &rows, &hint})
       if (b->cap > kKeep) {
         (void)hipFree(b->p);
         b->p = nullptr;
@@ -905,16 +899,6 @@ struct EngineDev {
     return CASK_E_DEVICE;
   }
 
-  // ring_out made on first use (false: it could not be; copies then take cask_copy)
-  bool out_ring() {
-    if (!ring_out_tried) {
-      ring_out_tried = true;
-      ring_out_ok = ring_out.init(device, kOutThreads);
-      if (!ring_out_ok) ring_out.release();
-    }
-    return ring_out_ok;
-  }
-
   // The hint bodies of the scanned files v (rows of the last scan) into hbuf, file k's at
   // [fo[k], fo[k + 1]); copied back through ring_out (open() reads the next files through `ring`).
   int hints(const std::vector<cask_file_view>& v, const std::vector<uint64_t>& row_off, RawBytes& hbuf,
@@ -927,7 +911,12 @@ struct EngineDev {
     if (st != CASK_OK) return st;
     if (!hbuf.resize(fo[v.size()])) return CASK_E_NOMEM;
     if (hbuf.empty()) return CASK_OK;
-    if (staged(hbuf.size()) && !out_ring()) return cask_copy(ctx, hbuf.data(), hint.p, hbuf.size());
+    if (staged(hbuf.size()) && !ring_out_tried) {
+      ring_out_tried = true;
+      ring_out_ok = ring_out.init(device, kOutThreads);
+      if (!ring_out_ok) ring_out.release();
+    }
+    if (staged(hbuf.size()) && !ring_out_ok) return cask_copy(ctx, hbuf.data(), hint.p, hbuf.size());
     return to_host(hbuf.data(), hint.p, hbuf.size(), &ring_out) != CASK_OK ? CASK_E_DEVICE : CASK_OK;
   }
 };
@@ -2028,7 +2017,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   // forward: one run per file per batch) get their hints appended on a thread each, and their bytes
   // written with pwrite in pieces of at most 64 MiB at their offsets in the file, all on threads.
   struct WBatch {
-    std::vector<HostBuf> regions;       // the batch's live records' bytes, in write order (one region)
+    std::vector<HostBuf> regions;       // per source file of the batch: its live records' bytes, in order
     std::vector<const uint8_t*> at;     // per record: its bytes (in a region)
     std::vector<uint64_t> len, foff;    // per record: length, offset in its output file
     std::vector<OutFile*> op;           // per record: its output file
@@ -2186,16 +2175,16 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
     struct stat stt;
     slen[i] = stat(data_path(path, srcs[i]).c_str(), &stt) == 0 ? (uint64_t)stt.st_size : 0;
   }
-  // Per batch of source files (at most ~kBatch bytes of them): the files that hold live records
-  // read whole to the device (the engine's reader threads and pinned ring, as open() reads), every
-  // live record read there at its hint position (cask_internal::read_gather_device: the header's
-  // length from the data file, XXH32 against the stored checksum — Log::read_entry + Entry::from_read,
-  // log.rs:150-166, data.rs:161-206 — a record cut short by the file's end is its UnexpectedEof) and
-  // the Ok records' bytes gathered on the device in write order, then brought back in one piece.
-  // The first failure in write order — a file that could not be opened or read (Io), an EOF or a
-  // checksum — is the reference's error. Then placement, and the batch to the writer thread.
-  // (Round 6; before, each file was mapped and its live records copied out on host threads: page
-  // faults over every source page bound that copy.)
+  // Per batch of source files (at most ~kBatch bytes of them): pass 1 on host threads, a source
+  // file each — the file mapped, each live record's header read at its hint position and its bytes
+  // copied, in write order, into the file's region of the batch (Log::read_entry's reads,
+  // log.rs:150-166; only the live records' lines are touched, not the dead 80 % of configs[3]); a
+  // record cut short by the file's end is its UnexpectedEof and ends that file's pass. Then the
+  // regions' bytes go to the device through the pinned ring and the device verifies every copied
+  // record (cask_read_entries_device: the header's length again, XXH32 against the stored
+  // checksum, Entry::from_read, data.rs:161-206). The first failure in write order — an EOF from
+  // pass 1 or a checksum from the device — is the reference's error. The batch's bytes are already
+  // in write order on the host: placement, and the batch to the writer thread.
   if (!ins.empty()) {
     EngineDev* ed = engine_dev(db->opts.device);
     if (!ed) return abort_w(CASK_E_DEVICE);
@@ -2223,62 +2212,116 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       fk[nf] = k1;
       const uint64_t n = k1 - k0;
       std::unique_ptr<WBatch> WB(new WBatch());
-      WB->regions.resize(1);
+      WB->regions.resize(nf);
       WB->at.assign(n, nullptr);
       WB->len.assign(n, 0);
-      // the files with live records, whole, to the device
-      auto ts = std::chrono::steady_clock::now();
-      std::vector<std::string> paths(nf);
-      std::vector<cask_file_view> views(nf);
-      std::vector<uint64_t> doff(nf + 1, 0);
-      for (size_t f = 0; f < nf; ++f) {
-        paths[f] = data_path(path, srcs[b0 + f]);
-        views[f].file_id = srcs[b0 + f];
-        views[f].len = fk[f] == fk[f + 1] ? 0 : slen[b0 + f];  // (a file with no live record is not read)
-        doff[f + 1] = doff[f] + ((views[f].len + 255) & ~255ull);
-      }
-      EngineDev::Buf& gb = ed->gath;
-      if (!ed->data.ensure(doff[nf] + 256) || !gb.ensure(doff[nf] + 256)) return abort_w(CASK_E_NOMEM);
-      for (size_t f = 0; f < nf; ++f) views[f].data = ed->data.p + doff[f];
+      std::vector<uint64_t> used(nf, 0);      // bytes copied into each region
+      std::vector<uint64_t> eof(nf, UINT64_MAX);  // per file: its first record cut short (batch index)
       std::vector<char> io_ok(nf, 1);
-      st = ed->read_to_device(paths, views, io_ok);
-      if (st != CASK_OK) return abort_w(st);
+      auto ts = std::chrono::steady_clock::now();
+      const unsigned ntf = std::max(1u, std::min<unsigned>(host_threads(), (unsigned)nf));
+      parallel_for(ntf, [&](unsigned t) {
+        for (size_t f = t; f < nf; f += ntf) {
+          if (fk[f] == fk[f + 1]) continue;
+          const int fdsc = open(data_path(path, srcs[b0 + f]).c_str(), O_RDONLY);  // File::open: Io
+          struct stat stt;
+          if (fdsc < 0 || fstat(fdsc, &stt) != 0) {
+            if (fdsc >= 0) close(fdsc);
+            io_ok[f] = 0;
+            continue;
+          }
+          const uint64_t flen = (uint64_t)stt.st_size;
+          const uint8_t* m = nullptr;
+          if (flen) {
+            void* q = mmap(nullptr, flen, PROT_READ, MAP_PRIVATE, fdsc, 0);
+            if (q == MAP_FAILED) {
+              close(fdsc);
+              io_ok[f] = 0;
+              continue;
+            }
+            m = (const uint8_t*)q;
+          }
+          close(fdsc);
+          HostBuf& rg = WB->regions[f];
+          if (!rg.alloc(std::max<uint64_t>(flen, 1))) {
+            if (m) munmap((void*)m, flen);
+            throw std::bad_alloc();
+          }
+          uint64_t o = 0;
+          for (size_t k = fk[f]; k < fk[f + 1]; ++k) {
+            const uint64_t pos = ins[k].pos;
+            if (pos > flen || flen - pos < 18) {  // header cut short (data.rs:163)
+              eof[f] = k - k0;
+              break;
+            }
+            const uint8_t* h = m + pos;
+            const uint32_t vsz = rd32(h + 14);
+            const uint64_t rl = 18ull + rd16(h + 12) + (vsz == CASK_ENTRY_TOMBSTONE ? 0ull : (uint64_t)vsz);
+            if (flen - pos < rl) {  // key or value cut short (data.rs:172,181)
+              eof[f] = k - k0;
+              break;
+            }
+            memcpy(rg.get() + o, h, rl);
+            WB->at[k - k0] = rg.get() + o;
+            WB->len[k - k0] = rl;
+            o += rl;
+          }
+          used[f] = o;
+          if (m) munmap((void*)m, flen);
+        }
+      });
       tr_read += ms_since(ts);
-      // read, verified and gathered on the device
-      ts = std::chrono::steady_clock::now();
-      std::vector<const uint8_t*> dsrc(nf);
-      std::vector<uint64_t> dlen(nf);
+      // the first file that could not be opened ends the batch there (its records come first in
+      // write order after the earlier files')
+      size_t nv = n;  // records verified: those before the batch's first failure from pass 1
       for (size_t f = 0; f < nf; ++f) {
-        dsrc[f] = views[f].data;
-        dlen[f] = views[f].len;
+        if (!io_ok[f] && fk[f] != fk[f + 1]) {
+          nv = std::min<size_t>(nv, fk[f] - k0);
+          break;
+        }
+        if (eof[f] != UINT64_MAX) {
+          nv = std::min<size_t>(nv, eof[f]);
+          break;
+        }
       }
-      std::vector<uint64_t> pos(n), len(n), off(n);
-      std::vector<uint32_t> src(n), ex(n), fd(n);
-      std::vector<uint8_t> stv(n);
-      for (uint64_t k = 0; k < n; ++k) {
-        pos[k] = ins[k0 + k].pos;
-        src[k] = (uint32_t)(ins[k0 + k].src - b0);
-      }
+      // the copied bytes to the device, contiguous; the device verifies records [0, nv)
       uint64_t total = 0;
-      st = cask_internal::read_gather_device(ed->ctx, dsrc.data(), dlen.data(), (uint32_t)nf, src.data(), pos.data(), n,
-                                             len.data(), stv.data(), ex.data(), fd.data(), off.data(), gb.p,
-                                             gb.cap, &total);
-      if (st != CASK_OK) return abort_w(st);
-      for (uint64_t k = 0; k < n; ++k) {  // in write order: the first failure is the reference's
-        const uint32_t fid = srcs[ins[k0 + k].src];
-        if (!io_ok[src[k]]) return abort_w(CASK_E_IO, fid);  // File::open / read: Io
-        if (stv[k] != CASK_ROW_OK)
-          return stv[k] == CASK_ROW_CHECKSUM ? abort_w(CASK_E_CHECKSUM, fid, ins[k0 + k].pos, ex[k], fd[k])
-                                             : abort_w(CASK_E_EOF, fid, ins[k0 + k].pos);
+      std::vector<uint64_t> doff(nf, 0);
+      for (size_t f = 0; f < nf; ++f) {
+        doff[f] = total;
+        total += used[f];
       }
-      HostBuf& rg = WB->regions[0];
-      if (!rg.alloc(std::max<uint64_t>(total, 1))) return abort_w(CASK_E_NOMEM);
-      if (total && ed->to_host(rg.get(), gb.p, total) != CASK_OK) return abort_w(CASK_E_DEVICE);
-      for (uint64_t k = 0; k < n; ++k) {
-        WB->at[k] = rg.get() + off[k];
-        WB->len[k] = len[k];
+      std::vector<uint64_t> pos(nv), len(nv);
+      std::vector<uint32_t> src(nv, 0u), ex(nv), fd(nv);
+      std::vector<uint8_t> stv(nv);
+      if (nv) {
+        if (!ed->data.ensure(total + 256)) return abort_w(CASK_E_NOMEM);
+        ts = std::chrono::steady_clock::now();
+        std::vector<cask_host::PinnedRing::Piece> ps;
+        for (size_t f = 0; f < nf; ++f)
+          if (used[f]) cask_host::PinnedRing::split(WB->regions[f].get(), ed->data.p + doff[f], used[f], ps);
+        if (!ed->ring.h2d(ps)) return abort_w(CASK_E_DEVICE);
+        tr_h2d += ms_since(ts);
+        size_t f = 0;
+        for (uint64_t k = 0; k < nv; ++k) {
+          while (k0 + k >= fk[f + 1]) ++f;
+          pos[k] = doff[f] + (uint64_t)(WB->at[k] - WB->regions[f].get());
+        }
+        const uint8_t* dsrc = ed->data.p;
+        st = cask_read_entries_device(ed->ctx, &dsrc, &total, 1, src.data(), pos.data(), nv, len.data(), stv.data(),
+                                      ex.data(), fd.data());
+        if (st != CASK_OK) return abort_w(st);
       }
-      tr_h2d += ms_since(ts);
+      for (uint64_t k = 0; k < nv; ++k)  // in write order: the first failure is the reference's
+        if (stv[k] != CASK_ROW_OK || len[k] != WB->len[k])
+          return stv[k] == CASK_ROW_CHECKSUM ? abort_w(CASK_E_CHECKSUM, srcs[ins[k0 + k].src], ins[k0 + k].pos, ex[k], fd[k])
+                                             : abort_w(CASK_E_EOF, srcs[ins[k0 + k].src], ins[k0 + k].pos);
+      if (nv < n) {  // pass 1's failure: File::open / read (Io) or a record cut short (UnexpectedEof)
+        const uint32_t fid = srcs[ins[k0 + nv].src];
+        const size_t f = ins[k0 + nv].src - b0;
+        if (!io_ok[f]) return abort_w(CASK_E_IO, fid);
+        return abort_w(CASK_E_EOF, fid, ins[k0 + nv].pos);
+      }
       t_verify += ms_since(tv);
       // placement (LogWriter::write's rollover, log.rs:282-306), in write order
       auto tg = std::chrono::steady_clock::now();
@@ -2306,7 +2349,6 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
       k0 = k1;
       b0 = b1;
     }
-    ed->trim();  // (the batch-sized device buffers go back, as after a large open)
   }
   // the last batch's writes (R.ms[3] counts what this thread waited for the writer, not the writer's
   // time beside the device work)
@@ -2318,7 +2360,7 @@ static int compact_files_impl(cask_db* db, const uint32_t* files_in, uint64_t nf
   R.ms[1] = t_verify;
   R.ms[2] = t_gather;
   if (tracing)
-    fprintf(stderr, "compact batches: sources read to the device %.1f ms, live records verified + gathered + to the host %.1f ms (of verify), writer busy %.1f ms\n",
+    fprintf(stderr, "compact batches: live records copied from the mapped sources %.1f ms, to the device %.1f ms (of verify), writer busy %.1f ms\n",
             tr_read, tr_h2d, writer.ms);
   // the tombstone tail: Entry::deleted(sequence, key).write_bytes (data.rs:90-121), in first-seen
   // order. The placement (the rollover) runs in order; the records, their checksums and their hints

@@ -813,33 +813,6 @@ void launch_read_entries(const uint64_t* pos, const uint32_t* src, uint64_t n, c
   hipLaunchKernelGGL(k_read_entries, dim3((uint32_t)g), dim3(256), 0, S(stream), pos, src, n, srcs, slen, len, st, expct, found);
 }
 
-// Compaction's live records gathered into write order: record r's len[r] bytes from its source
-// file at pos[r] to out + off[r] (a wave per record, 4 bytes per lane per step; len 0: skipped).
-__global__ __launch_bounds__(256) void k_gather_entries(const uint64_t* __restrict__ pos, const uint32_t* __restrict__ src,
-                                                        const uint64_t* __restrict__ len, const uint64_t* __restrict__ off,
-                                                        uint64_t n, const uint8_t* const* __restrict__ srcs, uint8_t* out) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x >> 6);
-  for (uint64_t r = blockIdx.x * (uint64_t)(blockDim.x >> 6) + (threadIdx.x >> 6); r < n; r += nw) {
-    const uint64_t L = len[r];
-    const uint8_t* s = srcs[src[r]] + pos[r];
-    uint8_t* d = out + off[r];
-    for (uint64_t b = 4ull * lane; b < L; b += 256) {
-#pragma unroll
-      for (uint32_t j = 0; j < 4; ++j)
-        if (b + j < L) d[b + j] = s[b + j];
-    }
-  }
-}
-
-void launch_gather_entries(const uint64_t* pos, const uint32_t* src, const uint64_t* len, const uint64_t* off, uint64_t n,
-                           const uint8_t* const* srcs, uint8_t* out, void* stream) {
-  if (!n) return;
-  uint64_t g = (n + 3) / 4;
-  if (g > 65536) g = 65536;
-  hipLaunchKernelGGL(k_gather_entries, dim3((uint32_t)g), dim3(256), 0, S(stream), pos, src, len, off, n, srcs, out);
-}
-
 void launch_compact(const ScanArgs& a, const uint64_t* summary, void* stream) {
   if (!a.total_chunks) return;
   // one wave per chunk where possible: each chunk's rows wait on a chain of dependent table loads

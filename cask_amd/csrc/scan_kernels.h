@@ -235,8 +235,6 @@ struct SummaryHead {
 // Host-callable launchers (defined in scan_kernels.hip).
 void launch_read_entries(const uint64_t* pos, const uint32_t* src, uint64_t n, const uint8_t* const* srcs,
                          const uint64_t* slen, uint64_t* len, uint8_t* st, uint32_t* expct, uint32_t* found, void* stream);
-void launch_gather_entries(const uint64_t* pos, const uint32_t* src, const uint64_t* len, const uint64_t* off, uint64_t n,
-                           const uint8_t* const* srcs, uint8_t* out, void* stream);
 uint32_t geometry_chunk(int geo);
 uint32_t geometry_halo(int geo);
 void launch_scan_chunks(const ScanArgs& a, int geo, void* stream);

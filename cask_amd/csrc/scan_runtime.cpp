@@ -1384,69 +1384,6 @@ extern "C" int cask_read_entries_device(cask_ctx* c, const uint8_t* const* srcs,
   });
 }
 
-// compact_files' Log::read_entry batch with the bytes kept (engine.cpp): records verified as
-// cask_read_entries_device does, then every Ok record's bytes gathered, in order, to out (device,
-// out_cap bytes) at off[r] (the prefix of the Ok lengths; a failed record has len 0 and takes no
-// bytes); *total: the bytes gathered.
-namespace cask_internal {
-int read_gather_device(cask_ctx* c, const uint8_t* const* srcs, const uint64_t* src_len, uint32_t nsrc,
-                       const uint32_t* src, const uint64_t* pos, uint64_t n, uint64_t* len, uint8_t* status,
-                       uint32_t* expected, uint32_t* found, uint64_t* off, uint8_t* out, uint64_t out_cap, uint64_t* total) {
-  return cask_abi::guard([&]() -> int {
-    *total = 0;
-    if (!c || (n && (!srcs || !src_len || !src || !pos || !len || !status || !expected || !found || !off || !out)))
-      return CASK_E_INVALID_ARG;
-    for (uint64_t r = 0; r < n; ++r)
-      if (src[r] >= nsrc) return CASK_E_INVALID_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
-    if (set_dev(c)) return CASK_E_DEVICE;
-    if (!n) return CASK_OK;
-    const size_t a8 = align_up(8 * n, 256), a4 = align_up(4 * n, 256), a1 = align_up(n, 256), as = align_up(8ull * nsrc, 256);
-    if (!c->gather.ensure(5 * a8 + 3 * a4 + a1 + 2 * as)) return CASK_E_NOMEM;
-    uint8_t* b = c->gather.as<uint8_t>();
-    uint64_t* d_pos = (uint64_t*)b;
-    uint64_t* d_len = (uint64_t*)(b + a8);
-    uint64_t* d_off = (uint64_t*)(b + 2 * a8);
-    uint32_t* d_src = (uint32_t*)(b + 3 * a8);
-    uint32_t* d_exp = (uint32_t*)(b + 3 * a8 + a4);
-    uint32_t* d_fnd = (uint32_t*)(b + 3 * a8 + 2 * a4);
-    uint8_t* d_st = b + 3 * a8 + 3 * a4;
-    const uint8_t** d_srcs = (const uint8_t**)(b + 3 * a8 + 3 * a4 + a1);
-    uint64_t* d_slen = (uint64_t*)(b + 3 * a8 + 3 * a4 + a1 + as);
-    hipStream_t st = c->stream;
-    bool ok = true;
-    auto H = [&](hipError_t e) { ok = ok && e == hipSuccess; };
-    H(hipMemcpyAsync(d_pos, pos, 8 * n, hipMemcpyHostToDevice, st));
-    H(hipMemcpyAsync(d_src, src, 4 * n, hipMemcpyHostToDevice, st));
-    H(hipMemcpyAsync(d_srcs, srcs, 8ull * nsrc, hipMemcpyHostToDevice, st));
-    H(hipMemcpyAsync(d_slen, src_len, 8ull * nsrc, hipMemcpyHostToDevice, st));
-    launch_read_entries(d_pos, d_src, n, d_srcs, d_slen, d_len, d_st, d_exp, d_fnd, st);
-    H(hipGetLastError());
-    H(hipMemcpyAsync(len, d_len, 8 * n, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(status, d_st, n, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(expected, d_exp, 4 * n, hipMemcpyDeviceToHost, st));
-    H(hipMemcpyAsync(found, d_fnd, 4 * n, hipMemcpyDeviceToHost, st));
-    H(hipStreamSynchronize(st));
-    if (!ok) return CASK_E_DEVICE;
-    uint64_t t = 0;
-    for (uint64_t r = 0; r < n; ++r) {
-      off[r] = t;
-      t += status[r] == CASK_ROW_OK ? len[r] : 0;
-    }
-    if (t > out_cap) return CASK_E_CAPACITY;
-    *total = t;
-    for (uint64_t r = 0; r < n; ++r)
-      if (status[r] != CASK_ROW_OK) len[r] = 0;
-    H(hipMemcpyAsync(d_off, off, 8 * n, hipMemcpyHostToDevice, st));
-    H(hipMemcpyAsync(d_len, len, 8 * n, hipMemcpyHostToDevice, st));
-    launch_gather_entries(d_pos, d_src, d_len, d_off, n, d_srcs, out, st);
-    H(hipGetLastError());
-    H(hipStreamSynchronize(st));
-    return ok ? CASK_OK : CASK_E_DEVICE;
-  });
-}
-}  // namespace cask_internal
-
 #ifdef CASK_STAMPS
 // Diagnostic build only: per-phase cycle sums of the last k_scan_chunks launch.
 extern "C" int cask_debug_stamps(cask_ctx* c, uint64_t* out16) {
