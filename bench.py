@@ -566,6 +566,9 @@ def main():
                 "traffic": traffic,
                 "traffic_source": traffic_src,
                 "kernel_ms_avg": k_avg,
+                "timer": ("mean over the K timed steps of HIP events recorded around the kernel on the "
+                          "scan's stream (cask_last_timings8); rocprofv3's figures for the same kernel "
+                          "are under profiles/ (kernel_stats.csv: mean and median per launch)"),
                 "algorithmic_bytes_per_launch": bytes_per_step,
                 "stream_ceiling": ceiling,
                 "frac_of_stream_ceiling": (achieved / ceiling["gbps"]) if ceiling and "gbps" in ceiling else None,
