@@ -184,3 +184,34 @@ def test_partition_rejects_bad_blocks(native):
     h = native.cask_keydir_new()
     assert native.cask_keydir_finish_terms(h, None, 3) == -10  # not a whole number of terms
     native.cask_db_close(h)
+
+
+@pytest.mark.parametrize("threads", [1, 8])
+def test_native_fold_grows_tables(native, threads, monkeypatch):
+    """Enough keys that every keydir table grows several times — from the first block's sizing, then
+    on demand in the later blocks (tables that hold keys grow only when they fill) — with deletions
+    and resurrections leaving deleted slots behind (rebuilds at the same size) and keys longer than
+    the 16 inline bytes (the arena): the native merge equals the in-order fold."""
+    monkeypatch.setenv("CASK_PAR_FOLD_MIN", "0" if threads > 1 else str(1 << 62))
+    monkeypatch.setenv("CASK_HOST_THREADS", str(threads))
+    rng = random.Random(4242)
+    keys = [rng.randbytes(rng.randrange(0, 31)) for _ in range(60000)]
+    files, seq = [], 1
+    for f in range(5):
+        rows, pos = [], 0
+        lo = 12000 * f  # each file mostly new keys, some of every earlier file's
+        for _ in range(30000):
+            k = keys[rng.randrange(lo, lo + 12000)] if rng.random() < 0.7 else keys[rng.randrange(0, lo + 12000)]
+            s = seq if rng.random() > 0.1 else max(0, seq - rng.randrange(1, 5000))
+            seq += 1
+            vsz = R.ENTRY_TOMBSTONE if rng.random() < 0.3 else rng.randrange(0, 50)
+            r = R.Row(pos=pos, seq=s, ksz=len(k), vsz_raw=vsz, key=k)
+            pos += r.entry_size
+            rows.append(r)
+        files.append((f + 1, rows))
+    want = _full_fold(files)
+    assert len(want[0]) > 20000
+    for cuts in ([0, 5], [0, 1, 2, 3, 4, 5]):
+        got = _native_fold(native, _blocks(files, cuts))
+        assert got[0] == want[0] and got[1] == want[1]
+        assert got[2] == max(want[2], 0)
