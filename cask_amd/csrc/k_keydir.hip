@@ -357,6 +357,15 @@ struct KdScratch {
     if (out) (void)hipFree(out);
     if (part) (void)hipFree(part);
   }
+  // The per-row scratch of a large build (~96 B per row: 23 GB for configs[3]'s 237 M rows) goes back
+  // once the block is written; the block itself stays until the next call.
+  void trim() {
+    if (p && cap > (4ull << 30)) {
+      (void)hipFree(p);
+      p = nullptr;
+      cap = 0;
+    }
+  }
   bool ensure_part(size_t b) {
     if (b <= part_cap) return true;
     if (part) (void)hipFree(part);
@@ -414,10 +423,9 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   const uint64_t n1 = n ? n : 1;
   const uint64_t o_fd = take(sizeof(FileDesc) * (nfiles + 1)), o_files = take(4ull * (nfiles + 1)), o_rowoff = take(8ull * (nfiles + 1)), o_h = take(8 * n1),
                  o_idx = take(4 * n1), o_fidx = take(4 * n1), o_hs = take(8 * n1), o_is = take(4 * n1),
-                 o_head = take(n1), o_kind = take(n1), o_tval = take(8 * n1), o_ecnt = take(8 * n1),
-                 o_ekey = take(8 * n1), o_eoff = take(8 * n1), o_koff = take(8 * n1), o_seg = take(4 * n1),
-                 o_sf = take(4 * n1), o_sksz = take(2 * n1), o_skey = take(16 * n1), o_rfld = take(16 * n1),
-                 o_rkey = take(16 * n1),
+                 o_head = take(n1), o_kind = take(n1), o_tval = take(8 * n1), o_ek = take(16 * n1),
+                 o_ok = take(16 * n1), o_seg = take(4 * n1), o_sf = take(4 * n1), o_sksz = take(2 * n1),
+                 o_skey = take(16 * n1),
                  o_nseg = take(8), o_fstat = take(32ull * (nfiles + 1)), o_tot = take(64), o_tmp = take(tmp);
   if (!S_.ensure(o)) return -13;
   uint8_t* b = (uint8_t*)S_.p;
@@ -447,18 +455,20 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   a.head = b + o_head;
   a.kind = b + o_kind;
   a.tval = (uint64_t*)(b + o_tval);
-  a.ecnt = (uint64_t*)(b + o_ecnt);
-  a.ekey = (uint64_t*)(b + o_ekey);
-  a.eoff = (uint64_t*)(b + o_eoff);
-  a.koff = (uint64_t*)(b + o_koff);
+  // (ecnt/ekey and eoff/koff are written from k_kd_segs on; until k_kd_gather has run, the same
+  // bytes hold k_kd_hash's packed rows: rfld and rkey)
+  a.ecnt = (uint64_t*)(b + o_ek);
+  a.ekey = (uint64_t*)(b + o_ek) + n1;
+  a.eoff = (uint64_t*)(b + o_ok);
+  a.koff = (uint64_t*)(b + o_ok) + n1;
   a.seg = (uint32_t*)(b + o_seg);
   a.sseq = (uint64_t*)(b + o_h);    // (the sort's inputs are dead once it has run)
   a.svsz = (uint32_t*)(b + o_idx);
   a.sf = (uint32_t*)(b + o_sf);
   a.sksz = (uint16_t*)(b + o_sksz);
   a.skey = (u32x4*)(b + o_skey);
-  a.rfld = (u32x4*)(b + o_rfld);
-  a.rkey = (u32x4*)(b + o_rkey);
+  a.rfld = (u32x4*)(b + o_ek);
+  a.rkey = (u32x4*)(b + o_ok);
   a.nseg = (uint32_t*)(b + o_nseg);
   a.fstat = (uint64_t*)(b + o_fstat);
   a.tot = (unsigned long long*)(b + o_tot);
@@ -504,6 +514,7 @@ int kd_build(void* scratch, const FileDesc* files_host, const uint32_t* file_ids
   hipLaunchKernelGGL(k_kd_header, dim3(1), dim3(256), 0, st, a, n, fstat_at, total);
   H(hipStreamSynchronize(st));
   H(hipGetLastError());
+  S_.trim();
   if (!ok) return -11;
   *out = S_.out;
   *bytes = total;
@@ -704,6 +715,7 @@ int kd_partition(void* scratch, const void* block, uint64_t bytes, uint32_t npar
   hipLaunchKernelGGL(k_pt_head, dim3((uint32_t)std::min<uint64_t>((th + 255) / 256, 4096)), dim3(256), 0, st, a);
   H(hipStreamSynchronize(st));
   H(hipGetLastError());
+  S_.trim();
   if (!ok) return -11;
   *out = S_.part;
   return 0;
