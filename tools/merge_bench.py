@@ -1,6 +1,6 @@
 """Host fold of one keydir block (cask_keydir_merge + cask_keydir_finish), timed on this machine's
 threads: a synthetic block of N unique 16-B keys (kind kKept, 64 files), the shape of configs[3]'s
-device-reduced open. CPU only (no GPU needed): python tools/merge_bench.py [N]."""
+device-reduced open. CPU only (no GPU needed): python tools/merge_bench.py [N [LIB]]."""
 import ctypes as C
 import os
 import sys
@@ -46,6 +46,8 @@ def main():
     os.environ.setdefault("CASK_OPEN_TRACE", "1")
     n = int(sys.argv[1]) if len(sys.argv) > 1 else 10_000_000
     import cask_amd
+    if len(sys.argv) > 2:  # an A/B build of the library
+        cask_amd._lib.use_library(sys.argv[2])
     L = cask_amd.lib()
     b = block(n)
     for _ in range(2):
