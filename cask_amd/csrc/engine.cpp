@@ -2612,8 +2612,8 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   // (parallel_fold's split), each table taking its records in block order — first the thresholds
   // against the keydir entering the shard, then the updates. Stale terms are per-file sums.
   // Pass 1, threads by piece of the block: each record with its key hash (and its key when short)
-  // appended to its (piece, table) list, so that pass 2 streams each table's lists instead of
-  // reaching back into the block for every record.
+  // written to its place in one array of items in (table, piece, block) order, so that pass 2
+  // streams each table's items instead of reaching back into the block for every record.
   const char* mv = cask_knobs::hook("CASK_PAR_FOLD_MIN");
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
   const unsigned nt = n < min_par ? 1u : std::min(host_threads(), Index::kSub);
@@ -2643,10 +2643,9 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     };
     const uint8_t* key() const { return ksz <= KeyDir::kInline ? kin : kp; }
   };
-  // (a) every record's key hash, and per (piece, table) how many: (b) one array of items in (table,
-  // piece, block) order — written once, in place, no list growing, huge pages (a list per piece and
-  // table of freshly allocated small vectors cost the pass its page faults: 0.39 s per 20 M records
-  // on 8 threads, tools/merge_bench.py)
+  // (a) every record's key hash, and per (piece, table) how many; (b) the items scattered to their
+  // places — written once, no list growing (a list per piece and table of freshly allocated small
+  // vectors cost the pass its page faults: 0.39 s per 20 M records on 8 threads, tools/merge_bench.py)
   const auto tmA = std::chrono::steady_clock::now();
   // (scratch in db: the next block reuses its pages; cask_keydir_finish gives it back)
   auto scratch = [](HostBuf& b, uint64_t bytes) -> uint8_t* {
@@ -2728,30 +2727,28 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
       if (!kd.live) kd.reserve(m);
       tres[t] += ms_since(tr);
       for (int phase = first_phase; phase < 2; ++phase) {
-        {
-          for (size_t jj = 0; jj < m; ++jj) {
-            if (jj + 16 < m) kd.prefetch(Lq[jj + 16].hash);
-            if (jj + 4 < m) kd.prefetch_key(Lq[jj + 4].hash);
-            const Item& r = Lq[jj];
-            auto entry = [&]() -> const cask_index_entry* {
-              const int64_t f = kd.find(r.key(), r.ksz, r.hash);
-              return f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
-            };
-            if (phase == 0) {  // 1. thresholds, against the keydir entering the shard
-              if (r.kind == kCond) {
-                const cask_index_entry* e = entry();
-                if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
-              }
-              continue;
-            }
-            // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
-            if (r.kind == kCond) continue;
-            if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
+        for (size_t jj = 0; jj < m; ++jj) {
+          if (jj + 16 < m) kd.prefetch(Lq[jj + 16].hash);
+          if (jj + 4 < m) kd.prefetch_key(Lq[jj + 4].hash);
+          const Item& r = Lq[jj];
+          auto entry = [&]() -> const cask_index_entry* {
+            const int64_t f = kd.find(r.key(), r.ksz, r.hash);
+            return f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
+          };
+          if (phase == 0) {  // 1. thresholds, against the keydir entering the shard
+            if (r.kind == kCond) {
               const cask_index_entry* e = entry();
-              if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+              if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
             }
-            kd.update_kd(r.key(), r.ksz, r.file_id, r.pos, r.vsz, r.seq, r.hash);
+            continue;
           }
+          // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
+          if (r.kind == kCond) continue;
+          if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
+            const cask_index_entry* e = entry();
+            if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+          }
+          kd.update_kd(r.key(), r.ksz, r.file_id, r.pos, r.vsz, r.seq, r.hash);
         }
       }
     }
