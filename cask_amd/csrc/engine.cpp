@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <deque>
+#include <initializer_list>
 #include <atomic>
 #include <condition_variable>
 #include <cerrno>
@@ -640,22 +641,7 @@ struct HostBuf {
     return true;
   }
   uint8_t* get() const { return p; }
-  // unmapped on a thread of its own (a multi-GiB mapping takes a while to give back, and nothing
-  // waits for it), or here when no thread can be had
-  void reset_async() {
-    if (!p) return;
-    uint8_t* q = p;
-    const size_t m = n;
-    p = nullptr;
-    n = 0;
-    try {
-      std::thread([q, m] { munmap(q, m); }).detach();
-    } catch (...) {
-      munmap(q, m);
-    }
-  }
 };
-
 // A whole file into a HostBuf (no zero fill before the read, huge pages); false on an I/O error.
 bool read_file_buf(const std::string& p, HostBuf& out, uint64_t& len) {
   len = 0;
@@ -1108,6 +1094,23 @@ struct cask_db {
   // the merge's scratch (key hashes, items), kept from block to block and given back after the
   // last one (cask_keydir_finish), off the calling thread
   HostBuf mhash, mitems;
+  // Host buffers of GiBs given back on a thread of the db's own (unmapping them takes a while and
+  // nothing waits for it), joined before the next discard and at close; here when no thread can
+  // be had.
+  std::vector<HostBuf> gone;
+  std::thread gone_th;
+  void discard(std::initializer_list<HostBuf*> bs) {
+    if (gone_th.joinable()) gone_th.join();
+    gone.clear();
+    for (HostBuf* b : bs)
+      if (b->p) gone.push_back(std::move(*b));
+    if (gone.empty()) return;
+    try {
+      gone_th = std::thread([this] { gone.clear(); });
+    } catch (...) {
+      gone.clear();
+    }
+  }
   // the bytes of files a compaction took out of the database, released on a thread of their own
   // (joined before the next compaction and at close)
   std::thread reclaim;
@@ -1116,6 +1119,7 @@ struct cask_db {
   }
   ~cask_db() {
     reclaim_join();
+    if (gone_th.joinable()) gone_th.join();
     if (lock_fd >= 0) {
       flock(lock_fd, LOCK_UN);  // Drop for Log (log.rs:225-229)
       close(lock_fd);
@@ -1627,7 +1631,7 @@ static cask_db* db_open_impl(const char* path_c, const cask_options* opts_in, ca
       fprintf(stderr, "open (device-reduced keydir): block %.1f ms on the device, %.1f ms to the host (%llu B); "
                       "waited %.1f ms; merge %.1f ms, finish %.1f ms\n",
               t_blk, t_blk_d2h, (unsigned long long)dblock_n, t_wait, t_merge, ms_since(tf3) - t_wait - t_merge);
-    dblock.reset_async();
+    db->discard({&dblock});
     if (st != CASK_OK) {
       fail = st;
       fail_fid = 0;
@@ -2648,9 +2652,9 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   // vectors cost the pass its page faults: 0.39 s per 20 M records on 8 threads, tools/merge_bench.py)
   const auto tmA = std::chrono::steady_clock::now();
   // (scratch in db: the next block reuses its pages; cask_keydir_finish gives it back)
-  auto scratch = [](HostBuf& b, uint64_t bytes) -> uint8_t* {
+  auto scratch = [&](HostBuf& b, uint64_t bytes) -> uint8_t* {
     if (b.n >= bytes) return b.get();
-    b.reset_async();
+    db->discard({&b});
     if (!b.alloc(bytes + bytes / 2)) throw std::bad_alloc();  // (headroom for a larger next block:
     return b.get();                                            // untouched pages cost nothing)
   };
@@ -2797,8 +2801,7 @@ int cask_keydir_finish(cask_db* db) {
     db->files.erase(std::unique(db->files.begin(), db->files.end()), db->files.end());
     db->file_seq = db->files.empty() ? 0u : db->files.back();
     db->merging = false;
-    db->mhash.reset_async();
-    db->mitems.reset_async();
+    db->discard({&db->mhash, &db->mitems});
     return CASK_OK;
   });
 }
