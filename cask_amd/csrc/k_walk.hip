@@ -112,18 +112,11 @@ static_assert(64 * kSwDw * 4 >= kSwStep, "every candidate byte of a window is sc
 #define CASK_SW_PROBE 16
 #endif
 constexpr uint32_t kProbeHops = CASK_SW_PROBE;  // phase 3: headers a long candidate's chain is followed for
-#ifndef CASK_SW_BACK  // (A/B variant: after this many forward windows, the window before b0 once)
-#define CASK_SW_BACK 0
-#endif
-constexpr uint32_t kSwBack = CASK_SW_BACK;
-constexpr uint32_t kBackList = 32;  // the backward window's candidates that reach b0
 struct SearchLdsSw {
   uint32_t wins[1][kSwWin / 4 + 16];
   uint32_t cand[16];
   uint32_t nl;
-  uint32_t nb;  // (kSwBack) candidates in bx / bl
-  uint32_t pad[2];
-  uint32_t bx[kBackList], bl[kBackList];  // (kSwBack) candidate: LDS byte; where its record ends - b0
+  uint32_t pad[3];
   // phase 3: a round's short records reached from long candidates (file offset, length, candidate)
   uint64_t pp[16];
   uint32_t prl[16], pcx[16];
@@ -131,93 +124,6 @@ struct SearchLdsSw {
   // run and kSearchPast past it, far below 2^32), 2 KiB instead of 4: more searching waves per CU
   uint32_t lx[kLongList], le[kLongList];
 };
-
-// (kSwBack) the window before b0 and its candidates' chains: the lowest verified end, as an offset
-// from b0, or kNone. Out of line: its registers stay out of the forward search's.
-__device__ __attribute__((noinline)) uint64_t search_back(SearchLdsSw& L, const uint8_t* data, uint64_t len,
-                                                          uint64_t b0, uint64_t lim, uint32_t sshort) {
-  const uint64_t wbB = b0 > kSwStep ? b0 - kSwStep : 0;
-  uint32_t* W = L.wins[0];
-  const uint32_t lane = threadIdx.x, q = lane >> 2, qa = lane & 3;
-  const uint32_t xB = walk_stage<kSwNL>(W, data, len, wbB);
-  if (lane == 0) L.nb = 0;
-  __syncthreads();
-  const uint32_t ob = (uint32_t)(b0 - wbB);  // candidate offsets [0, ob)
-  const uint32_t d0 = ((xB + 17) >> 2) + kSwDw * lane;
-  for (uint32_t k = 0; k < kSwDw; ++k) {
-    const uint32_t w = W[d0 + k], wp = W[d0 + k - 1];
-    const uint32_t kszhi_small = ~(((wp & 0x7F7F7F7Fu) + 0x6F6F6F6Fu) | wp) & 0x80808080u;
-    const uint32_t y = (w ^ (w >> 1)) & 0x7F7F7F7Fu;
-    uint32_t m = ~(y + 0x7F7F7F7Fu) & 0x80808080u & kszhi_small;
-    while (m) {
-      const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
-      m &= m - 1;
-      const int64_t o = (int64_t)(4 * (d0 + k) + b) - 17 - (int64_t)xB;
-      if (o < 0 || o >= (int64_t)ob) continue;
-      const uint64_t e = wbB + (uint64_t)o + lds_reclen(W, xB + (uint32_t)o);
-      if (e < b0 || e >= lim || e + 18 > len) continue;
-      const uint32_t r = atomicAdd(&L.nb, 1u);
-      if (r < kBackList) {
-        L.bx[r] = xB + (uint32_t)o;
-        L.bl[r] = (uint32_t)(e - b0);
-      }
-    }
-  }
-  __syncthreads();
-  const uint32_t nb = L.nb < kBackList ? L.nb : kBackList;
-  uint64_t tp = kNone;
-  uint32_t trl = 0;
-  if (lane < nb) {
-    uint64_t p = b0 + L.bl[lane];
-    uint64_t sq = lds_hdr(W, L.bx[lane]).seq;
-    for (uint32_t hop = 0; hop < kProbeHops; ++hop) {
-      if (p >= lim || p + 18 > len) break;
-      const u32x4 hd = gld16g((const g_u8*)(data + p + 2));  // header bytes 2..17
-      const uint32_t ksz = hd.z >> 16, vsz = hd.w;
-      const uint64_t sn = (uint64_t)fun(hd.x, hd.y, 2) | ((uint64_t)fun(hd.y, hd.z, 2) << 32);
-      if (ksz > 4351u || ((vsz >> 24) != 0u && vsz != 0xFFFFFFFFu)) break;
-      if (sn <= sq || sn - sq > (1ull << 32)) break;
-      sq = sn;
-      const uint64_t rl = 18ull + ksz + (vsz == 0xFFFFFFFFu ? 0ull : (uint64_t)vsz);
-      if (rl <= sshort) {
-        if (p + rl <= len) {
-          tp = p;
-          trl = (uint32_t)rl;
-        }
-        break;
-      }
-      p += rl;
-    }
-  }
-  const unsigned long long hm = __ballot(tp != kNone);
-  const uint32_t nh = (uint32_t)__builtin_popcountll(hm);
-  const uint32_t rank = (uint32_t)__builtin_popcountll(hm & (lane ? (~0ull >> (64 - lane)) : 0ull));
-  uint64_t best = kNone;
-  for (uint32_t r0 = 0; r0 < nh; r0 += 16) {
-    if (tp != kNone && rank >= r0 && rank < r0 + 16) {
-      L.pp[rank - r0] = tp;
-      L.prl[rank - r0] = trl;
-      L.pcx[rank - r0] = L.bl[lane];
-    }
-    __syncthreads();
-    const uint32_t nq = nh - r0 < 16 ? nh - r0 : 16u;
-    uint64_t x = kNone;
-    if (q < nq) {
-      const uint64_t pq = L.pp[q];
-      const uint32_t rq = L.prl[q];
-      const uint32_t st = gld4g((const g_u8*)(data + pq));
-      const uint32_t h = quad_gbl_xxh32<2>(data + pq + 4, rq - 4, qa);
-      if (qa == 0 && h == st) x = L.pcx[q];
-    }
-    for (int s2 = 32; s2; s2 >>= 1) {
-      const uint64_t y2 = __shfl_xor(x, s2, 64);
-      x = y2 < x ? y2 : x;
-    }
-    best = x < best ? x : best;
-    __syncthreads();
-  }
-  return best;
-}
 
 __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t* data, uint64_t len, uint64_t b0,
                                                    uint64_t b1, uint64_t* wst, uint32_t sshort) {
@@ -229,8 +135,6 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
   if (lane == 0) L.nl = 0;
   bool over = false;
   uint32_t nl0 = 0;  // long candidates already followed by phase 3
-  uint32_t nwin = 0;
-  bool back_found = false;
   // (staging the next window into registers while this one is searched measured no faster: 207
   // VGPRs, 2 waves per SIMD instead of 3)
   for (uint64_t wb = b0; wb < lim && kA == kNone; wb += kSwStep) {
@@ -418,22 +322,7 @@ __device__ __forceinline__ uint64_t walk_search_sw(SearchLdsSw& L, const uint8_t
       nl0 = n1;
       if (best != kNone) kA = b0 + best;
     }
-    // The window before b0, once, when kSwBack forward windows found nothing (kSwBack > 0): a long
-    // search is one whose b0 falls near the start of a long record, so the forward windows scan its
-    // value bytes; the record's own header then lies just before b0. A candidate there whose record
-    // reaches b0 or past it has its chain followed from that end, as in phase 3 (sequence rising
-    // by at most 2^32 per hop, to the first short record, whose XXH32 must match); the lowest end
-    // of a verified candidate is the first record start >= b0 (the candidate's record covers
-    // everything between), so the hop back is not needed. (Speed only: k_finish checks the start.)
-    if (kSwBack && kA == kNone && ++nwin == kSwBack && b0 > 0) {
-      const uint64_t best = search_back(L, data, len, b0, lim, sshort);
-      if (best != kNone) {
-        kA = b0 + best;
-        back_found = true;
-      }
-    }
   }
-  if (back_found) return kA;
   over = __any(over) || L.nl > kLongList;
   WST(th0)
   if (kA == kNone) return kNone;
