@@ -370,8 +370,7 @@ def cfg5_shard_secondary(ctx, torch, dev, rank, world, dist, backend, same_devic
         recv = exchange_parts(parts)
         got = sum(int(p.numel()) for p in recv)
         fold = KeydirFold()
-        for p in recv:
-            fold.merge(p)
+        fold.merge_all(recv)
         terms = all_gather_bytes(torch.from_numpy(fold.terms()))
         db = fold.finish_terms(b"".join(t.numpy().tobytes() for t in terms))
         del parts, recv
@@ -637,8 +636,7 @@ def main():
                 db, got = None, sum(int(b.numel()) for b in got_b) if got_b else int(blk.numel())
                 if rank == 0:
                     fold = KeydirFold()
-                    for b in got_b:
-                        fold.merge(b.cpu())
+                    fold.merge_all([b.cpu() for b in got_b])
                     db = fold.finish()
                 barrier()
                 te = time.perf_counter()

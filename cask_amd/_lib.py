@@ -156,6 +156,7 @@ SIGNATURES = [
     ("cask_keydir_finish_terms", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
     ("cask_keydir_new", C.c_void_p, []),
     ("cask_keydir_merge", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64]),
+    ("cask_keydir_merge_many", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_uint32]),
     ("cask_keydir_finish", C.c_int, [C.c_void_p]),
     ("cask_db_open_multi", C.c_void_p, [C.c_char_p, C.POINTER(Options), C.POINTER(C.c_int), C.c_int,
                                         C.POINTER(OpenError)]),

@@ -2584,11 +2584,11 @@ cask_db* cask_keydir_new(void) {
   return db;
 }
 
-static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes);
+static int keydir_merge_impl(cask_db* db, const uint8_t* const* blks, const uint64_t* bytes, uint32_t nb);
 
 int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   try {  // the block comes from a peer rank: no exception crosses the C ABI
-    return keydir_merge_impl(db, blk, bytes);
+    return keydir_merge_impl(db, &blk, &bytes, 1);
   } catch (const std::bad_alloc&) {
     return CASK_E_NOMEM;
   } catch (...) {
@@ -2596,45 +2596,96 @@ int cask_keydir_merge(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   }
 }
 
-static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
+int cask_keydir_merge_many(cask_db* db, const uint8_t* const* blocks, const uint64_t* bytes, uint32_t n) {
+  try {
+    if (n && (!blocks || !bytes)) return CASK_E_INVALID_ARG;
+    return keydir_merge_impl(db, blocks, bytes, n);
+  } catch (const std::bad_alloc&) {
+    return CASK_E_NOMEM;
+  } catch (...) {
+    return CASK_E_INVALID_ARG;
+  }
+}
+
+// Blocks [0, nb) merged in order, in one pass: each keydir table takes its records block after
+// block (for each, the thresholds of its conditional tombstones against the table as the block
+// finds it, then the updates), which is what merging the blocks one by one does — a key's outcome
+// depends on that key's records alone, in order — with one hashing and scatter pass over all the
+// blocks and a fresh table sized once for all of them (one by one, every later block grew the
+// tables: 8 blocks of 2 M records merged in 0.78-1.44 s against 0.46-0.83 s for one block of 16 M,
+// tools/merge_bench.py's blocks on this container's 8 threads).
+static int keydir_merge_impl(cask_db* db, const uint8_t* const* blks, const uint64_t* bytes, uint32_t nb) {
   using namespace cask_kd;
-  if (!db || !db->merging || (bytes && !blk) || bytes < sizeof(ShardHeader)) return CASK_E_INVALID_ARG;
-  ShardHeader hd;
-  memcpy(&hd, blk, sizeof(hd));
-  // counts bounded by the block's size before any offset is derived from them (no wrap-around)
-  if (hd.nrec > (bytes - sizeof(ShardHeader)) / sizeof(ShardRec) ||
-      (uint64_t)hd.nfiles > (bytes - sizeof(ShardHeader)) / sizeof(ShardFileStat))
-    return CASK_E_INVALID_ARG;
-  const uint64_t rec_at = sizeof(ShardHeader), fst_at = rec_at + sizeof(ShardRec) * hd.nrec,
-                 key_at = fst_at + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
-  if (hd.magic != kMagic || hd.version != kVersion || hd.bytes > bytes || key_at + hd.key_bytes > hd.bytes)
-    return CASK_E_INVALID_ARG;
-  const ShardRec* rec = (const ShardRec*)(blk + rec_at);
-  const uint8_t* keys = blk + key_at;
-  const uint64_t n = hd.nrec;
+  if (!db || !db->merging) return CASK_E_INVALID_ARG;
+  struct Blk {
+    ShardHeader hd;
+    const ShardRec* rec;
+    const uint8_t* keys;
+    const ShardFileStat* fs;
+    uint64_t n, r0;  // records, the first record's index over all blocks
+  };
+  std::vector<Blk> B(nb);
+  uint64_t n = 0;
+  for (uint32_t b = 0; b < nb; ++b) {  // every block checked before anything changes
+    const uint8_t* blk = blks[b];
+    if ((bytes[b] && !blk) || bytes[b] < sizeof(ShardHeader)) return CASK_E_INVALID_ARG;
+    ShardHeader& hd = B[b].hd;
+    memcpy(&hd, blk, sizeof(hd));
+    // counts bounded by the block's size before any offset is derived from them (no wrap-around)
+    if (hd.nrec > (bytes[b] - sizeof(ShardHeader)) / sizeof(ShardRec) ||
+        (uint64_t)hd.nfiles > (bytes[b] - sizeof(ShardHeader)) / sizeof(ShardFileStat))
+      return CASK_E_INVALID_ARG;
+    const uint64_t rec_at = sizeof(ShardHeader), fst_at = rec_at + sizeof(ShardRec) * hd.nrec,
+                   key_at = fst_at + sizeof(ShardFileStat) * (uint64_t)hd.nfiles;
+    if (hd.magic != kMagic || hd.version != kVersion || hd.bytes > bytes[b] || key_at + hd.key_bytes > hd.bytes)
+      return CASK_E_INVALID_ARG;
+    B[b].rec = (const ShardRec*)(blk + rec_at);
+    B[b].keys = blk + key_at;
+    B[b].fs = (const ShardFileStat*)(blk + fst_at);
+    B[b].n = hd.nrec;
+    B[b].r0 = n;
+    n += hd.nrec;
+  }
   // The fold of a block depends on each key's records alone, in order: on threads by keydir table
   // (parallel_fold's split), each table taking its records in block order — first the thresholds
-  // against the keydir entering the shard, then the updates. Stale terms are per-file sums.
-  // Pass 1, threads by piece of the block: each record with its key hash (and its key when short)
-  // written to its place in one array of items in (table, piece, block) order, so that pass 2
-  // streams each table's items instead of reaching back into the block for every record.
+  // against the keydir entering the block, then the updates. Stale terms are per-file sums.
+  // Pass 1, threads by piece of a block: each record with its key hash (and its key when short)
+  // written to its place in one array of items in (table, block, piece, record) order, so that
+  // pass 2 streams each table's items instead of reaching back into the blocks for every record.
   const char* mv = cask_knobs::hook("CASK_PAR_FOLD_MIN");
   const uint64_t min_par = mv ? strtoull(mv, nullptr, 10) : (1ull << 16);
   const unsigned nt = n < min_par ? 1u : std::min(host_threads(), Index::kSub);
   constexpr unsigned S = Index::kSub;
-  const unsigned np = nt == 1 ? 1u : 4 * nt;  // pieces
+  const unsigned np = nt == 1 ? 1u : 4 * nt;  // pieces per block
+  const size_t NP = (size_t)nb * np;          // pieces over all blocks: P = b * np + g
+  auto piece = [&](size_t P, uint64_t* lo, uint64_t* hi) {
+    const Blk& k = B[P / np];
+    const uint64_t g = P % np;
+    *lo = k.n * g / np;
+    *hi = k.n * (g + 1) / np;
+  };
   const auto tm0 = std::chrono::steady_clock::now();
-  // every piece's first key offset (the keys lie in record order), checked before anything changes
-  std::vector<uint64_t> pko(np + 1, 0);
+  // every piece's first key offset in its block (the keys lie in record order), checked first
+  std::vector<uint64_t> pko(NP + 1, 0);
   parallel_for(nt, [&](unsigned t) {
-    for (unsigned g = t; g < np; g += nt) {
-      uint64_t o = 0;
-      for (uint64_t i = n * g / np, e = n * (g + 1) / np; i < e; ++i) o += rec[i].ksz;
-      pko[g + 1] = o;
+    for (size_t P = t; P < NP; P += nt) {
+      uint64_t lo, hi, o = 0;
+      piece(P, &lo, &hi);
+      const ShardRec* rec = B[P / np].rec;
+      for (uint64_t i = lo; i < hi; ++i) o += rec[i].ksz;
+      pko[P + 1] = o;
     }
   });
-  for (unsigned g = 0; g < np; ++g) pko[g + 1] += pko[g];
-  if (pko[np] > hd.key_bytes) return CASK_E_INVALID_ARG;
+  for (uint32_t b = 0; b < nb; ++b) {  // (exclusive prefix within each block)
+    uint64_t o = 0;
+    for (unsigned g = 0; g < np; ++g) {
+      const uint64_t k = pko[(size_t)b * np + g + 1];
+      pko[(size_t)b * np + g + 1] = 0;
+      pko[(size_t)b * np + g] = o;
+      o += k;
+    }
+    if (o > B[b].hd.key_bytes) return CASK_E_INVALID_ARG;
+  }
   struct Item {
     uint64_t hash, seq, pos;
     uint32_t file_id, vsz;
@@ -2643,7 +2694,7 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     uint32_t pad1;
     union {
       uint8_t kin[KeyDir::kInline];
-      const uint8_t* kp;  // ksz > kInline: the key in the block
+      const uint8_t* kp;  // ksz > kInline: the key in its block
     };
     const uint8_t* key() const { return ksz <= KeyDir::kInline ? kin : kp; }
   };
@@ -2651,46 +2702,53 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
   // places — written once, no list growing (a list per piece and table of freshly allocated small
   // vectors cost the pass its page faults: 0.39 s per 20 M records on 8 threads, tools/merge_bench.py)
   const auto tmA = std::chrono::steady_clock::now();
-  // (scratch in db: the next block reuses its pages; cask_keydir_finish gives it back)
-  auto scratch = [&](HostBuf& b, uint64_t bytes) -> uint8_t* {
-    if (b.n >= bytes) return b.get();
-    db->discard({&b});
-    if (!b.alloc(bytes + bytes / 2)) throw std::bad_alloc();  // (headroom for a larger next block:
-    return b.get();                                            // untouched pages cost nothing)
+  // (scratch in db: the next call reuses its pages; cask_keydir_finish gives it back)
+  auto scratch = [&](HostBuf& hb, uint64_t nbytes) -> uint8_t* {
+    if (hb.n >= nbytes) return hb.get();
+    db->discard({&hb});
+    if (!hb.alloc(nbytes + nbytes / 2)) throw std::bad_alloc();  // (headroom for a larger next call:
+    return hb.get();                                              // untouched pages cost nothing)
   };
   uint64_t* hs = (uint64_t*)scratch(db->mhash, std::max<uint64_t>(n, 1) * sizeof(uint64_t));
-  std::vector<uint64_t> cnt((size_t)np * S, 0);
-  std::vector<uint64_t> nconds(np, 0);
+  std::vector<uint64_t> cnt(NP * S, 0);
+  std::vector<uint64_t> nconds(NP, 0);
   parallel_for(nt, [&](unsigned t) {
-    for (unsigned g = t; g < np; g += nt) {
-      uint64_t* c = &cnt[(size_t)g * S];
-      uint64_t ko = pko[g];
+    for (size_t P = t; P < NP; P += nt) {
+      uint64_t lo, hi;
+      piece(P, &lo, &hi);
+      const Blk& k = B[P / np];
+      uint64_t* c = &cnt[P * S];
+      uint64_t ko = pko[P];
       uint64_t lc[S] = {}, nc = 0;  // (locals: no stores to lines other threads write)
-      for (uint64_t i = n * g / np, e = n * (g + 1) / np; i < e; ++i) {
-        const uint64_t h = hash_key(keys + ko, rec[i].ksz);
-        hs[i] = h;
+      for (uint64_t i = lo; i < hi; ++i) {
+        const uint64_t h = hash_key(k.keys + ko, k.rec[i].ksz);
+        hs[k.r0 + i] = h;
         ++lc[Index::sub_of(h)];
-        nc += rec[i].kind == kCond;
-        ko += rec[i].ksz;
+        nc += k.rec[i].kind == kCond;
+        ko += k.rec[i].ksz;
       }
       for (unsigned q = 0; q < S; ++q) c[q] = lc[q];
-      nconds[g] = nc;
+      nconds[P] = nc;
     }
   });
-  std::vector<uint64_t> at((size_t)np * S + 1, 0);  // (table q, piece g) starts at at[q * np + g]
-  for (unsigned q = 0, k = 0; q < S; ++q)
-    for (unsigned g = 0; g < np; ++g, ++k) at[k + 1] = at[k] + cnt[(size_t)g * S + q];
+  std::vector<uint64_t> at(NP * S + 1, 0);  // (table q, piece P) starts at at[q * NP + P]
+  for (size_t q = 0, k = 0; q < S; ++q)
+    for (size_t P = 0; P < NP; ++P, ++k) at[k + 1] = at[k] + cnt[P * S + q];
   const auto tmB = std::chrono::steady_clock::now();
   Item* items = (Item*)scratch(db->mitems, std::max<uint64_t>(n, 1) * sizeof(Item));
   parallel_for(nt, [&](unsigned t) {
-    for (unsigned g = t; g < np; g += nt) {
+    for (size_t P = t; P < NP; P += nt) {
+      uint64_t lo, hi;
+      piece(P, &lo, &hi);
+      const Blk& k = B[P / np];
       uint64_t w[S];
-      for (unsigned q = 0; q < S; ++q) w[q] = at[(size_t)q * np + g];
-      uint64_t ko = pko[g];
-      for (uint64_t i = n * g / np, e = n * (g + 1) / np; i < e; ++i) {
-        const ShardRec& r = rec[i];
-        Item& it = items[w[Index::sub_of(hs[i])]++];
-        it.hash = hs[i];
+      for (unsigned q = 0; q < S; ++q) w[q] = at[q * NP + P];
+      uint64_t ko = pko[P];
+      for (uint64_t i = lo; i < hi; ++i) {
+        const ShardRec& r = k.rec[i];
+        const uint64_t h = hs[k.r0 + i];
+        Item& it = items[w[Index::sub_of(h)]++];
+        it.hash = h;
         it.seq = r.seq;
         it.pos = r.pos;
         it.file_id = r.file_id;
@@ -2699,21 +2757,18 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
         it.kind = r.kind;
         it.pad0 = 0;
         it.pad1 = 0;
-        if (r.ksz <= KeyDir::kInline) memcpy(it.kin, keys + ko, r.ksz);
-        else it.kp = keys + ko;
+        if (r.ksz <= KeyDir::kInline) memcpy(it.kin, k.keys + ko, r.ksz);
+        else it.kp = k.keys + ko;
         ko += r.ksz;
       }
     }
   });
   const bool tracing = cask_knobs::hook("CASK_OPEN_TRACE") != nullptr;
   const auto tm1 = std::chrono::steady_clock::now();
-  if (tracing) fprintf(stderr, "keydir merge: %llu records, lists %.1f ms (pko %.1f, hash %.1f)\n", (unsigned long long)n, ms_since(tm0), std::chrono::duration<double, std::milli>(tmA - tm0).count(), std::chrono::duration<double, std::milli>(tmB - tmA).count());
-  std::vector<double> tres(nt, 0.0);
-  // phase 0 (the thresholds) only for a block with conditional tombstones, against a keydir that
-  // holds something (an empty one stales none of them)
-  uint64_t ncond = 0;
-  for (uint64_t c : nconds) ncond += c;
-  const int first_phase = ncond && db->index.live() ? 0 : 1;
+  if (tracing) fprintf(stderr, "keydir merge: %u blocks, %llu records, lists %.1f ms (pko %.1f, hash %.1f)\n", nb, (unsigned long long)n, ms_since(tm0), std::chrono::duration<double, std::milli>(tmA - tm0).count(), std::chrono::duration<double, std::milli>(tmB - tmA).count());
+  std::vector<char> has_cond(nb, 0);  // the blocks with conditional tombstones
+  for (size_t P = 0; P < NP; ++P)
+    if (nconds[P]) has_cond[P / np] = 1;
   std::vector<std::unordered_map<uint32_t, cask_db::ShardTerms>> sterms(nt);
   parallel_for(nt, [&](unsigned t) {
     auto stale = [&](uint32_t fid, uint32_t ksz) {  // Stats add + remove of a stale tombstone
@@ -2723,60 +2778,63 @@ static int keydir_merge_impl(cask_db* db, const uint8_t* blk, uint64_t bytes) {
     };
     for (unsigned q = t; q < S; q += nt) {
       KeyDir& kd = db->index.sub[q];
-      const Item* Lq = items + at[(size_t)q * np];
-      const size_t m = at[(size_t)(q + 1) * np] - at[(size_t)q * np];  // the table's items, in block order
-      const auto tr = std::chrono::steady_clock::now();
       // (a fresh table: room for every record's key — a block holds about one record per key; a
       // table holding keys grows when it fills, as in parallel_fold)
-      if (!kd.live) kd.reserve(m);
-      tres[t] += ms_since(tr);
-      for (int phase = first_phase; phase < 2; ++phase) {
-        for (size_t jj = 0; jj < m; ++jj) {
-          if (jj + 16 < m) kd.prefetch(Lq[jj + 16].hash);
-          if (jj + 4 < m) kd.prefetch_key(Lq[jj + 4].hash);
-          const Item& r = Lq[jj];
-          auto entry = [&]() -> const cask_index_entry* {
-            const int64_t f = kd.find(r.key(), r.ksz, r.hash);
-            return f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
-          };
-          if (phase == 0) {  // 1. thresholds, against the keydir entering the shard
-            if (r.kind == kCond) {
-              const cask_index_entry* e = entry();
-              if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+      if (!kd.live) kd.reserve(at[(q + 1) * NP] - at[q * NP]);
+      for (uint32_t b = 0; b < nb; ++b) {
+        const Item* Lq = items + at[q * NP + (size_t)b * np];
+        const size_t m = at[q * NP + (size_t)(b + 1) * np] - at[q * NP + (size_t)b * np];  // block b's, in order
+        // phase 0 (the thresholds) only for a block with conditional tombstones, against a table
+        // that holds something (an empty one stales none of them)
+        for (int phase = has_cond[b] && kd.live ? 0 : 1; phase < 2; ++phase) {
+          for (size_t jj = 0; jj < m; ++jj) {
+            if (jj + 16 < m) kd.prefetch(Lq[jj + 16].hash);
+            if (jj + 4 < m) kd.prefetch_key(Lq[jj + 4].hash);
+            const Item& r = Lq[jj];
+            auto entry = [&]() -> const cask_index_entry* {
+              const int64_t f = kd.find(r.key(), r.ksz, r.hash);
+              return f >= 0 ? &kd.slots[(uint64_t)f].e : nullptr;
+            };
+            if (phase == 0) {  // 1. thresholds, against the keydir entering the block
+              if (r.kind == kCond) {
+                const cask_index_entry* e = entry();
+                if ((e ? e->sequence + 1 : 0ull) > r.seq) stale(r.file_id, r.ksz);
+              }
+              continue;
             }
-            continue;
+            // 2. the keydir: kept rows, and collided keys record by record, in the block's order
+            if (r.kind == kCond) continue;
+            if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
+              const cask_index_entry* e = entry();
+              if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
+            }
+            kd.update_kd(r.key(), r.ksz, r.file_id, r.pos, r.vsz, r.seq, r.hash);
           }
-          // 2. the keydir: kept rows, and collided keys record by record, in the shard's order
-          if (r.kind == kCond) continue;
-          if (r.kind == kRaw && r.vsz == CASK_ENTRY_TOMBSTONE) {
-            const cask_index_entry* e = entry();
-            if (e && e->sequence > r.seq) stale(r.file_id, r.ksz);
-          }
-          kd.update_kd(r.key(), r.ksz, r.file_id, r.pos, r.vsz, r.seq, r.hash);
         }
       }
     }
   });
-  if (tracing) fprintf(stderr, "keydir merge: tables %.1f ms (reserve %.1f per thread)\n", ms_since(tm1), tres[0]);
-  const auto tm2 = std::chrono::steady_clock::now();
+  if (tracing) fprintf(stderr, "keydir merge: tables %.1f ms\n", ms_since(tm1));
   for (const auto& m : sterms)
     for (const auto& kv : m) {
       cask_db::ShardTerms& x = db->terms[kv.first];
       x.stale += kv.second.stale;
       x.stale_bytes += kv.second.stale_bytes;
     }
-  const ShardFileStat* fs = (const ShardFileStat*)(blk + fst_at);
-  for (uint32_t f = 0; f < hd.nfiles; ++f) {
-    cask_db::ShardTerms& t = db->terms[fs[f].file_id];
-    t.puts += fs[f].puts;
-    t.put_bytes += fs[f].put_bytes;
-    t.stale += fs[f].stale;
-    t.stale_bytes += fs[f].stale_bytes;
-    db->files.push_back(fs[f].file_id);
+  for (uint32_t b = 0; b < nb; ++b) {
+    const ShardHeader& hd = B[b].hd;
+    for (uint32_t f = 0; f < hd.nfiles; ++f) {
+      const ShardFileStat& fs = B[b].fs[f];
+      cask_db::ShardTerms& t = db->terms[fs.file_id];
+      t.puts += fs.puts;
+      t.put_bytes += fs.put_bytes;
+      t.stale += fs.stale;
+      t.stale_bytes += fs.stale_bytes;
+      db->files.push_back(fs.file_id);
+    }
+    if (hd.max_seq_p1 && hd.max_seq_p1 - 1 > db->sequence) db->sequence = hd.max_seq_p1 - 1;
+    ++db->shards;
   }
-  if (hd.max_seq_p1 && hd.max_seq_p1 - 1 > db->sequence) db->sequence = hd.max_seq_p1 - 1;
-  ++db->shards;
-  if (tracing) fprintf(stderr, "keydir merge: terms %.1f ms\n", ms_since(tm2));
   return CASK_OK;
 }
 
@@ -3229,14 +3287,20 @@ static cask_db* open_multi_impl(const char* path_c, const cask_options* opts_in,
   std::vector<std::vector<uint8_t>>().swap(hints);
   auto tf = std::chrono::steady_clock::now();
   db->merging = true;
-  for (int r = 0; r < ndev; ++r)
-    for (const auto& b : sh[r].blocks) {
-      const int st = cask_keydir_merge(db, b.data(), b.size());
-      if (st != CASK_OK) {
-        set_err(err, st);
-        return nullptr;
+  {  // every range's blocks, in range order, in one pass
+    std::vector<const uint8_t*> bp;
+    std::vector<uint64_t> bl;
+    for (int r = 0; r < ndev; ++r)
+      for (const auto& b : sh[r].blocks) {
+        bp.push_back(b.data());
+        bl.push_back(b.size());
       }
+    const int st = cask_keydir_merge_many(db, bp.data(), bl.data(), (uint32_t)bp.size());
+    if (st != CASK_OK) {
+      set_err(err, st);
+      return nullptr;
     }
+  }
   cask_keydir_finish(db);
   db->timings[0] = rd;
   db->timings[1] = sc;

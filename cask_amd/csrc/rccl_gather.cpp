@@ -288,8 +288,16 @@ static int gather_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t bytes
   if (rank == root) {
     if (off[nranks] && hipMemcpy(host.data(), buf.p, off[nranks], hipMemcpyDeviceToHost) != hipSuccess) fst = CASK_E_DEVICE;
     if (fst == CASK_OK && cask_abi::take_inject(ctx, cask_abi::kInjFold)) fst = CASK_E_NOMEM;
-    for (int r = 0; r < nranks && fst == CASK_OK; ++r)
-      if (all[3ull * r]) fst = cask_keydir_merge(db, host.data() + off[r], all[3ull * r]);
+    if (fst == CASK_OK) {  // (one pass over the ranks' blocks, in rank order)
+      std::vector<const uint8_t*> bp;
+      std::vector<uint64_t> bl;
+      for (int r = 0; r < nranks; ++r)
+        if (all[3ull * r]) {
+          bp.push_back(host.data() + off[r]);
+          bl.push_back(all[3ull * r]);
+        }
+      fst = cask_keydir_merge_many(db, bp.data(), bl.data(), (uint32_t)bp.size());
+    }
   }
   return agree(K, st, fst);
 }
@@ -351,9 +359,17 @@ static int exchange_impl(cask_ctx* ctx, Comm& K, const void* block, uint64_t byt
   int fst = CASK_OK;
   if (roff[nranks] && hipMemcpy(host.data(), buf.p, roff[nranks], hipMemcpyDeviceToHost) != hipSuccess) fst = CASK_E_DEVICE;
   if (fst == CASK_OK && cask_abi::take_inject(ctx, cask_abi::kInjFold)) fst = CASK_E_NOMEM;
-  for (int r = 0; r < nranks && fst == CASK_OK; ++r) {
-    const uint64_t in = all[(uint64_t)r * N + rank];
-    if (in) fst = cask_keydir_merge(db, host.data() + roff[r], in);
+  if (fst == CASK_OK) {  // (one pass over the parts, in rank order)
+    std::vector<const uint8_t*> bp;
+    std::vector<uint64_t> bl;
+    for (int r = 0; r < nranks; ++r) {
+      const uint64_t in = all[(uint64_t)r * N + rank];
+      if (in) {
+        bp.push_back(host.data() + roff[r]);
+        bl.push_back(in);
+      }
+    }
+    fst = cask_keydir_merge_many(db, bp.data(), bl.data(), (uint32_t)bp.size());
   }
   // 5. Stats: every owner's per-file terms to every rank (counts, then the padded tables), summed
   int64_t tb = fst == CASK_OK ? cask_keydir_terms(db, nullptr, 0) : 0;

@@ -116,8 +116,7 @@ def partitioned_fold(block):
     world = dist.get_world_size()
     parts = [torch.from_numpy(np.ascontiguousarray(p)) for p in partition_host(block, world)]
     fold = KeydirFold()
-    for p in exchange_parts(parts):
-        fold.merge(p)
+    fold.merge_all(exchange_parts(parts))
     terms = all_gather_bytes(torch.from_numpy(fold.terms()))
     return fold.finish_terms(b"".join(t.numpy().tobytes() for t in terms))
 

@@ -116,6 +116,15 @@ class KeydirFold:
         a = _u8(block)
         raise_status(self.lib.cask_keydir_merge(self._h, a.ctypes.data, a.size), what="cask_keydir_merge")
 
+    def merge_all(self, blocks):
+        """blocks merged in order in one pass (cask_keydir_merge_many): the same result as merge()
+        of each in turn."""
+        arrs = [_u8(b) for b in blocks]
+        n = len(arrs)
+        ptrs = (C.c_void_p * max(n, 1))(*[a.ctypes.data for a in arrs])
+        lens = (C.c_uint64 * max(n, 1))(*[a.size for a in arrs])
+        raise_status(self.lib.cask_keydir_merge_many(self._h, ptrs, lens, n), what="cask_keydir_merge_many")
+
     def finish(self) -> Cask:
         raise_status(self.lib.cask_keydir_finish(self._h), what="cask_keydir_finish")
         h, self._h = self._h, None

@@ -348,6 +348,9 @@ int cask_copy(cask_ctx* ctx, void* dst, const void* src, uint64_t bytes);
  * _len / _files / _get_entry read it; cask_db_close frees it. */
 cask_db* cask_keydir_new(void);
 int cask_keydir_merge(cask_db* db, const uint8_t* block, uint64_t bytes);
+/* blocks[0..n) merged in order in one pass: the same keydir, terms and sequence as n calls of
+ * cask_keydir_merge, with the tables sized once for all of them. */
+int cask_keydir_merge_many(cask_db* db, const uint8_t* const* blocks, const uint64_t* bytes, uint32_t n);
 int cask_keydir_finish(cask_db* db);
 
 /* Key-hash partition, for a keyspace too large to gather on one host: a block splits

@@ -72,13 +72,20 @@ def test_hash_collisions_fold_record_by_record(monkeypatch):
     assert S.fold_blocks(blocks) == _full_fold(files)
 
 
-def _native_fold(native, blocks):
+def _native_fold(native, blocks, many=False):
+    """many: the blocks in one cask_keydir_merge_many call instead of one cask_keydir_merge each."""
     import ctypes as C
     from cask_amd.cask import Cask
     lib = native
     h = lib.cask_keydir_new()
-    for b in blocks:
-        buf = (C.c_uint8 * len(b)).from_buffer_copy(b)
+    bufs = [(C.c_uint8 * len(b)).from_buffer_copy(b) for b in blocks]
+    if many:
+        ptrs = (C.c_void_p * max(len(bufs), 1))(*[C.addressof(x) for x in bufs])
+        lens = (C.c_uint64 * max(len(bufs), 1))(*[len(b) for b in blocks])
+        assert lib.cask_keydir_merge_many(h, ptrs, lens, len(bufs)) == 0
+    for buf, b in zip(bufs, blocks):
+        if many:
+            break
         assert lib.cask_keydir_merge(h, buf, len(b)) == 0
     assert lib.cask_keydir_finish(h) == 0
     db = Cask(h, "")
@@ -98,9 +105,10 @@ def test_native_fold_matches(native, seed, threads, monkeypatch):
     files = _random_files(rng, 7, 60, rng.choice([2, 10, 50]), 0.25, 0.25)
     want = _full_fold(files)
     for cuts in ([0, 7], [0, 3, 7], [0, 1, 2, 4, 7]):
-        got = _native_fold(native, _blocks(files, cuts))
-        assert got[0] == want[0] and got[1] == want[1]
-        assert got[2] == max(want[2], 0)
+        for many in (False, True):
+            got = _native_fold(native, _blocks(files, cuts), many)
+            assert got[0] == want[0] and got[1] == want[1]
+            assert got[2] == max(want[2], 0)
 
 
 def test_native_fold_rejects_bad_blocks(native):
@@ -211,7 +219,7 @@ def test_native_fold_grows_tables(native, threads, monkeypatch):
         files.append((f + 1, rows))
     want = _full_fold(files)
     assert len(want[0]) > 20000
-    for cuts in ([0, 5], [0, 1, 2, 3, 4, 5]):
-        got = _native_fold(native, _blocks(files, cuts))
+    for cuts, many in (([0, 5], False), ([0, 1, 2, 3, 4, 5], False), ([0, 1, 2, 3, 4, 5], True)):
+        got = _native_fold(native, _blocks(files, cuts), many)
         assert got[0] == want[0] and got[1] == want[1]
         assert got[2] == max(want[2], 0)
