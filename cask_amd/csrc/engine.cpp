@@ -1094,22 +1094,19 @@ struct cask_db {
   // the merge's scratch (key hashes, items), kept from block to block and given back after the
   // last one (cask_keydir_finish), off the calling thread
   HostBuf mhash, mitems;
-  // Host buffers of GiBs given back on a thread of the db's own (unmapping them takes a while and
-  // nothing waits for it), joined before the next discard and at close; here when no thread can
-  // be had.
-  std::vector<HostBuf> gone;
-  std::thread gone_th;
+  // Host buffers of GiBs given back on threads of the db's own (unmapping them takes a while and
+  // nothing waits for it: a thread per discard, each owning what it unmaps), all joined at close;
+  // here when no thread can be had.
+  std::vector<std::thread> gone_th;
   void discard(std::initializer_list<HostBuf*> bs) {
-    if (gone_th.joinable()) gone_th.join();
-    gone.clear();
+    std::vector<HostBuf> g;
     for (HostBuf* b : bs)
-      if (b->p) gone.push_back(std::move(*b));
-    if (gone.empty()) return;
+      if (b->p) g.push_back(std::move(*b));
+    if (g.empty()) return;
     try {
-      gone_th = std::thread([this] { gone.clear(); });
+      gone_th.emplace_back([v = std::move(g)]() mutable { v.clear(); });
     } catch (...) {
-      gone.clear();
-    }
+    }  // (g, if not moved into a thread, is unmapped here)
   }
   // the bytes of files a compaction took out of the database, released on a thread of their own
   // (joined before the next compaction and at close)
@@ -1119,7 +1116,8 @@ struct cask_db {
   }
   ~cask_db() {
     reclaim_join();
-    if (gone_th.joinable()) gone_th.join();
+    for (std::thread& t : gone_th)
+      if (t.joinable()) t.join();
     if (lock_fd >= 0) {
       flock(lock_fd, LOCK_UN);  // Drop for Log (log.rs:225-229)
       close(lock_fd);
